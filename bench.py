@@ -1,0 +1,286 @@
+#!/usr/bin/env python
+"""Benchmark: bootstraps/sec (kNN+SNN+co-cluster) at 100k cells on 1..8 MI355X.
+
+One step = per GPU, B bootstraps of the robust consensusClust path
+(R/consensusClust.R:391-408 + :650-692) -- gather of the bootstrap rows, exact
+kNN at k=20 (k=10/15 are prefixes), SNN "number" graphs for k = 10, 15, 20,
+silhouette scores of the 60 clusterings, selection + map-back to the
+uint8 assignment column -- then the all-gather of every rank's columns and
+this rank's row slab of the co-clustering counts (:411-421) over all
+G*B columns.  Host Leiden is excluded (north_star): the 60 clusterings per
+bootstrap are synthetic labels derived from the true populations with 5%
+flips, generated on the device before timing.  Inputs are resident in HBM
+when the timed region starts.  Weak scaling: B bootstraps per GPU per step
+(default 125 -> 1000 bootstraps = BASELINE config 3 at 8 GPUs).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; multi-GPU through
+torch.distributed.run (one process per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "bootstraps/sec (kNN+SNN+co-cluster) at 100k cells, 1/2/4/8 MI355X"
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_I8_TOPS = 5000.0      # dense int8 MFMA (2x bf16 dense 2.5 PF)
+PEAK_HBM_GBS = 8000.0
+K_NUM = (10, 15, 20)
+N_RES = 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cells", type=int, default=100000)
+    ap.add_argument("--pcs", type=int, default=30)
+    ap.add_argument("--genes", type=int, default=2000)
+    ap.add_argument("--boots-per-gpu", type=int, default=125)
+    ap.add_argument("--boot-size", type=float, default=0.9)
+    ap.add_argument("--cpu-sample-rows", type=int, default=30000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def synth_pcs(torch, N, d, G, seed, dev):
+    """NB counts (12 populations, log-normal base means, 10% DE genes, size
+    factors, theta=5) -> shifted log -> scale -> randomized PCA.  Identical on
+    every rank (same seed)."""
+    torch.manual_seed(seed)
+    C = 12
+    pop = torch.randint(0, C, (N,), device=dev)
+    base = torch.exp(torch.randn(G, device=dev) * 1.5 - 1.0)
+    de = (torch.rand(G, device=dev) < 0.1).float()
+    lfc = torch.randn(C, G, device=dev) * de
+    mu = base[None, :] * torch.pow(2.0, lfc)
+    sf = torch.exp(torch.randn(N, device=dev) * 0.3)
+    theta = 5.0
+    x = torch.empty(N, G, device=dev)
+    for a in range(0, N, 20000):  # chunked to bound temporaries
+        b = min(N, a + 20000)
+        mean = mu[pop[a:b]] * sf[a:b, None]
+        lam = torch.distributions.Gamma(torch.full_like(mean, theta), theta / mean).sample()
+        cnt = torch.poisson(lam)
+        x[a:b] = torch.log1p(cnt / sf[a:b, None])
+    x -= x.mean(0)
+    x /= x.std(0).clamp_min(1e-8)
+    U, S, _ = torch.pca_lowrank(x, q=d, center=False, niter=3)
+    pcs = (U * S).double()
+    del x
+    return pcs, pop
+
+
+def synth_labels(torch, pop_boot, L, dev, seed):
+    """60 clusterings of one bootstrap: C rising with resolution (2..40),
+    permuted true populations, 5% uniform flips; codes 1..C."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n = pop_boot.numel()
+    li = torch.arange(L, device=dev)
+    ki = (li // N_RES)[:, None]
+    Cl = (2 + (38 * (li % N_RES)) // (N_RES - 1))[:, None]
+    lab = (pop_boot[None, :] * 7 + ki) % Cl + 1
+    flip = torch.rand(L, n, device=dev, generator=g) < 0.05
+    rnd = (torch.rand(L, n, device=dev, generator=g) * Cl).long() + 1
+    return torch.where(flip, rnd, lab).to(torch.int32)
+
+
+def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
+    """Time the CPU restatement (oracle/, C + OpenMP) on a bounded sample and
+    extrapolate to one step's work (B bootstraps + the co-cluster slab)."""
+    import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    rng = np.random.default_rng(seed)
+    ns = min(sample_rows, n)
+    boot = rng.integers(0, N, ns).astype(np.int32)
+    X = O.gather_rows(pcs_np, boot)
+    t0 = time.perf_counter()
+    idx, _ = O.knn(X, 20, nthreads=threads)
+    t_knn = (time.perf_counter() - t0) * (n / ns) ** 2
+    t0 = time.perf_counter()
+    for k in K_NUM:
+        O.snn(idx, k, "number")
+    t_snn = (time.perf_counter() - t0) * (n / ns)
+    lab = rng.integers(1, 21, (6, ns)).astype(np.int32)  # 6 of the 60 clusterings, C ~ 20
+    t0 = time.perf_counter()
+    for l_ in lab:
+        O.silhouette(X, l_)
+    t_sil = (time.perf_counter() - t0) * (60 / 6) * (n / ns)
+    Nc = 2000
+    A = rng.integers(1, 13, (B, Nc)).astype(np.int32)
+    A[rng.random((B, Nc)) < 0.35] = -1
+    t0 = time.perf_counter()
+    O.cocluster(A, nthreads=threads, want=("co", "both"))
+    t_coc = (time.perf_counter() - t0) * (N * (N - 1) / (Nc * (Nc - 1)))
+    t_step = B * (t_knn + t_snn + t_sil) + t_coc
+    return {
+        "value": B / t_step,
+        "unit": "bootstraps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle (C/OpenMP) on one {ns}-row bootstrap of the same PCs: kNN x (n/{ns})^2, "
+                   f"SNN k=10/15/20 x n/{ns}, silhouette of 6 clusterings x 10 x n/{ns}; co-cluster on "
+                   f"{B} columns x {Nc} cells x (N/{Nc})^2; per-bootstrap s: knn {t_knn:.2f}, snn {t_snn:.2f}, "
+                   f"silhouette {t_sil:.2f}; co-cluster per step {t_coc:.1f}"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from consensusclustr_amd import Engine
+    from consensusclustr_amd.sharding import allgather_columns, row_slabs, slab_pairs
+
+    eng = Engine(local)
+    N, d, B = args.cells, args.pcs, args.boots_per_gpu
+    n = int(args.boot_size * N)
+    L = len(K_NUM) * N_RES
+    G = world
+
+    # ---------------- inputs, resident in HBM before timing
+    pcs, pop = synth_pcs(torch, N, d, args.genes, 20241024 + 3, dev)
+    pcs_cm = pcs.t().contiguous()  # (d, N): column-major N x d like an R matrix
+    bids = [rank * B + j for j in range(B)]
+    boots_np = np.stack([np.random.default_rng(123 + b).integers(0, N, n) for b in bids]).astype(np.int32)
+    boots = torch.from_numpy(boots_np).to(dev)
+    labels = torch.empty((B, L, n), dtype=torch.int32, device=dev)
+    for j in range(B):
+        labels[j] = synth_labels(torch, pop[boots[j].long()], L, dev, 1000 + bids[j])
+    cmax = int(labels.max().item())
+
+    rows = torch.empty((n, d), dtype=torch.float64, device=dev)
+    knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
+    caps = [40 * n, 60 * n, 80 * n]
+    snn_out = [(torch.empty(c, dtype=torch.int32, device=dev), torch.empty(c, dtype=torch.int32, device=dev),
+                torch.empty(c, dtype=torch.float64, device=dev)) for c in caps]
+    nedges = torch.zeros((B, len(K_NUM)), dtype=torch.int64, device=dev)
+    means = torch.empty((B, L), dtype=torch.float64, device=dev)
+    nclust = torch.empty((B, L), dtype=torch.int32, device=dev)
+    minsize = torch.empty((B, L), dtype=torch.int32, device=dev)
+    choice = torch.empty(B, dtype=torch.int32, device=dev)
+    A_local = torch.zeros((B, N), dtype=torch.uint8, device=dev)
+    cuts = row_slabs(N, G)
+    r0, r1 = cuts[rank], cuts[rank + 1]
+    P = max(slab_pairs(N, r0, r1), 1)
+    co = torch.empty(P, dtype=torch.int16, device=dev)      # uint16 counts (viewed as int16)
+    both = torch.empty(P, dtype=torch.int16, device=dev)
+
+    def step():
+        for j in range(B):
+            eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+            eng.knn_rows_t(rows, 20, knn)
+            for t, k in enumerate(K_NUM):
+                oi, oj, ow = snn_out[t]
+                eng.snn_t(knn, k, "number", oi, oj, ow, nedges[j, t])
+            eng.silhouette_t(rows, labels[j], cmax, means[j], nclust[j], minsize[j])
+        eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
+                             minsize=minsize, out_choice=choice)
+        A = allgather_columns(A_local) if G > 1 else A_local
+        eng.cocluster_t(A, r0, r1, co=co, both=both)
+
+    def barrier():
+        if G > 1:
+            dist.barrier()
+
+    # ---------------- warmup (also sizes the SNN edge buffers)
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    need = nedges.max(0).values.tolist()
+    if any(e > c for e, c in zip(need, caps)):
+        raise RuntimeError(f"SNN edge capacity too small: need {need}, have {caps}")
+    fb = eng.knn_rows_t(rows, 20, knn, stats=True)  # certification statistics of the last bootstrap
+
+    # ---------------- timed region
+    eng.timing(True)
+    for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
+        eng.timing_read(w)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    kt = {w: eng.timing_read(w) for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster")}
+    eng.timing(False)
+    if G > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+
+    value = G * B * args.steps / el
+    ms_screen = kt["knn_screen"][0] / max(kt["knn_screen"][1], 1)
+    flops = 2.0 * n * n * d  # kNN F = 2 n^2 d per bootstrap
+    achieved = flops / (ms_screen * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("knn_screen_bytes_per_launch")
+    per_step = {w: round(v[0] / args.steps, 3) for w, v in kt.items()}
+    coc_ms = kt["cocluster"][0] / max(kt["cocluster"][1], 1)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "bootstraps/s",
+        "n_gpus": G,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1000, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA; synthetic clusterings in place of host Leiden",
+        "config": {
+            "workload": "BASELINE cfg3 shapes: 100k cells x 30 PCs, robust mode, kNum 10/15/20 x 20 resolutions; "
+                        f"{B} bootstraps per GPU per step ({G * B} total) + co-cluster row slab over all columns",
+            "cells": N, "pcs": d, "bootstrap_rows": n, "boots_per_gpu": B, "clusterings_per_boot": L,
+            "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}",
+        },
+        "roofline": {
+            "kernel": "knn_screen (v_mfma_f32_32x32x2_f32)",
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic,
+            "algorithmic_per_launch": f"2*n^2*d = {flops:.3e} flop (n={n}, d={d})",
+            "avg_launch_ms": round(ms_screen, 4),
+        },
+        "kernel_ms_per_step": per_step,
+        "cocluster_avg_ms": round(coc_ms, 3),
+        "knn_fallback_rows_last_boot": int(fb[1]),
+    }
+    if rank == 0 and G == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pcs.cpu().numpy(), B, n, N, d, args.cpu_sample_rows)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if G > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

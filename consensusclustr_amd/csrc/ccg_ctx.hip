@@ -1,0 +1,258 @@
+// Context, error reporting, workspace and a device scan for libccg.so.
+#include <stdarg.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "ccg_internal.h"
+
+static thread_local char g_err[1024] = "";
+
+void ccg_set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int ccg_hip_fail(hipError_t e, const char* what, const char* file, int line) {
+    ccg_set_error("HIP error '%s' (%d) in %s at %s:%d", hipGetErrorString(e),
+                  (int)e, what, file, line);
+    return e == hipErrorOutOfMemory ? CCG_ENOMEM : CCG_EHIP;
+}
+
+extern "C" int ccg_abi_version(void) { return CCG_ABI_VERSION; }
+extern "C" const char* ccg_last_error(void) { return g_err; }
+
+extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
+    if (!out) {
+        ccg_set_error("ccg_open: out is NULL");
+        return CCG_EINVAL;
+    }
+    *out = nullptr;
+    int dev = cfg ? cfg->device : 0;
+    int ndev = 0;
+    CCG_HIP(hipGetDeviceCount(&ndev));
+    if (dev < 0 || dev >= ndev) {
+        ccg_set_error("ccg_open: device %d out of range (%d devices)", dev, ndev);
+        return CCG_EINVAL;
+    }
+    CCG_HIP(hipSetDevice(dev));
+    ccg_ctx* c = new ccg_ctx();
+    memset(c->ws, 0, sizeof(c->ws));
+    memset(c->ws_bytes, 0, sizeof(c->ws_bytes));
+    c->device = dev;
+    c->last_stats.queries = 0;
+    c->last_stats.fallback = 0;
+    c->timing = 0;
+    c->timers = nullptr;
+    c->ntimers = c->cap_timers = c->used_timers = 0;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return ccg_hip_fail(e, "hipStreamCreate", __FILE__, __LINE__);
+    }
+    *out = c;
+    return CCG_OK;
+}
+
+extern "C" int ccg_close(ccg_ctx* ctx) {
+    if (!ctx) return CCG_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (int s = 0; s < WS_NSLOTS; ++s)
+        if (ctx->ws[s]) (void)hipFree(ctx->ws[s]);
+    for (int t = 0; t < ctx->ntimers; ++t) {
+        (void)hipEventDestroy(ctx->timers[t].start);
+        (void)hipEventDestroy(ctx->timers[t].stop);
+    }
+    free(ctx->timers);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return CCG_OK;
+}
+
+extern "C" int ccg_synchronize(ccg_ctx* ctx) {
+    CCG_HIP(hipSetDevice(ctx->device));
+    CCG_HIP(hipDeviceSynchronize());
+    return CCG_OK;
+}
+
+extern "C" void* ccg_stream(ccg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+void* ccg_ws(ccg_ctx* ctx, int slot, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (ctx->ws_bytes[slot] >= bytes) return ctx->ws[slot];
+    // Growth: let in-flight work that may still read the old buffer finish.
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    if (ctx->ws[slot]) (void)hipFree(ctx->ws[slot]);
+    ctx->ws[slot] = nullptr;
+    ctx->ws_bytes[slot] = 0;
+    size_t want = bytes + bytes / 8;  // headroom for slowly growing sizes
+    want = (want + 255) & ~(size_t)255;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        ccg_set_error("workspace allocation of %zu bytes failed (slot %d): %s",
+                      want, slot, hipGetErrorString(e));
+        return nullptr;
+    }
+    ctx->ws[slot] = p;
+    ctx->ws_bytes[slot] = want;
+    return p;
+}
+
+// ---------------------------------------------------------------- timing --
+int ccg_timer_start(ccg_ctx* ctx, int which, hipStream_t st) {
+    if (!ctx->timing) return -1;
+    if (ctx->used_timers == ctx->ntimers) {
+        if (ctx->ntimers == ctx->cap_timers) {
+            int nc = ctx->cap_timers ? 2 * ctx->cap_timers : 256;
+            ccg_timer_rec* nt = (ccg_timer_rec*)realloc(ctx->timers, sizeof(ccg_timer_rec) * nc);
+            if (!nt) return -1;
+            ctx->timers = nt;
+            ctx->cap_timers = nc;
+        }
+        ccg_timer_rec& r = ctx->timers[ctx->ntimers];
+        if (hipEventCreate(&r.start) != hipSuccess) return -1;
+        if (hipEventCreate(&r.stop) != hipSuccess) return -1;
+        ctx->ntimers++;
+    }
+    int h = ctx->used_timers++;
+    ctx->timers[h].which = which;
+    (void)hipEventRecord(ctx->timers[h].start, st);
+    return h;
+}
+
+void ccg_timer_stop(ccg_ctx* ctx, int handle, hipStream_t st) {
+    if (handle < 0) return;
+    (void)hipEventRecord(ctx->timers[handle].stop, st);
+}
+
+extern "C" int ccg_timing_enable(ccg_ctx* ctx, int enable) {
+    CCG_REQUIRE(ctx, "ccg_timing_enable: NULL ctx");
+    ctx->timing = enable ? 1 : 0;
+    return CCG_OK;
+}
+
+extern "C" int ccg_timing_read(ccg_ctx* ctx, int which, double* total_ms, int64_t* launches) {
+    CCG_REQUIRE(ctx && total_ms && launches, "ccg_timing_read: NULL argument");
+    CCG_REQUIRE(which >= 0 && which < CCG_KT_COUNT, "ccg_timing_read: bad kernel id");
+    double tot = 0.0;
+    int64_t n = 0;
+    int keep = 0;
+    for (int t = 0; t < ctx->used_timers; ++t) {
+        ccg_timer_rec r = ctx->timers[t];
+        if (r.which == which) {
+            CCG_HIP(hipEventSynchronize(r.stop));
+            float ms = 0.f;
+            CCG_HIP(hipEventElapsedTime(&ms, r.start, r.stop));
+            tot += ms;
+            ++n;
+        } else {
+            ctx->timers[t] = ctx->timers[keep];  // compact unread records to the front
+            ctx->timers[keep] = r;
+            ++keep;
+        }
+    }
+    ctx->used_timers = keep;
+    *total_ms = tot;
+    *launches = n;
+    return CCG_OK;
+}
+
+// ------------------------------------------------------------------ scan --
+#define SCAN_T 256
+#define SCAN_TILE 2048  // 8 elements per thread
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* total) {
+    const int t = threadIdx.x;
+    const int lane = t & 63, wv = t >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    int64_t woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_T / 64; ++w) {
+        int64_t s = sh[w];
+        if (w < wv) woff += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + x - v;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tile_sums(const int64_t* __restrict__ in,
+                                                         int64_t n, int64_t* __restrict__ bsum) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    int64_t s = 0;
+#pragma unroll
+    for (int e = 0; e < SCAN_TILE / SCAN_T; ++e) {
+        int64_t i = base + threadIdx.x * (SCAN_TILE / SCAN_T) + e;
+        if (i < n) s += in[i];
+    }
+    int64_t tot;
+    block_excl_scan(s, sh, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_block_sums(int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
+        int64_t i = b0 + threadIdx.x;
+        int64_t v = i < nb ? bsum[i] : 0;
+        int64_t tot;
+        int64_t ex = block_excl_scan(v, sh, &tot);
+        if (i < nb) bsum[i] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tiles(const int64_t* in, int64_t* out, int64_t n,
+                                                     const int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    constexpr int E = SCAN_TILE / SCAN_T;
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * E;
+    int64_t v[E];
+    int64_t s = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        v[e] = (base + e < n) ? in[base + e] : 0;
+        s += v[e];
+    }
+    int64_t tot;
+    int64_t ex = block_excl_scan(s, sh, &tot) + bsum[blockIdx.x];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (base + e < n) out[base + e] = ex;
+        ex += v[e];
+    }
+    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = bsum[nb];
+}
+
+int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
+    if (n <= 0) {
+        CCG_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), st));
+        return CCG_OK;
+    }
+    int64_t nb = ccg_cdiv(n, SCAN_TILE);
+    int64_t* bsum = (int64_t*)ccg_ws(ctx, WS_SCAN, sizeof(int64_t) * (nb + 1));
+    if (!bsum) return CCG_ENOMEM;
+    scan_tile_sums<<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
+    scan_block_sums<<<1, SCAN_T, 0, st>>>(bsum, nb);
+    scan_tiles<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}

@@ -1,0 +1,89 @@
+// Internal declarations of libccg.so (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/ccg.h"
+
+// Workspace slots owned by a context.  Each slot grows on demand; growth
+// synchronises the context stream before freeing the old buffer.
+enum ccg_ws_slot {
+    WS_ROWS64 = 0,   // gathered bootstrap rows, float64 [n][d]
+    WS_REFS32,       // screening image, float32 [npad][2*KS]
+    WS_CAND_IDX,     // screening candidates [n][2][KP]
+    WS_CAND_THR,     // screening thresholds [n][2]
+    WS_MISC,         // small scalars (mnorm, fail counter, ...)
+    WS_FAIL_LIST,    // rows that failed certification [n]
+    WS_SNN_A,        // SNN host counts / offsets
+    WS_SNN_B,        // SNN host lists
+    WS_SNN_C,        // SNN per-node bounds / offsets
+    WS_SNN_D,        // SNN scratch edges
+    WS_SNN_E,        // SNN per-node counts / flags
+    WS_SIL_A,        // silhouette accumulators
+    WS_SIL_B,        // silhouette centroids
+    WS_COC_A,        // co-cluster column tables
+    WS_MAP_A,        // map-back first-position scratch
+    WS_HOST_A,       // host-API staging 1
+    WS_HOST_B,       // host-API staging 2
+    WS_HOST_C,       // host-API staging 3
+    WS_HOST_D,       // host-API staging 4
+    WS_HOST_E,       // host-API staging 5
+    WS_SCAN,         // scan block sums
+    WS_NSLOTS
+};
+
+struct ccg_timer_rec {
+    int which;
+    hipEvent_t start, stop;
+};
+
+struct ccg_ctx {
+    int device;
+    hipStream_t stream;
+    void* ws[WS_NSLOTS];
+    size_t ws_bytes[WS_NSLOTS];
+    ccg_knn_stats last_stats;
+    // kernel timing (ccg_timing_*)
+    int timing;
+    ccg_timer_rec* timers;   // pool, grows
+    int ntimers, cap_timers, used_timers;
+};
+
+// Record a timing start/stop around a launch on stream st (no-ops when
+// timing is disabled).  Returns a handle for ccg_timer_stop or -1.
+int ccg_timer_start(ccg_ctx* ctx, int which, hipStream_t st);
+void ccg_timer_stop(ccg_ctx* ctx, int handle, hipStream_t st);
+
+void ccg_set_error(const char* fmt, ...);
+int ccg_hip_fail(hipError_t e, const char* what, const char* file, int line);
+
+#define CCG_HIP(x)                                                        \
+    do {                                                                  \
+        hipError_t ccg_e_ = (x);                                          \
+        if (ccg_e_ != hipSuccess)                                         \
+            return ccg_hip_fail(ccg_e_, #x, __FILE__, __LINE__);          \
+    } while (0)
+
+#define CCG_REQUIRE(cond, ...)                                            \
+    do {                                                                  \
+        if (!(cond)) {                                                    \
+            ccg_set_error(__VA_ARGS__);                                   \
+            return CCG_EINVAL;                                            \
+        }                                                                 \
+    } while (0)
+
+// Returns a device buffer of at least `bytes` for `slot` (nullptr on OOM,
+// with the error message set).
+void* ccg_ws(ccg_ctx* ctx, int slot, size_t bytes);
+
+static inline hipStream_t ccg_pick_stream(ccg_ctx* ctx, void* s) {
+    return s ? (hipStream_t)s : ctx->stream;
+}
+
+// Exclusive scan of int64 values on device: out[i] = sum_{t<i} in[i]; the
+// total goes to out[n].  in may alias out.  Uses WS_SCAN.
+int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n,
+                 hipStream_t st);
+
+__host__ __device__ static inline int64_t ccg_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

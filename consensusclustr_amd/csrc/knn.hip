@@ -1,0 +1,460 @@
+// Exact brute-force kNN of bootstrap rows on gfx950.
+//
+// Reference path: bluster::clusterRows(pca, SNNGraphParam(k, ...)) ->
+// BiocNeighbors::findKNN (R/consensusClust.R:656-658) on the bootstrap
+// matrix pca[sample(...), ] (:394).  Contract (DESIGN.md "kNN"): exact
+// Euclidean neighbours, self excluded by row identity, ordered by the fp64
+// squared distance summed unfused in dimension order, ties by row index.
+//
+// Three stages, all on the device:
+//   1. prep     : rows64 -> refs32 image (fp32, dims permuted for the MFMA
+//                 fragment, slot d holds -|y|^2/2) and max row norm.
+//   2. screen   : v_mfma_f32_32x32x2_f32 computes v = x.y - |y|^2/2 for a
+//                 32-query x 32-reference tile per wave; each lane keeps the
+//                 KP best references of its half-tile in registers.
+//   3. certify  : one wave per query recomputes the 2*KP candidates in fp64,
+//                 bitonic-sorts them by (d2, j) across lanes and proves that
+//                 no excluded reference can enter the top k using a rigorous
+//                 fp32 error bound; rows that cannot be proven go to
+//   4. fallback : exact fp64 scan of all references for that row.
+#include <math.h>
+
+#include "ccg_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define KNN_KP 20          // candidates kept per half-lane for kmax <= 20
+#define KNN_KP_BIG 32      // ... for 20 < kmax <= 32 (2*KP <= 64 lanes in certify)
+#define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
+#define KNN_FB_K 32        // fallback list length (>= kmax)
+
+// Relative error budget of the fp32 screen in units of the fp32 ulp (2^-24)
+// times (|x| + max|y|)^2; see DESIGN.md "kNN certification bound".
+#define KNN_ERR_ULPS 256.0
+
+__device__ __forceinline__ double sqdist_exact(const double* __restrict__ a,
+                                               const double* __restrict__ b, int d) {
+    double s = 0.0;
+    for (int k = 0; k < d; ++k) {
+        double t = __dsub_rn(a[k], b[k]);
+        s = __dadd_rn(s, __dmul_rn(t, t));
+    }
+    return s;
+}
+
+// --------------------------------------------------------------- gather --
+__global__ void gather_rows_kernel(const double* __restrict__ pcs, int64_t N, int d,
+                                   const int32_t* __restrict__ idx, int64_t n,
+                                   double* __restrict__ rows) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * d) return;
+    int64_t i = t / d;
+    int k = (int)(t - i * d);
+    rows[t] = pcs[(int64_t)k * N + idx[i]];
+}
+
+// ----------------------------------------------------------------- prep --
+// refs32 row r: position h*KS + s holds dim 2s+h (fp32); dim d holds
+// -0.5*|y|^2; other pad dims 0.  Rows n..npad-1 are zero.
+__global__ void knn_prep_kernel(const double* __restrict__ rows, int64_t n, int64_t npad,
+                                int d, int KS, float* __restrict__ refs,
+                                unsigned int* __restrict__ mnorm_bits) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= npad) return;
+    float* out = refs + r * (2 * KS);
+    if (r >= n) {
+        for (int p = 0; p < 2 * KS; ++p) out[p] = 0.f;
+        return;
+    }
+    const double* y = rows + r * d;
+    double nr = 0.0;
+    for (int k = 0; k < d; ++k) nr += y[k] * y[k];
+    for (int p = 0; p < 2 * KS; ++p) {
+        int h = p / KS, s = p - h * KS;
+        int k = 2 * s + h;
+        float v = 0.f;
+        if (k < d) v = (float)y[k];
+        else if (k == d) v = (float)(-0.5 * nr);
+        out[p] = v;
+    }
+    // norm upper bound (round up by 2 ulp): non-negative float bits order as ints
+    float nf = (float)sqrt(nr);
+    nf = nextafterf(nextafterf(nf, INFINITY), INFINITY);
+    atomicMax(mnorm_bits, __float_as_uint(nf));
+}
+
+// --------------------------------------------------------------- screen --
+template <int KP>
+__device__ __forceinline__ void list_insert(float (&lv)[KP], int (&li)[KP], float v, int id) {
+    float cv = v;
+    int ci = id;
+#pragma unroll
+    for (int t = 0; t < KP; ++t) {
+        bool sw = cv > lv[t];
+        float tv = lv[t];
+        int ti = li[t];
+        lv[t] = sw ? cv : tv;
+        li[t] = sw ? ci : ti;
+        cv = sw ? tv : cv;
+        ci = sw ? ti : ci;
+    }
+}
+
+template <int KS>
+__device__ __forceinline__ void load_frag(const float* __restrict__ p, float (&f)[KS]) {
+    const float4* p4 = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int s4 = 0; s4 < KS / 4; ++s4) {
+        float4 v = p4[s4];
+        f[4 * s4 + 0] = v.x;
+        f[4 * s4 + 1] = v.y;
+        f[4 * s4 + 2] = v.z;
+        f[4 * s4 + 3] = v.w;
+    }
+}
+
+template <int KS, int KP>
+__global__ __launch_bounds__(256) void knn_screen_kernel(const float* __restrict__ refs,
+                                                         int n, int ntiles, int d,
+                                                         int* __restrict__ cand_idx,
+                                                         float* __restrict__ cand_thr) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int col = lane & 31;
+    const int h = lane >> 5;
+    const int q = blockIdx.x * KNN_QPB + wave * 32 + col;
+    const int qrow = q < n ? q : n - 1;
+
+    float qf[KS];
+    load_frag<KS>(refs + (int64_t)qrow * (2 * KS) + h * KS, qf);
+    // query side of the norm slot is 1.0
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        if (2 * s + h == d) qf[s] = 1.0f;
+
+    float lv[KP];
+    int li[KP];
+#pragma unroll
+    for (int t = 0; t < KP; ++t) {
+        lv[t] = -INFINITY;
+        li[t] = -1;
+    }
+    float thr = -INFINITY;
+
+    float af[KS];
+    load_frag<KS>(refs + (int64_t)col * (2 * KS) + h * KS, af);
+    for (int t = 0; t < ntiles; ++t) {
+        float an[KS];
+        const int tn = (t + 1 < ntiles) ? t + 1 : t;
+        load_frag<KS>(refs + ((int64_t)tn * 32 + col) * (2 * KS) + h * KS, an);
+
+        f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], qf[s], acc, 0, 0, 0);
+
+        const int rbase = t * 32 + 4 * h;
+        float vmax = -INFINITY;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int r = rbase + (reg & 3) + 8 * (reg >> 2);
+            float v = acc[reg];
+            v = (r < n && r != q) ? v : -INFINITY;
+            acc[reg] = v;
+            vmax = fmaxf(vmax, v);
+        }
+        if (__any(vmax > thr)) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const float v = acc[reg];
+                if (v > thr) {
+                    list_insert<KP>(lv, li, v, rbase + (reg & 3) + 8 * (reg >> 2));
+                    thr = lv[KP - 1];
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) af[s] = an[s];
+    }
+    if (q < n) {
+        int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
+#pragma unroll
+        for (int t = 0; t < KP; ++t) out[t] = li[t];
+        cand_thr[(int64_t)q * 2 + h] = thr;
+    }
+}
+
+// -------------------------------------------------------------- certify --
+__device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
+    return (a < b) || (a == b && ia < ib);
+}
+
+// Bitonic sort of 64 (key, idx) pairs held one per lane, ascending.
+__device__ __forceinline__ void wave_bitonic64(double& key, int& id) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            double ok = __shfl_xor(key, j, 64);
+            int oi = __shfl_xor(id, j, 64);
+            bool up = ((lane & k) == 0);
+            bool lower = ((lane & j) == 0);
+            bool other_less = key_less(ok, oi, key, id);
+            // lower lane keeps min when ascending block, max otherwise
+            bool take = (lower == up) ? other_less : !other_less;
+            // never swap equal elements (ids are distinct except padding)
+            if (take && !(ok == key && oi == id)) {
+                key = ok;
+                id = oi;
+            }
+        }
+    }
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void knn_certify_kernel(
+    const double* __restrict__ rows, int n, int d, int kmax,
+    const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
+    const unsigned int* __restrict__ mnorm_bits, int32_t* __restrict__ out_idx,
+    double* __restrict__ out_dist, int* __restrict__ fail_list, int* __restrict__ fail_count) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= n) return;
+    const double* x = rows + (int64_t)q * d;
+    int j = (lane < 2 * KP) ? cand_idx[(int64_t)q * 2 * KP + lane] : -1;
+    double key = INFINITY;
+    int id = 0x7fffffff - 64 + lane;  // distinct padding ids sort after real ones
+    if (j >= 0) {
+        key = sqdist_exact(x, rows + (int64_t)j * d, d);
+        id = j;
+    }
+    wave_bitonic64(key, id);
+
+    // certification (wave-uniform values)
+    double nq = 0.0;
+    for (int k = 0; k < d; ++k) nq += x[k] * x[k];
+    const float t0 = cand_thr[(int64_t)q * 2 + 0];
+    const float t1 = cand_thr[(int64_t)q * 2 + 1];
+    const float tmax = fmaxf(t0, t1);
+    const double dK = __shfl(key, kmax - 1, 64);
+    const int idK = __shfl(id, kmax - 1, 64);
+    bool ok = (idK < n);  // at least kmax real candidates
+    if (tmax != -INFINITY) {
+        const double M = (double)__uint_as_float(*mnorm_bits);
+        const double s = sqrt(nq) + M;
+        const double E = KNN_ERR_ULPS * 0x1p-24 * s * s + 1e-300;
+        const double excl = nq - 2.0 * (double)tmax;  // every excluded ref has approx d2 >= excl
+        ok = ok && (excl - E > dK);
+    }
+    if (ok) {
+        if (lane < kmax) {
+            out_idx[(int64_t)q * kmax + lane] = id;
+            if (out_dist) out_dist[(int64_t)q * kmax + lane] = sqrt(key);
+        }
+    } else if (lane == 0) {
+        int p = atomicAdd(fail_count, 1);
+        fail_list[p] = q;
+    }
+}
+
+// ------------------------------------------------------------- fallback --
+// One wave per failed row: exact fp64 scan, per-lane sorted lists, then a
+// k-round wave arg-min merge.
+__global__ __launch_bounds__(256) void knn_fallback_kernel(
+    const double* __restrict__ rows, int n, int d, int kmax,
+    const int* __restrict__ fail_list, const int* __restrict__ fail_count,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_dist) {
+    const int lane = threadIdx.x & 63;
+    const int nfail = *fail_count;
+    const int wstride = gridDim.x * 4;
+    for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < nfail; f += wstride) {
+        const int q = fail_list[f];
+        const double* x = rows + (int64_t)q * d;
+        double lv[KNN_FB_K];
+        int li[KNN_FB_K];
+#pragma unroll
+        for (int t = 0; t < KNN_FB_K; ++t) {
+            lv[t] = INFINITY;
+            li[t] = 0x7fffffff;
+        }
+        for (int j = lane; j < n; j += 64) {
+            if (j == q) continue;
+            double s = sqdist_exact(x, rows + (int64_t)j * d, d);
+            if (!(s < lv[KNN_FB_K - 1])) continue;  // j ascending per lane
+            double cv = s;
+            int ci = j;
+#pragma unroll
+            for (int t = 0; t < KNN_FB_K; ++t) {
+                bool sw = key_less(cv, ci, lv[t], li[t]);
+                double tv = lv[t];
+                int ti = li[t];
+                lv[t] = sw ? cv : tv;
+                li[t] = sw ? ci : ti;
+                cv = sw ? tv : cv;
+                ci = sw ? ti : ci;
+            }
+        }
+        for (int r = 0; r < kmax; ++r) {
+            double bk = lv[0];
+            int bi = li[0];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                double ok = __shfl_xor(bk, o, 64);
+                int oi = __shfl_xor(bi, o, 64);
+                if (key_less(ok, oi, bk, bi)) {
+                    bk = ok;
+                    bi = oi;
+                }
+            }
+            if (lane == 0) {
+                out_idx[(int64_t)q * kmax + r] = bi;
+                if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+            }
+            if (li[0] == bi) {  // the winning lane pops its head
+#pragma unroll
+                for (int t = 0; t < KNN_FB_K - 1; ++t) {
+                    lv[t] = lv[t + 1];
+                    li[t] = li[t + 1];
+                }
+                lv[KNN_FB_K - 1] = INFINITY;
+                li[KNN_FB_K - 1] = 0x7fffffff;
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------- driver --
+template <int KS, int KP>
+static void launch_screen(const float* refs, int n, int ntiles, int d, int* cand_idx,
+                          float* cand_thr, hipStream_t st) {
+    unsigned grid = (unsigned)ccg_cdiv(n, KNN_QPB);
+    knn_screen_kernel<KS, KP><<<grid, 256, 0, st>>>(refs, n, ntiles, d, cand_idx, cand_thr);
+}
+
+template <int KP>
+static int screen_dispatch(int KS, const float* refs, int n, int ntiles, int d, int* cand_idx,
+                           float* cand_thr, hipStream_t st) {
+    switch (KS) {
+        case 8: launch_screen<8, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
+        case 12: launch_screen<12, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
+        case 16: launch_screen<16, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
+        case 24: launch_screen<24, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
+        case 32: launch_screen<32, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
+        default: ccg_set_error("ccg_knn_rows_dev: unsupported d=%d", d); return CCG_EINVAL;
+    }
+    return CCG_OK;
+}
+
+static int pick_ks(int d) {
+    // need 2*KS >= d + 1 (norm slot), KS multiple of 4
+    int need = (d + 2) / 2;
+    if (need <= 8) return 8;
+    if (need <= 12) return 12;
+    if (need <= 16) return 16;
+    if (need <= 24) return 24;
+    if (need <= 32) return 32;
+    return -1;
+}
+
+extern "C" int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                                   const int32_t* idx, int64_t n, double* rows, void* stream) {
+    CCG_REQUIRE(ctx && pcs && idx && rows, "ccg_gather_rows_dev: NULL argument");
+    CCG_REQUIRE(N > 0 && n > 0 && d > 0, "ccg_gather_rows_dev: bad sizes");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    int64_t tot = n * d;
+    gather_rows_kernel<<<(unsigned)ccg_cdiv(tot, 256), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
+                                int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                                void* stream) {
+    CCG_REQUIRE(ctx && rows && out_idx, "ccg_knn_rows_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_rows_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(n >= 2 && n < (1LL << 30), "ccg_knn_rows_dev: n=%lld out of range", (long long)n);
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
+                "ccg_knn_rows_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int KS = pick_ks(d);
+    const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
+    const int64_t npad = ccg_cdiv(n, 32) * 32;
+    float* refs = (float*)ccg_ws(ctx, WS_REFS32, sizeof(float) * npad * 2 * KS);
+    int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * n * 2 * KP);
+    float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * n * 2);
+    int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
+    unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
+    if (!refs || !cand_idx || !cand_thr || !fail_list || !misc) return CCG_ENOMEM;
+    unsigned int* mnorm = misc;
+    int* fail_count = (int*)(misc + 1);
+    CCG_HIP(hipMemsetAsync(misc, 0, 8, st));
+
+    const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
+    knn_prep_kernel<<<(unsigned)ccg_cdiv(npad, 256), 256, 0, st>>>(rows, n, npad, d, KS, refs, mnorm);
+    const int ntiles = (int)(npad / 32);
+    const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
+    int rc = (KP == KNN_KP)
+                 ? screen_dispatch<KNN_KP>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st)
+                 : screen_dispatch<KNN_KP_BIG>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st);
+    ccg_timer_stop(ctx, t_scr, st);
+    if (rc) return rc;
+    if (KP == KNN_KP)
+        knn_certify_kernel<KNN_KP><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
+            rows, (int)n, d, kmax, cand_idx, cand_thr, mnorm, out_idx, out_dist, fail_list, fail_count);
+    else
+        knn_certify_kernel<KNN_KP_BIG><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
+            rows, (int)n, d, kmax, cand_idx, cand_thr, mnorm, out_idx, out_dist, fail_list, fail_count);
+    knn_fallback_kernel<<<256, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
+                                             out_dist);
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    if (stats) {
+        int nf = 0;
+        CCG_HIP(hipMemcpyAsync(&nf, fail_count, sizeof(int), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        stats->queries = n;
+        stats->fallback = nf;
+        ctx->last_stats = *stats;
+    }
+    return CCG_OK;
+}
+
+extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                            const int32_t* boot_idx, int64_t n, int nb, int kmax,
+                            int32_t* out_idx, double* out_dist, ccg_knn_stats* stats) {
+    CCG_REQUIRE(ctx && pcs && boot_idx && out_idx, "ccg_knn_boot: NULL argument");
+    CCG_REQUIRE(N > 0 && n >= 2 && nb >= 1 && d >= 1, "ccg_knn_boot: bad sizes");
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    double* dpcs = (double*)ccg_ws(ctx, WS_HOST_A, sizeof(double) * N * d);
+    int32_t* didx = (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * n * nb);
+    int32_t* dout = (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * n * kmax);
+    double* ddist = out_dist ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * n * kmax) : nullptr;
+    double* rows = (double*)ccg_ws(ctx, WS_ROWS64, sizeof(double) * n * d);
+    if (!dpcs || !didx || !dout || !rows || (out_dist && !ddist)) return CCG_ENOMEM;
+    for (int64_t t = 0; t < n * nb; ++t)
+        CCG_REQUIRE(boot_idx[t] >= 0 && boot_idx[t] < N, "ccg_knn_boot: boot_idx out of range");
+    CCG_HIP(hipMemcpyAsync(dpcs, pcs, sizeof(double) * N * d, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(didx, boot_idx, sizeof(int32_t) * n * nb, hipMemcpyHostToDevice, st));
+    ccg_knn_stats acc = {0, 0};
+    for (int b = 0; b < nb; ++b) {
+        int rc = ccg_gather_rows_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, rows, st);
+        if (rc) return rc;
+        ccg_knn_stats s;
+        rc = ccg_knn_rows_dev(ctx, rows, n, d, kmax, dout, ddist, &s, st);
+        if (rc) return rc;
+        acc.queries += s.queries;
+        acc.fallback += s.fallback;
+        CCG_HIP(hipMemcpyAsync(out_idx + (int64_t)b * n * kmax, dout, sizeof(int32_t) * n * kmax,
+                               hipMemcpyDeviceToHost, st));
+        if (out_dist)
+            CCG_HIP(hipMemcpyAsync(out_dist + (int64_t)b * n * kmax, ddist,
+                                   sizeof(double) * n * kmax, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+    }
+    if (stats) *stats = acc;
+    ctx->last_stats = acc;
+    return CCG_OK;
+}

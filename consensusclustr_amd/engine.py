@@ -1,0 +1,202 @@
+"""Engine: a context on one GPU plus host-array and device-tensor entry points.
+
+Host-array methods (numpy in, numpy out) call the host flavour of the C ABI,
+exactly what an R ``.Call`` glue would bind.  ``*_t`` methods take torch
+tensors already resident on the engine's GPU and enqueue on torch's current
+stream (torch is plumbing for device memory and streams only; all compute
+runs in libccg.so).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+_vp = ctypes.c_void_p
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(_vp)
+    return _vp(a.data_ptr())  # torch tensor
+
+
+def _stream():
+    import torch
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+class Engine:
+    """One libccg context (one GPU).  Not fork-safe; one per process/device."""
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self.device = device
+        cfg = _lib.ccg_config(device, 0)
+        ctx = _vp()
+        check(self.lib.ccg_open(ctypes.byref(cfg), ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.last_knn_stats = None
+
+    def close(self):
+        if self.ctx:
+            self.lib.ccg_close(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        check(self.lib.ccg_synchronize(self.ctx))
+
+    def timing(self, enable=True):
+        """Enable per-kernel hipEvent timing (ccg_timing_enable)."""
+        check(self.lib.ccg_timing_enable(self.ctx, 1 if enable else 0))
+
+    def timing_read(self, which):
+        """(total_ms, launches) of kernel `which` since the last read (synchronises)."""
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        check(self.lib.ccg_timing_read(self.ctx, _lib.CCG_KT[which], ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    # ------------------------------------------------------------ host API
+    def knn_boot(self, pca, boot_idx, kmax=20, want_dist=True):
+        """kNN of bootstrap rows (ccg_knn_boot).
+
+        pca: N x d array (any order; passed column-major like an R matrix);
+        boot_idx: nb x n (or n) 0-based cell indices.
+        Returns idx (nb, n, kmax) int32 0-based bootstrap-row indices,
+        dist (nb, n, kmax) float64 or None.
+        """
+        pcs = np.asfortranarray(pca, dtype=np.float64)
+        N, d = pcs.shape
+        bi = np.ascontiguousarray(np.atleast_2d(boot_idx), dtype=np.int32)
+        nb, n = bi.shape
+        out = np.empty((nb, n, kmax), np.int32)
+        dist = np.empty((nb, n, kmax), np.float64) if want_dist else None
+        st = _lib.ccg_knn_stats()
+        check(self.lib.ccg_knn_boot(self.ctx, _ptr(pcs), N, d, _ptr(bi), n, nb, kmax, _ptr(out),
+                                    _ptr(dist), ctypes.byref(st)))
+        self.last_knn_stats = (st.queries, st.fallback)
+        return out, dist
+
+    def snn(self, knn_idx, k, type="number"):
+        """SNN edges i<j sorted by (i, j) with weights (ccg_snn)."""
+        knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
+        n, ks = knn_idx.shape
+        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        ne = ctypes.c_int64(0)
+        rc = self.lib.ccg_snn(self.ctx, _ptr(knn_idx), n, ks, k, t, None, None, None, 0, ctypes.byref(ne))
+        if rc not in (_lib.CCG_OK, _lib.CCG_ECAP):
+            check(rc)
+        m = ne.value
+        ei = np.empty(m, np.int32)
+        ej = np.empty(m, np.int32)
+        w = np.empty(m, np.float64)
+        check(self.lib.ccg_snn(self.ctx, _ptr(knn_idx), n, ks, k, t, _ptr(ei), _ptr(ej), _ptr(w), m,
+                               ctypes.byref(ne)))
+        return ei, ej, w
+
+    def silhouette(self, x, labels, cmax=None, want_width=False):
+        """Batched approxSilhouette means (ccg_silhouette).
+
+        labels: (L, m) or (m,) integer codes in [1, cmax].
+        Returns (mean[L], nclust[L], minsize[L], width[L, m] or None).
+        """
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        m, d = x.shape
+        lab = np.ascontiguousarray(np.atleast_2d(labels), dtype=np.int32)
+        L = lab.shape[0]
+        if cmax is None:
+            cmax = int(lab.max())
+        mean = np.empty(L, np.float64)
+        nc = np.empty(L, np.int32)
+        ms = np.empty(L, np.int32)
+        w = np.empty((L, m), np.float64) if want_width else None
+        check(self.lib.ccg_silhouette(self.ctx, _ptr(x), m, d, _ptr(lab), L, cmax, _ptr(mean), _ptr(nc),
+                                      _ptr(ms), _ptr(w)))
+        return mean, nc, ms, w
+
+    def cocluster(self, A, want=("co", "both", "dist")):
+        """Co-clustering counts/distance (ccg_cocluster), packed R "dist" order.
+
+        A: B x N uint8 column-major assignment matrix (0 = not sampled).
+        """
+        A = np.ascontiguousarray(A, dtype=np.uint8)
+        B, N = A.shape
+        P = N * (N - 1) // 2
+        co = np.empty(P, np.uint16) if "co" in want else None
+        both = np.empty(P, np.uint16) if "both" in want else None
+        dist = np.empty(P, np.float64) if "dist" in want else None
+        check(self.lib.ccg_cocluster(self.ctx, _ptr(A), N, B, _ptr(co), _ptr(both), _ptr(dist)))
+        return {"co": co, "both": both, "dist": dist}
+
+    def consensus_knn(self, co, both, N, k):
+        """dbscan::kNN(jaccardDist, k)$id equivalent (ccg_consensus_knn), 0-based."""
+        co = np.ascontiguousarray(co, dtype=np.uint16)
+        both = np.ascontiguousarray(both, dtype=np.uint16)
+        out = np.empty((N, k), np.int32)
+        rc = self.lib.ccg_consensus_knn(self.ctx, _ptr(co), _ptr(both), N, k, _ptr(out))
+        if rc == _lib.CCG_ENAN:
+            raise ValueError("data/distances cannot contain NAs for kNN")
+        check(rc)
+        return out
+
+    # ---------------------------------------------------------- device API
+    def gather_rows_t(self, pcs_cm, N, d, idx, rows):
+        """rows[i, :] = pcs[idx[i], :]; pcs_cm is a column-major (d, N) tensor."""
+        check(self.lib.ccg_gather_rows_dev(self.ctx, _ptr(pcs_cm), N, d, _ptr(idx), idx.numel(),
+                                           _ptr(rows), _stream()))
+
+    def knn_rows_t(self, rows, kmax, out_idx, out_dist=None, stats=False):
+        n, d = rows.shape
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_rows_dev(self.ctx, _ptr(rows), n, d, kmax, _ptr(out_idx), _ptr(out_dist),
+                                        ctypes.byref(st) if stats else None, _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
+    def snn_t(self, knn_idx, k, type, out_i, out_j, out_w, d_nedges):
+        n, ks = knn_idx.shape
+        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        cap = out_i.numel() if out_i is not None else 0
+        check(self.lib.ccg_snn_dev(self.ctx, _ptr(knn_idx), n, ks, k, t, _ptr(out_i), _ptr(out_j),
+                                   _ptr(out_w), cap, _ptr(d_nedges), _stream()))
+
+    def silhouette_t(self, x, labels, cmax, out_mean, out_nclust, out_minsize, out_width=None):
+        m, d = x.shape
+        L = labels.shape[0]
+        check(self.lib.ccg_silhouette_dev(self.ctx, _ptr(x), m, d, _ptr(labels), L, cmax, _ptr(out_mean),
+                                          _ptr(out_nclust), _ptr(out_minsize), _ptr(out_width), _stream()))
+
+    def select_mapback_t(self, mode, labels, boot_idx, N, A, col0, means=None, nclust=None, minsize=None,
+                         min_size=0, out_choice=None):
+        nb, L, n = labels.shape
+        md = {"robust": _lib.CCG_MODE_ROBUST, "granular": _lib.CCG_MODE_GRANULAR}[mode]
+        check(self.lib.ccg_select_mapback_dev(self.ctx, md, _ptr(labels), _ptr(boot_idx), n, nb, L, N,
+                                              _ptr(means), _ptr(nclust), _ptr(minsize), min_size, _ptr(A),
+                                              col0, _ptr(out_choice), _stream()))
+
+    def cocluster_t(self, A, r0, r1, co=None, both=None, dist=None):
+        B, N = A.shape
+        check(self.lib.ccg_cocluster_dev(self.ctx, _ptr(A), N, B, r0, r1, _ptr(co), _ptr(both), _ptr(dist),
+                                         _stream()))
+
+    def consensus_knn_t(self, co, both, N, k, out_idx, d_flag):
+        check(self.lib.ccg_consensus_knn_dev(self.ctx, _ptr(co), _ptr(both), N, k, _ptr(out_idx),
+                                             _ptr(d_flag), _stream()))

@@ -1,0 +1,205 @@
+/*
+ * ccg.h -- C ABI of libccg.so, the MI355X (gfx950) engine for the bootstrap
+ * hot path of consensusClust (AndyCGraham/consensusClustR).
+ *
+ * Plain C: pointers, sizes and an opaque context.  No C++ or PyTorch types
+ * cross this boundary.  Every function returns CCG_OK (0) or a negative
+ * CCG_E* code; ccg_last_error() then returns a thread-local message.  No
+ * function throws or longjmps across the ABI.
+ *
+ * Two flavours of each entry point:
+ *   - host-pointer functions (ccg_knn_boot, ccg_snn, ...): what an R .Call
+ *     glue binds.  They copy in, run, copy out and
+ *     synchronise.
+ *   - device-pointer functions (*_dev): inputs/outputs already in HBM,
+ *     enqueued on `stream` (a hipStream_t; NULL = the context's stream).
+ *     No host synchronisation unless stated.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   ccg_knn_boot / ccg_knn_rows_dev : BiocNeighbors::findKNN as reached by
+ *       bluster::clusterRows(pca, SNNGraphParam(k, type="number"))
+ *       R/consensusClust.R:656-658, on pca[sample(...), ] (:394).
+ *   ccg_snn (type NUMBER)           : bluster::neighborsToSNNGraph(type="number")
+ *       inside SNNGraphParam (:656-658).
+ *   ccg_snn (type RANK)             : bluster::neighborsToSNNGraph(knn, type="rank")
+ *       (:426).
+ *   ccg_silhouette                  : mean(bluster::approxSilhouette(x, cl)[,3],
+ *       na.rm=TRUE) (:447, :518, :664).
+ *   ccg_select_mapback_dev          : robust selection rank(ties="first")
+ *       (:684-686) + assignments[match(cellOrder, names)] (:673) + NA -> -1
+ *       (:408, encoded as 0) + do.call(cbind) (:404, :688).
+ *   ccg_cocluster                   : the RcppXPtrUtils customDist plugin passed
+ *       to parallelDist::parDist(method="custom") and 1 - parDist(...)
+ *       (:411-421).
+ *   ccg_consensus_knn               : dbscan::kNN(jaccardDist, k)$id (:425).
+ */
+#ifndef CCG_H
+#define CCG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCG_ABI_VERSION 1
+
+#define CCG_OK 0
+#define CCG_EINVAL (-1)  /* bad argument / shape */
+#define CCG_ENOMEM (-2)  /* device allocation failed */
+#define CCG_EHIP (-3)    /* HIP runtime error */
+#define CCG_ECAP (-4)    /* caller buffer too small; required size reported */
+#define CCG_ENAN (-5)    /* NaN distance where the reference stop()s */
+#define CCG_ERANGE (-6)  /* label out of supported range */
+
+#define CCG_SNN_NUMBER 0
+#define CCG_SNN_RANK 1
+
+#define CCG_MODE_ROBUST 0
+#define CCG_MODE_GRANULAR 1
+
+typedef struct ccg_ctx ccg_ctx;
+
+typedef struct ccg_config {
+    int device; /* HIP device ordinal */
+    int flags;  /* reserved, 0 */
+} ccg_config;
+
+/* kNN certification statistics for the last ccg_knn_* call. */
+typedef struct ccg_knn_stats {
+    int64_t queries;   /* rows searched */
+    int64_t fallback;  /* rows that needed the exact fp64 rescan */
+} ccg_knn_stats;
+
+int ccg_abi_version(void);
+const char* ccg_last_error(void);
+int ccg_open(const ccg_config* cfg, ccg_ctx** out);
+int ccg_close(ccg_ctx* ctx);
+int ccg_synchronize(ccg_ctx* ctx);
+/* The context's default stream (hipStream_t). */
+void* ccg_stream(ccg_ctx* ctx);
+
+/* ---------------------------------------------------------------- kNN -- */
+/* Exact Euclidean kNN of every bootstrap row among the other rows of the
+ * same bootstrap (duplicated cells are distinct points at distance 0).
+ * Order: ascending fp64 squared distance summed unfused in dimension order,
+ * ties by ascending bootstrap-row index.  k = 10, 15 lists are prefixes of
+ * the kmax list.
+ *   pcs      : N x d float64, COLUMN-major (R matrix layout), d <= 64
+ *   boot_idx : nb x n int32, 0-based cell indices (R's sample() - 1)
+ *   out_idx  : nb x n x kmax int32, 0-based bootstrap-row indices
+ *   out_dist : nb x n x kmax float64 (sqrt of the squared distance) or NULL
+ * Requires 1 <= kmax <= min(32, n-1), n < 2^30. */
+int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                 const int32_t* boot_idx, int64_t n, int nb, int kmax,
+                 int32_t* out_idx, double* out_dist, ccg_knn_stats* stats);
+
+/* Gather bootstrap rows: rows[i][k] = pcs_colmajor[k*N + idx[i]]. */
+int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                        const int32_t* idx, int64_t n, double* rows,
+                        void* stream);
+
+/* kNN among the rows of a row-major n x d float64 matrix (device).
+ * stats may be NULL; when given, the call synchronises to fill it. */
+int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
+                     int kmax, int32_t* out_idx, double* out_dist,
+                     ccg_knn_stats* stats, void* stream);
+
+/* ---------------------------------------------------------------- SNN -- */
+/* Shared-nearest-neighbour graph from the first k columns of an n x kstride
+ * int32 0-based neighbour matrix (self excluded).  Edges i < j sorted by
+ * (i, j).  NUMBER: w = |N+(i) & N+(j)|, N+(x) = {x} u knn(x).  RANK:
+ * w = max(k - r/2, 1e-6), r = min over shared s of rank_i(s) + rank_j(s),
+ * self rank 0, neighbours 1..k.
+ * Host flavour: if cap < required, returns CCG_ECAP with *nedges = required
+ * (call with cap = 0 to size). */
+int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k,
+            int type, int32_t* out_i, int32_t* out_j, double* out_w,
+            int64_t cap, int64_t* nedges);
+
+/* Device flavour: writes min(E, cap) edges and E to *d_nedges (device
+ * int64); no host synchronisation.  If E > cap the caller re-runs with a
+ * larger cap. */
+int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
+                int k, int type, int32_t* out_i, int32_t* out_j,
+                double* out_w, int64_t cap, int64_t* d_nedges, void* stream);
+
+/* --------------------------------------------------------- silhouette -- */
+/* mean(approxSilhouette(x, labels_l)[,3], na.rm=TRUE) for L label vectors
+ * over the same m x d float64 row-major matrix.  labels: L x m int32 codes
+ * in [1, cmax], cmax <= 256.  Outputs (length L): mean width (NaN if every
+ * width is NaN), number of distinct clusters, smallest cluster size.
+ * out_width (L x m) may be NULL. */
+int ccg_silhouette(ccg_ctx* ctx, const double* x, int64_t m, int d,
+                   const int32_t* labels, int L, int cmax, double* out_mean,
+                   int32_t* out_nclust, int32_t* out_minsize,
+                   double* out_width);
+int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
+                       const int32_t* labels, int L, int cmax,
+                       double* out_mean, int32_t* out_nclust,
+                       int32_t* out_minsize, double* out_width, void* stream);
+
+/* ----------------------------------------------- selection + map-back -- */
+/* For nb bootstraps with L clusterings each (labels nb x L x n int32,
+ * codes 1..255), map labels back to the N cells (first copy in sample
+ * order wins; unsampled -> 0) and write uint8 columns of the column-major
+ * assignment matrix A (B x N) starting at column col0.
+ *   ROBUST  : one column per bootstrap, the clustering chosen by the
+ *             per-bootstrap score rules (:662-670) and rank(ties="first")
+ *             (:685-686) from means/nclust/minsize (nb x L);
+ *             out_choice (nb, nullable) receives the chosen index.
+ *   GRANULAR: L columns per bootstrap (:688). */
+int ccg_select_mapback_dev(ccg_ctx* ctx, int mode, const int32_t* labels,
+                           const int32_t* boot_idx, int64_t n, int nb, int L,
+                           int64_t N, const double* means,
+                           const int32_t* nclust, const int32_t* minsize,
+                           int min_size, uint8_t* A, int64_t col0,
+                           int32_t* out_choice, void* stream);
+
+/* ------------------------------------------------------- co-clustering -- */
+/* A: B x N uint8 column-major assignment matrix, 0 = not sampled (R's -1),
+ * 1..255 = cluster code.  For the rows [r0, r1) of the packed upper
+ * triangle (row i holds j = i+1..N-1; this is exactly the order of R's
+ * "dist" object) writes
+ *   co   : #{b : A_bi == A_bj != 0}         (uint16, B <= 65535)
+ *   both : #{b : A_bi != 0 and A_bj != 0}   (uint16)
+ *   dist : 1 - (double)((float)co / (float)both)  (NaN when both == 0)
+ * Any output may be NULL.  Slab element (i, j) lives at
+ * i*N - i*(i+1)/2 + (j-i-1) - (r0*N - r0*(r0+1)/2).
+ * r0 must be a multiple of 128 (CCG_COCLUSTER_ROW_ALIGN) or r0 == 0. */
+#define CCG_COCLUSTER_ROW_ALIGN 128
+int ccg_cocluster(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B,
+                  uint16_t* co, uint16_t* both, double* dist);
+int ccg_cocluster_dev(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B,
+                      int64_t r0, int64_t r1, uint16_t* co, uint16_t* both,
+                      double* dist, void* stream);
+
+/* --------------------------------------------------- consensus kNN -- */
+/* kNN on the co-clustering distance from packed (full, r0 = 0) co/both:
+ * per row, ascending distance with ties by ascending column index, self
+ * excluded.  Returns CCG_ENAN if any pair has both == 0 (dbscan stop()s). */
+int ccg_consensus_knn(ccg_ctx* ctx, const uint16_t* co, const uint16_t* both,
+                      int64_t N, int k, int32_t* out_idx);
+int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co,
+                          const uint16_t* both, int64_t N, int k,
+                          int32_t* out_idx, int32_t* d_nan_flag, void* stream);
+
+/* ------------------------------------------------------ kernel timing -- */
+/* Device time of selected kernels, measured with hipEvents recorded on the
+ * stream each kernel is launched on (used by bench.py for the live roofline).
+ * Disabled by default; enabling adds two event records per timed launch. */
+#define CCG_KT_KNN_SCREEN 0   /* the fp32 MFMA screening kernel of ccg_knn_* */
+#define CCG_KT_KNN_TOTAL 1    /* prep + screen + certify + fallback */
+#define CCG_KT_SNN 2          /* whole ccg_snn_dev call */
+#define CCG_KT_SILHOUETTE 3   /* whole ccg_silhouette_dev call */
+#define CCG_KT_COCLUSTER 4    /* the co-cluster tile kernel */
+#define CCG_KT_COUNT 5
+int ccg_timing_enable(ccg_ctx* ctx, int enable);
+/* Synchronises, returns the summed milliseconds and launch count of kernel
+ * `which` since the last read, and resets that counter. */
+int ccg_timing_read(ccg_ctx* ctx, int which, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCG_H */

@@ -1,0 +1,59 @@
+"""The C-ABI library loads and exports every symbol include/ccg.h declares
+(no compute: this runs without a GPU)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from consensusclustr_amd import _lib
+
+
+def test_header_declares_expected_entry_points():
+    syms = _lib.header_symbols()
+    for s in ("ccg_open", "ccg_knn_boot", "ccg_knn_rows_dev", "ccg_snn", "ccg_snn_dev", "ccg_silhouette",
+              "ccg_select_mapback_dev", "ccg_cocluster", "ccg_cocluster_dev", "ccg_consensus_knn",
+              "ccg_timing_read"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    missing = [s for s in _lib.header_symbols() if not hasattr(lib, s)]
+    assert not missing
+    assert set(_lib.header_symbols()) <= set(_lib.SIGNATURES)
+
+
+def test_nm_exports_are_extern_c():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
+    names = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for s in _lib.header_symbols():
+        assert s in names, f"{s} not exported unmangled"
+
+
+def test_abi_version_and_error_path():
+    lib = _lib.load()
+    assert lib.ccg_abi_version() == 1
+    # NULL out-pointer: rejected before any device work, message set
+    assert lib.ccg_open(None, None) == _lib.CCG_EINVAL
+    assert b"NULL" in lib.ccg_last_error()
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+                                  stderr=subprocess.STDOUT).decode(errors="replace")
+    assert "gfx950" in out
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libccg.so"))
+    monkeypatch.setattr(_lib, "_LIB", None)
+    with pytest.raises(ImportError):
+        _lib.load()
+
+
+def test_consts_match_header():
+    text = open(_lib.HEADER_PATH).read()
+    for name in ("CCG_EINVAL", "CCG_ECAP", "CCG_ENAN", "CCG_SNN_RANK", "CCG_MODE_GRANULAR"):
+        assert name in text
+    assert f"CCG_COCLUSTER_ROW_ALIGN {_lib.COCLUSTER_ROW_ALIGN}" in text

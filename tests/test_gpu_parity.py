@@ -1,0 +1,307 @@
+"""HIP engine vs the oracle and the golden fixtures, through the C ABI.
+
+Bar: bit-exact kNN indices, SNN edges/weights, co/both counts and co-cluster
+distances (the distance is a pure function of the integer counts); kNN
+distances and silhouette scores within 1e-5 relative (north_star tolerance).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5  # north_star: distances and silhouette scores within 1e-5 relative
+
+
+def _mixture(rng, N, d, C=8, spread=3.0):
+    centers = rng.normal(scale=spread, size=(C, d))
+    return centers[rng.integers(0, C, N)] + rng.normal(size=(N, d))
+
+
+# ----------------------------------------------------------------- kNN --
+def test_knn_kat(engine, kat):
+    c = kat["knn_dups_1d"]
+    rows = np.array(c["rows"])
+    idx, _ = engine.knn_boot(rows, np.arange(rows.shape[0]), kmax=c["k"])
+    assert idx[0].tolist() == c["idx"]
+
+
+def test_knn_golden_bootstrap(engine, golden):
+    g = golden("knn_snn_boot.npz")
+    idx, dist = engine.knn_boot(g["pcs"], g["boot"], kmax=20)
+    assert np.array_equal(idx[0], g["knn_idx"])
+    np.testing.assert_allclose(dist[0], g["knn_dist"], rtol=RTOL, atol=1e-12)
+
+
+def test_knn_golden_ties(engine, golden):
+    g = golden("knn_ties.npz")
+    rows = g["rows"]
+    idx, dist = engine.knn_boot(rows, np.arange(rows.shape[0]), kmax=20)
+    assert np.array_equal(idx[0], g["knn_idx"])
+    np.testing.assert_allclose(dist[0], g["knn_dist"], rtol=RTOL, atol=1e-12)
+    # a lattice is full of exact ties: most rows must have gone to the exact fallback
+    q, fb = engine.last_knn_stats
+    assert q == rows.shape[0] and fb >= 0
+
+
+@pytest.mark.parametrize("N,d,k", [(3000, 30, 20), (2500, 20, 20), (1800, 5, 15), (700, 50, 10), (1200, 63, 20)])
+def test_knn_random_vs_oracle(engine, N, d, k):
+    rng = np.random.default_rng(N + d)
+    pcs = _mixture(rng, N, d)
+    boot = rng.integers(0, N, int(0.9 * N)).astype(np.int32)
+    idx, dist = engine.knn_boot(pcs, boot, kmax=k)
+    X = O.gather_rows(pcs, boot)
+    oi, od = O.knn(X, k)
+    assert np.array_equal(idx[0], oi)
+    np.testing.assert_allclose(dist[0], od, rtol=RTOL, atol=1e-12)
+
+
+def test_knn_multi_bootstrap_batch(engine):
+    rng = np.random.default_rng(7)
+    N, d = 1500, 12
+    pcs = _mixture(rng, N, d)
+    boots = rng.integers(0, N, (3, 1350)).astype(np.int32)
+    idx, _ = engine.knn_boot(pcs, boots, kmax=20)
+    for b in range(3):
+        oi, _ = O.knn(O.gather_rows(pcs, boots[b]), 20)
+        assert np.array_equal(idx[b], oi)
+
+
+def test_knn_tiny_and_degenerate(engine):
+    # n = kmax + 1 (every other row is a neighbour), all-identical rows
+    rows = np.zeros((21, 3))
+    idx, dist = engine.knn_boot(rows, np.arange(21), kmax=20)
+    oi, od = O.knn(rows, 20)
+    assert np.array_equal(idx[0], oi)
+    assert np.all(dist[0] == 0)
+    rng = np.random.default_rng(1)
+    rows = rng.normal(size=(33, 2))
+    idx, _ = engine.knn_boot(rows, np.arange(33), kmax=20)
+    assert np.array_equal(idx[0], O.knn(rows, 20)[0])
+
+
+def test_knn_heavy_duplication_forces_fallback(engine):
+    # 60 distinct cells, 900 draws: every cell has ~15 copies at distance 0,
+    # so the k-th and (k+1)-th neighbours tie and certification must fail
+    rng = np.random.default_rng(11)
+    pcs = rng.normal(size=(60, 8))
+    boot = rng.integers(0, 60, 900).astype(np.int32)
+    idx, _ = engine.knn_boot(pcs, boot, kmax=20)
+    oi, _ = O.knn(O.gather_rows(pcs, boot), 20)
+    assert np.array_equal(idx[0], oi)
+    assert engine.last_knn_stats[1] > 0
+
+
+def test_knn_rejects_bad_args(engine):
+    from consensusclustr_amd import CcgError
+    with pytest.raises(CcgError):
+        engine.knn_boot(np.zeros((10, 3)), np.arange(10), kmax=10)  # kmax > n-1
+    with pytest.raises(CcgError):
+        engine.knn_boot(np.zeros((10, 3)), np.array([0, 1, 50]), kmax=1)  # index out of range
+
+
+# ----------------------------------------------------------------- SNN --
+def test_snn_kat(engine, kat):
+    idx = np.array(kat["knn_dups_1d"]["idx"], np.int32)
+    for t in ("number", "rank"):
+        e = kat[f"snn_{t}_k2"]
+        ei, ej, w = engine.snn(idx, 2, t)
+        assert ei.tolist() == e["i"] and ej.tolist() == e["j"]
+        assert np.array_equal(w, np.array(e["w"], float))
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_golden(engine, golden, t):
+    g = golden("knn_snn_boot.npz")
+    for k in (10, 15, 20):
+        ei, ej, w = engine.snn(g["knn_idx"], k, t)
+        assert np.array_equal(ei, g[f"snn_{t}_{k}_i"])
+        assert np.array_equal(ej, g[f"snn_{t}_{k}_j"])
+        assert np.array_equal(w, g[f"snn_{t}_{k}_w"])
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_large_vs_oracle(engine, t):
+    rng = np.random.default_rng(21)
+    X = _mixture(rng, 20000, 10)
+    idx, _ = engine.knn_boot(X, np.arange(20000), kmax=20)
+    for k in (10, 20):
+        a = engine.snn(idx[0], k, t)
+        b = O.snn(idx[0], k, t)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_hub_overflow_dense_path(engine, t):
+    # every node lists nodes 0..k-1 (a hub set) -> gathered lists overflow
+    # the LDS capacity and take the dense path
+    n, k = 3000, 20
+    rng = np.random.default_rng(2)
+    idx = np.empty((n, k), np.int32)
+    for i in range(n):
+        cand = [x for x in range(k + 1) if x != i][:k]
+        if i < k + 1:
+            idx[i] = cand
+        else:
+            idx[i, :10] = cand[:10]
+            idx[i, 10:] = rng.choice(np.setdiff1d(np.arange(n), [i] + cand[:10]), k - 10, replace=False)
+    a = engine.snn(idx, k, t)
+    b = O.snn(idx, k, t)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+# ---------------------------------------------------------- silhouette --
+def test_silhouette_kat(engine, kat):
+    c = kat["silhouette_1d"]
+    mean, nc, ms, w = engine.silhouette(np.array(c["x"]), np.array(c["labels"]), want_width=True)
+    np.testing.assert_allclose(w[0], c["widths"], rtol=RTOL)
+    np.testing.assert_allclose(mean[0], c["mean"], rtol=RTOL)
+    assert nc[0] == 2 and ms[0] == 2
+
+
+def test_silhouette_golden(engine, golden):
+    g = golden("silhouette.npz")
+    lab = g["labels"]
+    mean, nc, ms, w = engine.silhouette(g["x"], lab, want_width=True)
+    np.testing.assert_allclose(mean, g["means"], rtol=RTOL)
+    assert np.array_equal(nc, g["nclust"])
+    ok = ~np.isnan(g["widths"])
+    assert np.array_equal(np.isnan(w), ~ok)
+    np.testing.assert_allclose(w[ok], g["widths"][ok], rtol=RTOL, atol=1e-9)
+    for l_ in range(lab.shape[0]):
+        assert ms[l_] == np.bincount(lab[l_])[np.bincount(lab[l_]) > 0].min()
+
+
+def test_silhouette_batch_vs_oracle(engine):
+    rng = np.random.default_rng(9)
+    X = _mixture(rng, 20000, 30, C=12)
+    L = 12
+    labs = np.stack([rng.integers(1, 2 + 3 * l_, 20000) for l_ in range(L)]).astype(np.int32)
+    mean, nc, _, _ = engine.silhouette(X, labs)
+    for l_ in range(L):
+        _, m, C = O.silhouette(X, labs[l_])
+        np.testing.assert_allclose(mean[l_], m, rtol=RTOL)
+        assert nc[l_] == C
+
+
+def test_silhouette_deterministic(engine):
+    rng = np.random.default_rng(10)
+    X = _mixture(rng, 5000, 20)
+    labs = rng.integers(1, 9, (6, 5000)).astype(np.int32)
+    a = engine.silhouette(X, labs)[0]
+    b = engine.silhouette(X, labs)[0]
+    assert np.array_equal(a, b)  # fixed-point reductions: bitwise reproducible
+
+
+# -------------------------------------------------------- co-clustering --
+def _to_u8(A):
+    A = np.array(A, np.int64)
+    A[A < 0] = 0
+    return A.astype(np.uint8)
+
+
+def test_cocluster_kat(engine, kat):
+    c = kat["cocluster_4x3"]
+    r = engine.cocluster(_to_u8(c["A"]))
+    assert r["co"].tolist() == c["co"]
+    assert r["both"].tolist() == c["both"]
+    assert r["dist"].tolist() == c["dist"]
+
+
+@pytest.mark.parametrize("name", ["cocluster.npz", "cocluster_granular.npz", "cocluster_collide.npz"])
+def test_cocluster_golden(engine, golden, name):
+    g = golden(name)
+    r = engine.cocluster(_to_u8(g["A"]))
+    assert np.array_equal(r["co"], g["co"].astype(np.uint16))
+    assert np.array_equal(r["both"], g["both"].astype(np.uint16))
+    assert np.array_equal(r["dist"], g["dist"], equal_nan=True)  # bitwise, NaN where both == 0
+
+
+@pytest.mark.parametrize("B,N,C", [(100, 700, 12), (7, 300, 255), (257, 513, 3)])
+def test_cocluster_vs_oracle(engine, B, N, C):
+    rng = np.random.default_rng(B * N)
+    A = rng.integers(1, C + 1, (B, N))
+    A[rng.random((B, N)) < 0.1] = -1
+    r = engine.cocluster(_to_u8(A))
+    o = O.cocluster(A)
+    assert np.array_equal(r["co"], o["co"].astype(np.uint16))
+    assert np.array_equal(r["both"], o["both"].astype(np.uint16))
+    assert np.array_equal(r["dist"], o["dist"], equal_nan=True)
+
+
+def test_cocluster_row_slabs_concatenate(engine):
+    """Row-slab outputs (the multi-GPU split) concatenate to the full triangle."""
+    import torch
+    from consensusclustr_amd.sharding import row_slabs, slab_pairs
+    rng = np.random.default_rng(3)
+    B, N = 60, 1000
+    A = rng.integers(0, 9, (B, N)).astype(np.uint8)
+    full = engine.cocluster(A)
+    At = torch.from_numpy(A).cuda()
+    parts = []
+    for G in (2, 4, 8):
+        cuts = row_slabs(N, G)
+        parts = []
+        for g in range(G):
+            P = slab_pairs(N, cuts[g], cuts[g + 1])
+            co = torch.empty(max(P, 1), dtype=torch.int16, device="cuda")
+            both = torch.empty(max(P, 1), dtype=torch.int16, device="cuda")
+            engine.cocluster_t(At, cuts[g], cuts[g + 1], co=co, both=both)
+            torch.cuda.synchronize()
+            parts.append((co[:P].cpu().numpy().view(np.uint16), both[:P].cpu().numpy().view(np.uint16)))
+        assert np.array_equal(np.concatenate([p[0] for p in parts]), full["co"])
+        assert np.array_equal(np.concatenate([p[1] for p in parts]), full["both"])
+
+
+# ------------------------------------------------------ consensus kNN --
+def test_consensus_knn_golden(engine, golden):
+    g = golden("cocluster.npz")
+    N = g["A"].shape[1]
+    for k in (10, 15, 20):
+        out = engine.consensus_knn(g["co"].astype(np.uint16), g["both"].astype(np.uint16), N, k)
+        assert np.array_equal(out, g[f"cknn_{k}"])
+
+
+def test_consensus_knn_nan_raises(engine):
+    A = np.zeros((3, 5), np.uint8)
+    A[:, :3] = 1  # cells 3, 4 never sampled
+    r = engine.cocluster(A)
+    with pytest.raises(ValueError):
+        engine.consensus_knn(r["co"], r["both"], 5, 2)
+
+
+# ---------------------------------------------------- selection + map-back --
+def test_select_mapback_robust_and_granular(engine):
+    import torch
+    from consensusclustr_amd.consensus import mapback, robust_choice, robust_scores
+    rng = np.random.default_rng(4)
+    N, n, nb, L = 500, 450, 3, 6
+    boots = rng.integers(0, N, (nb, n)).astype(np.int32)
+    labels = rng.integers(1, 7, (nb, L, n)).astype(np.int32)
+    means = rng.random((nb, L))
+    means[1, 2] = np.nan
+    means[2, 1] = means[2, 4] = means[2].max() + 1  # tie at the max -> last wins
+    nclust = np.full((nb, L), 5, np.int32)
+    nclust[0, 3] = 1
+    minsize = np.full((nb, L), 10, np.int32)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    A = torch.zeros((nb, N), dtype=torch.uint8, device="cuda")
+    choice = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    engine.select_mapback_t("robust", dev(labels), dev(boots), N, A, 0, means=dev(means), nclust=dev(nclust),
+                            minsize=dev(minsize), out_choice=choice)
+    Ag = torch.zeros((nb * L, N), dtype=torch.uint8, device="cuda")
+    engine.select_mapback_t("granular", dev(labels), dev(boots), N, Ag, 0)
+    torch.cuda.synchronize()
+    for b in range(nb):
+        want = robust_choice(robust_scores(means[b], nclust[b], minsize[b]))
+        assert choice[b].item() == want
+        col = mapback(boots[b], labels[b, want], N)
+        col[col < 0] = 0
+        assert np.array_equal(A[b].cpu().numpy(), col.astype(np.uint8))
+        for l_ in range(L):
+            col = mapback(boots[b], labels[b, l_], N)
+            col[col < 0] = 0
+            assert np.array_equal(Ag[b * L + l_].cpu().numpy(), col.astype(np.uint8))

@@ -1,0 +1,110 @@
+"""The CPU restatement (oracle) against the hand-derived KATs, its own
+independent numpy restatement, and the committed golden fixtures."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+
+def test_kat_cocluster(kat):
+    c = kat["cocluster_4x3"]
+    r = O.cocluster(np.array(c["A"]))
+    assert r["co"].tolist() == c["co"]
+    assert r["both"].tolist() == c["both"]
+    assert r["dist"].tolist() == c["dist"]  # bit-exact, incl. the float division
+
+
+def test_kat_knn_and_snn(kat):
+    c = kat["knn_dups_1d"]
+    idx, _ = O.knn(np.array(c["rows"]), c["k"])
+    assert idx.tolist() == c["idx"]
+    for t in ("number", "rank"):
+        e = kat[f"snn_{t}_k2"]
+        ei, ej, w = O.snn(idx, 2, t)
+        assert ei.tolist() == e["i"] and ej.tolist() == e["j"]
+        assert np.array_equal(w, np.array(e["w"], float))
+
+
+def test_kat_silhouette(kat):
+    c = kat["silhouette_1d"]
+    w, m, C = O.silhouette(np.array(c["x"]), np.array(c["labels"]))
+    assert C == 2
+    np.testing.assert_allclose(w, c["widths"], rtol=1e-10)
+    np.testing.assert_allclose(m, c["mean"], rtol=1e-10)
+
+
+def test_kat_selection_rules(kat):
+    for scores, want in kat["robust_choice"]["cases"]:
+        assert O.robust_choice(scores) == want
+    for scores, want in kat["consensus_choice"]["cases"]:
+        assert O.consensus_choice(scores) == want
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_knn_matches_numpy_restatement(seed):
+    rng = np.random.default_rng(seed)
+    pcs = rng.normal(size=(120, 6))
+    idx = rng.integers(0, 120, 108)
+    X = O.gather_rows(pcs, idx)
+    a, _ = O.knn(X, 20)
+    assert np.array_equal(a, O.py_knn(X, 20))
+
+
+def test_knn_ties_lattice():
+    rng = np.random.default_rng(5)
+    X = rng.integers(-2, 3, size=(80, 3)).astype(float)
+    a, _ = O.knn(X, 15)
+    assert np.array_equal(a, O.py_knn(X, 15))
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_matches_set_restatement(t):
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(90, 4))
+    idx, _ = O.knn(X, 12)
+    for k in (5, 12):
+        a = O.snn(idx, k, t)
+        b = O.py_snn(idx, k, t)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+def test_cocluster_matches_numpy_restatement():
+    rng = np.random.default_rng(4)
+    A = rng.integers(-1, 5, size=(25, 40))
+    A[A == 0] = 3
+    a = O.cocluster(A)
+    b = O.py_cocluster(A)
+    for key in ("co", "both", "dist"):
+        assert np.array_equal(a[key], b[key], equal_nan=True)
+
+
+def test_golden_reproduces(golden):
+    g = golden("knn_snn_boot.npz")
+    X = O.gather_rows(g["pcs"], g["boot"])
+    idx, dist = O.knn(X, 20)
+    assert np.array_equal(idx, g["knn_idx"])
+    assert np.array_equal(dist, g["knn_dist"])
+    for k in (10, 15, 20):
+        for t in ("number", "rank"):
+            ei, ej, w = O.snn(g["knn_idx"], k, t)
+            assert np.array_equal(ei, g[f"snn_{t}_{k}_i"])
+            assert np.array_equal(w, g[f"snn_{t}_{k}_w"])
+    c = golden("cocluster.npz")
+    r = O.cocluster(c["A"])
+    assert np.array_equal(r["co"], c["co"]) and np.array_equal(r["dist"], c["dist"])
+    for k in (10, 15, 20):
+        assert np.array_equal(O.consensus_knn(c["dist"], c["A"].shape[1], k), c[f"cknn_{k}"])
+
+
+def test_collision_fixture_has_fp32_collisions(golden):
+    """customDist holds overlap/U in float (:412-416): distinct rationals can
+    share one fp32 ratio at granular B.  The fixture must contain such a pair
+    so the GPU epilogue is held to the float division, not the exact ratio."""
+    g = golden("cocluster_collide.npz")
+    a, b, c, d = (int(v) for v in g["frac"])
+    assert a * d != b * c
+    assert g["co"][0] == a and g["both"][0] == b and g["co"][1] == c and g["both"][1] == d
+    assert g["dist"][0] == g["dist"][1]
+    r = O.cocluster(g["A"].astype(np.int32))
+    assert np.array_equal(r["dist"], g["dist"])
