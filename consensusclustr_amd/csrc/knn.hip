@@ -242,11 +242,16 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int idK = __shfl(id, kmax - 1, 64);
     bool ok = (idK < n);  // at least kmax real candidates
     if (tmax != -INFINITY) {
-        const double M = (double)__uint_as_float(*mnorm_bits);
-        const double s = sqrt(nq) + M;
+        // An excluded ref y has approx d2 >= excl.  If it were as close as the
+        // k-th candidate (|x-y|^2 <= dK) then |y| <= |x| + sqrt(dK), so its
+        // screening error is at most E = c*u*(2|x| + sqrt(dK))^2 and its approx
+        // d2 at most dK + E.  excl > dK + E therefore proves it is farther
+        // (independent of the largest norm in the data).
+        const double s = 2.0 * sqrt(nq) + sqrt(dK);
         const double E = KNN_ERR_ULPS * 0x1p-24 * s * s + 1e-300;
-        const double excl = nq - 2.0 * (double)tmax;  // every excluded ref has approx d2 >= excl
+        const double excl = nq - 2.0 * (double)tmax;
         ok = ok && (excl - E > dK);
+        (void)mnorm_bits;
     }
     if (ok) {
         if (lane < kmax) {
@@ -260,18 +265,24 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
 }
 
 // ------------------------------------------------------------- fallback --
-// One wave per failed row: exact fp64 scan, per-lane sorted lists, then a
-// k-round wave arg-min merge.
+// One 256-thread block per failed row: each thread scans refs j = tid + 256t
+// with the query held in registers (exact fp64, unfused, dimension order),
+// keeping a sorted list; each wave merges its 64 lists by k rounds of wave
+// arg-min into LDS, then wave 0 merges the 4 wave lists.
+template <int DMAX>
 __global__ __launch_bounds__(256) void knn_fallback_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ fail_list, const int* __restrict__ fail_count,
     int32_t* __restrict__ out_idx, double* __restrict__ out_dist) {
-    const int lane = threadIdx.x & 63;
+    __shared__ double sd[4][KNN_FB_K];
+    __shared__ int si[4][KNN_FB_K];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nfail = *fail_count;
-    const int wstride = gridDim.x * 4;
-    for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < nfail; f += wstride) {
+    for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
         const int q = fail_list[f];
-        const double* x = rows + (int64_t)q * d;
+        double xq[DMAX];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
         double lv[KNN_FB_K];
         int li[KNN_FB_K];
 #pragma unroll
@@ -279,10 +290,19 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
             lv[t] = INFINITY;
             li[t] = 0x7fffffff;
         }
-        for (int j = lane; j < n; j += 64) {
-            if (j == q) continue;
-            double s = sqdist_exact(x, rows + (int64_t)j * d, d);
-            if (!(s < lv[KNN_FB_K - 1])) continue;  // j ascending per lane
+        for (int j = threadIdx.x; j < n; j += 256) {
+            const double* y = rows + (int64_t)j * d;
+            double yv[DMAX];
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) yv[k] = k < d ? y[k] : 0.0;
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k)
+                if (k < d) {
+                    const double t = __dsub_rn(xq[k], yv[k]);
+                    s = __dadd_rn(s, __dmul_rn(t, t));
+                }
+            if (j == q || !(s < lv[KNN_FB_K - 1])) continue;  // j ascending per thread
             double cv = s;
             int ci = j;
 #pragma unroll
@@ -296,6 +316,7 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                 ci = sw ? ti : ci;
             }
         }
+        // per-wave merge of 64 sorted lists -> sd[wv][0..kmax)
         for (int r = 0; r < kmax; ++r) {
             double bk = lv[0];
             int bi = li[0];
@@ -309,10 +330,10 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                 }
             }
             if (lane == 0) {
-                out_idx[(int64_t)q * kmax + r] = bi;
-                if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+                sd[wv][r] = bk;
+                si[wv][r] = bi;
             }
-            if (li[0] == bi) {  // the winning lane pops its head
+            if (li[0] == bi) {  // the winning thread pops its head (ids are unique)
 #pragma unroll
                 for (int t = 0; t < KNN_FB_K - 1; ++t) {
                     lv[t] = lv[t + 1];
@@ -322,6 +343,36 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                 li[KNN_FB_K - 1] = 0x7fffffff;
             }
         }
+        __syncthreads();
+        if (wv == 0) {
+            // lanes 0..3 walk the 4 wave lists; k rounds of arg-min over heads
+            int pos = 0;
+            for (int r = 0; r < kmax; ++r) {
+                double bk = INFINITY;
+                int bi = 0x7fffffff;
+                if (lane < 4 && pos < kmax) {
+                    bk = sd[lane][pos];
+                    bi = si[lane][pos];
+                }
+                const double mk = bk;
+                const int mi = bi;
+#pragma unroll
+                for (int o = 2; o > 0; o >>= 1) {
+                    double ok = __shfl_xor(bk, o, 64);
+                    int oi = __shfl_xor(bi, o, 64);
+                    if (key_less(ok, oi, bk, bi)) {
+                        bk = ok;
+                        bi = oi;
+                    }
+                }
+                if (lane == 0) {
+                    out_idx[(int64_t)q * kmax + r] = bi;
+                    if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+                }
+                if (lane < 4 && mi == bi && mk == bk) ++pos;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -406,8 +457,15 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
     else
         knn_certify_kernel<KNN_KP_BIG><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
             rows, (int)n, d, kmax, cand_idx, cand_thr, mnorm, out_idx, out_dist, fail_list, fail_count);
-    knn_fallback_kernel<<<256, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
-                                             out_dist);
+    if (d <= 16)
+        knn_fallback_kernel<16><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
+                                                     out_dist);
+    else if (d <= 32)
+        knn_fallback_kernel<32><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
+                                                     out_dist);
+    else
+        knn_fallback_kernel<64><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
+                                                     out_dist);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {

@@ -1,28 +1,51 @@
 // Shared-nearest-neighbour graphs on gfx950.
 //
 // Reference path: bluster::neighborsToSNNGraph(index, type="number") inside
-// SNNGraphParam (R/consensusClust.R:656-658) and type="rank" on the
-// consensus kNN (:426); bluster's C++ build_snn_number / build_snn_rank.
+// SNNGraphParam (R/consensusClust.R:656-658) for each k of kNum (:653), and
+// type="rank" on the consensus kNN (:426); bluster's C++ build_snn_number /
+// build_snn_rank.
 //
-// For node j, every shared member s of N+(j) = {j} u knn(j) contributes to
-// the partners p with s in N+(p), i.e. p in {s} u hosts(s) where hosts(s)
-// lists the nodes that have s as a neighbour (with s's 1-based rank there).
-// NUMBER counts the shared members; RANK keeps min(rank_j(s) + rank_p(s)).
-// Each undirected edge is emitted by its smaller endpoint, so node j keeps
-// partners p > j only.  One wave per node gathers (p, value) keys into LDS,
-// bitonic-sorts them and reduces runs.  Two passes (count, emit) give a
-// deterministic, (i, j)-sorted edge list without scratch memory; nodes whose
-// gathered list exceeds the LDS capacity take an exact O(n) dense path.
+// For node j, every member s of N+(j) = {j} u knn(j) is shared with each
+// partner p in {s} u hosts(s) (hosts(s) = nodes listing s as a neighbour).
+// NUMBER counts shared members; RANK keeps min(rank_j(s) + rank_p(s)), self
+// rank 0.  Because the k-lists are prefixes of the kmax list, one pass over
+// the kmax graph serves every k in kNum: a shared member with ranks
+// (rj, rp) belongs to graph k iff max(rj, rp) <= k.  Per graph t the value
+// lives in byte t of a 32-bit word (counts <= 33, rank sums <= 64).
+//
+// Each undirected edge is emitted by its smaller endpoint (partners p > j).
+// Per node one wave builds an LDS open-addressing hash table of its
+// partners (key p, packed per-graph values), then (pass 2) compacts it,
+// bitonic-sorts by p and emits each graph's edges in (i, j) order at offsets
+// from a device scan of pass-1 counts -- deterministic and sorted, no
+// scratch.  Nodes with more partners than the wave table holds use a
+// 256-thread table of 16K slots; beyond that an exact O(n) dense path.
 #include <algorithm>
 
 #include "ccg_internal.h"
 
-// Compiler-only barrier: LDS operations of one wave execute in order.
 #define WAVE_LDS_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
 
-#define SNN_CAP 1024        // LDS keys per wave
-#define SNN_WAVES 4
-#define SNN_DENSE_BLOCKS 64 // concurrent overflow nodes
+#define SNN_MAXK 4           // graphs per pass (|kNum| <= 4)
+#define SNN_WT 2048          // wave table slots
+#define SNN_WAVES 4          // waves per block in the wave kernel
+#define SNN_BT 16384         // block table slots (overflow path)
+#define SNN_DENSE_BLOCKS 64  // concurrent dense-path nodes
+#define SNN_EMPTY (-1)
+
+struct SnnSpec {
+    int nk;
+    int kk[SNN_MAXK];  // ascending
+    int type;
+    unsigned init;     // empty value word (0 for NUMBER, 0xFFFFFFFF for RANK)
+};
+
+struct SnnOut {
+    int32_t* oi[SNN_MAXK];
+    int32_t* oj[SNN_MAXK];
+    double* ow[SNN_MAXK];
+    int64_t cap[SNN_MAXK];
+};
 
 __global__ void snn_count_hosts(const int32_t* __restrict__ knn, int64_t n, int kstride, int k,
                                 unsigned long long* __restrict__ hcnt, int* __restrict__ err) {
@@ -55,289 +78,594 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-// Gather node j's partner keys (p << 32 | value), p > j, into lds.
-// Returns the (wave-uniform) number of keys; > SNN_CAP means overflow.
-__device__ int snn_gather(int64_t j, const int32_t* __restrict__ knn, int kstride, int k,
-                          const int64_t* __restrict__ hoff, const int2* __restrict__ hosts,
-                          unsigned long long* lds) {
-    const int lane = threadIdx.x & 63;
-    int pos = 0;
-    for (int i = 0; i <= k; ++i) {
-        const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
-        const int64_t h0 = hoff[cur];
-        const int64_t len = hoff[cur + 1] - h0 + 1;  // hosts + cur itself
-        for (int64_t o0 = 0; o0 < len; o0 += 64) {
-            const int64_t o = o0 + lane;
-            bool keep = false;
-            unsigned long long key = 0;
-            if (o < len) {
-                int p, val;
-                if (o == len - 1) {
-                    p = cur;
-                    val = i;
-                } else {
-                    int2 hr = hosts[h0 + o];
-                    p = hr.x;
-                    val = hr.y + i;
-                }
-                keep = p > j;
-                key = ((unsigned long long)(unsigned)p << 32) | (unsigned)val;
-            }
-            const unsigned long long m = __ballot(keep);
-            const int pre = __popcll(m & lanemask_lt());
-            if (keep && pos + pre < SNN_CAP) lds[pos + pre] = key;
-            pos += __popcll(m);
+// Contribution of one shared member with ranks (rj, rp) to the packed word.
+__device__ __forceinline__ unsigned snn_contrib(const SnnSpec& sp, int rj, int rp) {
+    const int m = rj > rp ? rj : rp;
+    unsigned w = sp.init;
+#pragma unroll
+    for (int t = 0; t < SNN_MAXK; ++t) {
+        if (t < sp.nk && m <= sp.kk[t]) {
+            if (sp.type == CCG_SNN_NUMBER) w += 1u << (8 * t);
+            else w = (w & ~(0xFFu << (8 * t))) | ((unsigned)(rj + rp) << (8 * t));
         }
     }
-    return pos;
+    return w;
 }
 
-__device__ void wave_sort_lds(unsigned long long* lds, int cnt) {
-    const int lane = threadIdx.x & 63;
-    int P = 64;
-    while (P < cnt) P <<= 1;
-    for (int i = cnt + lane; i < P; i += 64) lds[i] = ~0ull;
-    WAVE_LDS_SYNC();
-    for (int kk = 2; kk <= P; kk <<= 1) {
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            for (int i = lane; i < P; i += 64) {
-                int l = i ^ jj;
-                if (l > i) {
-                    unsigned long long a = lds[i], b = lds[l];
-                    bool up = (i & kk) == 0;
-                    if ((a > b) == up) {
-                        lds[i] = b;
-                        lds[l] = a;
+__device__ __forceinline__ unsigned bytewise_min(unsigned a, unsigned b) {
+    unsigned r = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const unsigned x = (a >> (8 * t)) & 0xFFu, y = (b >> (8 * t)) & 0xFFu;
+        r |= (x < y ? x : y) << (8 * t);
+    }
+    return r;
+}
+
+template <typename V>
+__device__ __forceinline__ void snn_update(const SnnSpec& sp, V* v, unsigned c) {
+    if (sp.type == CCG_SNN_NUMBER) {
+        atomicAdd(v, c);
+    } else {
+        unsigned old = __hip_atomic_load(v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (true) {
+            const unsigned nw = bytewise_min(old, c);
+            if (nw == old) break;
+            const unsigned prev = atomicCAS(v, old, nw);
+            if (prev == old) break;
+            old = prev;
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned snn_hash(int p, int bits) {
+    return ((unsigned)p * 2654435761u) >> (32 - bits);
+}
+
+// Insert partner p with contribution c; returns false when the table is full.
+template <int T>
+__device__ __forceinline__ bool table_insert(int* keys, unsigned* vals, int* count, int p, unsigned c,
+                                             const SnnSpec& sp, int bits) {
+    unsigned s = snn_hash(p, bits);
+    for (int probe = 0; probe < T; ++probe) {
+        int k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == SNN_EMPTY) {
+            const int prev = atomicCAS(&keys[s], SNN_EMPTY, p);
+            if (prev == SNN_EMPTY) {
+                atomicAdd(count, 1);
+                k = p;
+            } else {
+                k = prev;
+            }
+        }
+        if (k == p) {
+            snn_update(sp, &vals[s], c);
+            return true;
+        }
+        s = (s + 1) & (T - 1);
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool graph_has(const SnnSpec& sp, unsigned v, int t) {
+    const unsigned b = (v >> (8 * t)) & 0xFFu;
+    return sp.type == CCG_SNN_NUMBER ? b != 0u : b != 0xFFu;
+}
+
+__device__ __forceinline__ double graph_weight(const SnnSpec& sp, unsigned v, int t) {
+    const unsigned b = (v >> (8 * t)) & 0xFFu;
+    if (sp.type == CCG_SNN_NUMBER) return (double)b;
+    double w = (double)sp.kk[t] - 0.5 * (double)b;
+    return w < 1e-6 ? 1e-6 : w;
+}
+
+// ---------------------------------------------------------------- wave path --
+// Pass 1 (EMIT=false): per-graph partner counts cnt[t][j]; overflow rows are
+// appended to ov_list.  Pass 2 (EMIT=true): emit at off[t][j].
+template <bool EMIT>
+__global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
+    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
+    int* __restrict__ ov_list, int* __restrict__ ov_count, const int* __restrict__ ov_flag, SnnOut out) {
+    __shared__ int keys_all[SNN_WAVES][SNN_WT];
+    __shared__ unsigned vals_all[SNN_WAVES][SNN_WT];
+    __shared__ int count_all[SNN_WAVES];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* keys = keys_all[wv];
+    unsigned* vals = vals_all[wv];
+    int* count = &count_all[wv];
+    const int kmax = sp.kk[sp.nk - 1];
+    constexpr int BITS = 11;  // log2(SNN_WT)
+    const int cap_entries = SNN_WT * 3 / 4;
+    for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
+        if (EMIT && ov_flag[j]) continue;  // handled by the overflow paths
+        for (int s = lane; s < SNN_WT; s += 64) {
+            keys[s] = SNN_EMPTY;
+            vals[s] = sp.init;
+        }
+        if (lane == 0) *count = 0;
+        WAVE_LDS_SYNC();
+        bool full = false;
+        for (int i = 0; i <= kmax && !full; ++i) {
+            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
+            const int64_t h0 = hoff[cur];
+            const int64_t len = hoff[cur + 1] - h0 + 1;  // hosts + cur itself
+            for (int64_t o0 = 0; o0 < len; o0 += 64) {
+                const int64_t o = o0 + lane;
+                bool ok = true;
+                if (o < len) {
+                    int p, rp;
+                    if (o == len - 1) {
+                        p = cur;
+                        rp = 0;
+                    } else {
+                        const int2 hr = hosts[h0 + o];
+                        p = hr.x;
+                        rp = hr.y;
+                    }
+                    if (p > j) {
+                        const unsigned c = snn_contrib(sp, i, rp);
+                        if (c != sp.init) ok = table_insert<SNN_WT>(keys, vals, count, p, c, sp, BITS);
                     }
                 }
+                WAVE_LDS_SYNC();
+                full = __any(!ok) || (*count > cap_entries);
+                if (full) break;
+            }
+        }
+        if (full) {
+            if (!EMIT && lane == 0) {
+                const int q = atomicAdd(ov_count, 1);
+                ov_list[q] = (int)j;
+            }
+            continue;
+        }
+        if (!EMIT) {
+            int64_t c[SNN_MAXK] = {0, 0, 0, 0};
+            for (int s = lane; s < SNN_WT; s += 64)
+                if (keys[s] != SNN_EMPTY) {
+                    const unsigned v = vals[s];
+#pragma unroll
+                    for (int t = 0; t < SNN_MAXK; ++t)
+                        if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
+                }
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t) {
+                int64_t v = c[t];
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
             }
             WAVE_LDS_SYNC();
+            continue;
         }
+        // ---- pass 2: compact in place (dest index <= source slot), sort, emit
+        int u = 0;
+        for (int s0 = 0; s0 < SNN_WT; s0 += 64) {
+            const int k = keys[s0 + lane];
+            const unsigned v = vals[s0 + lane];
+            const bool occ = k != SNN_EMPTY;
+            const unsigned long long m = __ballot(occ);
+            WAVE_LDS_SYNC();
+            if (occ) {
+                const int dst = u + __popcll(m & lanemask_lt());
+                keys[dst] = k;
+                vals[dst] = v;
+            }
+            u += __popcll(m);
+            WAVE_LDS_SYNC();
+        }
+        int P = 64;
+        while (P < u) P <<= 1;
+        for (int s = u + lane; s < P; s += 64) keys[s] = 0x7fffffff;
+        WAVE_LDS_SYNC();
+        for (int kk = 2; kk <= P; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (int i = lane; i < P; i += 64) {
+                    const int l = i ^ jj;
+                    if (l > i) {
+                        const int a = keys[i], b = keys[l];
+                        const bool up = (i & kk) == 0;
+                        if ((a > b) == up) {
+                            keys[i] = b;
+                            keys[l] = a;
+                            const unsigned va = vals[i];
+                            vals[i] = vals[l];
+                            vals[l] = va;
+                        }
+                    }
+                }
+                WAVE_LDS_SYNC();
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < SNN_MAXK; ++t) {
+            if (t >= sp.nk) break;
+            int64_t e = cnt[(int64_t)t * (n + 1) + j];
+            for (int c0 = 0; c0 < u; c0 += 64) {
+                const int c = c0 + lane;
+                const bool in = c < u;
+                const unsigned v = in ? vals[c] : sp.init;
+                const bool has = in && graph_has(sp, v, t);
+                const unsigned long long m = __ballot(has);
+                if (has) {
+                    const int64_t pos = e + __popcll(m & lanemask_lt());
+                    if (pos < out.cap[t]) {
+                        out.oi[t][pos] = (int32_t)j;
+                        out.oj[t][pos] = keys[c];
+                        out.ow[t][pos] = graph_weight(sp, v, t);
+                    }
+                }
+                e += __popcll(m);
+            }
+        }
+        WAVE_LDS_SYNC();
     }
 }
 
-// Reduce sorted runs.  emit == false: returns the number of runs.
-// emit == true: writes edges (j, p, w) starting at out index `base`.
-__device__ int64_t snn_reduce_runs(const unsigned long long* lds, int cnt, int64_t j, int k,
-                                   int type, bool emit, int64_t base, int64_t cap,
-                                   int32_t* __restrict__ oi, int32_t* __restrict__ oj,
-                                   double* __restrict__ ow) {
-    const int lane = threadIdx.x & 63;
-    int64_t runs = 0;
-    int carry_start = 0;
-    for (int c0 = 0; c0 < cnt; c0 += 64) {
-        const int i = c0 + lane;
-        const bool in = i < cnt;
-        unsigned long long key = in ? lds[i] : ~0ull;
-        const unsigned p = (unsigned)(key >> 32);
-        const bool start = in && (i == 0 || (unsigned)(lds[i - 1] >> 32) != p);
-        const bool last = in && (i == cnt - 1 || (unsigned)(lds[i + 1] >> 32) != p);
-        const unsigned long long sm = __ballot(start);
-        if (emit) {
-            // run start for this position: inclusive prefix max over lanes
-            int rs = start ? i : -1;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                int y = __shfl_up(rs, o, 64);
-                if (lane >= o) rs = max(rs, y);
-            }
-            if (rs < 0) rs = carry_start;
-            const int64_t rid = runs + __popcll(sm & (lanemask_lt() | (1ull << lane))) - 1;
-            if (last) {
-                const int64_t e = base + rid;
-                if (e < cap) {
-                    double w;
-                    if (type == CCG_SNN_NUMBER) {
-                        w = (double)(i - rs + 1);
-                    } else {
-                        const unsigned mn = (unsigned)(lds[rs] & 0xffffffffu);
-                        w = (double)k - 0.5 * (double)mn;
-                        w = w < 1e-6 ? 1e-6 : w;
-                    }
-                    oi[e] = (int32_t)j;
-                    oj[e] = (int32_t)p;
-                    ow[e] = w;
+// --------------------------------------------------------------- block path --
+// Same algorithm with one 256-thread block and a 16K-slot table per node, for
+// the overflow list of the wave path.  Nodes that overflow here too are
+// appended to ov2 for the dense path.
+template <bool EMIT>
+__global__ __launch_bounds__(256) void snn_block_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
+    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
+    const int* __restrict__ ov_list, const int* __restrict__ ov_count, int* __restrict__ ov2_list,
+    int* __restrict__ ov2_count, const int* __restrict__ ov2_flag, SnnOut out) {
+    __shared__ int keys[SNN_BT];
+    __shared__ unsigned vals[SNN_BT];
+    __shared__ int count;
+    __shared__ int full_s;
+    __shared__ int u_s;
+    __shared__ int tcount[256];
+    __shared__ int64_t wsum[4][SNN_MAXK];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int kmax = sp.kk[sp.nk - 1];
+    constexpr int BITS = 14;
+    constexpr int PER = SNN_BT / 256;  // slots owned per thread during compaction
+    const int cap_entries = SNN_BT * 3 / 4;
+    const int nov = *ov_count;
+    for (int f = blockIdx.x; f < nov; f += gridDim.x) {
+        const int64_t j = ov_list[f];
+        if (EMIT && ov2_flag[j]) continue;  // uniform across the block
+        for (int s = tid; s < SNN_BT; s += 256) {
+            keys[s] = SNN_EMPTY;
+            vals[s] = sp.init;
+        }
+        if (tid == 0) {
+            count = 0;
+            full_s = 0;
+        }
+        __syncthreads();
+        for (int i = 0; i <= kmax; ++i) {
+            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
+            const int64_t h0 = hoff[cur];
+            const int64_t len = hoff[cur + 1] - h0 + 1;
+            for (int64_t o = tid; o < len; o += 256) {
+                int p, rp;
+                if (o == len - 1) {
+                    p = cur;
+                    rp = 0;
+                } else {
+                    const int2 hr = hosts[h0 + o];
+                    p = hr.x;
+                    rp = hr.y;
+                }
+                if (p > j) {
+                    const unsigned c = snn_contrib(sp, i, rp);
+                    if (c != sp.init && !table_insert<SNN_BT>(keys, vals, &count, p, c, sp, BITS)) full_s = 1;
                 }
             }
-            // carry: last run start seen in this chunk
-            int cs = start ? i : -1;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) cs = max(cs, __shfl_xor(cs, o, 64));
-            if (cs >= 0) carry_start = cs;
         }
-        runs += __popcll(sm);
-    }
-    return runs;
-}
-
-// Pass 1 (emit=false): cnt[j] = #partners > j, overflow nodes appended to ov.
-// Pass 2 (emit=true): write edges at eoff[j].
-template <bool EMIT>
-__global__ __launch_bounds__(64 * SNN_WAVES) void snn_node_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, int k, int type,
-    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts,
-    int64_t* __restrict__ cnt_or_off, int* __restrict__ ov_list, int* __restrict__ ov_count,
-    int64_t cap, int32_t* __restrict__ oi, int32_t* __restrict__ oj, double* __restrict__ ow) {
-    __shared__ unsigned long long lds_all[SNN_WAVES][SNN_CAP];
-    const int wv = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    unsigned long long* lds = lds_all[wv];
-    for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
-        const int c = snn_gather(j, knn, kstride, k, hoff, hosts, lds);
-        if (c > SNN_CAP) {
-            if (!EMIT && lane == 0) {
-                int p = atomicAdd(ov_count, 1);
-                ov_list[p] = (int)j;
+        __syncthreads();
+        if (full_s || count > cap_entries) {
+            if (!EMIT && tid == 0) {
+                const int q = atomicAdd(ov2_count, 1);
+                ov2_list[q] = (int)j;
             }
-            continue;  // dense path handles this node in both passes
+            __syncthreads();
+            continue;
         }
-        WAVE_LDS_SYNC();
-        wave_sort_lds(lds, c);
         if (!EMIT) {
-            int64_t r = snn_reduce_runs(lds, c, j, k, type, false, 0, 0, oi, oj, ow);
-            if (lane == 0) cnt_or_off[j] = r;
-        } else {
-            snn_reduce_runs(lds, c, j, k, type, true, cnt_or_off[j], cap, oi, oj, ow);
+            int64_t c[SNN_MAXK] = {0, 0, 0, 0};
+            for (int s = tid; s < SNN_BT; s += 256)
+                if (keys[s] != SNN_EMPTY) {
+                    const unsigned v = vals[s];
+#pragma unroll
+                    for (int t = 0; t < SNN_MAXK; ++t)
+                        if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
+                }
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t) {
+                int64_t v = c[t];
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                if (lane == 0) wsum[wv][t] = v;
+            }
+            __syncthreads();
+            if (tid < sp.nk)
+                cnt[(int64_t)tid * (n + 1) + j] = wsum[0][tid] + wsum[1][tid] + wsum[2][tid] + wsum[3][tid];
+            __syncthreads();
+            continue;
         }
-        WAVE_LDS_SYNC();
+        // compact: thread t owns slots [t*PER, (t+1)*PER); block scan of counts
+        int mine = 0;
+        for (int s = tid * PER; s < tid * PER + PER; ++s) mine += keys[s] != SNN_EMPTY;
+        tcount[tid] = mine;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int t = 0; t < 256; ++t) {
+                const int v = tcount[t];
+                tcount[t] = acc;
+                acc += v;
+            }
+            u_s = acc;
+        }
+        __syncthreads();
+        // every thread reads all its slots into registers before anyone writes
+        int myk[PER];
+        unsigned myv[PER];
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            myk[s] = keys[tid * PER + s];
+            myv[s] = vals[tid * PER + s];
+        }
+        __syncthreads();
+        int dst = tcount[tid];
+#pragma unroll
+        for (int s = 0; s < PER; ++s)
+            if (myk[s] != SNN_EMPTY) {
+                keys[dst] = myk[s];
+                vals[dst] = myv[s];
+                ++dst;
+            }
+        const int u = u_s;
+        int P = 256;
+        while (P < u) P <<= 1;
+        for (int s = u + tid; s < P; s += 256) keys[s] = 0x7fffffff;
+        __syncthreads();
+        for (int kk = 2; kk <= P; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (int i = tid; i < P; i += 256) {
+                    const int l = i ^ jj;
+                    if (l > i) {
+                        const int a = keys[i], b = keys[l];
+                        const bool up = (i & kk) == 0;
+                        if ((a > b) == up) {
+                            keys[i] = b;
+                            keys[l] = a;
+                            const unsigned va = vals[i];
+                            vals[i] = vals[l];
+                            vals[l] = va;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int t = 0; t < sp.nk; ++t) {
+            int64_t e = cnt[(int64_t)t * (n + 1) + j];
+            for (int c0 = 0; c0 < u; c0 += 256) {
+                const int c = c0 + tid;
+                const bool in = c < u;
+                const unsigned v = in ? vals[c] : sp.init;
+                const bool has = in && graph_has(sp, v, t);
+                const unsigned long long m = __ballot(has);
+                if (lane == 0) wsum[wv][0] = __popcll(m);
+                __syncthreads();
+                int64_t before = 0, tot = 0;
+                for (int w = 0; w < 4; ++w) {
+                    if (w < wv) before += wsum[w][0];
+                    tot += wsum[w][0];
+                }
+                if (has) {
+                    const int64_t pos = e + before + __popcll(m & lanemask_lt());
+                    if (pos < out.cap[t]) {
+                        out.oi[t][pos] = (int32_t)j;
+                        out.oj[t][pos] = keys[c];
+                        out.ow[t][pos] = graph_weight(sp, v, t);
+                    }
+                }
+                e += tot;
+                __syncthreads();
+            }
+        }
+        __syncthreads();
     }
 }
 
-// Dense path for overflow nodes: one block per node, dense int array of n.
+// --------------------------------------------------------------- dense path --
+// Exact O(n) per node with a dense word per partner.  Reads/writes go
+// through agent-scope atomics so the block never sees stale L1 lines.
 template <bool EMIT>
 __global__ __launch_bounds__(256) void snn_dense_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, int k, int type,
-    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts,
-    const int* __restrict__ ov_list, const int* __restrict__ ov_count, int* __restrict__ dense_all,
-    int64_t* __restrict__ cnt_or_off, int64_t cap, int32_t* __restrict__ oi,
-    int32_t* __restrict__ oj, double* __restrict__ ow) {
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
+    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, const int* __restrict__ ov_list,
+    const int* __restrict__ ov_count, unsigned* __restrict__ dense_all, int64_t* __restrict__ cnt,
+    SnnOut out) {
     __shared__ int64_t wsum[4];
-    int* dense = dense_all + (int64_t)blockIdx.x * n;
+    unsigned* dense = dense_all + (int64_t)blockIdx.x * n;
     const int nov = *ov_count;
-    const int EMPTY = (type == CCG_SNN_NUMBER) ? 0 : 0x7fffffff;
+    const int kmax = sp.kk[sp.nk - 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int f = blockIdx.x; f < nov; f += gridDim.x) {
         const int64_t j = ov_list[f];
         for (int64_t p = j + 1 + threadIdx.x; p < n; p += 256)
-            __hip_atomic_store(&dense[p], EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&dense[p], sp.init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        for (int i = 0; i <= k; ++i) {
+        for (int i = 0; i <= kmax; ++i) {
             const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
             const int64_t h0 = hoff[cur];
             const int64_t len = hoff[cur + 1] - h0 + 1;
             for (int64_t o = threadIdx.x; o < len; o += 256) {
-                int p, val;
+                int p, rp;
                 if (o == len - 1) {
                     p = cur;
-                    val = i;
+                    rp = 0;
                 } else {
-                    int2 hr = hosts[h0 + o];
+                    const int2 hr = hosts[h0 + o];
                     p = hr.x;
-                    val = hr.y + i;
+                    rp = hr.y;
                 }
                 if (p > j) {
-                    if (type == CCG_SNN_NUMBER) atomicAdd(&dense[p], 1);
-                    else atomicMin(&dense[p], val);
+                    const unsigned c = snn_contrib(sp, i, rp);
+                    if (c != sp.init) snn_update(sp, &dense[p], c);
                 }
             }
         }
         __syncthreads();
-        int64_t base = EMIT ? cnt_or_off[j] : 0;
-        int64_t total = 0;
-        for (int64_t p0 = j + 1; p0 < n; p0 += 256) {
-            const int64_t p = p0 + threadIdx.x;
-            const int v = (p < n) ? __hip_atomic_load(&dense[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : EMPTY;
-            const bool hit = v != EMPTY;
-            const unsigned long long m = __ballot(hit);
-            const int wv = threadIdx.x >> 6;
-            if ((threadIdx.x & 63) == 0) wsum[wv] = __popcll(m);
-            __syncthreads();
-            int64_t before = 0, tot = 0;
-            for (int w = 0; w < 4; ++w) {
-                if (w < wv) before += wsum[w];
-                tot += wsum[w];
-            }
-            if (EMIT && hit) {
-                const int64_t e = base + total + before + __popcll(m & lanemask_lt());
-                if (e < cap) {
-                    double w;
-                    if (type == CCG_SNN_NUMBER) w = (double)v;
-                    else {
-                        w = (double)k - 0.5 * (double)v;
-                        w = w < 1e-6 ? 1e-6 : w;
+        for (int t = 0; t < sp.nk; ++t) {
+            int64_t base = EMIT ? cnt[(int64_t)t * (n + 1) + j] : 0;
+            int64_t total = 0;
+            for (int64_t p0 = j + 1; p0 < n; p0 += 256) {
+                const int64_t p = p0 + threadIdx.x;
+                const unsigned v = (p < n) ? __hip_atomic_load(&dense[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : sp.init;
+                const bool hit = (p < n) && graph_has(sp, v, t);
+                const unsigned long long m = __ballot(hit);
+                if (lane == 0) wsum[wv] = __popcll(m);
+                __syncthreads();
+                int64_t before = 0, tot = 0;
+                for (int w = 0; w < 4; ++w) {
+                    if (w < wv) before += wsum[w];
+                    tot += wsum[w];
+                }
+                if (EMIT && hit) {
+                    const int64_t e = base + total + before + __popcll(m & lanemask_lt());
+                    if (e < out.cap[t]) {
+                        out.oi[t][e] = (int32_t)j;
+                        out.oj[t][e] = (int32_t)p;
+                        out.ow[t][e] = graph_weight(sp, v, t);
                     }
-                    oi[e] = (int32_t)j;
-                    oj[e] = (int32_t)p;
-                    ow[e] = w;
                 }
+                total += tot;
+                __syncthreads();
             }
-            total += tot;
+            if (!EMIT && threadIdx.x == 0) cnt[(int64_t)t * (n + 1) + j] = total;
             __syncthreads();
         }
-        if (!EMIT && threadIdx.x == 0) cnt_or_off[j] = total;
-        __syncthreads();
     }
 }
 
-__global__ void snn_copy_total(const int64_t* __restrict__ off, int64_t n, int64_t* __restrict__ dst) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *dst = off[n];
+__global__ void snn_mark_kernel(const int* __restrict__ list, const int* __restrict__ count,
+                                int* __restrict__ flag) {
+    const int nl = *count;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) flag[list[i]] = 1;
 }
 
-extern "C" int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k,
-                           int type, int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap,
-                           int64_t* d_nedges, void* stream) {
-    CCG_REQUIRE(ctx && knn && d_nedges, "ccg_snn_dev: NULL argument");
-    CCG_REQUIRE(n >= 1 && n < (1LL << 31), "ccg_snn_dev: bad n");
-    CCG_REQUIRE(k >= 1 && k <= kstride, "ccg_snn_dev: need 1 <= k <= kstride");
-    CCG_REQUIRE(type == CCG_SNN_NUMBER || type == CCG_SNN_RANK, "ccg_snn_dev: bad type");
-    CCG_REQUIRE(cap == 0 || (out_i && out_j && out_w), "ccg_snn_dev: NULL outputs with cap > 0");
+__global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int nk, int64_t* d0, int64_t* d1,
+                                int64_t* d2, int64_t* d3) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t* ds[4] = {d0, d1, d2, d3};
+    for (int t = 0; t < nk; ++t)
+        if (ds[t]) *ds[t] = cnt[(int64_t)t * (n + 1) + n];
+}
+
+extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks,
+                                 int nk, int type, int32_t* const* out_i, int32_t* const* out_j,
+                                 double* const* out_w, const int64_t* caps, int64_t* const* d_nedges,
+                                 void* stream) {
+    CCG_REQUIRE(ctx && knn && ks && d_nedges, "ccg_snn_multi_dev: NULL argument");
+    CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1, "ccg_snn_multi_dev: bad n");
+    CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "ccg_snn_multi_dev: 1 <= nk <= %d", SNN_MAXK);
+    CCG_REQUIRE(type == CCG_SNN_NUMBER || type == CCG_SNN_RANK, "ccg_snn_multi_dev: bad type");
+    SnnSpec sp;
+    sp.nk = nk;
+    sp.type = type;
+    sp.init = type == CCG_SNN_NUMBER ? 0u : 0xFFFFFFFFu;
+    SnnOut out;
+    for (int t = 0; t < SNN_MAXK; ++t) {
+        sp.kk[t] = t < nk ? ks[t] : 0;
+        out.cap[t] = 0;
+        out.oi[t] = nullptr;
+        out.oj[t] = nullptr;
+        out.ow[t] = nullptr;
+    }
+    for (int t = 0; t < nk; ++t) {
+        CCG_REQUIRE(ks[t] >= 1 && ks[t] <= kstride && ks[t] <= 32 && (t == 0 || ks[t] > ks[t - 1]),
+                    "ccg_snn_multi_dev: ks must be ascending in [1, min(kstride, 32)]");
+        out.cap[t] = caps ? caps[t] : 0;
+        if (out.cap[t] > 0) {
+            CCG_REQUIRE(out_i && out_j && out_w && out_i[t] && out_j[t] && out_w[t],
+                        "ccg_snn_multi_dev: NULL outputs with cap > 0");
+            out.oi[t] = out_i[t];
+            out.oj[t] = out_j[t];
+            out.ow[t] = out_w[t];
+        }
+    }
+    const int kmax = ks[nk - 1];
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    // layout of WS_SNN_A: hcnt/hoff [n+1] i64 | cursor [n+1] i64 | misc
     int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
-    int2* hosts = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (n * k + 1));
-    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * (n + 1));
-    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (n + 16));
-    int* dense = (int*)ccg_ws(ctx, WS_SNN_D, sizeof(int) * n * SNN_DENSE_BLOCKS);
+    int2* hosts = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (n * kmax + 1));
+    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * nk * (n + 1));
+    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (4 * n + 64));
+    unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
     if (!hoff || !hosts || !cnt || !ov || !dense) return CCG_ENOMEM;
     unsigned long long* cursor = (unsigned long long*)(hoff + (n + 1));
     int* err = (int*)(hoff + 2 * (n + 1));
-    int* ov_count = ov + n;
-    const int64_t nk = n * k;
+    int* ov_list = ov;
+    int* ov2_list = ov + n;
+    int* flag1 = ov + 2 * n;
+    int* flag2 = ov + 3 * n;
+    int* ov_count = ov + 4 * n;
+    int* ov2_count = ov_count + 1;
+    const int64_t nkk = (int64_t)n * kmax;
     const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
-    CCG_HIP(hipMemsetAsync(hoff, 0, sizeof(int64_t) * (n + 1) + 0, st));
+    CCG_HIP(hipMemsetAsync(hoff, 0, sizeof(int64_t) * (n + 1), st));
     CCG_HIP(hipMemsetAsync(err, 0, sizeof(int) * 4, st));
-    CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int), st));
-    snn_count_hosts<<<(unsigned)ccg_cdiv(nk, 256), 256, 0, st>>>(knn, n, kstride, k,
-                                                                 (unsigned long long*)hoff, err);
+    CCG_HIP(hipMemsetAsync(flag1, 0, sizeof(int) * (2 * n + 64), st));
+    CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * nk * (n + 1), st));
+    snn_count_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax,
+                                                                  (unsigned long long*)hoff, err);
     int rc = ccg_scan_i64(ctx, hoff, hoff, n, st);
     if (rc) return rc;
     CCG_HIP(hipMemcpyAsync(cursor, hoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
-    snn_fill_hosts<<<(unsigned)ccg_cdiv(nk, 256), 256, 0, st>>>(knn, n, kstride, k, cursor, hosts);
-    const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 8192);
-    snn_node_kernel<false><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, k, type, hoff, hosts,
-                                                           cnt, ov, ov_count, 0, out_i, out_j, out_w);
-    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, k, type, hoff, hosts,
-                                                             ov, ov_count, dense, cnt, 0, out_i,
-                                                             out_j, out_w);
-    rc = ccg_scan_i64(ctx, cnt, cnt, n, st);
-    if (rc) return rc;
-    if (cap > 0) {
-        snn_node_kernel<true><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, k, type, hoff, hosts,
-                                                              cnt, ov, ov_count, cap, out_i, out_j,
-                                                              out_w);
-        snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, k, type, hoff,
-                                                                hosts, ov, ov_count, dense, cnt, cap,
-                                                                out_i, out_j, out_w);
+    snn_fill_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, cursor, hosts);
+    const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
+    // pass 1: per-graph counts (wave tables, then block tables, then dense)
+    snn_wave_kernel<false><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
+                                                           ov_count, flag1, out);
+    snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
+                                                 ov2_list, ov2_count, flag2, out);
+    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
+                                                             ov2_count, dense, cnt, out);
+    snn_mark_kernel<<<64, 256, 0, st>>>(ov_list, ov_count, flag1);
+    snn_mark_kernel<<<64, 256, 0, st>>>(ov2_list, ov2_count, flag2);
+    for (int t = 0; t < nk; ++t) {
+        rc = ccg_scan_i64(ctx, cnt + (int64_t)t * (n + 1), cnt + (int64_t)t * (n + 1), n, st);
+        if (rc) return rc;
     }
-    snn_copy_total<<<1, 64, 0, st>>>(cnt, n, d_nedges);
+    bool any_cap = false;
+    for (int t = 0; t < nk; ++t) any_cap |= out.cap[t] > 0;
+    if (any_cap) {
+        snn_wave_kernel<true><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
+                                                              ov_count, flag1, out);
+        snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
+                                                    ov2_list, ov2_count, flag2, out);
+        snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
+                                                                ov2_count, dense, cnt, out);
+    }
+    snn_copy_totals<<<1, 64, 0, st>>>(cnt, n, nk, d_nedges[0], nk > 1 ? d_nedges[1] : nullptr,
+                                      nk > 2 ? d_nedges[2] : nullptr, nk > 3 ? d_nedges[3] : nullptr);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
 
+extern "C" int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k, int type,
+                           int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap, int64_t* d_nedges,
+                           void* stream) {
+    CCG_REQUIRE(k >= 1 && k <= kstride, "ccg_snn_dev: need 1 <= k <= kstride");
+    int32_t* oi[1] = {out_i};
+    int32_t* oj[1] = {out_j};
+    double* ow[1] = {out_w};
+    int64_t caps[1] = {cap};
+    int64_t* dn[1] = {d_nedges};
+    return ccg_snn_multi_dev(ctx, knn, n, kstride, &k, 1, type, oi, oj, ow, caps, dn, stream);
+}
+
 extern "C" int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k, int type,
-                       int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap,
-                       int64_t* nedges) {
+                       int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap, int64_t* nedges) {
     CCG_REQUIRE(ctx && knn && nedges, "ccg_snn: NULL argument");
     CCG_REQUIRE(n >= 1 && kstride >= 1, "ccg_snn: bad sizes");
     CCG_HIP(hipSetDevice(ctx->device));

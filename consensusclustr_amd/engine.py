@@ -178,6 +178,22 @@ class Engine:
         check(self.lib.ccg_snn_dev(self.ctx, _ptr(knn_idx), n, ks, k, t, _ptr(out_i), _ptr(out_j),
                                    _ptr(out_w), cap, _ptr(d_nedges), _stream()))
 
+    def snn_multi_t(self, knn_idx, ks, type, outs, d_nedges):
+        """All graphs of ks (ascending) in one pass.  outs: list of (i, j, w)
+        tensors per graph (or None for count-only); d_nedges: int64 tensor (nk,)."""
+        n, kst = knn_idx.shape
+        nk = len(ks)
+        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        karr = (ctypes.c_int * nk)(*ks)
+        P = _vp * nk
+        oi = P(*[_ptr(o[0]) if o else None for o in outs])
+        oj = P(*[_ptr(o[1]) if o else None for o in outs])
+        ow = P(*[_ptr(o[2]) if o else None for o in outs])
+        caps = (ctypes.c_int64 * nk)(*[o[0].numel() if o else 0 for o in outs])
+        dn = P(*[_vp(d_nedges.data_ptr() + 8 * i) for i in range(nk)])
+        check(self.lib.ccg_snn_multi_dev(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, oi, oj, ow, caps, dn,
+                                         _stream()))
+
     def silhouette_t(self, x, labels, cmax, out_mean, out_nclust, out_minsize, out_width=None):
         m, d = x.shape
         L = labels.shape[0]

@@ -124,6 +124,16 @@ int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                 int k, int type, int32_t* out_i, int32_t* out_j,
                 double* out_w, int64_t cap, int64_t* d_nedges, void* stream);
 
+/* Several graphs in one pass: ks[0..nk) ascending (nk <= 4, ks <= 32) -- the
+ * kNum loop of getClustAssignments (:653) over one kmax neighbour matrix.
+ * Graph t goes to out_i[t]/out_j[t]/out_w[t] (capacity caps[t]); its edge
+ * count to *d_nedges[t] (device int64). */
+int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n,
+                      int kstride, const int* ks, int nk, int type,
+                      int32_t* const* out_i, int32_t* const* out_j,
+                      double* const* out_w, const int64_t* caps,
+                      int64_t* const* d_nedges, void* stream);
+
 /* --------------------------------------------------------- silhouette -- */
 /* mean(approxSilhouette(x, labels_l)[,3], na.rm=TRUE) for L label vectors
  * over the same m x d float64 row-major matrix.  labels: L x m int32 codes

@@ -153,6 +153,30 @@ def test_snn_hub_overflow_dense_path(engine, t):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_multi_pass_matches_single_graphs(engine, t):
+    """One pass over kmax=20 builds the k=10/15/20 graphs (kNum, :653)."""
+    import torch
+    rng = np.random.default_rng(31)
+    X = _mixture(rng, 12000, 16)
+    idx, _ = engine.knn_boot(X, np.arange(12000), kmax=20)
+    knn_t = torch.from_numpy(idx[0]).cuda()
+    ks = (10, 15, 20)
+    cap = 12000 * 400
+    outs = [(torch.empty(cap, dtype=torch.int32, device="cuda"), torch.empty(cap, dtype=torch.int32, device="cuda"),
+             torch.empty(cap, dtype=torch.float64, device="cuda")) for _ in ks]
+    ne = torch.zeros(len(ks), dtype=torch.int64, device="cuda")
+    engine.snn_multi_t(knn_t, ks, t, outs, ne)
+    torch.cuda.synchronize()
+    for g, k in enumerate(ks):
+        m = int(ne[g].item())
+        ei, ej, w = O.snn(idx[0], k, t)
+        assert m == ei.size
+        assert np.array_equal(outs[g][0][:m].cpu().numpy(), ei)
+        assert np.array_equal(outs[g][1][:m].cpu().numpy(), ej)
+        assert np.array_equal(outs[g][2][:m].cpu().numpy(), w)
+
+
 # ---------------------------------------------------------- silhouette --
 def test_silhouette_kat(engine, kat):
     c = kat["silhouette_1d"]
