@@ -30,6 +30,7 @@ enum ccg_ws_slot {
     WS_HOST_D,       // host-API staging 4
     WS_HOST_E,       // host-API staging 5
     WS_SCAN,         // scan block sums
+    WS_ORDER,        // kNN spatial ordering (bucket histogram, permutation)
     WS_NSLOTS
 };
 

@@ -18,6 +18,9 @@
 //                 fp32 error bound; rows that cannot be proven go to
 //   4. fallback : exact fp64 scan of all references for that row.
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "ccg_internal.h"
 
@@ -31,6 +34,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Relative error budget of the fp32 screen in units of the fp32 ulp (2^-24)
 // times (|x| + max|y|)^2; see DESIGN.md "kNN certification bound".
 #define KNN_ERR_ULPS 256.0
+// fp16 hi/lo screen: 3 x 16*KSTEPS products accumulated in fp32
+#define KNN_ERR_ULPS_F16 1024.0
 
 __device__ __forceinline__ double sqdist_exact(const double* __restrict__ a,
                                                const double* __restrict__ b, int d) {
@@ -185,6 +190,329 @@ __global__ __launch_bounds__(256) void knn_screen_kernel(const float* __restrict
     }
 }
 
+// ------------------------------------------------- fp16 hi/lo screen --
+// Each value x (scaled by sigma = 2^e so max|x| <= 2^13) is split into
+// fp16 hi = rn(x) and lo = rn(x - hi); x.y ~ hi.hi + hi.lo + lo.hi with
+// |error| <= ~2^-22 |x||y| per product plus fp32 accumulation, i.e. fp32-class
+// accuracy from three v_mfma_f32_32x32x16_f16 (16 cycles/K-block each at
+// 16x the fp32 MFMA rate).  -|y|^2/2 enters as the accumulator init.
+// Row image (64*KSTEPS bytes): for lane-half h in {0,1}: KSTEPS hi chunks
+// then KSTEPS lo chunks of 8 halves (dims 16s + 8h .. +7), so a lane reads
+// one contiguous 32*KSTEPS-byte run.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+#define KNN_CHUNK 64   // refs per LDS stage (2 MFMA tiles)
+#define KNN_QCAP 24    // per-lane insertion queue slots (flush when > QCAP-16)
+
+__global__ void knn_maxabs_kernel(const double* __restrict__ x, int64_t tot, unsigned* __restrict__ bits) {
+    unsigned local = 0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        float f = (float)fabs(x[t]);
+        f = nextafterf(f, INFINITY);
+        local = max(local, __float_as_uint(f));
+    }
+    for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(bits, local);
+}
+
+__device__ __forceinline__ int knn_scale_exp(const unsigned* maxabs_bits) {
+    const float m = __uint_as_float(*maxabs_bits);
+    if (!(m > 0.f)) return 0;
+    return 13 - (ilogbf(m) + 1);  // max|x| * 2^e < 2^13
+}
+
+template <int KSTEPS>
+__global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, int64_t npad, int d,
+                                  const unsigned* __restrict__ maxabs_bits, const int* __restrict__ perm,
+                                  uint4* __restrict__ img, float* __restrict__ nrm,
+                                  double* __restrict__ inv_scale2) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in spatial order
+    if (r >= npad) return;
+    const int64_t src = r < n ? perm[r] : 0;
+    const int e = knn_scale_exp(maxabs_bits);
+    if (r == 0) *inv_scale2 = ldexp(1.0, -2 * e);
+    _Float16 hv[KSTEPS * 32];  // [h][hi s..][lo s..] flattened below
+    double nr = 0.0;
+#pragma unroll
+    for (int k = 0; k < KSTEPS * 16; ++k) {
+        double xs = 0.0;
+        if (r < n && k < d) {
+            const double x = rows[src * d + k];
+            nr += x * x;
+            xs = ldexp(x, e);
+        }
+        const _Float16 hi = (_Float16)(float)xs;
+        const _Float16 lo = (_Float16)(float)(xs - (double)(float)hi);
+        const int s = k / 16, h = (k % 16) / 8, j = k % 8;
+        hv[h * (KSTEPS * 16) + s * 8 + j] = hi;
+        hv[h * (KSTEPS * 16) + KSTEPS * 8 + s * 8 + j] = lo;
+    }
+    uint4* out = img + r * (KSTEPS * 4);
+#pragma unroll
+    for (int c = 0; c < KSTEPS * 4; ++c) out[c] = *reinterpret_cast<const uint4*>(&hv[c * 8]);
+    nrm[r] = (r < n) ? (float)(-0.5 * ldexp(nr, 2 * e)) : -INFINITY;
+}
+
+template <int KSTEPS>
+__device__ __forceinline__ int swz_chunk(int row, int c) {
+    // rows of 64*KSTEPS bytes; spread the 16-B chunk over the 256-B bank row
+    if constexpr (KSTEPS == 1) return c ^ ((row >> 2) & 3);
+    else if constexpr (KSTEPS == 2) return c ^ ((row >> 1) & 7);
+    else return c ^ (row & 15);
+}
+
+// ---------------------------------------------------- spatial ordering --
+// Bucket rows by a 15-bit Morton code of their first three coordinates (the
+// leading PCs) so that rows close in space sit in nearby chunks.  Any
+// permutation is correct; only screening speed depends on it.
+#define KNN_MORTON_BITS 5
+__device__ __forceinline__ unsigned f2ord(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+__global__ void knn_bounds_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                  unsigned* __restrict__ bnd /* [3] min, [3] max (ordered) */) {
+    const int nd = d < 3 ? d : 3;
+    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        for (int k = 0; k < nd; ++k) {
+            const unsigned o = f2ord((float)rows[r * d + k]);
+            mn[k] = min(mn[k], o);
+            mx[k] = max(mx[k], o);
+        }
+    for (int k = 0; k < nd; ++k) {
+        unsigned a = mn[k], b = mx[k];
+        for (int o = 32; o > 0; o >>= 1) {
+            a = min(a, (unsigned)__shfl_xor((int)a, o, 64));
+            b = max(b, (unsigned)__shfl_xor((int)b, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&bnd[k], a);
+            atomicMax(&bnd[3 + k], b);
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned morton_key(const double* __restrict__ x, int d,
+                                               const unsigned* __restrict__ bnd) {
+    const int nd = d < 3 ? d : 3;
+    unsigned code = 0;
+    for (int k = 0; k < nd; ++k) {
+        const float lo = ord2f(bnd[k]), hi = ord2f(bnd[3 + k]);
+        const float span = hi - lo;
+        float t = span > 0.f ? ((float)x[k] - lo) / span : 0.f;
+        t = fminf(fmaxf(t, 0.f), 0.999999f);
+        const unsigned qv = (unsigned)(t * (float)(1u << KNN_MORTON_BITS));
+        for (int b = 0; b < KNN_MORTON_BITS; ++b) code |= ((qv >> b) & 1u) << (3 * b + k);
+    }
+    return code;
+}
+
+__global__ void knn_bucket_count_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                        const unsigned* __restrict__ bnd, int64_t* __restrict__ hist) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    atomicAdd((unsigned long long*)&hist[morton_key(rows + r * d, d, bnd)], 1ull);
+}
+
+__global__ void knn_bucket_scatter_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                          const unsigned* __restrict__ bnd, int64_t* __restrict__ cursor,
+                                          int* __restrict__ perm) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const unsigned key = morton_key(rows + r * d, d, bnd);
+    const int64_t pos = (int64_t)atomicAdd((unsigned long long*)&cursor[key], 1ull);
+    perm[pos] = (int)r;
+}
+
+__device__ __forceinline__ int knn_chunk_at(int k, int c0, int Lc, int Rc, int Mc) {
+    if (k == 0) return c0;
+    if (k <= 2 * Mc) return (k & 1) ? c0 + (k + 1) / 2 : c0 - k / 2;
+    const int m = k - 2 * Mc;
+    return Rc > Lc ? c0 + Mc + m : c0 - Mc - m;
+}
+
+template <int KSTEPS, int KP, int EXP = 0>
+__global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restrict__ img,
+                                                           const float* __restrict__ nrm, int n, int nchunks,
+                                                           int* __restrict__ cand_idx,
+                                                           float* __restrict__ cand_thr) {
+    constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
+    constexpr int ROWB = KSTEPS * 64;               // bytes per row
+    constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage (no norms)
+    constexpr int LOADS = (KNN_CHUNK * C16) / 256;  // uint4 loads per thread per stage
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2][STAGE + KNN_CHUNK * 4];
+    // Per-lane insertion queues (slot-major, so a wave's enqueue is one
+    // conflict-free ds_write_b64).  Candidates above the running threshold are
+    // queued per tile and inserted in batches: a flush costs max-queue-length
+    // insertion rounds for the whole wave instead of one round per (tile,
+    // register) that any lane touched.
+    __shared__ uint2 qbuf[4][KNN_QCAP][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const int q0 = blockIdx.x * KNN_QPB + wave * 32;
+    const int q = q0 + col;
+    const int qrow = q < n ? q : n - 1;
+
+    h8 qh[KSTEPS], ql[KSTEPS];
+    {
+        const uint4* qp = img + (int64_t)qrow * C16 + h * 2 * KSTEPS;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            uint4 a = qp[s], b = qp[KSTEPS + s];
+            qh[s] = *reinterpret_cast<h8*>(&a);
+            ql[s] = *reinterpret_cast<h8*>(&b);
+        }
+    }
+    float lv[KP];
+    int li[KP];
+#pragma unroll
+    for (int t = 0; t < KP; ++t) {
+        lv[t] = -INFINITY;
+        li[t] = -1;
+    }
+    float thr = -INFINITY;
+
+    // register staging (issue early, write to LDS after the compute); no
+    // lambdas/arrays captured by reference, so nothing lands in scratch
+#define KNN_STAGE_LOAD(cidx)                                                                  \
+    do {                                                                                      \
+        const uint4* src_ = img + (int64_t)(cidx) * KNN_CHUNK * C16;                          \
+        p0 = src_[tid];                                                                       \
+        if (LOADS > 1) p1 = src_[tid + 256];                                                  \
+        if (LOADS > 2) p2 = src_[tid + 512];                                                  \
+        if (LOADS > 3) p3 = src_[tid + 768];                                                  \
+        if (tid < KNN_CHUNK / 4) pn = reinterpret_cast<const float4*>(nrm + (int64_t)(cidx) * KNN_CHUNK)[tid]; \
+    } while (0)
+#define KNN_STAGE_PUT(bb, i, v)                                                               \
+    do {                                                                                      \
+        const int L_ = tid + 256 * (i);                                                       \
+        const int row_ = L_ / C16, c_ = L_ % C16;                                             \
+        *reinterpret_cast<uint4*>(&lds[bb][row_ * ROWB + swz_chunk<KSTEPS>(row_, c_) * 16]) = (v); \
+    } while (0)
+#define KNN_STAGE_STORE(bb)                                                                   \
+    do {                                                                                      \
+        KNN_STAGE_PUT(bb, 0, p0);                                                             \
+        if (LOADS > 1) KNN_STAGE_PUT(bb, 1, p1);                                              \
+        if (LOADS > 2) KNN_STAGE_PUT(bb, 2, p2);                                              \
+        if (LOADS > 3) KNN_STAGE_PUT(bb, 3, p3);                                              \
+        if (tid < KNN_CHUNK / 4) reinterpret_cast<float4*>(&lds[bb][STAGE])[tid] = pn;         \
+    } while (0)
+    uint4 p0, p1, p2, p3;
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+    // Rows are in spatial (Morton) order, so scan ref chunks outward from the
+    // block's own position: near neighbours arrive first, the threshold tightens
+    // within a few tiles and later tiles rarely insert (the order only changes
+    // speed; certification makes the result exact for any order).
+    const int c0 = min((int)(blockIdx.x * KNN_QPB) / KNN_CHUNK, nchunks - 1);
+    const int Lc = c0, Rc = nchunks - 1 - c0, Mc = min(Lc, Rc);
+#define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
+    float T = -INFINITY;  // max of both halves' thresholds (see below)
+    int qc = 0;           // this lane's queued candidates
+#define KNN_FLUSH()                                                                   \
+    do {                                                                              \
+        for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
+            if (i_ < qc) {                                                            \
+                const uint2 e_ = qbuf[wave][i_][lane];                                \
+                const float v_ = __uint_as_float(e_.x);                               \
+                if (v_ > T) {                                                         \
+                    list_insert<KP>(lv, li, v_, (int)e_.y);                           \
+                    thr = lv[KP - 1];                                                 \
+                    T = fmaxf(T, thr);                                                \
+                }                                                                     \
+            }                                                                         \
+        }                                                                             \
+        qc = 0;                                                                       \
+    } while (0)
+    KNN_STAGE_LOAD(chunk_at(0));
+    KNN_STAGE_STORE(0);
+    __syncthreads();
+    for (int k = 0; k < nchunks; ++k) {
+        const int b = k & 1;
+        const int c = chunk_at(k);
+        if (k + 1 < nchunks) KNN_STAGE_LOAD(chunk_at(k + 1));
+#pragma nounroll  // unrolling the two tiles doubles live registers (248 vs 162 VGPRs)
+        for (int tau = 0; tau < 2; ++tau) {
+            const int row = tau * 32 + col;
+            h8 ah[KSTEPS], al[KSTEPS];
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                uint4 a = *reinterpret_cast<const uint4*>(
+                    &lds[b][row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + s) * 16]);
+                uint4 bb = *reinterpret_cast<const uint4*>(
+                    &lds[b][row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + KSTEPS + s) * 16]);
+                ah[s] = *reinterpret_cast<h8*>(&a);
+                al[s] = *reinterpret_cast<h8*>(&bb);
+            }
+            f32x16 acc;
+            const float* nb = reinterpret_cast<const float*>(&lds[b][STAGE]) + tau * 32 + 4 * h;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = *reinterpret_cast<const float4*>(nb + 8 * g);
+                acc[4 * g + 0] = v.x;
+                acc[4 * g + 1] = v.y;
+                acc[4 * g + 2] = v.z;
+                acc[4 * g + 3] = v.w;
+            }
+            const int rbase = c * KNN_CHUNK + tau * 32;
+            if (rbase == q0) {  // diagonal tile: exclude self (wave-uniform branch)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg)
+                    if ((reg & 3) + 8 * (reg >> 2) + 4 * h == col) acc[reg] = -INFINITY;
+            }
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], qh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], ql[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], qh[s], acc, 0, 0, 0);
+            }
+            float vmax = acc[0];
+#pragma unroll
+            for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
+            if (EXP == 1) {  // timing-only experiment: no insertion (results invalid)
+                T = fmaxf(T, vmax * 0.0f);
+                thr += vmax;
+                continue;
+            }
+            if (__any(vmax > T)) {
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const float v = acc[reg];
+                    if (v > T) {
+                        qbuf[wave][qc][lane] = make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
+                        ++qc;
+                    }
+                }
+                if (__any(qc > KNN_QCAP - 16)) KNN_FLUSH();
+            }
+            // Both halves of a query may reject anything at or below the better
+            // of their two KP-th values: the union of the lists still holds the
+            // query's overall top KP, and every rejected/evicted ref is <= the
+            // final max(thr_h0, thr_h1) that certification uses.
+            T = fmaxf(thr, __shfl_xor(thr, 32, 64));
+        }
+        if (k + 1 < nchunks) KNN_STAGE_STORE(b ^ 1);
+        __syncthreads();
+    }
+    KNN_FLUSH();
+#undef KNN_FLUSH
+#undef KNN_STAGE_LOAD
+#undef KNN_STAGE_PUT
+#undef KNN_STAGE_STORE
+#undef chunk_at
+    if (q < n) {
+        int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
+#pragma unroll
+        for (int t = 0; t < KP; ++t) out[t] = li[t];
+        cand_thr[(int64_t)q * 2 + h] = thr;
+    }
+}
+
 // -------------------------------------------------------------- certify --
 __device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
     return (a < b) || (a == b && ia < ib);
@@ -217,13 +545,16 @@ template <int KP>
 __global__ __launch_bounds__(256) void knn_certify_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
-    const unsigned int* __restrict__ mnorm_bits, int32_t* __restrict__ out_idx,
-    double* __restrict__ out_dist, int* __restrict__ fail_list, int* __restrict__ fail_count) {
+    const double* __restrict__ inv_scale2, double err_ulps, const int* __restrict__ perm,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_dist, int* __restrict__ fail_list,
+    int* __restrict__ fail_count) {
     const int lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= n) return;
+    const int qs = blockIdx.x * 4 + (threadIdx.x >> 6);  // screening order
+    if (qs >= n) return;
+    const int q = perm ? perm[qs] : qs;                   // bootstrap row
     const double* x = rows + (int64_t)q * d;
-    int j = (lane < 2 * KP) ? cand_idx[(int64_t)q * 2 * KP + lane] : -1;
+    int j = (lane < 2 * KP) ? cand_idx[(int64_t)qs * 2 * KP + lane] : -1;
+    if (j >= 0 && perm) j = perm[j];
     double key = INFINITY;
     int id = 0x7fffffff - 64 + lane;  // distinct padding ids sort after real ones
     if (j >= 0) {
@@ -235,8 +566,8 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     // certification (wave-uniform values)
     double nq = 0.0;
     for (int k = 0; k < d; ++k) nq += x[k] * x[k];
-    const float t0 = cand_thr[(int64_t)q * 2 + 0];
-    const float t1 = cand_thr[(int64_t)q * 2 + 1];
+    const float t0 = cand_thr[(int64_t)qs * 2 + 0];
+    const float t1 = cand_thr[(int64_t)qs * 2 + 1];
     const float tmax = fmaxf(t0, t1);
     const double dK = __shfl(key, kmax - 1, 64);
     const int idK = __shfl(id, kmax - 1, 64);
@@ -248,10 +579,9 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
         // d2 at most dK + E.  excl > dK + E therefore proves it is farther
         // (independent of the largest norm in the data).
         const double s = 2.0 * sqrt(nq) + sqrt(dK);
-        const double E = KNN_ERR_ULPS * 0x1p-24 * s * s + 1e-300;
-        const double excl = nq - 2.0 * (double)tmax;
+        const double E = err_ulps * 0x1p-24 * s * s + 1e-300;
+        const double excl = nq - 2.0 * (double)tmax * (*inv_scale2);  // thresholds are in scaled units
         ok = ok && (excl - E > dK);
-        (void)mnorm_bits;
     }
     if (ok) {
         if (lane < kmax) {
@@ -429,34 +759,97 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
     CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
                 "ccg_knn_rows_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    const int KS = pick_ks(d);
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
-    const int64_t npad = ccg_cdiv(n, 32) * 32;
-    float* refs = (float*)ccg_ws(ctx, WS_REFS32, sizeof(float) * npad * 2 * KS);
+    const bool f32path = getenv("CCG_KNN_F32") != nullptr;  // A/B switch for the fp32-MFMA screen
     int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * n * 2 * KP);
     float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * n * 2);
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
-    if (!refs || !cand_idx || !cand_thr || !fail_list || !misc) return CCG_ENOMEM;
-    unsigned int* mnorm = misc;
+    if (!cand_idx || !cand_thr || !fail_list || !misc) return CCG_ENOMEM;
+    // misc: [0] max-norm / max|x| bits, [1] fail count, [2..3] double 1/sigma^2
+    unsigned int* mbits = misc;
     int* fail_count = (int*)(misc + 1);
-    CCG_HIP(hipMemsetAsync(misc, 0, 8, st));
-
+    double* inv_scale2 = (double*)(misc + 2);
+    CCG_HIP(hipMemsetAsync(misc, 0, 16, st));
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
-    knn_prep_kernel<<<(unsigned)ccg_cdiv(npad, 256), 256, 0, st>>>(rows, n, npad, d, KS, refs, mnorm);
-    const int ntiles = (int)(npad / 32);
-    const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
-    int rc = (KP == KNN_KP)
-                 ? screen_dispatch<KNN_KP>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st)
-                 : screen_dispatch<KNN_KP_BIG>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st);
-    ccg_timer_stop(ctx, t_scr, st);
+    int rc = CCG_OK;
+    double err_ulps;
+    int* order_perm = nullptr;  // screening order -> bootstrap row (identity on the fp32 path)
+    if (f32path) {
+        const int KS = pick_ks(d);
+        const int64_t npad = ccg_cdiv(n, 32) * 32;
+        float* refs = (float*)ccg_ws(ctx, WS_REFS32, sizeof(float) * npad * 2 * KS);
+        if (!refs) return CCG_ENOMEM;
+        const double one = 1.0;
+        CCG_HIP(hipMemcpyAsync(inv_scale2, &one, sizeof(double), hipMemcpyHostToDevice, st));
+        knn_prep_kernel<<<(unsigned)ccg_cdiv(npad, 256), 256, 0, st>>>(rows, n, npad, d, KS, refs, mbits);
+        const int ntiles = (int)(npad / 32);
+        const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
+        rc = (KP == KNN_KP) ? screen_dispatch<KNN_KP>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st)
+                            : screen_dispatch<KNN_KP_BIG>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st);
+        ccg_timer_stop(ctx, t_scr, st);
+        err_ulps = KNN_ERR_ULPS;
+    } else {
+        const int KSTEPS = d <= 16 ? 1 : (d <= 32 ? 2 : 4);
+        const int64_t npad = ccg_cdiv(n, KNN_CHUNK) * KNN_CHUNK;
+        uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
+        if (!img) return CCG_ENOMEM;
+        float* nrm = (float*)((char*)img + (size_t)npad * 64 * KSTEPS);
+        knn_maxabs_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 256), 1024), 256, 0, st>>>(rows, n * d,
+                                                                                                 mbits);
+        // spatial order: Morton buckets of the leading coordinates
+        const int64_t NB = 1LL << (3 * KNN_MORTON_BITS);
+        int64_t* hist = (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
+        if (!hist) return CCG_ENOMEM;
+        int64_t* cursor = hist + (NB + 1);
+        order_perm = (int*)(cursor + (NB + 1));
+        unsigned* bnd = misc + 8;
+        CCG_HIP(hipMemsetAsync(bnd, 0xff, 3 * sizeof(unsigned), st));
+        CCG_HIP(hipMemsetAsync(bnd + 3, 0, 3 * sizeof(unsigned), st));
+        CCG_HIP(hipMemsetAsync(hist, 0, sizeof(int64_t) * (NB + 1), st));
+        knn_bounds_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 256), 512), 256, 0, st>>>(rows, n, d, bnd);
+        knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
+        rc = ccg_scan_i64(ctx, hist, hist, NB, st);
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(cursor, hist, sizeof(int64_t) * (NB + 1), hipMemcpyDeviceToDevice, st));
+        knn_bucket_scatter_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, cursor, order_perm);
+        const unsigned pg = (unsigned)ccg_cdiv(npad, 256);
+        if (KSTEPS == 1)
+            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+        else if (KSTEPS == 2)
+            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+        else
+            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+        const int nch = (int)(npad / KNN_CHUNK);
+        const unsigned grid = (unsigned)ccg_cdiv(n, KNN_QPB);
+        const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
+#define CCG_SCREEN16(KS_, KP_) \
+    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr)
+        const char* exp_env = getenv("CCG_KNN_EXP");
+        if (exp_env && atoi(exp_env) == 1 && KSTEPS == 2 && KP == KNN_KP) {
+            knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+        } else if (KP == KNN_KP) {
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
+            else CCG_SCREEN16(4, KNN_KP);
+        } else {
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG);
+            else CCG_SCREEN16(4, KNN_KP_BIG);
+        }
+#undef CCG_SCREEN16
+        ccg_timer_stop(ctx, t_scr, st);
+        err_ulps = KNN_ERR_ULPS_F16;
+    }
     if (rc) return rc;
     if (KP == KNN_KP)
         knn_certify_kernel<KNN_KP><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
-            rows, (int)n, d, kmax, cand_idx, cand_thr, mnorm, out_idx, out_dist, fail_list, fail_count);
+            rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist,
+            fail_list, fail_count);
     else
         knn_certify_kernel<KNN_KP_BIG><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
-            rows, (int)n, d, kmax, cand_idx, cand_thr, mnorm, out_idx, out_dist, fail_list, fail_count);
+            rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist,
+            fail_list, fail_count);
     if (d <= 16)
         knn_fallback_kernel<16><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
                                                      out_dist);

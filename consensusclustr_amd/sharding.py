@@ -49,19 +49,31 @@ def boot_shard(nboots, G, rank):
 
 
 def allgather_columns(local_cols, group=None):
-    """All-gather each rank's (b_local x N) uint8 assignment columns.
+    """All-gather every rank's (b_r x N) uint8 assignment columns.
 
-    Every rank must hold the same b_local (weak scaling: fixed bootstraps per
-    GPU).  Returns the (G*b_local x N) matrix with rank r's columns at rows
-    [r*b_local, (r+1)*b_local) -- the column-major B x N layout of the C ABI.
+    Returns the (sum_r b_r x N) matrix with rank r's columns after rank r-1's
+    -- the column-major B x N layout of the C ABI.  Equal b_r (weak scaling:
+    fixed bootstraps per GPU) is one all_gather_into_tensor; unequal counts
+    are padded to the largest and trimmed.
     """
     import torch
     import torch.distributed as dist
     G = dist.get_world_size(group)
-    out = torch.empty((G * local_cols.shape[0],) + tuple(local_cols.shape[1:]), dtype=local_cols.dtype,
-                      device=local_cols.device)
-    dist.all_gather_into_tensor(out, local_cols.contiguous(), group=group)
-    return out
+    b = torch.tensor([local_cols.shape[0]], dtype=torch.int64, device=local_cols.device)
+    sizes = [torch.zeros_like(b) for _ in range(G)]
+    dist.all_gather(sizes, b, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    bmax = max(sizes)
+    tail = tuple(local_cols.shape[1:])
+    src = local_cols.contiguous()
+    if src.shape[0] < bmax:
+        pad = torch.zeros((bmax - src.shape[0],) + tail, dtype=src.dtype, device=src.device)
+        src = torch.cat([src, pad])
+    out = torch.empty((G * bmax,) + tail, dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    if all(s == bmax for s in sizes):
+        return out
+    return torch.cat([out[r * bmax:r * bmax + sizes[r]] for r in range(G)])
 
 
 def gather_slabs_host(parts, N):
@@ -69,3 +81,21 @@ def gather_slabs_host(parts, N):
     full = np.concatenate(parts)
     assert full.size == N * (N - 1) // 2
     return full
+
+
+def sharded_cocluster(local_cols, N, slab_fn, group=None):
+    """One rank's part of the multi-GPU co-clustering step.
+
+    local_cols: this rank's (b_local x N) uint8 assignment columns (tensor);
+    slab_fn(A, r0, r1) computes and returns this rank's packed slab of rows
+    [r0, r1) from the full (G*b_local x N) matrix A (the engine's
+    cocluster_t on the GPU; a CPU function in tests).  Returns
+    (slab, (r0, r1), A).
+    """
+    import torch.distributed as dist
+    G = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    A = allgather_columns(local_cols, group) if G > 1 else local_cols
+    cuts = row_slabs(N, G)
+    r0, r1 = cuts[rank], cuts[rank + 1]
+    return slab_fn(A, r0, r1), (r0, r1), A

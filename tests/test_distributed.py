@@ -1,0 +1,20 @@
+"""Multi-rank sharding on CPU with gloo (world_size 2 and 3)."""
+import os
+import random
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_cocluster_matches_single_process(tmp_path, world):
+    out = tmp_path / "ok.txt"
+    port = random.randint(20000, 40000)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "_dist_worker.py"), str(world), str(port), str(out)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert out.read_text() == "ok"

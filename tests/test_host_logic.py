@@ -1,0 +1,90 @@
+"""Host-side logic of the drop-in (no GPU): selection rules, map-back,
+assignment matrix, sharding arithmetic and the host clustering stand-in."""
+import numpy as np
+import pytest
+
+import oracle as O
+from consensusclustr_amd import consensus as C
+from consensusclustr_amd.cluster_host import louvain
+from consensusclustr_amd.sharding import boot_shard, row_slabs, slab_offset, slab_pairs
+
+
+def test_selection_rules_match_kat_and_oracle(kat):
+    for scores, want in kat["robust_choice"]["cases"]:
+        assert C.robust_choice(scores) == want == O.robust_choice(scores)
+    for scores, want in kat["consensus_choice"]["cases"]:
+        assert C.consensus_choice(scores) == want == O.consensus_choice(scores)
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        s = rng.integers(0, 4, 12).astype(float) / 4
+        if rng.random() < 0.2:
+            s[rng.integers(0, 12)] = np.nan
+        assert C.robust_choice(s) == O.robust_choice(s)
+        assert C.consensus_choice(s) == O.consensus_choice(s)
+
+
+def test_robust_score_rules():
+    # :663-670 with minSize: >1 cluster & min size > minSize -> silhouette; 1 cluster -> 0; small -> 0.15
+    s = C.robust_scores([0.3, 0.4, 0.5], [3, 1, 4], [10, 100, 2], minSize=5)
+    assert s.tolist() == [0.3, 0.0, 0.15]
+    assert C.robust_scores([0.7], [1], [50])[0] == 0.0
+
+
+def test_mapback_first_copy_and_na():
+    rng = np.random.default_rng(1)
+    N, n = 200, 180
+    idx = rng.integers(0, N, n).astype(np.int32)
+    lab = rng.integers(1, 9, n).astype(np.int32)
+    got = C.mapback(idx, lab, N)
+    assert np.array_equal(got, O.mapback(idx, lab, N))
+    assert (got[np.setdiff1d(np.arange(N), idx)] == -1).all()
+
+
+def test_assignment_matrix():
+    cols = [np.array([1, -1, 3]), np.array([[2, 1], [-1, 5], [4, 4]])]
+    A = C.assignment_matrix(cols)
+    assert A.dtype == np.uint8 and A.shape == (3, 3)
+    assert A.tolist() == [[1, 0, 3], [2, 0, 4], [1, 5, 4]]
+    with pytest.raises(ValueError):
+        C.assignment_matrix([np.array([1, 300])])
+
+
+@pytest.mark.parametrize("N,G", [(100000, 8), (100000, 2), (250000, 8), (1000, 4), (130, 8)])
+def test_row_slabs_partition_and_balance(N, G):
+    cuts = row_slabs(N, G)
+    assert cuts[0] == 0 and cuts[-1] == N and all(a <= b for a, b in zip(cuts, cuts[1:]))
+    assert all(c % 128 == 0 for c in cuts[1:-1])
+    P = N * (N - 1) // 2
+    pairs = [slab_pairs(N, cuts[g], cuts[g + 1]) for g in range(G)]
+    assert sum(pairs) == P
+    assert slab_offset(N, cuts[-1]) == P
+    if N >= 100000:
+        assert max(pairs) / (P / G) < 1.02
+
+
+def test_boot_shard_covers():
+    for nb, G in [(1000, 8), (10, 3), (5, 8)]:
+        spans = [boot_shard(nb, G, r) for r in range(G)]
+        assert spans[0][0] == 0 and spans[-1][1] == nb
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_bootstrap_indices():
+    b = C.bootstrap_indices(1000, 3, 0.9, seed=123)
+    assert b.shape == (3, 900) and b.dtype == np.int32
+    assert np.array_equal(b, C.bootstrap_indices(1000, 3, 0.9, seed=123))
+    assert b.min() >= 0 and b.max() < 1000
+
+
+def test_louvain_recovers_two_cliques():
+    ei, ej = [], []
+    for base in (0, 10):
+        for a in range(10):
+            for b in range(a + 1, 10):
+                ei.append(base + a)
+                ej.append(base + b)
+    ei.append(0)
+    ej.append(10)
+    lab = louvain(20, np.array(ei), np.array(ej), np.ones(len(ei)), resolution=1.0, seed=0)
+    assert len(set(lab[:10])) == 1 and len(set(lab[10:])) == 1 and lab[0] != lab[10]
+    assert lab.min() == 1
