@@ -160,30 +160,58 @@ __device__ __forceinline__ double graph_weight(const SnnSpec& sp, unsigned v, in
 }
 
 // ---------------------------------------------------------------- wave path --
-// Pass 1 (EMIT=false): per-graph partner counts cnt[t][j]; overflow rows are
-// appended to ov_list.  Pass 2 (EMIT=true): emit at off[t][j].
-template <bool EMIT>
-__global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_kernel(
+// Pass 1 (build): one wave per node builds a 2048-slot LDS hash table of
+// 64-bit slots (partner p << 32 | packed per-graph values): a new partner
+// costs one CAS, a repeat one add.  The table is compacted, bitonic-sorted by
+// p and parked in a fixed-capacity scratch row; per-graph edge counts go to
+// cnt[t][j].  Nodes with more than SNN_WCAP partners go to the overflow list.
+// Pass 2 (emit) streams the sorted rows into the caller's edge arrays.
+#define SNN_WCAP (SNN_WT * 3 / 4)
+#define SNN_EMPTY64 (~0ull)
+
+__device__ __forceinline__ bool table_insert64(unsigned long long* tab, int p, unsigned c, const SnnSpec& sp,
+                                               int bits, int T) {
+    unsigned s = snn_hash(p, bits);
+    const unsigned long long want = ((unsigned long long)(unsigned)p << 32) | c;
+    for (int probe = 0; probe < T; ++probe) {
+        unsigned long long cur = __hip_atomic_load(&tab[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == SNN_EMPTY64) {
+            const unsigned long long old = atomicCAS(&tab[s], SNN_EMPTY64, want);
+            if (old == SNN_EMPTY64) return true;
+            cur = old;
+        }
+        if ((unsigned)(cur >> 32) == (unsigned)p) {
+            if (sp.type == CCG_SNN_NUMBER) {
+                atomicAdd(&tab[s], (unsigned long long)c);  // per-byte counts never carry
+            } else {
+                while (true) {
+                    const unsigned nv = bytewise_min((unsigned)cur, c);
+                    if (nv == (unsigned)cur) break;
+                    const unsigned long long nw = (cur & 0xFFFFFFFF00000000ull) | nv;
+                    const unsigned long long old = atomicCAS(&tab[s], cur, nw);
+                    if (old == cur) break;
+                    cur = old;
+                }
+            }
+            return true;
+        }
+        s = (s + 1) & (T - 1);
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
     const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
-    int* __restrict__ ov_list, int* __restrict__ ov_count, const int* __restrict__ ov_flag, SnnOut out) {
-    __shared__ int keys_all[SNN_WAVES][SNN_WT];
-    __shared__ unsigned vals_all[SNN_WAVES][SNN_WT];
-    __shared__ int count_all[SNN_WAVES];
+    int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
+    int* __restrict__ ucount) {
+    __shared__ unsigned long long tab_all[SNN_WAVES][SNN_WT];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int* keys = keys_all[wv];
-    unsigned* vals = vals_all[wv];
-    int* count = &count_all[wv];
+    unsigned long long* tab = tab_all[wv];
     const int kmax = sp.kk[sp.nk - 1];
     constexpr int BITS = 11;  // log2(SNN_WT)
-    const int cap_entries = SNN_WT * 3 / 4;
     for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
-        if (EMIT && ov_flag[j]) continue;  // handled by the overflow paths
-        for (int s = lane; s < SNN_WT; s += 64) {
-            keys[s] = SNN_EMPTY;
-            vals[s] = sp.init;
-        }
-        if (lane == 0) *count = 0;
+        for (int s = lane; s < SNN_WT; s += 64) tab[s] = SNN_EMPTY64;
         WAVE_LDS_SYNC();
         bool full = false;
         for (int i = 0; i <= kmax && !full; ++i) {
@@ -205,100 +233,102 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_kernel(
                     }
                     if (p > j) {
                         const unsigned c = snn_contrib(sp, i, rp);
-                        if (c != sp.init) ok = table_insert<SNN_WT>(keys, vals, count, p, c, sp, BITS);
+                        if (c != sp.init) ok = table_insert64(tab, p, c, sp, BITS, SNN_WT);
                     }
                 }
-                WAVE_LDS_SYNC();
-                full = __any(!ok) || (*count > cap_entries);
+                full = __any(!ok);
                 if (full) break;
             }
         }
-        if (full) {
-            if (!EMIT && lane == 0) {
+        WAVE_LDS_SYNC();
+        // compact in place (destination index <= source slot)
+        int u = 0;
+        if (!full) {
+            for (int s0 = 0; s0 < SNN_WT; s0 += 64) {
+                const unsigned long long e = tab[s0 + lane];
+                const bool occ = e != SNN_EMPTY64;
+                const unsigned long long m = __ballot(occ);
+                WAVE_LDS_SYNC();
+                if (occ) tab[u + __popcll(m & lanemask_lt())] = e;
+                u += __popcll(m);
+                WAVE_LDS_SYNC();
+            }
+        }
+        if (full || u > SNN_WCAP) {
+            if (lane == 0) {
                 const int q = atomicAdd(ov_count, 1);
                 ov_list[q] = (int)j;
             }
             continue;
         }
-        if (!EMIT) {
-            int64_t c[SNN_MAXK] = {0, 0, 0, 0};
-            for (int s = lane; s < SNN_WT; s += 64)
-                if (keys[s] != SNN_EMPTY) {
-                    const unsigned v = vals[s];
-#pragma unroll
-                    for (int t = 0; t < SNN_MAXK; ++t)
-                        if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
-                }
-#pragma unroll
-            for (int t = 0; t < SNN_MAXK; ++t) {
-                int64_t v = c[t];
-                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
-            }
-            WAVE_LDS_SYNC();
-            continue;
-        }
-        // ---- pass 2: compact in place (dest index <= source slot), sort, emit
-        int u = 0;
-        for (int s0 = 0; s0 < SNN_WT; s0 += 64) {
-            const int k = keys[s0 + lane];
-            const unsigned v = vals[s0 + lane];
-            const bool occ = k != SNN_EMPTY;
-            const unsigned long long m = __ballot(occ);
-            WAVE_LDS_SYNC();
-            if (occ) {
-                const int dst = u + __popcll(m & lanemask_lt());
-                keys[dst] = k;
-                vals[dst] = v;
-            }
-            u += __popcll(m);
-            WAVE_LDS_SYNC();
-        }
         int P = 64;
         while (P < u) P <<= 1;
-        for (int s = u + lane; s < P; s += 64) keys[s] = 0x7fffffff;
+        for (int s = u + lane; s < P; s += 64) tab[s] = SNN_EMPTY64;
         WAVE_LDS_SYNC();
         for (int kk = 2; kk <= P; kk <<= 1) {
             for (int jj = kk >> 1; jj > 0; jj >>= 1) {
                 for (int i = lane; i < P; i += 64) {
                     const int l = i ^ jj;
                     if (l > i) {
-                        const int a = keys[i], b = keys[l];
-                        const bool up = (i & kk) == 0;
-                        if ((a > b) == up) {
-                            keys[i] = b;
-                            keys[l] = a;
-                            const unsigned va = vals[i];
-                            vals[i] = vals[l];
-                            vals[l] = va;
+                        const unsigned long long x = tab[i], y = tab[l];
+                        if ((x > y) == ((i & kk) == 0)) {
+                            tab[i] = y;
+                            tab[l] = x;
                         }
                     }
                 }
                 WAVE_LDS_SYNC();
             }
         }
+        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+        unsigned long long* dst = scratch + j * SNN_WCAP;
+        for (int c = lane; c < u; c += 64) {
+            const unsigned long long e = tab[c];
+            dst[c] = e;
+            const unsigned v = (unsigned)e;
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t)
+                if (t < sp.nk && graph_has(sp, v, t)) ++c4[t];
+        }
 #pragma unroll
         for (int t = 0; t < SNN_MAXK; ++t) {
-            if (t >= sp.nk) break;
-            int64_t e = cnt[(int64_t)t * (n + 1) + j];
+            int64_t v = c4[t];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
+        }
+        if (lane == 0) ucount[j] = u;
+        WAVE_LDS_SYNC();
+    }
+}
+
+__global__ __launch_bounds__(256) void snn_wave_emit_kernel(int64_t n, SnnSpec sp, const int64_t* __restrict__ off,
+                                                            const int* __restrict__ ov_flag,
+                                                            const unsigned long long* __restrict__ scratch,
+                                                            const int* __restrict__ ucount, SnnOut out) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+        if (ov_flag[j]) continue;
+        const int u = ucount[j];
+        const unsigned long long* src = scratch + j * SNN_WCAP;
+        for (int t = 0; t < sp.nk; ++t) {
+            int64_t e = off[(int64_t)t * (n + 1) + j];
             for (int c0 = 0; c0 < u; c0 += 64) {
                 const int c = c0 + lane;
-                const bool in = c < u;
-                const unsigned v = in ? vals[c] : sp.init;
-                const bool has = in && graph_has(sp, v, t);
+                const unsigned long long x = c < u ? src[c] : 0ull;
+                const unsigned v = (unsigned)x;
+                const bool has = c < u && graph_has(sp, v, t);
                 const unsigned long long m = __ballot(has);
                 if (has) {
                     const int64_t pos = e + __popcll(m & lanemask_lt());
                     if (pos < out.cap[t]) {
                         out.oi[t][pos] = (int32_t)j;
-                        out.oj[t][pos] = keys[c];
+                        out.oj[t][pos] = (int32_t)(x >> 32);
                         out.ow[t][pos] = graph_weight(sp, v, t);
                     }
                 }
                 e += __popcll(m);
             }
         }
-        WAVE_LDS_SYNC();
     }
 }
 
@@ -600,7 +630,10 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * nk * (n + 1));
     int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (4 * n + 64));
     unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
-    if (!hoff || !hosts || !cnt || !ov || !dense) return CCG_ENOMEM;
+    unsigned long long* scratch =
+        (unsigned long long*)ccg_ws(ctx, WS_SNN_F, sizeof(unsigned long long) * n * SNN_WCAP + sizeof(int) * (n + 64));
+    if (!hoff || !hosts || !cnt || !ov || !dense || !scratch) return CCG_ENOMEM;
+    int* ucount = (int*)(scratch + n * SNN_WCAP);
     unsigned long long* cursor = (unsigned long long*)(hoff + (n + 1));
     int* err = (int*)(hoff + 2 * (n + 1));
     int* ov_list = ov;
@@ -623,8 +656,8 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     snn_fill_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, cursor, hosts);
     const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
     // pass 1: per-graph counts (wave tables, then block tables, then dense)
-    snn_wave_kernel<false><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
-                                                           ov_count, flag1, out);
+    snn_wave_build_kernel<<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
+                                                           ov_count, scratch, ucount);
     snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
                                                  ov2_list, ov2_count, flag2, out);
     snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
@@ -638,8 +671,8 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     bool any_cap = false;
     for (int t = 0; t < nk; ++t) any_cap |= out.cap[t] > 0;
     if (any_cap) {
-        snn_wave_kernel<true><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
-                                                              ov_count, flag1, out);
+        snn_wave_emit_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(
+            n, sp, cnt, flag1, scratch, ucount, out);
         snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
                                                     ov2_list, ov2_count, flag2, out);
         snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
