@@ -32,6 +32,8 @@ enum ccg_ws_slot {
     WS_HOST_E,       // host-API staging 5
     WS_SCAN,         // scan block sums
     WS_ORDER,        // kNN spatial ordering (bucket histogram, permutation)
+    WS_FB_D,         // kNN fallback per-range lists (keys)
+    WS_FB_I,         // kNN fallback per-range lists (ids)
     WS_NSLOTS
 };
 

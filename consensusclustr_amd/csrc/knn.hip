@@ -30,6 +30,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_KP_BIG 32      // ... for 20 < kmax <= 32 (2*KP <= 64 lanes in certify)
 #define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
 #define KNN_FB_K 32        // fallback list length (>= kmax)
+#define KNN_FB_S 64        // max reference ranges per failed row
+#define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
 
 // Relative error budget of the fp32 screen in units of the fp32 ulp (2^-24)
 // times (|x| + max|y|)^2; see DESIGN.md "kNN certification bound".
@@ -337,6 +339,16 @@ __device__ __forceinline__ int knn_chunk_at(int k, int c0, int Lc, int Rc, int M
     return Rc > Lc ? c0 + Mc + m : c0 - Mc - m;
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// 4 MB L2).  Give XCD x a contiguous range of query blocks: neighbouring
+// blocks scan nearly the same chunk sequence a few steps apart, so each
+// staged chunk is fetched into an XCD's L2 once and re-read from there.
+// A bijection on [0, G) for any G; only speed depends on it.
+__device__ __forceinline__ int xcd_block(int bid, int G) {
+    const int q = G >> 3, r = G & 7, x = bid & 7, i = bid >> 3;
+    return x * q + min(x, r) + i;
+}
+
 template <int KSTEPS, int KP, int EXP = 0>
 __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restrict__ img,
                                                            const float* __restrict__ nrm, int n, int nchunks,
@@ -355,7 +367,8 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
     __shared__ uint2 qbuf[4][KNN_QCAP][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
-    const int q0 = blockIdx.x * KNN_QPB + wave * 32;
+    const int bx = xcd_block(blockIdx.x, gridDim.x);
+    const int q0 = bx * KNN_QPB + wave * 32;
     const int q = q0 + col;
     const int qrow = q < n ? q : n - 1;
 
@@ -409,7 +422,7 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
     // block's own position: near neighbours arrive first, the threshold tightens
     // within a few tiles and later tiles rarely insert (the order only changes
     // speed; certification makes the result exact for any order).
-    const int c0 = min((int)(blockIdx.x * KNN_QPB) / KNN_CHUNK, nchunks - 1);
+    const int c0 = min((int)(bx * KNN_QPB) / KNN_CHUNK, nchunks - 1);
     const int Lc = c0, Rc = nchunks - 1 - c0, Mc = min(Lc, Rc);
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
     float T = -INFINITY;  // max of both halves' thresholds (see below)
@@ -595,21 +608,34 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
 }
 
 // ------------------------------------------------------------- fallback --
-// One 256-thread block per failed row: each thread scans refs j = tid + 256t
-// with the query held in registers (exact fp64, unfused, dimension order),
-// keeping a sorted list; each wave merges its 64 lists by k rounds of wave
-// arg-min into LDS, then wave 0 merges the 4 wave lists.
+// Exact fp64 search for the rows certification could not prove.  Each failed
+// row is split over S reference ranges (S chosen on the device so that
+// nfail * S lists fit the scratch); one 256-thread block per (row, range)
+// scans its range with the query in registers (unfused, dimension order),
+// each thread keeping a sorted list, then merges 64 lists per wave by wave
+// arg-min and the 4 wave lists into one sorted top-kmax list in scratch.
+// knn_fallback_merge_kernel merges the S lists of each row.
+__device__ __forceinline__ int knn_fb_splits(int nfail, int slots) {
+    if (nfail <= 0) return 1;
+    int S = slots / nfail;
+    return S < 1 ? 1 : (S > KNN_FB_S ? KNN_FB_S : S);
+}
+
 template <int DMAX>
 __global__ __launch_bounds__(256) void knn_fallback_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
-    const int* __restrict__ fail_list, const int* __restrict__ fail_count,
-    int32_t* __restrict__ out_idx, double* __restrict__ out_dist) {
+    const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
+    double* __restrict__ lst_d, int* __restrict__ lst_i) {
     __shared__ double sd[4][KNN_FB_K];
     __shared__ int si[4][KNN_FB_K];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nfail = *fail_count;
-    for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
+    const int S = knn_fb_splits(nfail, slots);
+    const int span = (n + S - 1) / S;
+    for (int64_t w = blockIdx.x; w < (int64_t)nfail * S; w += gridDim.x) {
+        const int f = (int)(w / S), sp = (int)(w - (int64_t)f * S);
         const int q = fail_list[f];
+        const int j0 = sp * span, j1 = min(n, j0 + span);
         double xq[DMAX];
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
@@ -620,7 +646,7 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
             lv[t] = INFINITY;
             li[t] = 0x7fffffff;
         }
-        for (int j = threadIdx.x; j < n; j += 256) {
+        for (int j = j0 + threadIdx.x; j < j1; j += 256) {
             const double* y = rows + (int64_t)j * d;
             double yv[DMAX];
 #pragma unroll
@@ -663,7 +689,7 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                 sd[wv][r] = bk;
                 si[wv][r] = bi;
             }
-            if (li[0] == bi) {  // the winning thread pops its head (ids are unique)
+            if (bi != 0x7fffffff && li[0] == bi) {  // the winning thread pops its head (ids are unique)
 #pragma unroll
                 for (int t = 0; t < KNN_FB_K - 1; ++t) {
                     lv[t] = lv[t + 1];
@@ -677,6 +703,8 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
         if (wv == 0) {
             // lanes 0..3 walk the 4 wave lists; k rounds of arg-min over heads
             int pos = 0;
+            double* od = lst_d + w * KNN_FB_K;
+            int* oi_ = lst_i + w * KNN_FB_K;
             for (int r = 0; r < kmax; ++r) {
                 double bk = INFINITY;
                 int bi = 0x7fffffff;
@@ -696,13 +724,53 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                     }
                 }
                 if (lane == 0) {
-                    out_idx[(int64_t)q * kmax + r] = bi;
-                    if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+                    od[r] = bk;
+                    oi_[r] = bi;
                 }
                 if (lane < 4 && mi == bi && mk == bk) ++pos;
             }
         }
         __syncthreads();
+    }
+}
+
+// One wave per failed row: lane s walks the sorted list of range s.
+__global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
+    int kmax, const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
+    const double* __restrict__ lst_d, const int* __restrict__ lst_i,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_dist) {
+    const int lane = threadIdx.x;
+    const int nfail = *fail_count;
+    const int S = knn_fb_splits(nfail, slots);
+    for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
+        const int q = fail_list[f];
+        const double* ld = lst_d + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
+        const int* li = lst_i + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
+        int pos = 0;
+        for (int r = 0; r < kmax; ++r) {
+            double bk = INFINITY;
+            int bi = 0x7fffffff;
+            if (lane < S && pos < kmax) {
+                bk = ld[pos];
+                bi = li[pos];
+            }
+            const double mk = bk;
+            const int mi = bi;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                double ok = __shfl_xor(bk, o, 64);
+                int oi = __shfl_xor(bi, o, 64);
+                if (key_less(ok, oi, bk, bi)) {
+                    bk = ok;
+                    bi = oi;
+                }
+            }
+            if (lane == 0) {
+                out_idx[(int64_t)q * kmax + r] = bi;
+                if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+            }
+            if (lane < S && mi == bi && mk == bk) ++pos;
+        }
     }
 }
 
@@ -850,15 +918,21 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         knn_certify_kernel<KNN_KP_BIG><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
             rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist,
             fail_list, fail_count);
+    const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
+    double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
+    int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
+    if (!fb_d || !fb_i) return CCG_ENOMEM;
     if (d <= 16)
-        knn_fallback_kernel<16><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
-                                                     out_dist);
+        knn_fallback_kernel<16><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
+                                                      fb_d, fb_i);
     else if (d <= 32)
-        knn_fallback_kernel<32><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
-                                                     out_dist);
+        knn_fallback_kernel<32><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
+                                                      fb_d, fb_i);
     else
-        knn_fallback_kernel<64><<<512, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, out_idx,
-                                                     out_dist);
+        knn_fallback_kernel<64><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
+                                                      fb_d, fb_i);
+    knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
+                                                   out_dist);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {

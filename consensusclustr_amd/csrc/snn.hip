@@ -206,6 +206,9 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
     int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
     int* __restrict__ ucount) {
     __shared__ unsigned long long tab_all[SNN_WAVES][SNN_WT];
+    __shared__ int m_pre[SNN_WAVES][65];
+    __shared__ long long m_h0[SNN_WAVES][64];
+    __shared__ int m_cur[SNN_WAVES][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned long long* tab = tab_all[wv];
     const int kmax = sp.kk[sp.nk - 1];
@@ -213,32 +216,67 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
     for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
         for (int s = lane; s < SNN_WT; s += 64) tab[s] = SNN_EMPTY64;
         WAVE_LDS_SYNC();
-        bool full = false;
-        for (int i = 0; i <= kmax && !full; ++i) {
-            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
-            const int64_t h0 = hoff[cur];
-            const int64_t len = hoff[cur + 1] - h0 + 1;  // hosts + cur itself
-            for (int64_t o0 = 0; o0 < len; o0 += 64) {
-                const int64_t o = o0 + lane;
-                bool ok = true;
-                if (o < len) {
-                    int p, rp;
-                    if (o == len - 1) {
-                        p = cur;
-                        rp = 0;
-                    } else {
-                        const int2 hr = hosts[h0 + o];
-                        p = hr.x;
-                        rp = hr.y;
-                    }
-                    if (p > j) {
-                        const unsigned c = snn_contrib(sp, i, rp);
-                        if (c != sp.init) ok = table_insert64(tab, p, c, sp, BITS, SNN_WT);
-                    }
+        // Flat gather: item t of M = sum over members i of (|hosts(cur_i)| + 1)
+        // (the +1 is cur_i itself, rank 0).  Member headers are loaded
+        // lane-parallel once; host entries are fetched one round ahead so
+        // their latency hides behind the current round's LDS inserts.
+        int mcur = 0, mlen = 0;
+        long long mh0 = 0;
+        if (lane <= kmax) {
+            mcur = lane == 0 ? (int)j : knn[j * kstride + lane - 1];
+            mh0 = hoff[mcur];
+            mlen = (int)(hoff[mcur + 1] - mh0) + 1;
+        }
+        int incl = mlen;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int M = __shfl(incl, 63);
+        int* pre = m_pre[wv];
+        long long* mh = m_h0[wv];
+        int* mc = m_cur[wv];
+        if (lane <= kmax) {
+            pre[lane] = incl - mlen;
+            mh[lane] = mh0;
+            mc[lane] = mcur;
+        }
+        if (lane == 0) pre[kmax + 1] = M;
+        WAVE_LDS_SYNC();
+        int mi = 0;
+        auto fetch = [&](int t, int& p, int& rp, int& ii) {
+            p = -1;
+            rp = 0;
+            ii = 0;
+            if (t < M) {
+                while (pre[mi + 1] <= t) ++mi;
+                ii = mi;
+                if (t == pre[mi + 1] - 1) {
+                    p = mc[mi];
+                } else {
+                    const int2 hr = hosts[mh[mi] + (t - pre[mi])];
+                    p = hr.x;
+                    rp = hr.y;
                 }
-                full = __any(!ok);
-                if (full) break;
             }
+        };
+        int p, rp, ii;
+        fetch(lane, p, rp, ii);
+        bool full = false;
+        for (int t0 = 0; t0 < M; t0 += 64) {
+            int np, nrp, nii;
+            fetch(t0 + 64 + lane, np, nrp, nii);
+            bool ok = true;
+            if (p > j) {
+                const unsigned c = snn_contrib(sp, ii, rp);
+                if (c != sp.init) ok = table_insert64(tab, p, c, sp, BITS, SNN_WT);
+            }
+            full = __any(!ok);
+            if (full) break;
+            p = np;
+            rp = nrp;
+            ii = nii;
         }
         WAVE_LDS_SYNC();
         // compact in place (destination index <= source slot)
