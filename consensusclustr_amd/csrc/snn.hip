@@ -21,6 +21,7 @@
 // scratch.  Nodes with more partners than the wave table holds use a
 // 256-thread table of 16K slots; beyond that an exact O(n) dense path.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ccg_internal.h"
 
@@ -200,13 +201,71 @@ __device__ __forceinline__ bool table_insert64(unsigned long long* tab, int p, u
     return false;
 }
 
+// Sort a node's u compacted entries (tab[0..u), distinct partners p in (j, n))
+// by p and store them to dst[0..u).  Each lane holds entries c = r*64 + lane
+// in registers; a 128-bucket split on p (monotone in p) gives every entry its
+// bucket's start by a histogram + wave scan, the entries are scattered into
+// bucket order in tab, and each entry's final place is its bucket start plus
+// the number of smaller partners in its (small) bucket.
+#define SNN_NB 128
+template <int RMAX>
+__device__ __forceinline__ void snn_bucket_store(unsigned long long* tab, int u, int lane, int64_t j, int64_t n,
+                                                 int* hist, int* bst, unsigned long long* __restrict__ dst) {
+    unsigned long long e[RMAX];
+    int bk[RMAX];
+    const float inv = (float)SNN_NB / (float)(n - j - 1);
+    for (int b = lane; b < SNN_NB; b += 64) hist[b] = 0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+        const int c = r * 64 + lane;
+        e[r] = c < u ? tab[c] : SNN_EMPTY64;
+        const int p = (int)(e[r] >> 32);
+        bk[r] = min(SNN_NB - 1, (int)((float)(p - (int)j - 1) * inv));
+    }
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r)
+        if (r * 64 + lane < u) atomicAdd(&hist[bk[r]], 1);
+    WAVE_LDS_SYNC();
+    const int h0 = hist[2 * lane], h1 = hist[2 * lane + 1];
+    int incl = h0 + h1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - h0 - h1;
+    bst[2 * lane] = excl;
+    bst[2 * lane + 1] = excl + h0;
+    hist[2 * lane] = excl;  // hist becomes the scatter cursor
+    hist[2 * lane + 1] = excl + h0;
+    if (lane == 0) bst[SNN_NB] = u;
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r)
+        if (r * 64 + lane < u) tab[atomicAdd(&hist[bk[r]], 1)] = e[r];
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+        if (r * 64 + lane < u) {
+            const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
+            const unsigned p = (unsigned)(e[r] >> 32);
+            int rank = 0;
+            for (int i = b0; i < b1; ++i) rank += (unsigned)(tab[i] >> 32) < p;
+            dst[b0 + rank] = e[r];
+        }
+    }
+}
+
 __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
     const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
     int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
-    int* __restrict__ ucount) {
+    int* __restrict__ ucount, int exp) {
     __shared__ unsigned long long tab_all[SNN_WAVES][SNN_WT];
     __shared__ int m_pre[SNN_WAVES][65];
+    __shared__ int m_hist[SNN_WAVES][SNN_NB];
+    __shared__ int m_bst[SNN_WAVES][SNN_NB + 1];
     __shared__ long long m_h0[SNN_WAVES][64];
     __shared__ int m_cur[SNN_WAVES][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -268,7 +327,7 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             int np, nrp, nii;
             fetch(t0 + 64 + lane, np, nrp, nii);
             bool ok = true;
-            if (p > j) {
+            if (p > j && !(exp & 1)) {
                 const unsigned c = snn_contrib(sp, ii, rp);
                 if (c != sp.init) ok = table_insert64(tab, p, c, sp, BITS, SNN_WT);
             }
@@ -279,18 +338,22 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             ii = nii;
         }
         WAVE_LDS_SYNC();
-        // compact in place (destination index <= source slot)
+        // Compact: every lane reads its 32 slots (slot r*64 + lane) to registers
+        // first, so the in-place writes cannot overtake a pending read.
         int u = 0;
         if (!full) {
-            for (int s0 = 0; s0 < SNN_WT; s0 += 64) {
-                const unsigned long long e = tab[s0 + lane];
-                const bool occ = e != SNN_EMPTY64;
+            unsigned long long e[SNN_WT / 64];
+#pragma unroll
+            for (int r = 0; r < SNN_WT / 64; ++r) e[r] = tab[r * 64 + lane];
+            WAVE_LDS_SYNC();
+#pragma unroll
+            for (int r = 0; r < SNN_WT / 64; ++r) {
+                const bool occ = e[r] != SNN_EMPTY64;
                 const unsigned long long m = __ballot(occ);
-                WAVE_LDS_SYNC();
-                if (occ) tab[u + __popcll(m & lanemask_lt())] = e;
+                if (occ) tab[u + __popcll(m & lanemask_lt())] = e[r];
                 u += __popcll(m);
-                WAVE_LDS_SYNC();
             }
+            WAVE_LDS_SYNC();
         }
         if (full || u > SNN_WCAP) {
             if (lane == 0) {
@@ -299,31 +362,22 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             }
             continue;
         }
-        int P = 64;
-        while (P < u) P <<= 1;
-        for (int s = u + lane; s < P; s += 64) tab[s] = SNN_EMPTY64;
-        WAVE_LDS_SYNC();
-        for (int kk = 2; kk <= P; kk <<= 1) {
-            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                for (int i = lane; i < P; i += 64) {
-                    const int l = i ^ jj;
-                    if (l > i) {
-                        const unsigned long long x = tab[i], y = tab[l];
-                        if ((x > y) == ((i & kk) == 0)) {
-                            tab[i] = y;
-                            tab[l] = x;
-                        }
-                    }
-                }
-                WAVE_LDS_SYNC();
-            }
-        }
-        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+        // Rank sort by partner (keys are distinct): each lane ranks its entries
+        // c = r*64 + lane against all u keys read as LDS broadcasts, then
+        // writes them straight to their sorted place in the scratch row.
         unsigned long long* dst = scratch + j * SNN_WCAP;
+        const int R = (u + 63) >> 6;
+        int* hist = m_hist[wv];
+        int* bst = m_bst[wv];
+        if (u == 0 || (exp & 2)) {
+        } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, dst);
+        else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, dst);
+        else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, dst);
+        else snn_bucket_store<SNN_WCAP / 64>(tab, u, lane, j, n, hist, bst, dst);
+        WAVE_LDS_SYNC();
+        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
         for (int c = lane; c < u; c += 64) {
-            const unsigned long long e = tab[c];
-            dst[c] = e;
-            const unsigned v = (unsigned)e;
+            const unsigned v = (unsigned)tab[c];
 #pragma unroll
             for (int t = 0; t < SNN_MAXK; ++t)
                 if (t < sp.nk && graph_has(sp, v, t)) ++c4[t];
@@ -694,8 +748,9 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     snn_fill_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, cursor, hosts);
     const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
     // pass 1: per-graph counts (wave tables, then block tables, then dense)
+    static const int snn_exp = getenv("CCG_SNN_EXP") ? atoi(getenv("CCG_SNN_EXP")) : 0;  // timing experiments only
     snn_wave_build_kernel<<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
-                                                           ov_count, scratch, ucount);
+                                                           ov_count, scratch, ucount, snn_exp);
     snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
                                                  ov2_list, ov2_count, flag2, out);
     snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
