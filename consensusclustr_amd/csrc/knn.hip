@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void knn_screen_kernel(const float* __restrict
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 #define KNN_CHUNK 64   // refs per LDS stage (2 MFMA tiles)
-#define KNN_QCAP 24    // per-lane insertion queue slots (flush when > QCAP-16)
+#define KNN_QCAP 12    // per-lane insertion queue slots (flush before a tile that would overflow)
 
 __global__ void knn_maxabs_kernel(const double* __restrict__ x, int64_t tot, unsigned* __restrict__ bits) {
     unsigned local = 0;
@@ -349,8 +349,11 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
     return x * q + min(x, r) + i;
 }
 
-template <int KSTEPS, int KP, int EXP = 0>
-__global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restrict__ img,
+// EXP 4: product kernel plus event counters (timing experiments only)
+__device__ unsigned long long g_knn_dbg[8];
+
+template <int KSTEPS, int KP, int EXP = 0, int QC = KNN_QCAP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(const uint4* __restrict__ img,
                                                            const float* __restrict__ nrm, int n, int nchunks,
                                                            int* __restrict__ cand_idx,
                                                            float* __restrict__ cand_thr) {
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
     // queued per tile and inserted in batches: a flush costs max-queue-length
     // insertion rounds for the whole wave instead of one round per (tile,
     // register) that any lane touched.
-    __shared__ uint2 qbuf[4][KNN_QCAP][64];
+    __shared__ uint2 qbuf[4][QC + 1][64];  // slot QC takes the discarded branchless writes
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
     const int bx = xcd_block(blockIdx.x, gridDim.x);
@@ -391,33 +394,25 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
     }
     float thr = -INFINITY;
 
-    // register staging (issue early, write to LDS after the compute); no
-    // lambdas/arrays captured by reference, so nothing lands in scratch
-#define KNN_STAGE_LOAD(cidx)                                                                  \
-    do {                                                                                      \
-        const uint4* src_ = img + (int64_t)(cidx) * KNN_CHUNK * C16;                          \
-        p0 = src_[tid];                                                                       \
-        if (LOADS > 1) p1 = src_[tid + 256];                                                  \
-        if (LOADS > 2) p2 = src_[tid + 512];                                                  \
-        if (LOADS > 3) p3 = src_[tid + 768];                                                  \
-        if (tid < KNN_CHUNK / 4) pn = reinterpret_cast<const float4*>(nrm + (int64_t)(cidx) * KNN_CHUNK)[tid]; \
+    // Staging by LDS-DMA (global_load_lds_dwordx4): the LDS image is written
+    // lane-linearly, so the row swizzle goes on the per-lane SOURCE address
+    // (swz_chunk is an involution) and the same swizzle on the fragment reads.
+    // No staging registers; the __syncthreads() ending each chunk waits for
+    // the DMA (vmcnt(0)) before the buffer is read.
+    typedef __attribute__((address_space(3))) void* lds_vp;
+#define KNN_STAGE_GLDS(bb, cidx)                                                                   \
+    do {                                                                                           \
+        const uint4* src_ = img + (int64_t)(cidx) * KNN_CHUNK * C16;                               \
+        _Pragma("unroll") for (int i_ = 0; i_ < LOADS; ++i_) {                                     \
+            const int p_ = i_ * 256 + tid;                                                         \
+            const int row_ = p_ / C16, cs_ = p_ % C16;                                             \
+            __builtin_amdgcn_global_load_lds((const void*)(src_ + row_ * C16 + swz_chunk<KSTEPS>(row_, cs_)), \
+                                             (lds_vp)(&lds[bb][(i_ * 256 + wave * 64) * 16]), 16, 0, 0); \
+        }                                                                                          \
+        if (wave == 0 && lane < KNN_CHUNK / 4)                                                     \
+            __builtin_amdgcn_global_load_lds((const void*)(nrm + (int64_t)(cidx) * KNN_CHUNK + lane * 4), \
+                                             (lds_vp)(&lds[bb][STAGE]), 16, 0, 0);                 \
     } while (0)
-#define KNN_STAGE_PUT(bb, i, v)                                                               \
-    do {                                                                                      \
-        const int L_ = tid + 256 * (i);                                                       \
-        const int row_ = L_ / C16, c_ = L_ % C16;                                             \
-        *reinterpret_cast<uint4*>(&lds[bb][row_ * ROWB + swz_chunk<KSTEPS>(row_, c_) * 16]) = (v); \
-    } while (0)
-#define KNN_STAGE_STORE(bb)                                                                   \
-    do {                                                                                      \
-        KNN_STAGE_PUT(bb, 0, p0);                                                             \
-        if (LOADS > 1) KNN_STAGE_PUT(bb, 1, p1);                                              \
-        if (LOADS > 2) KNN_STAGE_PUT(bb, 2, p2);                                              \
-        if (LOADS > 3) KNN_STAGE_PUT(bb, 3, p3);                                              \
-        if (tid < KNN_CHUNK / 4) reinterpret_cast<float4*>(&lds[bb][STAGE])[tid] = pn;         \
-    } while (0)
-    uint4 p0, p1, p2, p3;
-    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
     // Rows are in spatial (Morton) order, so scan ref chunks outward from the
     // block's own position: near neighbours arrive first, the threshold tightens
     // within a few tiles and later tiles rarely insert (the order only changes
@@ -430,10 +425,12 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
 #define KNN_FLUSH()                                                                   \
     do {                                                                              \
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
+            if (EXP == 4 && lane == 0) atomicAdd(&g_knn_dbg[2], 1ull);                \
             if (i_ < qc) {                                                            \
                 const uint2 e_ = qbuf[wave][i_][lane];                                \
                 const float v_ = __uint_as_float(e_.x);                               \
                 if (v_ > T) {                                                         \
+                    if (EXP == 4) atomicAdd(&g_knn_dbg[3], 1ull);                     \
                     list_insert<KP>(lv, li, v_, (int)e_.y);                           \
                     thr = lv[KP - 1];                                                 \
                     T = fmaxf(T, thr);                                                \
@@ -442,13 +439,12 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
         }                                                                             \
         qc = 0;                                                                       \
     } while (0)
-    KNN_STAGE_LOAD(chunk_at(0));
-    KNN_STAGE_STORE(0);
+    KNN_STAGE_GLDS(0, chunk_at(0));
     __syncthreads();
     for (int k = 0; k < nchunks; ++k) {
         const int b = k & 1;
         const int c = chunk_at(k);
-        if (k + 1 < nchunks) KNN_STAGE_LOAD(chunk_at(k + 1));
+        if (k + 1 < nchunks && EXP != 3) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
 #pragma nounroll  // unrolling the two tiles doubles live registers (248 vs 162 VGPRs)
         for (int tau = 0; tau < 2; ++tau) {
             const int row = tau * 32 + col;
@@ -493,15 +489,29 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
                 continue;
             }
             if (__any(vmax > T)) {
+                if (EXP == 4 && lane == 0) atomicAdd(&g_knn_dbg[0], 1ull);
+                // per half-tile of 8 registers: flush first if its candidates
+                // could overflow a queue (QC >= 8), then enqueue branch-free (a
+                // write at slot qc is kept only if qc advances; slot QC absorbs
+                // the rest)
+                static_assert(QC >= 8, "queue must hold a half tile");
+                int cnt = 0;
 #pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const float v = acc[reg];
-                    if (v > T) {
-                        qbuf[wave][qc][lane] = make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
-                        ++qc;
+                for (int hh = 0; hh < 2; ++hh) {
+                    int c8 = 0;
+#pragma unroll
+                    for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) c8 += acc[reg] > T ? 1 : 0;
+                    if (__any(qc + c8 > QC)) KNN_FLUSH();
+#pragma unroll
+                    for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
+                        const float v = acc[reg];
+                        qbuf[wave][qc][lane] =
+                            make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
+                        qc += v > T ? 1 : 0;
                     }
+                    cnt += c8;
                 }
-                if (__any(qc > KNN_QCAP - 16)) KNN_FLUSH();
+                if (EXP == 4) atomicAdd(&g_knn_dbg[1], (unsigned long long)cnt);
             }
             // Both halves of a query may reject anything at or below the better
             // of their two KP-th values: the union of the lists still holds the
@@ -509,14 +519,11 @@ __global__ __launch_bounds__(256) void knn_screen16_kernel(const uint4* __restri
             // final max(thr_h0, thr_h1) that certification uses.
             T = fmaxf(thr, __shfl_xor(thr, 32, 64));
         }
-        if (k + 1 < nchunks) KNN_STAGE_STORE(b ^ 1);
-        __syncthreads();
+        if (EXP != 2) __syncthreads();  // EXP 2 / 3: timing-only (no barrier / no global loads)
     }
     KNN_FLUSH();
 #undef KNN_FLUSH
-#undef KNN_STAGE_LOAD
-#undef KNN_STAGE_PUT
-#undef KNN_STAGE_STORE
+#undef KNN_STAGE_GLDS
 #undef chunk_at
     if (q < n) {
         int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
@@ -894,8 +901,22 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
 #define CCG_SCREEN16(KS_, KP_) \
     knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr)
         const char* exp_env = getenv("CCG_KNN_EXP");
-        if (exp_env && atoi(exp_env) == 1 && KSTEPS == 2 && KP == KNN_KP) {
-            knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+        const int kexp = exp_env ? atoi(exp_env) : 0;
+        if (kexp >= 1 && kexp <= 6 && KSTEPS == 2 && KP == KNN_KP) {
+            if (kexp == 4) {
+                unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                CCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_knn_dbg), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
+                knn_screen16_kernel<2, KNN_KP, 4><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+                CCG_HIP(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_knn_dbg), sizeof(z), 0, hipMemcpyDeviceToHost, st));
+                CCG_HIP(hipStreamSynchronize(st));
+                fprintf(stderr, "knn_dbg tiles_any=%llu enq=%llu flush_rounds=%llu inserts=%llu tile_waves=%llu\n",
+                        z[0], z[1], z[2], z[3], (unsigned long long)grid * 4 * nch * 2);
+            }
+            if (kexp == 1) knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+            if (kexp == 2) knn_screen16_kernel<2, KNN_KP, 2><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+            if (kexp == 3) knn_screen16_kernel<2, KNN_KP, 3><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+            if (kexp == 6) knn_screen16_kernel<2, KNN_KP, 0, 16><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+            if (kexp == 5) knn_screen16_kernel<2, KNN_KP, 0, 8><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
         } else if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);

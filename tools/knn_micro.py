@@ -1,6 +1,8 @@
 """Micro-benchmark of ccg_knn_rows_dev at BASELINE cfg3 shapes (n=90000, d=30).
 
 Times the screen kernel and the whole kNN with the library's hipEvent timers.
+Data: one 90k-row bootstrap of bench.py's synthetic NB-count PCs (KM_DATA=gauss:
+a 12-component Gaussian mixture instead).
 Variants come from environment variables read by libccg (CCG_KNN_F32,
 CCG_KNN_EXP); run each in its own process.
 """
@@ -12,16 +14,24 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 from consensusclustr_amd import Engine  # noqa: E402
 
 
 def main():
     n, d, reps = int(os.environ.get("KM_N", 90000)), int(os.environ.get("KM_D", 30)), 5
-    rng = np.random.default_rng(0)
-    centers = rng.normal(scale=3.0, size=(12, d))
-    X = centers[rng.integers(0, 12, n)] + rng.normal(size=(n, d))
     eng = Engine(0)
-    rows = torch.from_numpy(X).cuda()
+    if os.environ.get("KM_DATA") == "gauss":
+        rng = np.random.default_rng(0)
+        centers = rng.normal(scale=3.0, size=(12, d))
+        X = centers[rng.integers(0, 12, n)] + rng.normal(size=(n, d))
+        rows = torch.from_numpy(X).cuda()
+    else:
+        N = int(n / 0.9)
+        pcs, _ = bench.synth_pcs(torch, N, d, 2000, 20241024 + 3, torch.device("cuda", 0))
+        boot = torch.from_numpy(np.random.default_rng(123).integers(0, N, n).astype(np.int32)).cuda()
+        rows = torch.empty((n, d), dtype=torch.float64, device="cuda")
+        eng.gather_rows_t(pcs.t().contiguous(), N, d, boot, rows)
     idx = torch.empty((n, 20), dtype=torch.int32, device="cuda")
     eng.knn_rows_t(rows, 20, idx)
     torch.cuda.synchronize()
@@ -33,7 +43,7 @@ def main():
     scr = eng.timing_read("knn_screen")
     tot = eng.timing_read("knn_total")
     st = eng.knn_rows_t(rows, 20, idx, stats=True)
-    out = {"variant": {k: os.environ.get(k) for k in ("CCG_KNN_F32", "CCG_KNN_EXP")},
+    out = {"variant": {k: os.environ.get(k) for k in ("CCG_KNN_F32", "CCG_KNN_EXP", "CCG_KNN_QF")},
            "screen_ms": scr[0] / scr[1], "knn_total_ms": tot[0] / tot[1], "fallback": st[1]}
     print(json.dumps(out))
 
