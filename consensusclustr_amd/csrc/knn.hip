@@ -339,6 +339,24 @@ __device__ __forceinline__ int knn_chunk_at(int k, int c0, int Lc, int Rc, int M
     return Rc > Lc ? c0 + Mc + m : c0 - Mc - m;
 }
 
+// 16-byte LDS-DMA: lane l's 16 bytes from sbase + voff land at LDS byte
+// address lds + 16*l (sbase and lds wave-uniform).
+__device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
+    int keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds))
+        : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own
 // 4 MB L2).  Give XCD x a contiguous range of query blocks: neighbouring
 // blocks scan nearly the same chunk sequence a few steps apart, so each
@@ -361,13 +379,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     constexpr int ROWB = KSTEPS * 64;               // bytes per row
     constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage (no norms)
     constexpr int LOADS = (KNN_CHUNK * C16) / 256;  // uint4 loads per thread per stage
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2][STAGE + KNN_CHUNK * 4];
+    // ALL of the kernel's LDS is this one array (two staging buffers, then the
+    // queues): with a second __shared__ object beside the LDS-DMA target,
+    // hipcc waits vmcnt(0) before the first ds_read of every tile, which
+    // serialises the next chunk's DMA with this chunk's compute.
+    constexpr int SBUF = STAGE + KNN_CHUNK * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SBUF + 4 * (QC + 1) * 64 * 8];
+#define lds(bb_) (smem + (bb_) * SBUF)
     // Per-lane insertion queues (slot-major, so a wave's enqueue is one
     // conflict-free ds_write_b64).  Candidates above the running threshold are
     // queued per tile and inserted in batches: a flush costs max-queue-length
     // insertion rounds for the whole wave instead of one round per (tile,
     // register) that any lane touched.
-    __shared__ uint2 qbuf[4][QC + 1][64];  // slot QC takes the discarded branchless writes
+    // per-wave queues [slot][lane] (slot QC takes the discarded branchless writes)
+    uint2* const qbw = reinterpret_cast<uint2*>(smem + 2 * SBUF) + (threadIdx.x >> 6) * (QC + 1) * 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
     const int bx = xcd_block(blockIdx.x, gridDim.x);
@@ -381,6 +406,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
         for (int s = 0; s < KSTEPS; ++s) {
             uint4 a = qp[s], b = qp[KSTEPS + s];
+            // retire the loads here: hipcc does not see the asm DMA in the
+            // chunk loop and would otherwise put its waits for these (which
+            // then drain the DMA too) in front of the loop's MFMAs
+            asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
             qh[s] = *reinterpret_cast<h8*>(&a);
             ql[s] = *reinterpret_cast<h8*>(&b);
         }
@@ -397,21 +426,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // Staging by LDS-DMA (global_load_lds_dwordx4): the LDS image is written
     // lane-linearly, so the row swizzle goes on the per-lane SOURCE address
     // (swz_chunk is an involution) and the same swizzle on the fragment reads.
-    // No staging registers; the __syncthreads() ending each chunk waits for
-    // the DMA (vmcnt(0)) before the buffer is read.
-    typedef __attribute__((address_space(3))) void* lds_vp;
+    // Issued as inline asm: hipcc would otherwise wait vmcnt(0) before the
+    // first ds_read of every tile (it cannot tell the DMA target from the
+    // buffer being read), serialising the next chunk's DMA with this chunk's
+    // compute.  The explicit vmcnt(0) before each chunk's closing barrier is
+    // the only wait the DMA needs.
 #define KNN_STAGE_GLDS(bb, cidx)                                                                   \
     do {                                                                                           \
-        const uint4* src_ = img + (int64_t)(cidx) * KNN_CHUNK * C16;                               \
+        const unsigned char* src_ = reinterpret_cast<const unsigned char*>(img) +                 \
+                                    (int64_t)(cidx) * (KNN_CHUNK * ROWB);                          \
         _Pragma("unroll") for (int i_ = 0; i_ < LOADS; ++i_) {                                     \
             const int p_ = i_ * 256 + tid;                                                         \
             const int row_ = p_ / C16, cs_ = p_ % C16;                                             \
-            __builtin_amdgcn_global_load_lds((const void*)(src_ + row_ * C16 + swz_chunk<KSTEPS>(row_, cs_)), \
-                                             (lds_vp)(&lds[bb][(i_ * 256 + wave * 64) * 16]), 16, 0, 0); \
+            glds16(src_, (unsigned)(row_ * ROWB + swz_chunk<KSTEPS>(row_, cs_) * 16),             \
+                   lds_addr(lds(bb) + (i_ * 256 + wave * 64) * 16));                              \
         }                                                                                          \
         if (wave == 0 && lane < KNN_CHUNK / 4)                                                     \
-            __builtin_amdgcn_global_load_lds((const void*)(nrm + (int64_t)(cidx) * KNN_CHUNK + lane * 4), \
-                                             (lds_vp)(&lds[bb][STAGE]), 16, 0, 0);                 \
+            glds16(reinterpret_cast<const unsigned char*>(nrm) + (int64_t)(cidx) * (KNN_CHUNK * 4), \
+                   (unsigned)(lane * 16), lds_addr(lds(bb) + STAGE));                              \
     } while (0)
     // Rows are in spatial (Morton) order, so scan ref chunks outward from the
     // block's own position: near neighbours arrive first, the threshold tightens
@@ -427,7 +459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
             if (EXP == 4 && lane == 0) atomicAdd(&g_knn_dbg[2], 1ull);                \
             if (i_ < qc) {                                                            \
-                const uint2 e_ = qbuf[wave][i_][lane];                                \
+                const uint2 e_ = qbw[i_ * 64 + lane];                                 \
                 const float v_ = __uint_as_float(e_.x);                               \
                 if (v_ > T) {                                                         \
                     if (EXP == 4) atomicAdd(&g_knn_dbg[3], 1ull);                     \
@@ -440,6 +472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         qc = 0;                                                                       \
     } while (0)
     KNN_STAGE_GLDS(0, chunk_at(0));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int k = 0; k < nchunks; ++k) {
         const int b = k & 1;
@@ -452,14 +485,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
             for (int s = 0; s < KSTEPS; ++s) {
                 uint4 a = *reinterpret_cast<const uint4*>(
-                    &lds[b][row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + s) * 16]);
+                    lds(b) + row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + s) * 16);
                 uint4 bb = *reinterpret_cast<const uint4*>(
-                    &lds[b][row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + KSTEPS + s) * 16]);
+                    lds(b) + row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + KSTEPS + s) * 16);
                 ah[s] = *reinterpret_cast<h8*>(&a);
                 al[s] = *reinterpret_cast<h8*>(&bb);
             }
             f32x16 acc;
-            const float* nb = reinterpret_cast<const float*>(&lds[b][STAGE]) + tau * 32 + 4 * h;
+            const float* nb = reinterpret_cast<const float*>(lds(b) + STAGE) + tau * 32 + 4 * h;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 v = *reinterpret_cast<const float4*>(nb + 8 * g);
@@ -505,7 +538,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
                     for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
                         const float v = acc[reg];
-                        qbuf[wave][qc][lane] =
+                        qbw[qc * 64 + lane] =
                             make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
                         qc += v > T ? 1 : 0;
                     }
@@ -519,12 +552,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             // final max(thr_h0, thr_h1) that certification uses.
             T = fmaxf(thr, __shfl_xor(thr, 32, 64));
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (EXP != 2) __syncthreads();  // EXP 2 / 3: timing-only (no barrier / no global loads)
     }
     KNN_FLUSH();
 #undef KNN_FLUSH
 #undef KNN_STAGE_GLDS
 #undef chunk_at
+#undef lds
     if (q < n) {
         int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
 #pragma unroll
@@ -915,7 +950,7 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
             if (kexp == 1) knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
             if (kexp == 2) knn_screen16_kernel<2, KNN_KP, 2><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
             if (kexp == 3) knn_screen16_kernel<2, KNN_KP, 3><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-            if (kexp == 6) knn_screen16_kernel<2, KNN_KP, 0, 16><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
+            if (kexp == 6) knn_screen16_kernel<2, KNN_KP, 0, 10><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
             if (kexp == 5) knn_screen16_kernel<2, KNN_KP, 0, 8><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
         } else if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
