@@ -206,18 +206,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #define KNN_CHUNK 64   // refs per LDS stage (2 MFMA tiles)
 #define KNN_QCAP 12    // per-lane insertion queue slots (flush before a tile that would overflow)
 
-__global__ void knn_maxabs_kernel(const double* __restrict__ x, int64_t tot, unsigned* __restrict__ bits) {
-    unsigned local = 0;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
-         t += (int64_t)gridDim.x * blockDim.x) {
-        float f = (float)fabs(x[t]);
-        f = nextafterf(f, INFINITY);
-        local = max(local, __float_as_uint(f));
-    }
-    for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(bits, local);
-}
-
 __device__ __forceinline__ int knn_scale_exp(const unsigned* maxabs_bits) {
     const float m = __uint_as_float(*maxabs_bits);
     if (!(m > 0.f)) return 0;
@@ -277,26 +265,51 @@ __device__ __forceinline__ float ord2f(unsigned o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-__global__ void knn_bounds_kernel(const double* __restrict__ rows, int64_t n, int d,
-                                  unsigned* __restrict__ bnd /* [3] min, [3] max (ordered) */) {
-    const int nd = d < 3 ? d : 3;
-    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-        for (int k = 0; k < nd; ++k) {
-            const unsigned o = f2ord((float)rows[r * d + k]);
-            mn[k] = min(mn[k], o);
-            mx[k] = max(mx[k], o);
+// max|x| (fp32 bits, rounded up) and the ordered-float bounds of the first
+// three coordinates in one coalesced pass; block-level reduction so each
+// block issues 7 atomics (a per-wave atomic on one word serialises at ~13 ns
+// each).
+__global__ __launch_bounds__(256) void knn_rowstats_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                                           unsigned* __restrict__ maxabs_bits,
+                                                           unsigned* __restrict__ bnd) {
+    __shared__ unsigned red[4][7];
+    unsigned v7[7] = {0u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    const int64_t tot = n * d;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    const int kstep = (int)(S % d);
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int k = (int)(t % d);
+    for (; t < tot; t += S) {
+        const double v = rows[t];
+        float f = (float)fabs(v);
+        f = nextafterf(f, INFINITY);
+        v7[0] = max(v7[0], __float_as_uint(f));
+        if (k < 3) {
+            const unsigned o = f2ord((float)v);
+            v7[1 + k] = min(v7[1 + k], o);
+            v7[4 + k] = max(v7[4 + k], o);
         }
-    for (int k = 0; k < nd; ++k) {
-        unsigned a = mn[k], b = mx[k];
+        k += kstep;
+        if (k >= d) k -= d;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        unsigned a = v7[i];
         for (int o = 32; o > 0; o >>= 1) {
-            a = min(a, (unsigned)__shfl_xor((int)a, o, 64));
-            b = max(b, (unsigned)__shfl_xor((int)b, o, 64));
+            const unsigned b = (unsigned)__shfl_xor((int)a, o, 64);
+            a = (i >= 1 && i <= 3) ? min(a, b) : max(a, b);
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&bnd[k], a);
-            atomicMax(&bnd[3 + k], b);
-        }
+        if (lane == 0) red[wv][i] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        const int i = threadIdx.x;
+        unsigned a = red[0][i];
+        for (int w = 1; w < 4; ++w) a = (i >= 1 && i <= 3) ? min(a, red[w][i]) : max(a, red[w][i]);
+        if (i == 0) atomicMax(maxabs_bits, a);
+        else if (i <= 3) { if (i - 1 < d) atomicMin(&bnd[i - 1], a); }
+        else if (i - 4 < d) atomicMax(&bnd[3 + (i - 4)], a);
     }
 }
 
@@ -596,7 +609,7 @@ __device__ __forceinline__ void wave_bitonic64(double& key, int& id) {
     }
 }
 
-template <int KP>
+template <int KP, int DMAX>
 __global__ __launch_bounds__(256) void knn_certify_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
@@ -610,17 +623,33 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const double* x = rows + (int64_t)q * d;
     int j = (lane < 2 * KP) ? cand_idx[(int64_t)qs * 2 * KP + lane] : -1;
     if (j >= 0 && perm) j = perm[j];
+    // unrolled over DMAX so all of a row's loads are in flight together
+    double xq[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? x[k] : 0.0;
     double key = INFINITY;
     int id = 0x7fffffff - 64 + lane;  // distinct padding ids sort after real ones
     if (j >= 0) {
-        key = sqdist_exact(x, rows + (int64_t)j * d, d);
+        const double* y = rows + (int64_t)j * d;
+        double yv[DMAX];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) yv[k] = k < d ? y[k] : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k)
+            if (k < d) {
+                const double t = __dsub_rn(xq[k], yv[k]);
+                s = __dadd_rn(s, __dmul_rn(t, t));
+            }
+        key = s;
         id = j;
     }
     wave_bitonic64(key, id);
 
     // certification (wave-uniform values)
     double nq = 0.0;
-    for (int k = 0; k < d; ++k) nq += x[k] * x[k];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) nq += xq[k] * xq[k];
     const float t0 = cand_thr[(int64_t)qs * 2 + 0];
     const float t1 = cand_thr[(int64_t)qs * 2 + 1];
     const float tmax = fmaxf(t0, t1);
@@ -905,9 +934,6 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
         if (!img) return CCG_ENOMEM;
         float* nrm = (float*)((char*)img + (size_t)npad * 64 * KSTEPS);
-        knn_maxabs_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 256), 1024), 256, 0, st>>>(rows, n * d,
-                                                                                                 mbits);
-        // spatial order: Morton buckets of the leading coordinates
         const int64_t NB = 1LL << (3 * KNN_MORTON_BITS);
         int64_t* hist = (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
         if (!hist) return CCG_ENOMEM;
@@ -917,7 +943,8 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         CCG_HIP(hipMemsetAsync(bnd, 0xff, 3 * sizeof(unsigned), st));
         CCG_HIP(hipMemsetAsync(bnd + 3, 0, 3 * sizeof(unsigned), st));
         CCG_HIP(hipMemsetAsync(hist, 0, sizeof(int64_t) * (NB + 1), st));
-        knn_bounds_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 256), 512), 256, 0, st>>>(rows, n, d, bnd);
+        knn_rowstats_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 1024), 256), 256, 0, st>>>(rows, n, d,
+                                                                                                    mbits, bnd);
         knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
         rc = ccg_scan_i64(ctx, hist, hist, NB, st);
         if (rc) return rc;
@@ -966,14 +993,20 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         err_ulps = KNN_ERR_ULPS_F16;
     }
     if (rc) return rc;
-    if (KP == KNN_KP)
-        knn_certify_kernel<KNN_KP><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
-            rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist,
-            fail_list, fail_count);
-    else
-        knn_certify_kernel<KNN_KP_BIG><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(
-            rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist,
-            fail_list, fail_count);
+#define CCG_CERTIFY(KP_, DM_)                                                                            \
+    knn_certify_kernel<KP_, DM_><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(                                \
+        rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist, \
+        fail_list, fail_count)
+    if (KP == KNN_KP) {
+        if (d <= 16) CCG_CERTIFY(KNN_KP, 16);
+        else if (d <= 32) CCG_CERTIFY(KNN_KP, 32);
+        else CCG_CERTIFY(KNN_KP, 64);
+    } else {
+        if (d <= 16) CCG_CERTIFY(KNN_KP_BIG, 16);
+        else if (d <= 32) CCG_CERTIFY(KNN_KP_BIG, 32);
+        else CCG_CERTIFY(KNN_KP_BIG, 64);
+    }
+#undef CCG_CERTIFY
     const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
     double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);

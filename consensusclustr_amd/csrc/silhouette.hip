@@ -29,7 +29,9 @@ __device__ __forceinline__ int scale_exp(double bound) {
     return e > 52 ? 52 : e;
 }
 
-__global__ void sil_maxabs(const double* __restrict__ x, int64_t tot, unsigned* __restrict__ bits) {
+__global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, int64_t tot,
+                                                  unsigned* __restrict__ bits) {
+    __shared__ unsigned red[4];
     unsigned local = 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
          t += (int64_t)gridDim.x * blockDim.x) {
@@ -38,7 +40,9 @@ __global__ void sil_maxabs(const double* __restrict__ x, int64_t tot, unsigned* 
         local = max(local, __float_as_uint(f));
     }
     for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(bits, local);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(bits, max(max(red[0], red[1]), max(red[2], red[3])));  // one atomic per block
 }
 
 template <int DMAX>
@@ -91,48 +95,80 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
     }
 }
 
-// Centroids of labeling l into LDS (all codes 0..cmax).
-__device__ __forceinline__ void load_centroids(double* mu, const unsigned long long* __restrict__ gsum,
-                                               const unsigned long long* __restrict__ gcnt, int l,
-                                               int cmax, int d, double inv_sc) {
-    const int nacc = (cmax + 1) * d;
-    const unsigned long long* gs = gsum + (int64_t)l * nacc;
+// K2: per labeling, the present codes (ascending = sort(unique(clusters)))
+// and the centroids mu[l][c][0..DMAX) (zero padded) plus |mu_c|^2, from the
+// fixed-point sums.  One block per labeling.
+template <int DMAX>
+__global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
+                                                const unsigned* __restrict__ maxabs_bits,
+                                                const unsigned long long* __restrict__ gsum,
+                                                const unsigned long long* __restrict__ gcnt,
+                                                int* __restrict__ npres, int* __restrict__ codes,
+                                                int* __restrict__ pos, double* __restrict__ mu,
+                                                double* __restrict__ muc, double* __restrict__ auxc) {
+    __shared__ int pos_s[257];
+    const int l = blockIdx.x;
+    const double maxabs = (double)__uint_as_float(*maxabs_bits);
+    const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
+    const unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
     const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
-    for (int t = threadIdx.x; t < nacc; t += SIL_T) {
-        const int c = t / d;
+    if (threadIdx.x == 0) {
+        int np = 0;
+        pos_s[0] = -1;
+        for (int c = 1; c <= cmax; ++c) {
+            pos_s[c] = gc[c] ? np : -1;
+            if (gc[c]) codes[(int64_t)l * cmax + np++] = c;
+        }
+        npres[l] = np;
+    }
+    __syncthreads();
+    double* ml = mu + (int64_t)l * (cmax + 1) * DMAX;
+    double* mcl = muc + (int64_t)l * cmax * DMAX;
+    for (int t = threadIdx.x; t < (cmax + 1) * DMAX; t += SIL_T) {
+        const int c = t / DMAX, k = t - c * DMAX;
         const unsigned long long n = gc[c];
-        mu[t] = n ? ((double)(long long)gs[t] * inv_sc) / (double)n : 0.0;
+        const double v = (n && k < d) ? ((double)(long long)gs[c * d + k] * inv_sc) / (double)n : 0.0;
+        ml[t] = v;
+        if (pos_s[c] >= 0) mcl[pos_s[c] * DMAX + k] = v;
+    }
+    for (int c = threadIdx.x; c <= cmax; c += SIL_T) pos[(int64_t)l * (cmax + 1) + c] = pos_s[c];
+    __syncthreads();
+    for (int c = threadIdx.x; c <= cmax; c += SIL_T) {
+        if (pos_s[c] < 0) continue;
+        double s = 0.0;
+        for (int k = 0; k < d; ++k) s = fma(ml[c * DMAX + k], ml[c * DMAX + k], s);
+        auxc[((int64_t)l * cmax + pos_s[c]) * 2] = s;
     }
 }
 
-// K2: fixed-point within-cluster sum of squared distances to the centroid.
+// K3: fixed-point within-cluster sum of squared distances to the centroid
+// (the exact difference form, as colMeans(sweep(x, 2, centroid)^2)).
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_var(const double* __restrict__ x, int64_t m, int d,
                                                  const int32_t* __restrict__ labels, int L, int cmax,
                                                  const unsigned* __restrict__ maxabs_bits,
-                                                 const unsigned long long* __restrict__ gsum,
-                                                 const unsigned long long* __restrict__ gcnt,
+                                                 const double* __restrict__ mu,
                                                  unsigned long long* __restrict__ gvar) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* mu = (double*)smem;                                          // [cmax+1][d]
-    unsigned long long* vacc = (unsigned long long*)(mu + (int64_t)(cmax + 1) * d);  // [cmax+1]
+    double* mus = (double*)smem;                                              // [cmax+1][DMAX]
+    unsigned long long* vacc = (unsigned long long*)(mus + (int64_t)(cmax + 1) * DMAX);  // [cmax+1]
     const int64_t r = (int64_t)blockIdx.x * SIL_T + threadIdx.x;
     const bool in = r < m;
     double xr[DMAX];
     load_row<DMAX>(x, in ? r : 0, d, xr);
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
     const double vb = 4.0 * maxabs * maxabs * (double)d * (double)m;
     const double vsc = ldexp(1.0, scale_exp(vb));
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
-        load_centroids(mu, gsum, gcnt, l, cmax, d, inv_sc);
+        const double* ml = mu + (int64_t)l * (cmax + 1) * DMAX;
+        for (int t = threadIdx.x; t < (cmax + 1) * DMAX; t += SIL_T) mus[t] = ml[t];
         for (int t = threadIdx.x; t <= cmax; t += SIL_T) vacc[t] = 0ull;
         __syncthreads();
         if (in) {
             const int lab = labels[(int64_t)l * m + r];
             if (lab >= 1 && lab <= cmax) {
-                const double* mc = mu + lab * d;
+                const double* mc = mus + lab * DMAX;
                 double s = 0.0;
 #pragma unroll
                 for (int k = 0; k < DMAX; ++k)
@@ -151,86 +187,137 @@ __global__ __launch_bounds__(SIL_T) void sil_var(const double* __restrict__ x, i
     }
 }
 
-// K3: widths and their fixed-point sum over non-NaN rows.
+// K4: v_c = (sum of squared distances) / n_c next to |mu_c|^2 in auxc.
+__global__ void sil_vfin(int64_t m, int d, int L, int cmax, const unsigned* __restrict__ maxabs_bits,
+                         const unsigned long long* __restrict__ gcnt,
+                         const unsigned long long* __restrict__ gvar, const int* __restrict__ pos,
+                         double* __restrict__ auxc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)L * (cmax + 1)) return;
+    const int p = pos[t];
+    if (p < 0) return;
+    const int64_t l = t / (cmax + 1);
+    const double maxabs = (double)__uint_as_float(*maxabs_bits);
+    const double vb = 4.0 * maxabs * maxabs * (double)d * (double)m;
+    const double inv_vsc = ldexp(1.0, -scale_exp(vb));
+    auxc[(l * cmax + p) * 2 + 1] = ((double)gvar[t] * inv_vsc) / (double)gcnt[t];
+}
+
+// K5: widths and their fixed-point sum over non-NaN rows.  Each thread
+// owns two rows (r and r + SIL_T of a 2*SIL_T-row tile) so that every
+// centroid value read from LDS (a broadcast ds_read_b128 = 2 dims) feeds 4
+// FMAs.  Squared distances to the other clusters use |x|^2 + |mu|^2 - 2 x.mu
+// (one FMA per dimension), clamped at 0 (|error| ~ 1e-16 |x|^2, far inside
+// the 1e-5 tolerance); the own-cluster distance, the one that can be ~0, is
+// taken in the difference form.  D is monotone in s + v_c, so the minimum is
+// taken on the squares and one sqrt applied at the end.
+template <int DMAX>
+__device__ __forceinline__ void sil_row_width(const double (&xr)[DMAX], double selfsq, double oth2, bool in,
+                                              int np, double wsc, double* out_w, long long& wq, unsigned& wn) {
+    if (!in) return;
+    const double selfd = sqrt(selfsq), othd = sqrt(oth2);
+    double w;
+    if (np > 1) {
+        double mx = fmax(othd, selfd);
+        if (isnan(othd) || isnan(selfd)) mx = NAN;
+        w = (othd - selfd) / mx;
+    } else {
+        w = 0.0;
+    }
+    if (out_w) *out_w = w;
+    if (!isnan(w)) {
+        wq += __double2ll_rn(w * wsc);
+        wn += 1;
+    }
+}
+
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x, int64_t m, int d,
                                                    const int32_t* __restrict__ labels, int L, int cmax,
-                                                   const unsigned* __restrict__ maxabs_bits,
-                                                   const unsigned long long* __restrict__ gsum,
-                                                   const unsigned long long* __restrict__ gcnt,
-                                                   const unsigned long long* __restrict__ gvar,
+                                                   const int* __restrict__ npres,
+                                                   const int* __restrict__ codes,
+                                                   const int* __restrict__ pos,
+                                                   const double* __restrict__ muc,
+                                                   const double* __restrict__ auxc,
                                                    unsigned long long* __restrict__ wsum,
                                                    unsigned long long* __restrict__ wcnt,
                                                    double* __restrict__ out_width) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* mu = (double*)smem;                                  // [npres][d]
-    double* vv = mu + (int64_t)(cmax + 1) * d;                   // [npres]
-    int* code = (int*)(vv + (cmax + 1));                         // [npres]
-    int* npres_s = code + (cmax + 1);
-    const int64_t r = (int64_t)blockIdx.x * SIL_T + threadIdx.x;
-    const bool in = r < m;
-    double xr[DMAX];
-    load_row<DMAX>(x, in ? r : 0, d, xr);
-    const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
-    const double vb = 4.0 * maxabs * maxabs * (double)d * (double)m;
-    const double inv_vsc = ldexp(1.0, -scale_exp(vb));
+    double* smu = (double*)smem;                  // [np][DMAX]
+    double* sau = smu + (int64_t)cmax * DMAX;     // [np][2]
+    int* scode = (int*)(sau + 2 * (int64_t)cmax); // [np]
+    const int64_t ra = (int64_t)blockIdx.x * (2 * SIL_T) + threadIdx.x, rb = ra + SIL_T;
+    const bool ina = ra < m, inb = rb < m;
+    double xa[DMAX], xb[DMAX];
+    load_row<DMAX>(x, ina ? ra : 0, d, xa);
+    load_row<DMAX>(x, inb ? rb : 0, d, xb);
+    double xxa = 0.0, xxb = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) {
+        xxa = fma(xa[k], xa[k], xxa);
+        xxb = fma(xb[k], xb[k], xxb);
+    }
     const double wsc = ldexp(1.0, scale_exp((double)m));
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
-        const unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
-        const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
-        const unsigned long long* gv = gvar + (int64_t)l * (cmax + 1);
-        if (threadIdx.x == 0) {
-            int np = 0;
-            for (int c = 1; c <= cmax; ++c)
-                if (gc[c]) code[np++] = c;  // ascending = sort(unique(clusters))
-            *npres_s = np;
+        const int np = npres[l];
+        {
+            const double* ml = muc + (int64_t)l * cmax * DMAX;
+            for (int t = threadIdx.x; t < np * DMAX; t += SIL_T) smu[t] = ml[t];
+            const double* al = auxc + (int64_t)l * cmax * 2;
+            for (int t = threadIdx.x; t < 2 * np; t += SIL_T) sau[t] = al[t];
+            for (int t = threadIdx.x; t < np; t += SIL_T) scode[t] = codes[(int64_t)l * cmax + t];
         }
         __syncthreads();
-        const int np = *npres_s;
-        for (int t = threadIdx.x; t < np * d; t += SIL_T) {
-            const int pi = t / d, k = t - pi * d;
-            const int c = code[pi];
-            mu[t] = ((double)(long long)gs[c * d + k] * inv_sc) / (double)gc[c];
+        const int laba = ina ? labels[(int64_t)l * m + ra] : 0;
+        const int labb = inb ? labels[(int64_t)l * m + rb] : 0;
+        double otha = INFINITY, othb = INFINITY;
+        for (int pi = 0; pi < np; ++pi) {
+            const double2* mc = reinterpret_cast<const double2*>(smu + pi * DMAX);
+            double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+#pragma unroll
+            for (int k2 = 0; k2 < DMAX / 2; ++k2) {
+                const double2 mv = mc[k2];
+                a0 = fma(xa[2 * k2], mv.x, a0);
+                a1 = fma(xa[2 * k2 + 1], mv.y, a1);
+                b0 = fma(xb[2 * k2], mv.x, b0);
+                b1 = fma(xb[2 * k2 + 1], mv.y, b1);
+            }
+            const double mm = sau[2 * pi], vc = sau[2 * pi + 1];
+            const int c = scode[pi];
+            const double sa = fmax(fma(-2.0, a0 + a1, xxa + mm), 0.0) + vc;
+            const double sb = fmax(fma(-2.0, b0 + b1, xxb + mm), 0.0) + vc;
+            if (c != laba && sa < otha) otha = sa;
+            if (c != labb && sb < othb) othb = sb;
         }
-        for (int t = threadIdx.x; t < np; t += SIL_T) {
-            const int c = code[t];
-            vv[t] = ((double)gv[c] * inv_vsc) / (double)gc[c];
+        // own cluster in the difference form: exact 0 for a singleton, as in R
+        double selfa = INFINITY, selfb = INFINITY;
+        if (ina && laba >= 1 && laba <= cmax) {
+            const int p = pos[(int64_t)l * (cmax + 1) + laba];
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) {
+                const double t = xa[k] - smu[p * DMAX + k];
+                s = fma(t, t, s);
+            }
+            selfa = s + sau[2 * p + 1];
         }
-        __syncthreads();
+        if (inb && labb >= 1 && labb <= cmax) {
+            const int p = pos[(int64_t)l * (cmax + 1) + labb];
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) {
+                const double t = xb[k] - smu[p * DMAX + k];
+                s = fma(t, t, s);
+            }
+            selfb = s + sau[2 * p + 1];
+        }
         long long wq = 0;
         unsigned wn = 0;
-        if (in) {
-            const int lab = labels[(int64_t)l * m + r];
-            double selfd = INFINITY, othd = INFINITY;
-            for (int pi = 0; pi < np; ++pi) {
-                const double* mc = mu + pi * d;
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k < DMAX; ++k)
-                    if (k < d) {
-                        const double t = xr[k] - mc[k];
-                        s += t * t;
-                    }
-                const double Dc = sqrt(s + vv[pi]);
-                if (code[pi] == lab) selfd = Dc;
-                else if (Dc < othd) othd = Dc;
-            }
-            double w;
-            if (np > 1) {
-                double mx = fmax(othd, selfd);
-                if (isnan(othd) || isnan(selfd)) mx = NAN;
-                w = (othd - selfd) / mx;
-            } else {
-                w = 0.0;
-            }
-            if (out_width) out_width[(int64_t)l * m + r] = w;
-            if (!isnan(w)) {
-                wq = __double2ll_rn(w * wsc);
-                wn = 1;
-            }
-        }
+        sil_row_width<DMAX>(xa, selfa, otha, ina, np, wsc, out_width ? out_width + (int64_t)l * m + ra : nullptr,
+                            wq, wn);
+        sil_row_width<DMAX>(xb, selfb, othb, inb, np, wsc, out_width ? out_width + (int64_t)l * m + rb : nullptr,
+                            wq, wn);
         // integer wave reduction (order-independent), one atomic per wave
         for (int o = 32; o > 0; o >>= 1) {
             wq += __shfl_xor(wq, o, 64);
@@ -240,7 +327,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
             if (wq) atomicAdd(&wsum[l], (unsigned long long)wq);
             if (wn) atomicAdd(&wcnt[l], (unsigned long long)wn);
         }
-        __syncthreads();
+        __syncthreads();  // before the next labeling overwrites the centroids
     }
 }
 
@@ -269,15 +356,20 @@ template <int DMAX>
 static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels, int L, int cmax,
                        unsigned* maxabs, unsigned long long* gsum, unsigned long long* gcnt,
                        unsigned long long* gvar, unsigned long long* wsum, unsigned long long* wcnt,
+                       int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc,
                        double* out_width, hipStream_t st) {
     dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
     size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
-    size_t lds2 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 8;
-    size_t lds3 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 8 + (size_t)(cmax + 2) * 4;
+    size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
     sil_centroid<DMAX><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
-    sil_var<DMAX><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar);
-    sil_width<DMAX><<<grid, SIL_T, lds3, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar,
-                                               wsum, wcnt, out_width);
+    sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gcnt, npres, codes, pos, mu, muc, auxc);
+    sil_var<DMAX><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
+    sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
+                                                                                gvar, pos, auxc);
+    dim3 grid2((unsigned)ccg_cdiv(m, 2 * SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
+    size_t lds5 = (size_t)cmax * DMAX * 8 + (size_t)cmax * 16 + (size_t)cmax * 4;
+    sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, pos, muc, auxc, wsum,
+                                            wcnt, out_width);
 }
 
 extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
@@ -299,15 +391,28 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     unsigned long long* wsum = gvar + (int64_t)L * (cmax + 1);
     unsigned long long* wcnt = wsum + L;
     unsigned* maxabs = (unsigned*)(wcnt + L);
+    const int dmax = d <= 16 ? 16 : (d <= 32 ? 32 : 64);
+    const size_t mu_words = (size_t)L * (cmax + 1) * dmax + (size_t)L * cmax * dmax + 2 * (size_t)L * cmax;
+    const size_t tab_ints = (size_t)L * cmax + (size_t)L * (cmax + 1) + L + 8;
+    double* mu = (double*)ccg_ws(ctx, WS_SIL_B, sizeof(double) * mu_words + sizeof(int) * tab_ints);
+    if (!mu) return CCG_ENOMEM;
+    double* muc = mu + (size_t)L * (cmax + 1) * dmax;
+    double* auxc = muc + (size_t)L * cmax * dmax;
+    int* npres = (int*)(auxc + 2 * (size_t)L * cmax);
+    int* codes = npres + L;
+    int* pos = codes + (size_t)L * cmax;
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 256), 1024), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
     if (d <= 16)
-        sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, out_width, st);
+        sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+                        out_width, st);
     else if (d <= 32)
-        sil_launch<32>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, out_width, st);
+        sil_launch<32>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+                        out_width, st);
     else
-        sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, out_width, st);
+        sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+                        out_width, st);
     sil_final<<<(unsigned)ccg_cdiv(L, 64), 64, 0, st>>>(m, L, cmax, gcnt, wsum, wcnt, out_mean,
                                                        out_nclust, out_minsize);
     ccg_timer_stop(ctx, t_all, st);
