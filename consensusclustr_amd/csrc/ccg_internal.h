@@ -24,6 +24,7 @@ enum ccg_ws_slot {
     WS_SIL_A,        // silhouette accumulators
     WS_SIL_B,        // silhouette centroids
     WS_COC_A,        // co-cluster column tables
+    WS_COC_B,        // co-cluster fused-path slot tables
     WS_MAP_A,        // map-back first-position scratch
     WS_HOST_A,       // host-API staging 1
     WS_HOST_B,       // host-API staging 2

@@ -244,11 +244,18 @@ def test_cocluster_golden(engine, golden, name):
     assert np.array_equal(r["dist"], g["dist"], equal_nan=True)  # bitwise, NaN where both == 0
 
 
-@pytest.mark.parametrize("B,N,C", [(100, 700, 12), (7, 300, 255), (257, 513, 3)])
+@pytest.mark.parametrize("B,N,C", [(100, 700, 12), (7, 300, 255), (257, 513, 3), (1000, 1024, 40),
+                                   (16383, 64, 3), (300, 2048, 17), (33, 1028, 31)])
 def test_cocluster_vs_oracle(engine, B, N, C):
+    """N % 4 == 0 and B <= 16383 take the fused one-hot kernel (co + 16384*both in
+    one accumulator); the others the two-GEMM kernel.  Edge cases: an all-unsampled
+    column (no K slots), a column using label 255 (16 slots), B at the fused limit."""
     rng = np.random.default_rng(B * N)
     A = rng.integers(1, C + 1, (B, N))
     A[rng.random((B, N)) < 0.1] = -1
+    A[0, :] = -1
+    if B > 2:
+        A[1, ::7] = 255
     r = engine.cocluster(_to_u8(A))
     o = O.cocluster(A)
     assert np.array_equal(r["co"], o["co"].astype(np.uint16))
