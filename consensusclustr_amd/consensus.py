@@ -139,6 +139,23 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
     raise ValueError("mode must be 'robust' or 'granular'")
 
 
+def subcluster_bootstrap_knn(pcas, boot_idx, kmax=20, engine=None):
+    """The kNN step of every subcluster's bootstrap in ONE batched call.
+
+    iterate=TRUE (R/consensusClust.R:541-566) re-runs consensusClust on each
+    cluster with > minSize cells; each run starts with its own bootstrap loop
+    (CS1 -> getClustAssignments, :391-400 / :650-658) on a small N_c x d_c PC
+    matrix.  The engine searches all of them together (BASELINE config 5):
+    pcas: list of N_c x d_c PC matrices (d_c may differ; smaller ones are
+    zero-padded); boot_idx: list of index arrays into each pca (R's sample()
+    - 1).  Returns a list of n_c x kmax int32 bootstrap-row indices, each
+    identical to eng.knn_boot(pcas[c], boot_idx[c], kmax).
+    """
+    eng = engine or default_engine()
+    mats = [np.asarray(p_, dtype=np.float64)[np.asarray(b_, dtype=np.int64)] for p_, b_ in zip(pcas, boot_idx)]
+    return [idx for idx, _ in eng.knn_segments(mats, kmax=kmax, want_dist=False)]
+
+
 def assignment_matrix(columns):
     """do.call(cbind, ...) (:404) with NA -> -1 (:408), as the uint8 B x N
     column-major matrix of the C ABI (0 = not sampled)."""

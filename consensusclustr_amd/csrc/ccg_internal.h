@@ -35,6 +35,7 @@ enum ccg_ws_slot {
     WS_ORDER,        // kNN spatial ordering (bucket histogram, permutation)
     WS_FB_D,         // kNN fallback per-range lists (keys)
     WS_FB_I,         // kNN fallback per-range lists (ids)
+    WS_SEGS,         // kNN batched-segment plan (offsets, blocks, positions)
     WS_NSLOTS
 };
 

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "ccg_internal.h"
 
@@ -219,7 +220,8 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
                                   double* __restrict__ inv_scale2) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in spatial order
     if (r >= npad) return;
-    const int64_t src = r < n ? perm[r] : 0;
+    const int64_t src = r < n ? perm[r] : -1;  // -1: padding position (segment padding or r >= n)
+    const bool valid = src >= 0;
     const int e = knn_scale_exp(maxabs_bits);
     if (r == 0) *inv_scale2 = ldexp(1.0, -2 * e);
     _Float16 hv[KSTEPS * 32];  // [h][hi s..][lo s..] flattened below
@@ -227,7 +229,7 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
 #pragma unroll
     for (int k = 0; k < KSTEPS * 16; ++k) {
         double xs = 0.0;
-        if (r < n && k < d) {
+        if (valid && k < d) {
             const double x = rows[src * d + k];
             nr += x * x;
             xs = ldexp(x, e);
@@ -241,7 +243,7 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
     uint4* out = img + r * (KSTEPS * 4);
 #pragma unroll
     for (int c = 0; c < KSTEPS * 4; ++c) out[c] = *reinterpret_cast<const uint4*>(&hv[c * 8]);
-    nrm[r] = (r < n) ? (float)(-0.5 * ldexp(nr, 2 * e)) : -INFINITY;
+    nrm[r] = valid ? (float)(-0.5 * ldexp(nr, 2 * e)) : -INFINITY;
 }
 
 template <int KSTEPS>
@@ -387,7 +389,8 @@ template <int KSTEPS, int KP, int EXP = 0, int QC = KNN_QCAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(const uint4* __restrict__ img,
                                                            const float* __restrict__ nrm, int n, int nchunks,
                                                            int* __restrict__ cand_idx,
-                                                           float* __restrict__ cand_thr) {
+                                                           float* __restrict__ cand_thr,
+                                                           const int4* __restrict__ blk) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
     constexpr int ROWB = KSTEPS * 64;               // bytes per row
     constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage (no norms)
@@ -409,9 +412,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
     const int bx = xcd_block(blockIdx.x, gridDim.x);
+    // the block's reference chunks [cl, ch) and query limit qhi: the whole
+    // image, or (batched segments) its own segment
+    int cl = 0, ch = nchunks, qhi = n;
+    if (blk) {
+        const int4 bi = blk[bx];
+        cl = bi.x;
+        ch = bi.y;
+        qhi = bi.z;
+    }
     const int q0 = bx * KNN_QPB + wave * 32;
     const int q = q0 + col;
-    const int qrow = q < n ? q : n - 1;
+    const int qrow = q < qhi ? q : qhi - 1;
 
     h8 qh[KSTEPS], ql[KSTEPS];
     {
@@ -462,8 +474,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // block's own position: near neighbours arrive first, the threshold tightens
     // within a few tiles and later tiles rarely insert (the order only changes
     // speed; certification makes the result exact for any order).
-    const int c0 = min((int)(bx * KNN_QPB) / KNN_CHUNK, nchunks - 1);
-    const int Lc = c0, Rc = nchunks - 1 - c0, Mc = min(Lc, Rc);
+    const int c0 = min((int)(bx * KNN_QPB) / KNN_CHUNK, ch - 1);
+    const int Lc = c0 - cl, Rc = ch - 1 - c0, Mc = min(Lc, Rc);
+    const int nck = ch - cl;
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
     float T = -INFINITY;  // max of both halves' thresholds (see below)
     int qc = 0;           // this lane's queued candidates
@@ -487,10 +500,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     KNN_STAGE_GLDS(0, chunk_at(0));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int k = 0; k < nchunks; ++k) {
+    for (int k = 0; k < nck; ++k) {
         const int b = k & 1;
         const int c = chunk_at(k);
-        if (k + 1 < nchunks && EXP != 3) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
+        if (k + 1 < nck && EXP != 3) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
 #pragma nounroll  // unrolling the two tiles doubles live registers (248 vs 162 VGPRs)
         for (int tau = 0; tau < 2; ++tau) {
             const int row = tau * 32 + col;
@@ -573,7 +586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #undef KNN_STAGE_GLDS
 #undef chunk_at
 #undef lds
-    if (q < n) {
+    if (q < qhi) {
         int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
 #pragma unroll
         for (int t = 0; t < KP; ++t) out[t] = li[t];
@@ -582,6 +595,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 }
 
 // -------------------------------------------------------------- certify --
+// segment s of global row q: seg_off[s] <= q < seg_off[s+1] (binary search)
+__device__ __forceinline__ int knn_seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t q) {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (seg_off[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 __device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
     return (a < b) || (a == b && ia < ib);
 }
@@ -615,11 +638,13 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
     const double* __restrict__ inv_scale2, double err_ulps, const int* __restrict__ perm,
     int32_t* __restrict__ out_idx, double* __restrict__ out_dist, int* __restrict__ fail_list,
-    int* __restrict__ fail_count) {
+    int* __restrict__ fail_count, int npos, const int64_t* __restrict__ seg_off, int nseg) {
     const int lane = threadIdx.x & 63;
-    const int qs = blockIdx.x * 4 + (threadIdx.x >> 6);  // screening order
-    if (qs >= n) return;
+    const int qs = blockIdx.x * 4 + (threadIdx.x >> 6);  // screening position
+    if (qs >= npos) return;
     const int q = perm ? perm[qs] : qs;                   // bootstrap row
+    if (q < 0) return;                                    // segment padding
+    const int base = seg_off ? (int)seg_off[knn_seg_of(seg_off, nseg, q)] : 0;  // output ids are segment-local
     const double* x = rows + (int64_t)q * d;
     int j = (lane < 2 * KP) ? cand_idx[(int64_t)qs * 2 * KP + lane] : -1;
     if (j >= 0 && perm) j = perm[j];
@@ -669,7 +694,7 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     }
     if (ok) {
         if (lane < kmax) {
-            out_idx[(int64_t)q * kmax + lane] = id;
+            out_idx[(int64_t)q * kmax + lane] = id - base;
             if (out_dist) out_dist[(int64_t)q * kmax + lane] = sqrt(key);
         }
     } else if (lane == 0) {
@@ -696,17 +721,23 @@ template <int DMAX>
 __global__ __launch_bounds__(256) void knn_fallback_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
-    double* __restrict__ lst_d, int* __restrict__ lst_i) {
+    double* __restrict__ lst_d, int* __restrict__ lst_i, const int64_t* __restrict__ seg_off, int nseg) {
     __shared__ double sd[4][KNN_FB_K];
     __shared__ int si[4][KNN_FB_K];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nfail = *fail_count;
     const int S = knn_fb_splits(nfail, slots);
-    const int span = (n + S - 1) / S;
     for (int64_t w = blockIdx.x; w < (int64_t)nfail * S; w += gridDim.x) {
         const int f = (int)(w / S), sp = (int)(w - (int64_t)f * S);
         const int q = fail_list[f];
-        const int j0 = sp * span, j1 = min(n, j0 + span);
+        int s0 = 0, s1 = n;  // the row's reference range (its segment)
+        if (seg_off) {
+            const int sg = knn_seg_of(seg_off, nseg, q);
+            s0 = (int)seg_off[sg];
+            s1 = (int)seg_off[sg + 1];
+        }
+        const int span = (s1 - s0 + S - 1) / S;
+        const int j0 = s0 + sp * span, j1 = min(s1, j0 + span);
         double xq[DMAX];
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
@@ -809,12 +840,13 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
 __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
     int kmax, const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
     const double* __restrict__ lst_d, const int* __restrict__ lst_i,
-    int32_t* __restrict__ out_idx, double* __restrict__ out_dist) {
+    int32_t* __restrict__ out_idx, double* __restrict__ out_dist, const int64_t* __restrict__ seg_off, int nseg) {
     const int lane = threadIdx.x;
     const int nfail = *fail_count;
     const int S = knn_fb_splits(nfail, slots);
     for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
         const int q = fail_list[f];
+        const int base = seg_off ? (int)seg_off[knn_seg_of(seg_off, nseg, q)] : 0;
         const double* ld = lst_d + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
         const int* li = lst_i + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
         int pos = 0;
@@ -837,7 +869,7 @@ __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
                 }
             }
             if (lane == 0) {
-                out_idx[(int64_t)q * kmax + r] = bi;
+                out_idx[(int64_t)q * kmax + r] = bi - base;
                 if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
             }
             if (lane < S && mi == bi && mk == bk) ++pos;
@@ -889,19 +921,23 @@ extern "C" int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, i
     return CCG_OK;
 }
 
-extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
-                                int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
-                                void* stream) {
-    CCG_REQUIRE(ctx && rows && out_idx, "ccg_knn_rows_dev: NULL argument");
-    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_rows_dev: d=%d must be in [1, 63]", d);
-    CCG_REQUIRE(n >= 2 && n < (1LL << 30), "ccg_knn_rows_dev: n=%lld out of range", (long long)n);
-    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
-                "ccg_knn_rows_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
-    hipStream_t st = ccg_pick_stream(ctx, stream);
+// Batched-segment description (ccg_knn_segments_dev): screening positions
+// are the segments laid end to end, each padded to a multiple of KNN_QPB.
+struct KnnSegs {
+    int nseg;
+    const int64_t* seg_off;  // device, nseg + 1 row offsets
+    int64_t npos;            // padded positions
+    const int* perm;         // device, position -> row (-1: padding)
+    const int4* blk;         // device, per query block: chunk range [x, y), query limit z
+};
+
+static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, int32_t* out_idx,
+                   double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg) {
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
-    const bool f32path = getenv("CCG_KNN_F32") != nullptr;  // A/B switch for the fp32-MFMA screen
-    int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * n * 2 * KP);
-    float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * n * 2);
+    const bool f32path = !sg && getenv("CCG_KNN_F32") != nullptr;  // A/B switch for the fp32-MFMA screen
+    const int64_t npos = sg ? sg->npos : n;                          // screening positions
+    int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * npos * 2 * KP);
+    float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * npos * 2);
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
     if (!cand_idx || !cand_thr || !fail_list || !misc) return CCG_ENOMEM;
@@ -913,7 +949,7 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     int rc = CCG_OK;
     double err_ulps;
-    int* order_perm = nullptr;  // screening order -> bootstrap row (identity on the fp32 path)
+    const int* order_perm = nullptr;  // screening position -> bootstrap row (identity on the fp32 path)
     if (f32path) {
         const int KS = pick_ks(d);
         const int64_t npad = ccg_cdiv(n, 32) * 32;
@@ -930,56 +966,47 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         err_ulps = KNN_ERR_ULPS;
     } else {
         const int KSTEPS = d <= 16 ? 1 : (d <= 32 ? 2 : 4);
-        const int64_t npad = ccg_cdiv(n, KNN_CHUNK) * KNN_CHUNK;
+        const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
         if (!img) return CCG_ENOMEM;
         float* nrm = (float*)((char*)img + (size_t)npad * 64 * KSTEPS);
-        const int64_t NB = 1LL << (3 * KNN_MORTON_BITS);
-        int64_t* hist = (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
-        if (!hist) return CCG_ENOMEM;
-        int64_t* cursor = hist + (NB + 1);
-        order_perm = (int*)(cursor + (NB + 1));
         unsigned* bnd = misc + 8;
         CCG_HIP(hipMemsetAsync(bnd, 0xff, 3 * sizeof(unsigned), st));
         CCG_HIP(hipMemsetAsync(bnd + 3, 0, 3 * sizeof(unsigned), st));
-        CCG_HIP(hipMemsetAsync(hist, 0, sizeof(int64_t) * (NB + 1), st));
         knn_rowstats_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 1024), 256), 256, 0, st>>>(rows, n, d,
                                                                                                     mbits, bnd);
-        knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
-        rc = ccg_scan_i64(ctx, hist, hist, NB, st);
-        if (rc) return rc;
-        CCG_HIP(hipMemcpyAsync(cursor, hist, sizeof(int64_t) * (NB + 1), hipMemcpyDeviceToDevice, st));
-        knn_bucket_scatter_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, cursor, order_perm);
+        if (sg) {
+            order_perm = sg->perm;  // segments keep their rows in input order
+        } else {
+            // spatial order: Morton buckets of the leading coordinates
+            const int64_t NB = 1LL << (3 * KNN_MORTON_BITS);
+            int64_t* hist =
+                (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
+            if (!hist) return CCG_ENOMEM;
+            int64_t* cursor = hist + (NB + 1);
+            int* perm = (int*)(cursor + (NB + 1));
+            CCG_HIP(hipMemsetAsync(hist, 0, sizeof(int64_t) * (NB + 1), st));
+            knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
+            rc = ccg_scan_i64(ctx, hist, hist, NB, st);
+            if (rc) return rc;
+            CCG_HIP(hipMemcpyAsync(cursor, hist, sizeof(int64_t) * (NB + 1), hipMemcpyDeviceToDevice, st));
+            knn_bucket_scatter_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, cursor, perm);
+            order_perm = perm;
+        }
         const unsigned pg = (unsigned)ccg_cdiv(npad, 256);
         if (KSTEPS == 1)
-            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
         else if (KSTEPS == 2)
-            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
         else
-            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, n, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
         const int nch = (int)(npad / KNN_CHUNK);
-        const unsigned grid = (unsigned)ccg_cdiv(n, KNN_QPB);
+        const unsigned grid = (unsigned)ccg_cdiv(npos, KNN_QPB);
+        const int4* blk = sg ? sg->blk : nullptr;
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
 #define CCG_SCREEN16(KS_, KP_) \
-    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr)
-        const char* exp_env = getenv("CCG_KNN_EXP");
-        const int kexp = exp_env ? atoi(exp_env) : 0;
-        if (kexp >= 1 && kexp <= 6 && KSTEPS == 2 && KP == KNN_KP) {
-            if (kexp == 4) {
-                unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                CCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_knn_dbg), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
-                knn_screen16_kernel<2, KNN_KP, 4><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-                CCG_HIP(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_knn_dbg), sizeof(z), 0, hipMemcpyDeviceToHost, st));
-                CCG_HIP(hipStreamSynchronize(st));
-                fprintf(stderr, "knn_dbg tiles_any=%llu enq=%llu flush_rounds=%llu inserts=%llu tile_waves=%llu\n",
-                        z[0], z[1], z[2], z[3], (unsigned long long)grid * 4 * nch * 2);
-            }
-            if (kexp == 1) knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-            if (kexp == 2) knn_screen16_kernel<2, KNN_KP, 2><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-            if (kexp == 3) knn_screen16_kernel<2, KNN_KP, 3><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-            if (kexp == 6) knn_screen16_kernel<2, KNN_KP, 0, 10><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-            if (kexp == 5) knn_screen16_kernel<2, KNN_KP, 0, 8><<<grid, 256, 0, st>>>(img, nrm, (int)n, nch, cand_idx, cand_thr);
-        } else if (KP == KNN_KP) {
+    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk)
+        if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
             else CCG_SCREEN16(4, KNN_KP);
@@ -993,10 +1020,12 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         err_ulps = KNN_ERR_ULPS_F16;
     }
     if (rc) return rc;
-#define CCG_CERTIFY(KP_, DM_)                                                                            \
-    knn_certify_kernel<KP_, DM_><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(                                \
+    const int64_t* seg_off = sg ? sg->seg_off : nullptr;
+    const int nseg = sg ? sg->nseg : 1;
+#define CCG_CERTIFY(KP_, DM_)                                                                             \
+    knn_certify_kernel<KP_, DM_><<<(unsigned)ccg_cdiv(npos, 4), 256, 0, st>>>(                              \
         rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist, \
-        fail_list, fail_count)
+        fail_list, fail_count, (int)npos, seg_off, nseg)
     if (KP == KNN_KP) {
         if (d <= 16) CCG_CERTIFY(KNN_KP, 16);
         else if (d <= 32) CCG_CERTIFY(KNN_KP, 32);
@@ -1013,15 +1042,15 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
     if (!fb_d || !fb_i) return CCG_ENOMEM;
     if (d <= 16)
         knn_fallback_kernel<16><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i);
+                                                      fb_d, fb_i, seg_off, nseg);
     else if (d <= 32)
         knn_fallback_kernel<32><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i);
+                                                      fb_d, fb_i, seg_off, nseg);
     else
         knn_fallback_kernel<64><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i);
+                                                      fb_d, fb_i, seg_off, nseg);
     knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
-                                                   out_dist);
+                                                   out_dist, seg_off, nseg);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {
@@ -1033,6 +1062,61 @@ extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int
         ctx->last_stats = *stats;
     }
     return CCG_OK;
+}
+
+extern "C" int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
+                                int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                                void* stream) {
+    CCG_REQUIRE(ctx && rows && out_idx, "ccg_knn_rows_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_rows_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(n >= 2 && n < (1LL << 30), "ccg_knn_rows_dev: n=%lld out of range", (long long)n);
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
+                "ccg_knn_rows_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
+    return knn_run(ctx, rows, n, d, kmax, out_idx, out_dist, stats, ccg_pick_stream(ctx, stream), nullptr);
+}
+
+extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d, const int64_t* seg_off,
+                                    int nseg, int kmax, int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                                    void* stream) {
+    CCG_REQUIRE(ctx && rows && seg_off && out_idx, "ccg_knn_segments_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_segments_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(nseg >= 1 && n >= 2 && n < (1LL << 30), "ccg_knn_segments_dev: bad sizes");
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG, "ccg_knn_segments_dev: kmax=%d must be in [1, %d]", kmax,
+                KNN_KP_BIG);
+    CCG_REQUIRE(seg_off[0] == 0 && seg_off[nseg] == n, "ccg_knn_segments_dev: seg_off must run from 0 to n");
+    // host plan: segment s occupies positions [po_s, po_s + n_s), po_s a multiple of KNN_QPB
+    std::vector<int64_t> po(nseg + 1, 0);
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t ns = seg_off[s + 1] - seg_off[s];
+        CCG_REQUIRE(ns >= kmax + 1, "ccg_knn_segments_dev: segment %d has %lld rows, needs >= kmax+1 = %d", s,
+                    (long long)ns, kmax + 1);
+        po[s + 1] = po[s] + ccg_cdiv(ns, KNN_QPB) * KNN_QPB;
+    }
+    const int64_t npos = po[nseg];
+    CCG_REQUIRE(npos < (1LL << 30), "ccg_knn_segments_dev: too many positions");
+    const int64_t nblk = npos / KNN_QPB;
+    std::vector<int> hperm(npos, -1);
+    std::vector<int4> hblk(nblk);
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t ns = seg_off[s + 1] - seg_off[s];
+        for (int64_t i = 0; i < ns; ++i) hperm[po[s] + i] = (int)(seg_off[s] + i);
+        const int cl = (int)(po[s] / KNN_CHUNK), ch = (int)((po[s] + ns + KNN_CHUNK - 1) / KNN_CHUNK);
+        for (int64_t b = po[s] / KNN_QPB; b < po[s + 1] / KNN_QPB; ++b)
+            hblk[b] = make_int4(cl, ch, (int)(po[s] + ns), 0);
+    }
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    char* tab = (char*)ccg_ws(ctx, WS_SEGS, sizeof(int64_t) * (nseg + 1) + sizeof(int) * npos + sizeof(int4) * nblk + 64);
+    if (!tab) return CCG_ENOMEM;
+    int64_t* d_off = (int64_t*)tab;
+    int4* d_blk = (int4*)(tab + ccg_cdiv(sizeof(int64_t) * (nseg + 1), 16) * 16);
+    int* d_perm = (int*)(d_blk + nblk);
+    CCG_HIP(hipMemcpyAsync(d_off, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(d_blk, hblk.data(), sizeof(int4) * nblk, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(d_perm, hperm.data(), sizeof(int) * npos, hipMemcpyHostToDevice, st));
+    KnnSegs sg{nseg, d_off, npos, d_perm, d_blk};
+    const int rc = knn_run(ctx, rows, n, d, kmax, out_idx, out_dist, stats, st, &sg);
+    CCG_HIP(hipStreamSynchronize(st));  // the host plan buffers must outlive the uploads
+    return rc;
 }
 
 extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
@@ -1070,5 +1154,26 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
     }
     if (stats) *stats = acc;
     ctx->last_stats = acc;
+    return CCG_OK;
+}
+
+extern "C" int ccg_knn_segments(ccg_ctx* ctx, const double* rows, int64_t n, int d, const int64_t* seg_off,
+                                int nseg, int kmax, int32_t* out_idx, double* out_dist, ccg_knn_stats* stats) {
+    CCG_REQUIRE(ctx && rows && seg_off && out_idx, "ccg_knn_segments: NULL argument");
+    CCG_REQUIRE(n >= 2 && d >= 1 && nseg >= 1, "ccg_knn_segments: bad sizes");
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    double* drows = (double*)ccg_ws(ctx, WS_HOST_A, sizeof(double) * n * d);
+    int32_t* dout = (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * n * kmax);
+    double* ddist = out_dist ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * n * kmax) : nullptr;
+    if (!drows || !dout || (out_dist && !ddist)) return CCG_ENOMEM;
+    CCG_HIP(hipMemcpyAsync(drows, rows, sizeof(double) * n * d, hipMemcpyHostToDevice, st));
+    ccg_knn_stats s;
+    const int rc = ccg_knn_segments_dev(ctx, drows, n, d, seg_off, nseg, kmax, dout, ddist, &s, st);
+    if (rc) return rc;
+    CCG_HIP(hipMemcpyAsync(out_idx, dout, sizeof(int32_t) * n * kmax, hipMemcpyDeviceToHost, st));
+    if (out_dist) CCG_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(double) * n * kmax, hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
+    if (stats) *stats = s;
     return CCG_OK;
 }

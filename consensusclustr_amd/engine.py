@@ -93,6 +93,30 @@ class Engine:
         self.last_knn_stats = (st.queries, st.fallback)
         return out, dist
 
+    def knn_segments(self, mats, kmax=20, want_dist=True):
+        """Batched kNN of independent row sets (ccg_knn_segments): the
+        iterate=TRUE subclusters' bootstrap matrices in one set of launches.
+
+        mats: list of (n_s, d_s) arrays; they are zero-padded to a common d
+        (padding dims do not change distances).  Returns a list of
+        (idx (n_s, kmax) int32 segment-local, dist (n_s, kmax) or None).
+        """
+        d = max(m.shape[1] for m in mats)
+        rows = np.zeros((sum(m.shape[0] for m in mats), d), np.float64)
+        off = np.zeros(len(mats) + 1, np.int64)
+        for s, m in enumerate(mats):
+            off[s + 1] = off[s] + m.shape[0]
+            rows[off[s]:off[s + 1], :m.shape[1]] = m
+        n = rows.shape[0]
+        out = np.empty((n, kmax), np.int32)
+        dist = np.empty((n, kmax), np.float64) if want_dist else None
+        st = _lib.ccg_knn_stats()
+        check(self.lib.ccg_knn_segments(self.ctx, _ptr(rows), n, d, _ptr(off), len(mats), kmax, _ptr(out),
+                                        _ptr(dist), ctypes.byref(st)))
+        self.last_knn_stats = (st.queries, st.fallback)
+        return [(out[off[s]:off[s + 1]], None if dist is None else dist[off[s]:off[s + 1]])
+                for s in range(len(mats))]
+
     def snn(self, knn_idx, k, type="number"):
         """SNN edges i<j sorted by (i, j) with weights (ccg_snn)."""
         knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
@@ -170,6 +194,17 @@ class Engine:
             self.last_knn_stats = (st.queries, st.fallback)
             return self.last_knn_stats
         return None
+
+    def knn_segments_t(self, rows, seg_off, kmax, out_idx, out_dist=None, stats=False):
+        """Device flavour: rows (n, d) tensor of concatenated segments, seg_off a
+        host int64 array of nseg+1 offsets; out_idx (n, kmax) segment-local."""
+        n, d = rows.shape
+        off = np.ascontiguousarray(seg_off, dtype=np.int64)
+        st = _lib.ccg_knn_stats()
+        check(self.lib.ccg_knn_segments_dev(self.ctx, _ptr(rows), n, d, _ptr(off), off.size - 1, kmax,
+                                            _ptr(out_idx), _ptr(out_dist), ctypes.byref(st), _stream()))
+        self.last_knn_stats = (st.queries, st.fallback)
+        return self.last_knn_stats if stats else None
 
     def snn_t(self, knn_idx, k, type, out_i, out_j, out_w, d_nedges):
         n, ks = knn_idx.shape

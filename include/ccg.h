@@ -105,6 +105,26 @@ int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
                      int kmax, int32_t* out_idx, double* out_dist,
                      ccg_knn_stats* stats, void* stream);
 
+/* Batched kNN over independent segments: the iterate=TRUE subclustering
+ * (R/consensusClust.R:541-566, BASELINE config 5) runs one bootstrap loop per
+ * subcluster; their (small) bootstrap matrices are searched in ONE set of
+ * launches.  rows: the segments' row-major n_s x d matrices concatenated
+ * (n = sum n_s rows, one common d -- zero-pad smaller pcNum; padding dims do
+ * not change distances).  seg_off: HOST array of nseg+1 row offsets (0 ..
+ * n).  Each row's neighbours are searched within its own segment only and
+ * returned as segment-local 0-based indices, in the same order and tie
+ * contract as ccg_knn_rows_dev.  Requires n_s >= kmax + 1 for every segment.
+ * rows / out_idx / out_dist are device pointers; the call uploads a small
+ * plan and synchronises `stream` before returning. */
+int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
+                         const int64_t* seg_off, int nseg, int kmax,
+                         int32_t* out_idx, double* out_dist,
+                         ccg_knn_stats* stats, void* stream);
+/* Host flavour of ccg_knn_segments_dev (all pointers host). */
+int ccg_knn_segments(ccg_ctx* ctx, const double* rows, int64_t n, int d,
+                     const int64_t* seg_off, int nseg, int kmax,
+                     int32_t* out_idx, double* out_dist, ccg_knn_stats* stats);
+
 /* ---------------------------------------------------------------- SNN -- */
 /* Shared-nearest-neighbour graph from the first k columns of an n x kstride
  * int32 0-based neighbour matrix (self excluded).  Edges i < j sorted by

@@ -93,6 +93,44 @@ def test_knn_heavy_duplication_forces_fallback(engine):
     assert engine.last_knn_stats[1] > 0
 
 
+def test_knn_segments_vs_oracle(engine):
+    """iterate=TRUE (BASELINE cfg 5): many subclusters' bootstrap matrices in
+    one batched call; each segment must equal its own independent kNN."""
+    rng = np.random.default_rng(41)
+    sizes = [21, 64, 127, 128, 129, 900, 2000, 333, 4100]
+    dims = [5, 7, 12, 15, 5, 10, 15, 8, 14]
+    mats = []
+    for n_s, d_s in zip(sizes, dims):
+        X = _mixture(rng, n_s, d_s, C=4)
+        if n_s > 300:
+            X[: n_s // 10] = X[n_s // 10: 2 * (n_s // 10)]  # bootstrap-like duplicates
+        mats.append(X)
+    res = engine.knn_segments(mats, kmax=20)
+    for X, (idx, dist) in zip(mats, res):
+        oi, od = O.knn(X, 20)
+        assert np.array_equal(idx, oi)
+        np.testing.assert_allclose(dist, od, rtol=RTOL, atol=1e-12)
+
+
+def test_knn_segments_single_equals_rows(engine):
+    rng = np.random.default_rng(42)
+    X = _mixture(rng, 3000, 30)
+    (idx, _), = engine.knn_segments([X], kmax=15)
+    ref, _ = engine.knn_boot(X, np.arange(3000), kmax=15)
+    assert np.array_equal(idx, ref[0])
+
+
+def test_subcluster_bootstrap_knn_matches_per_cluster(engine):
+    from consensusclustr_amd.consensus import subcluster_bootstrap_knn
+    rng = np.random.default_rng(43)
+    pcas = [_mixture(rng, n_c, d_c, C=3) for n_c, d_c in ((400, 5), (1500, 9), (90, 6), (3000, 13))]
+    boots = [rng.integers(0, p_.shape[0], int(0.9 * p_.shape[0])) for p_ in pcas]
+    got = subcluster_bootstrap_knn(pcas, boots, kmax=20, engine=engine)
+    for p_, b_, g in zip(pcas, boots, got):
+        ref, _ = engine.knn_boot(p_, b_, kmax=20)
+        assert np.array_equal(g, ref[0])
+
+
 def test_knn_rejects_bad_args(engine):
     from consensusclustr_amd import CcgError
     with pytest.raises(CcgError):
