@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "bootstraps/sec (kNN+SNN+co-cluster) at 100k cells, 1/2/4/8 MI355X"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_F16_TFLOPS = 2500.0   # dense fp16/bf16 MFMA (the screen's v_mfma_f32_32x32x16_f16)
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA (2x bf16 dense 2.5 PF)
 PEAK_HBM_GBS = 8000.0
 K_NUM = (10, 15, 20)
@@ -91,6 +92,16 @@ def synth_labels(torch, pop_boot, L, dev, seed):
     flip = torch.rand(L, n, device=dev, generator=g) < 0.05
     rnd = (torch.rand(L, n, device=dev, generator=g) * Cl).long() + 1
     return torch.where(flip, rnd, lab).to(torch.int32)
+
+
+def A_full_C(torch, A_local, G):
+    """sum over all G*B columns of C_b (= max label per column), via one
+    all-reduce of the per-rank sums (labels are codes 1..C_b)."""
+    c = A_local.max(dim=1).values.to(torch.int64).sum()
+    if G > 1:
+        import torch.distributed as dist
+        dist.all_reduce(c)
+    return int(c.item())
 
 
 def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
@@ -237,8 +248,14 @@ def main():
 
     value = G * B * args.steps / el
     ms_screen = kt["knn_screen"][0] / max(kt["knn_screen"][1], 1)
-    flops = 2.0 * n * n * d  # kNN F = 2 n^2 d per bootstrap
+    flops = 2.0 * n * n * d  # kNN F = 2 n^2 d per bootstrap (one screen launch)
     achieved = flops / (ms_screen * 1e-3) / 1e12
+    # the screen runs on the fp16 MFMA pipe: 3 products (hi.hi, hi.lo, lo.hi)
+    # per 16-dim block, d padded to 16*ceil(d/16)
+    mfma_exec = 3 * 2.0 * n * n * (16 * ((d + 15) // 16))
+    # co-cluster roofline: OPS = 2 * P * (sum_b C_b + B) over this rank's slab
+    colC = A_full_C(torch, A_local, G)
+    coc_ops = 2.0 * P * (colC + G * B)
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
@@ -256,7 +273,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64",
+        "dtype_detail": "kNN order exact in f64 (fp16 hi/lo x3 MFMA screen, f32 accumulate, f64 certify); "
+                        "silhouette f64 with fixed-point sums; co-cluster int8 MFMA, int32 counts",
         "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA; synthetic clusterings in place of host Leiden",
         "config": {
             "workload": "BASELINE cfg3 shapes: 100k cells x 30 PCs, robust mode, kNum 10/15/20 x 20 resolutions; "
@@ -265,15 +284,29 @@ def main():
             "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}",
         },
         "roofline": {
-            "kernel": "knn_screen (v_mfma_f32_32x32x2_f32)",
+            "kernel": "knn_screen16_kernel (fp16 hi/lo split, v_mfma_f32_32x32x16_f16)",
             "bound": "mfma",
             "achieved": round(achieved, 2),
-            "peak": PEAK_FP32_TFLOPS,
+            "peak": PEAK_F16_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "frac": round(achieved / PEAK_F16_TFLOPS, 4),
             "traffic": traffic,
-            "algorithmic_per_launch": f"2*n^2*d = {flops:.3e} flop (n={n}, d={d})",
+            "algorithmic_per_launch": f"2*n^2*d = {flops:.3e} flop (n={n}, d={d}), SURVEY 8(d)",
             "avg_launch_ms": round(ms_screen, 4),
+            "mfma_flops_executed_per_launch": mfma_exec,
+            "mfma_pipe_frac": round(mfma_exec / (ms_screen * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
+            "fp32_equivalent_frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+        },
+        "roofline_cocluster": {
+            "kernel": "cof_tile_kernel (one-hot int8, v_mfma_i32_32x32x32_i8)",
+            "bound": "mfma",
+            "achieved": round(coc_ops / (coc_ms * 1e-3) / 1e12, 2),
+            "peak": PEAK_I8_TOPS,
+            "unit": "TOP/s",
+            "frac": round(coc_ops / (coc_ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
+            "algorithmic_per_launch": f"2*P*(sum C_b + B) = {coc_ops:.3e} (P={P} pairs in this slab, "
+                                      f"sum C_b={colC}, B={G * B})",
+            "avg_launch_ms": round(coc_ms, 4),
         },
         "kernel_ms_per_step": per_step,
         "cocluster_avg_ms": round(coc_ms, 3),
