@@ -58,6 +58,11 @@ class Engine:
         except Exception:
             pass
 
+    def torch_stream(self):
+        """The context's own HIP stream (ccg_stream) as a torch stream object."""
+        import torch
+        return torch.cuda.ExternalStream(self.lib.ccg_stream(self.ctx))
+
     def synchronize(self):
         check(self.lib.ccg_synchronize(self.ctx))
 
