@@ -108,6 +108,27 @@ __device__ __forceinline__ void list_insert(float (&lv)[KP], int (&li)[KP], floa
     }
 }
 
+// Insert (v, id) into a descending register list (v > lv[KP-1] assumed) by
+// "position + shift": the keep-flags c_t = !(v > lv[t]) are independent
+// compares, and each slot is then a two-level select
+// (keep / take v / take the left neighbour), so the dependency depth is 3
+// instead of the KP-long compare-swap chain of list_insert.
+template <int KP>
+__device__ __forceinline__ void list_insert_par(float (&lv)[KP], int (&li)[KP], float v, int id) {
+    bool keep[KP];
+#pragma unroll
+    for (int t = 0; t < KP; ++t) keep[t] = !(v > lv[t]);  // slot t keeps its entry (ties keep the old one)
+#pragma unroll
+    for (int t = KP - 1; t >= 1; --t) {
+        const float sv = keep[t - 1] ? v : lv[t - 1];
+        const int si = keep[t - 1] ? id : li[t - 1];
+        lv[t] = keep[t] ? lv[t] : sv;
+        li[t] = keep[t] ? li[t] : si;
+    }
+    lv[0] = keep[0] ? lv[0] : v;
+    li[0] = keep[0] ? li[0] : id;
+}
+
 template <int KS>
 __device__ __forceinline__ void load_frag(const float* __restrict__ p, float (&f)[KS]) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
@@ -489,7 +510,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 const float v_ = __uint_as_float(e_.x);                               \
                 if (v_ > T) {                                                         \
                     if (EXP == 4) atomicAdd(&g_knn_dbg[3], 1ull);                     \
-                    list_insert<KP>(lv, li, v_, (int)e_.y);                           \
+                    list_insert_par<KP>(lv, li, v_, (int)e_.y);                       \
                     thr = lv[KP - 1];                                                 \
                     T = fmaxf(T, thr);                                                \
                 }                                                                     \
