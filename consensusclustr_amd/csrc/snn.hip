@@ -74,23 +74,60 @@ __global__ void snn_fill_hosts(const int32_t* __restrict__ knn, int64_t n, int k
     hosts[p] = make_int2((int)h, r + 1);
 }
 
+// Sort every host list by host id (one wave per list; rank of each entry =
+// number of smaller ids, ids in a list are distinct) into hosts_s, and record
+// where each kNN entry landed: bp[h * kmax + r - 1] = position of h in
+// hosts_s(knn[h][r - 1]), split[x] = number of hosts of x below x.  The
+// build then starts member s of node j at the entry after j itself, so it
+// only ever fetches partners p > j.
+#define SNN_SORT_LDS 512
+__global__ __launch_bounds__(256) void snn_sort_hosts(const int64_t* __restrict__ hoff, int64_t n, int kmax,
+                                                      const int2* __restrict__ hosts, int2* __restrict__ hosts_s,
+                                                      int* __restrict__ bp, int* __restrict__ split) {
+    __shared__ int buf_all[4][SNN_SORT_LDS];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* buf = buf_all[wv];
+    for (int64_t x = (int64_t)blockIdx.x * 4 + wv; x < n; x += (int64_t)gridDim.x * 4) {
+        const int64_t h0 = hoff[x];
+        const int len = (int)(hoff[x + 1] - h0);
+        const int2* src = hosts + h0;
+        const bool in_lds = len <= SNN_SORT_LDS;
+        if (in_lds)
+            for (int c = lane; c < len; c += 64) buf[c] = src[c].x;
+        WAVE_LDS_SYNC();
+        int below = 0;
+        for (int c = lane; c < len; c += 64) {
+            const int2 e = src[c];
+            int rank = 0;
+            if (in_lds)
+                for (int i = 0; i < len; ++i) rank += buf[i] < e.x;
+            else
+                for (int i = 0; i < len; ++i) rank += src[i].x < e.x;
+            hosts_s[h0 + rank] = e;
+            bp[(int64_t)e.x * kmax + e.y - 1] = rank;
+            below += e.x < x;
+        }
+        for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+        if (lane == 0) split[x] = below;
+        WAVE_LDS_SYNC();
+    }
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     const int lane = threadIdx.x & 63;
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-// Contribution of one shared member with ranks (rj, rp) to the packed word.
+// Contribution of one shared member with ranks (rj, rp) to the packed word
+// (branch-free: byte t is live iff max(rj, rp) <= kk[t]).
 __device__ __forceinline__ unsigned snn_contrib(const SnnSpec& sp, int rj, int rp) {
     const int m = rj > rp ? rj : rp;
-    unsigned w = sp.init;
+    unsigned live = 0;
 #pragma unroll
-    for (int t = 0; t < SNN_MAXK; ++t) {
-        if (t < sp.nk && m <= sp.kk[t]) {
-            if (sp.type == CCG_SNN_NUMBER) w += 1u << (8 * t);
-            else w = (w & ~(0xFFu << (8 * t))) | ((unsigned)(rj + rp) << (8 * t));
-        }
-    }
-    return w;
+    for (int t = 0; t < SNN_MAXK; ++t) live |= (t < sp.nk && m <= sp.kk[t]) ? (0xFFu << (8 * t)) : 0u;
+    const unsigned num = live & 0x01010101u;
+    const unsigned rank = (((unsigned)(rj + rp) * 0x01010101u) & live) | ~live;
+    return sp.type == CCG_SNN_NUMBER ? num : rank;
 }
 
 __device__ __forceinline__ unsigned bytewise_min(unsigned a, unsigned b) {
@@ -161,11 +198,12 @@ __device__ __forceinline__ double graph_weight(const SnnSpec& sp, unsigned v, in
 }
 
 // ---------------------------------------------------------------- wave path --
-// Pass 1 (build): one wave per node builds a 2048-slot LDS hash table of
-// 64-bit slots (partner p << 32 | packed per-graph values): a new partner
-// costs one CAS, a repeat one add.  The table is compacted, bitonic-sorted by
-// p and parked in a fixed-capacity scratch row; per-graph edge counts go to
-// cnt[t][j].  Nodes with more than SNN_WCAP partners go to the overflow list.
+// Pass 1 (build): one wave per node builds an LDS hash table of 64-bit slots
+// (partner p << 32 | packed per-graph values): a new partner costs one CAS, a
+// repeat one add.  The table is compacted, sorted by p and parked in a
+// fixed-capacity scratch row; per-graph edge counts go to cnt[t][j].  It
+// serves the nodes the sort path below cannot stage (more than 1024 items);
+// nodes beyond its capacity go to the block path.
 // Pass 2 (emit) streams the sorted rows into the caller's edge arrays.
 #define SNN_WCAP (SNN_WT * 3 / 4)
 #define SNN_EMPTY64 (~0ull)
@@ -199,6 +237,54 @@ __device__ __forceinline__ bool table_insert64(unsigned long long* tab, int p, u
         s = (s + 1) & (T - 1);
     }
     return false;
+}
+
+template <int WT>
+constexpr int snn_log2() {
+    int b = 0;
+    while ((1 << b) < WT) ++b;
+    return b;
+}
+
+// One item per active lane into a WT-slot table, probing with CAS only (a
+// CAS on an empty slot inserts, a returned equal key means the partner is
+// already there).  The loop runs while any lane still has its item, so the
+// control flow stays wave-uniform.  Returns false on lanes that found no slot.
+template <int WT>
+__device__ __forceinline__ bool wave_insert64(unsigned long long* tab, int p, unsigned c, bool active, int type) {
+    unsigned s = snn_hash(p, snn_log2<WT>());
+    const unsigned long long want = ((unsigned long long)(unsigned)p << 32) | c;
+    int probes = 0;
+    bool ok = true;
+    while (__any(active)) {
+        if (active) {
+            unsigned long long old = atomicCAS(&tab[s], SNN_EMPTY64, want);
+            if (old == SNN_EMPTY64) {
+                active = false;
+            } else if ((unsigned)(old >> 32) == (unsigned)p) {
+                if (type == CCG_SNN_NUMBER) {
+                    atomicAdd(&tab[s], (unsigned long long)c);  // per-byte counts never carry
+                } else {
+                    while (true) {
+                        const unsigned nv = bytewise_min((unsigned)old, c);
+                        if (nv == (unsigned)old) break;
+                        const unsigned long long nw = (old & 0xFFFFFFFF00000000ull) | nv;
+                        const unsigned long long prev = atomicCAS(&tab[s], old, nw);
+                        if (prev == old) break;
+                        old = prev;
+                    }
+                }
+                active = false;
+            } else {
+                s = (s + 1) & (WT - 1);
+                if (++probes == WT) {
+                    active = false;
+                    ok = false;
+                }
+            }
+        }
+    }
+    return ok;
 }
 
 // Sort a node's u compacted entries (tab[0..u), distinct partners p in (j, n))
@@ -257,34 +343,63 @@ __device__ __forceinline__ void snn_bucket_store(unsigned long long* tab, int u,
     }
 }
 
-__global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
-    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
+template <int WT>
+struct SnnWaveLds {
+    unsigned long long tab[WT];
+    union {
+        struct {  // gather phase: member headers
+            long long h0[64];
+            long long hend[64];
+            int cur[64];
+            int pre[65];
+        } g;
+        struct {  // sort phase: bucket histogram / starts
+            int hist[SNN_NB];
+            int bst[SNN_NB + 1];
+        } s;
+    } u;
+};
+
+// Tier kernel: WT-slot tables (WT = 1024: 4 waves/SIMD, fits ~96% of nodes at
+// cfg3; WT = 2048 for the overflow list of the first tier).  in_list = nullptr
+// walks every node, else the in_count nodes of in_list.
+template <int WT>
+__global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_build_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
+    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
+    int64_t* __restrict__ cnt, const int* __restrict__ in_list, const int* __restrict__ in_count,
     int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
     int* __restrict__ ucount, int exp) {
-    __shared__ unsigned long long tab_all[SNN_WAVES][SNN_WT];
-    __shared__ int m_pre[SNN_WAVES][65];
-    __shared__ int m_hist[SNN_WAVES][SNN_NB];
-    __shared__ int m_bst[SNN_WAVES][SNN_NB + 1];
-    __shared__ long long m_h0[SNN_WAVES][64];
-    __shared__ int m_cur[SNN_WAVES][64];
+    __shared__ SnnWaveLds<WT> lds_all[SNN_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    unsigned long long* tab = tab_all[wv];
+    SnnWaveLds<WT>& L = lds_all[wv];
+    unsigned long long* tab = L.tab;
     const int kmax = sp.kk[sp.nk - 1];
-    constexpr int BITS = 11;  // log2(SNN_WT)
-    for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
-        for (int s = lane; s < SNN_WT; s += 64) tab[s] = SNN_EMPTY64;
-        WAVE_LDS_SYNC();
-        // Flat gather: item t of M = sum over members i of (|hosts(cur_i)| + 1)
-        // (the +1 is cur_i itself, rank 0).  Member headers are loaded
-        // lane-parallel once; host entries are fetched one round ahead so
-        // their latency hides behind the current round's LDS inserts.
+    constexpr int CAP = WT * 3 / 4;
+    const int64_t nn = in_list ? (int64_t)*in_count : n;
+    for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
+        const int64_t j = in_list ? (int64_t)in_list[f] : f;
+        for (int s = lane; s < WT; s += 64) tab[s] = SNN_EMPTY64;
+        // Flat gather over the partners p > j only: member 0 (j itself) from
+        // its first host above j, member i (s = knn[j][i-1]) from the entry
+        // after j in the sorted hosts(s), plus s itself (rank 0) when s > j.
+        // Item t of M = sum of member lengths; host entries are fetched one
+        // round ahead so their latency hides behind the current LDS inserts.
         int mcur = 0, mlen = 0;
-        long long mh0 = 0;
+        long long mh0 = 0, mend = 0;
         if (lane <= kmax) {
-            mcur = lane == 0 ? (int)j : knn[j * kstride + lane - 1];
-            mh0 = hoff[mcur];
-            mlen = (int)(hoff[mcur + 1] - mh0) + 1;
+            if (lane == 0) {
+                mcur = (int)j;
+                mh0 = hoff[j] + split[j];
+                mend = hoff[j + 1];
+                mlen = (int)(mend - mh0);
+            } else {
+                mcur = knn[j * kstride + lane - 1];
+                const int q = bp[j * kmax + lane - 1];
+                mh0 = hoff[mcur] + q + 1;
+                mend = hoff[mcur + 1];
+                mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+            }
         }
         int incl = mlen;
 #pragma unroll
@@ -293,15 +408,13 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             if (lane >= o) incl += y;
         }
         const int M = __shfl(incl, 63);
-        int* pre = m_pre[wv];
-        long long* mh = m_h0[wv];
-        int* mc = m_cur[wv];
         if (lane <= kmax) {
-            pre[lane] = incl - mlen;
-            mh[lane] = mh0;
-            mc[lane] = mcur;
+            L.u.g.pre[lane] = incl - mlen;
+            L.u.g.h0[lane] = mh0;
+            L.u.g.hend[lane] = mend;
+            L.u.g.cur[lane] = mcur;
         }
-        if (lane == 0) pre[kmax + 1] = M;
+        if (lane == 0) L.u.g.pre[kmax + 1] = M;
         WAVE_LDS_SYNC();
         int mi = 0;
         auto fetch = [&](int t, int& p, int& rp, int& ii) {
@@ -309,14 +422,20 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             rp = 0;
             ii = 0;
             if (t < M) {
-                while (pre[mi + 1] <= t) ++mi;
+                while (L.u.g.pre[mi + 1] <= t) ++mi;
                 ii = mi;
-                if (t == pre[mi + 1] - 1) {
-                    p = mc[mi];
+                const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
+                if (q < L.u.g.hend[mi]) {
+                    if (exp & 2) {
+                        p = (int)(j + 1 + (q * 7919) % (n - j));
+                        rp = (int)(q & 15) + 1;
+                    } else {
+                        const int2 hr = hosts_s[q];
+                        p = hr.x;
+                        rp = hr.y;
+                    }
                 } else {
-                    const int2 hr = hosts[mh[mi] + (t - pre[mi])];
-                    p = hr.x;
-                    rp = hr.y;
+                    p = L.u.g.cur[mi];
                 }
             }
         };
@@ -327,9 +446,9 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             int np, nrp, nii;
             fetch(t0 + 64 + lane, np, nrp, nii);
             bool ok = true;
-            if (p > j && !(exp & 1)) {
+            if (p >= 0 && !(exp & 1)) {
                 const unsigned c = snn_contrib(sp, ii, rp);
-                if (c != sp.init) ok = table_insert64(tab, p, c, sp, BITS, SNN_WT);
+                if (c != sp.init) ok = table_insert64(tab, p, c, sp, snn_log2<WT>(), WT);
             }
             full = __any(!ok);
             if (full) break;
@@ -338,16 +457,16 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             ii = nii;
         }
         WAVE_LDS_SYNC();
-        // Compact: every lane reads its 32 slots (slot r*64 + lane) to registers
-        // first, so the in-place writes cannot overtake a pending read.
+        // Compact: every lane reads its WT/64 slots (slot r*64 + lane) to
+        // registers first, so the in-place writes cannot overtake a pending read.
         int u = 0;
         if (!full) {
-            unsigned long long e[SNN_WT / 64];
+            unsigned long long e[WT / 64];
 #pragma unroll
-            for (int r = 0; r < SNN_WT / 64; ++r) e[r] = tab[r * 64 + lane];
+            for (int r = 0; r < WT / 64; ++r) e[r] = tab[r * 64 + lane];
             WAVE_LDS_SYNC();
 #pragma unroll
-            for (int r = 0; r < SNN_WT / 64; ++r) {
+            for (int r = 0; r < WT / 64; ++r) {
                 const bool occ = e[r] != SNN_EMPTY64;
                 const unsigned long long m = __ballot(occ);
                 if (occ) tab[u + __popcll(m & lanemask_lt())] = e[r];
@@ -355,25 +474,23 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
             }
             WAVE_LDS_SYNC();
         }
-        if (full || u > SNN_WCAP) {
+        if (full || u > CAP) {
             if (lane == 0) {
                 const int q = atomicAdd(ov_count, 1);
                 ov_list[q] = (int)j;
             }
             continue;
         }
-        // Rank sort by partner (keys are distinct): each lane ranks its entries
-        // c = r*64 + lane against all u keys read as LDS broadcasts, then
-        // writes them straight to their sorted place in the scratch row.
+        // Sort by partner and park the row in scratch (bucket split + in-bucket rank).
         unsigned long long* dst = scratch + j * SNN_WCAP;
         const int R = (u + 63) >> 6;
-        int* hist = m_hist[wv];
-        int* bst = m_bst[wv];
-        if (u == 0 || (exp & 2)) {
+        int* hist = L.u.s.hist;
+        int* bst = L.u.s.bst;
+        if (u == 0 || (exp & 4)) {
         } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, dst);
         else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, dst);
         else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, dst);
-        else snn_bucket_store<SNN_WCAP / 64>(tab, u, lane, j, n, hist, bst, dst);
+        else if constexpr (CAP > 768) snn_bucket_store<CAP / 64>(tab, u, lane, j, n, hist, bst, dst);
         WAVE_LDS_SYNC();
         int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
         for (int c = lane; c < u; c += 64) {
@@ -381,6 +498,245 @@ __global__ __launch_bounds__(64 * SNN_WAVES) void snn_wave_build_kernel(
 #pragma unroll
             for (int t = 0; t < SNN_MAXK; ++t)
                 if (t < sp.nk && graph_has(sp, v, t)) ++c4[t];
+        }
+#pragma unroll
+        for (int t = 0; t < SNN_MAXK; ++t) {
+            int64_t v = c4[t];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
+        }
+        if (lane == 0) ucount[j] = u;
+        WAVE_LDS_SYNC();
+    }
+}
+
+// ------------------------------------------------------- sort (ESC) path --
+// Nodes with at most SI items (partners p > j, with multiplicity) skip the
+// hash table: the items are gathered to registers (all host loads in flight
+// at once), bucketed by p into an LDS stage (histogram, scan, scatter),
+// ranked inside their bucket by (p, stage slot) and rewritten in sorted
+// order; one pass over the sorted stage then merges equal partners (sum for
+// NUMBER, bytewise min for RANK) and writes the row.  Every item costs a
+// fixed handful of LDS operations instead of a probe sequence.
+#define SNN_SNB 240  // buckets: SI*8 + 2*SNN_SNB*4 + 4 bytes of LDS per wave
+
+template <int SI>
+struct SnnSortLds {
+    unsigned long long stage[SI];
+    union {
+        struct {  // gather phase: member headers
+            long long h0[64];
+            long long hend[64];
+            int cur[64];
+            int pre[65];
+        } g;
+        struct {  // bucket phase
+            int hist[SNN_SNB];
+            int bst[SNN_SNB + 1];
+        } s;
+    } u;
+};
+
+__device__ __forceinline__ unsigned snn_combine(int type, unsigned a, unsigned b) {
+    return type == CCG_SNN_NUMBER ? a + b : bytewise_min(a, b);  // per-byte counts never carry
+}
+
+template <int SI>
+__global__ __launch_bounds__(64 * SNN_WAVES, SI <= 1024 ? 4 : 2) void snn_sort_build_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
+    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
+    int64_t* __restrict__ cnt, const int* __restrict__ in_list, const int* __restrict__ in_count,
+    int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
+    int* __restrict__ ucount) {
+    constexpr int R = SI / 64;
+    __shared__ SnnSortLds<SI> lds_all[SNN_WAVES];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    SnnSortLds<SI>& L = lds_all[wv];
+    unsigned long long* stage = L.stage;
+    const int kmax = sp.kk[sp.nk - 1];
+    const int64_t nn = in_list ? (int64_t)*in_count : n;
+    for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
+        const int64_t j = in_list ? (int64_t)in_list[f] : f;
+        // members: as in snn_wave_build_kernel (partners p > j only)
+        int mcur = 0, mlen = 0;
+        long long mh0 = 0, mend = 0;
+        if (lane <= kmax) {
+            if (lane == 0) {
+                mcur = (int)j;
+                mh0 = hoff[j] + split[j];
+                mend = hoff[j + 1];
+                mlen = (int)(mend - mh0);
+            } else {
+                mcur = knn[j * kstride + lane - 1];
+                const int q = bp[j * kmax + lane - 1];
+                mh0 = hoff[mcur] + q + 1;
+                mend = hoff[mcur + 1];
+                mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+            }
+        }
+        int incl = mlen;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int M = __shfl(incl, 63);
+        if (M > SI) {
+            if (lane == 0) {
+                const int q = atomicAdd(ov_count, 1);
+                ov_list[q] = (int)j;
+            }
+            continue;
+        }
+        if (lane <= kmax) {
+            L.u.g.pre[lane] = incl - mlen;
+            L.u.g.h0[lane] = mh0;
+            L.u.g.hend[lane] = mend;
+            L.u.g.cur[lane] = mcur;
+        }
+        if (lane == 0) L.u.g.pre[kmax + 1] = M;
+        WAVE_LDS_SYNC();
+        // gather: every host load of the node is issued before any is used
+        int2 hr[R];
+        int im[R];
+        int mi = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int t = 64 * r + lane;
+            im[r] = -1;
+            hr[r] = make_int2(-1, 0);
+            if (t < M) {
+                while (L.u.g.pre[mi + 1] <= t) ++mi;
+                im[r] = mi;
+                const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
+                if (q < L.u.g.hend[mi]) hr[r] = hosts_s[q];
+                else hr[r] = make_int2(L.u.g.cur[mi], 0);
+            }
+        }
+        WAVE_LDS_SYNC();
+        int* hist = L.u.s.hist;
+        int* bst = L.u.s.bst;
+        for (int b = lane; b < SNN_SNB; b += 64) hist[b] = 0;
+        WAVE_LDS_SYNC();
+        const float inv = (float)SNN_SNB / (float)(n - j);
+        unsigned long long e[R];
+        int bk[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            e[r] = SNN_EMPTY64;
+            bk[r] = -1;
+            if (im[r] >= 0) {
+                const unsigned c = snn_contrib(sp, im[r], hr[r].y);
+                if (c != sp.init) {
+                    e[r] = ((unsigned long long)(unsigned)hr[r].x << 32) | c;
+                    bk[r] = min(SNN_SNB - 1, (int)((float)(hr[r].x - (int)j - 1) * inv));
+                    atomicAdd(&hist[bk[r]], 1);
+                }
+            }
+        }
+        WAVE_LDS_SYNC();
+        // bucket starts: lane owns buckets 4*lane .. 4*lane+3
+        int hv[4], hs = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = 4 * lane + i;
+            hv[i] = b < SNN_SNB ? hist[b] : 0;
+            hs += hv[i];
+        }
+        int sc = hs;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(sc, o);
+            if (lane >= o) sc += y;
+        }
+        const int V = __shfl(sc, 63);
+        int run = sc - hs;
+        WAVE_LDS_SYNC();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int b = 4 * lane + i;
+            if (b < SNN_SNB) {
+                bst[b] = run;
+                hist[b] = run;  // scatter cursor
+            }
+            run += hv[i];
+        }
+        if (lane == 0) bst[SNN_SNB] = V;
+        WAVE_LDS_SYNC();
+        int pos[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            pos[r] = 0;
+            if (bk[r] >= 0) {
+                pos[r] = atomicAdd(&hist[bk[r]], 1);
+                stage[pos[r]] = e[r];
+            }
+        }
+        WAVE_LDS_SYNC();
+        // rank inside the bucket by (p, slot)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (bk[r] >= 0) {
+                const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
+                const unsigned key = (unsigned)(e[r] >> 32);
+                int rank = 0;
+                for (int q = b0; q < b1; ++q) {
+                    const unsigned kq = (unsigned)(stage[q] >> 32);
+                    rank += (kq < key || (kq == key && q < pos[r])) ? 1 : 0;
+                }
+                pos[r] = b0 + rank;
+            }
+        }
+        WAVE_LDS_SYNC();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (bk[r] >= 0) stage[pos[r]] = e[r];
+        WAVE_LDS_SYNC();
+        // unique partners: first of each run of equal keys
+        auto is_first = [&](int q, unsigned& key) {
+            const unsigned long long x = stage[q];
+            key = (unsigned)(x >> 32);
+            return q == 0 || (unsigned)(stage[q - 1] >> 32) != key;
+        };
+        if constexpr (SI > SNN_WCAP) {
+            int uu = 0;
+            for (int q0 = 0; q0 < V; q0 += 64) {
+                unsigned key;
+                const bool first = q0 + lane < V && is_first(q0 + lane, key);
+                uu += __popcll(__ballot(first));
+            }
+            if (uu > SNN_WCAP) {
+                if (lane == 0) {
+                    const int q = atomicAdd(ov_count, 1);
+                    ov_list[q] = (int)j;
+                }
+                WAVE_LDS_SYNC();
+                continue;
+            }
+        }
+        unsigned long long* dst = scratch + j * SNN_WCAP;
+        int u = 0;
+        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+        for (int q0 = 0; q0 < V; q0 += 64) {
+            const int q = q0 + lane;
+            unsigned key = 0, agg = 0;
+            const bool first = q < V && is_first(q, key);
+            if (first) {
+                agg = (unsigned)stage[q];
+                for (int q2 = q + 1; q2 < V; ++q2) {
+                    const unsigned long long y = stage[q2];
+                    if ((unsigned)(y >> 32) != key) break;
+                    agg = snn_combine(sp.type, agg, (unsigned)y);
+                }
+            }
+            const unsigned long long m = __ballot(first);
+            if (first) {
+                dst[u + __popcll(m & lanemask_lt())] = ((unsigned long long)key << 32) | agg;
+#pragma unroll
+                for (int t = 0; t < SNN_MAXK; ++t)
+                    if (t < sp.nk && graph_has(sp, agg, t)) ++c4[t];
+            }
+            u += __popcll(m);
         }
 #pragma unroll
         for (int t = 0; t < SNN_MAXK; ++t) {
@@ -718,27 +1074,33 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     const int kmax = ks[nk - 1];
     hipStream_t st = ccg_pick_stream(ctx, stream);
     int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
-    int2* hosts = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (n * kmax + 1));
+    int2* hosts = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * 2 * (n * kmax + 1));
     int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * nk * (n + 1));
-    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (4 * n + 64));
+    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (5 * n + 64));
     unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
     unsigned long long* scratch =
         (unsigned long long*)ccg_ws(ctx, WS_SNN_F, sizeof(unsigned long long) * n * SNN_WCAP + sizeof(int) * (n + 64));
-    if (!hoff || !hosts || !cnt || !ov || !dense || !scratch) return CCG_ENOMEM;
+    int* bp = (int*)ccg_ws(ctx, WS_SNN_G, sizeof(int) * (n * kmax + n + 64));
+    if (!hoff || !hosts || !cnt || !ov || !dense || !scratch || !bp) return CCG_ENOMEM;
+    int2* hosts_s = hosts + (n * kmax + 1);
+    int* split = bp + n * kmax;
     int* ucount = (int*)(scratch + n * SNN_WCAP);
     unsigned long long* cursor = (unsigned long long*)(hoff + (n + 1));
     int* err = (int*)(hoff + 2 * (n + 1));
-    int* ov_list = ov;
+    int* ov_list = ov;  // nodes for the block path (overflowed both wave tiers)
     int* ov2_list = ov + n;
     int* flag1 = ov + 2 * n;
     int* flag2 = ov + 3 * n;
-    int* ov_count = ov + 4 * n;
+    int* ova_list = ov + 4 * n;  // more than 1024 items -> 2048-slot hash tier
+    int* ov_count = ov + 5 * n;
     int* ov2_count = ov_count + 1;
+    int* ova_count = ov_count + 2;
     const int64_t nkk = (int64_t)n * kmax;
     const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
     CCG_HIP(hipMemsetAsync(hoff, 0, sizeof(int64_t) * (n + 1), st));
     CCG_HIP(hipMemsetAsync(err, 0, sizeof(int) * 4, st));
-    CCG_HIP(hipMemsetAsync(flag1, 0, sizeof(int) * (2 * n + 64), st));
+    CCG_HIP(hipMemsetAsync(flag1, 0, sizeof(int) * 2 * n, st));
+    CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
     CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * nk * (n + 1), st));
     snn_count_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax,
                                                                   (unsigned long long*)hoff, err);
@@ -746,14 +1108,22 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     if (rc) return rc;
     CCG_HIP(hipMemcpyAsync(cursor, hoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
     snn_fill_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, cursor, hosts);
+    snn_sort_hosts<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(hoff, n, kmax, hosts,
+                                                                                      hosts_s, bp, split);
     const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
-    // pass 1: per-graph counts (wave tables, then block tables, then dense)
     static const int snn_exp = getenv("CCG_SNN_EXP") ? atoi(getenv("CCG_SNN_EXP")) : 0;  // timing experiments only
-    snn_wave_build_kernel<<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list,
-                                                           ov_count, scratch, ucount, snn_exp);
-    snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
+    // pass 1: per-graph counts (sort tier for nodes with <= 1024 items, 2048-slot hash tables,
+    // then block tables, then dense)
+    snn_sort_build_kernel<1024><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
+                                                                 nullptr, nullptr, ova_list, ova_count, scratch,
+                                                                 ucount);
+    const unsigned nblk2 = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 1024);
+    snn_wave_build_kernel<2048><<<nblk2, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
+                                                                  ova_list, ova_count, ov_list, ov_count, scratch,
+                                                                  ucount, snn_exp);
+    snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, ov_list, ov_count,
                                                  ov2_list, ov2_count, flag2, out);
-    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
+    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
                                                              ov2_count, dense, cnt, out);
     snn_mark_kernel<<<64, 256, 0, st>>>(ov_list, ov_count, flag1);
     snn_mark_kernel<<<64, 256, 0, st>>>(ov2_list, ov2_count, flag2);
@@ -766,9 +1136,9 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     if (any_cap) {
         snn_wave_emit_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(
             n, sp, cnt, flag1, scratch, ucount, out);
-        snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, cnt, ov_list, ov_count,
+        snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, ov_list, ov_count,
                                                     ov2_list, ov2_count, flag2, out);
-        snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts, ov2_list,
+        snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
                                                                 ov2_count, dense, cnt, out);
     }
     snn_copy_totals<<<1, 64, 0, st>>>(cnt, n, nk, d_nedges[0], nk > 1 ? d_nedges[1] : nullptr,

@@ -192,6 +192,27 @@ def test_snn_hub_overflow_dense_path(engine, t):
 
 
 @pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_table_tiers_vs_oracle(engine, t):
+    # two groups whose members all list the group's 5 hub nodes: node j's
+    # partners p > j are the later group members, so the partner count runs
+    # from 0 to ~4000 and crosses the 1024-slot tier, the 2048-slot tier and
+    # the block-table path
+    n, k = 6000, 20
+    rng = np.random.default_rng(5)
+    idx = np.empty((n, k), np.int32)
+    for i in range(n):
+        base = 0 if i < 2000 else 2000
+        hubs = [base + h for h in range(6) if base + h != i][:5]
+        rest = rng.choice(n, 3 * k, replace=False)
+        rest = [int(x) for x in rest if x != i and x not in hubs][:k - 5]
+        idx[i] = hubs + rest
+    a = engine.snn(idx, k, t)
+    b = O.snn(idx, k, t)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
 def test_snn_multi_pass_matches_single_graphs(engine, t):
     """One pass over kmax=20 builds the k=10/15/20 graphs (kNum, :653)."""
     import torch

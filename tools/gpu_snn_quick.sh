@@ -6,6 +6,6 @@ timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/snn/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 : > gpurun_out/snn/micro.log
-for v in ${SNN_VARIANTS:-0 2}; do
+for v in ${SNN_VARIANTS:-0}; do
   CCG_SNN_EXP=$v timeout -k 10 300 python tools/snn_micro.py >> gpurun_out/snn/micro.log 2>>gpurun_out/snn/micro.err || exit $?
 done
