@@ -29,6 +29,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define KNN_KP 20          // candidates kept per half-lane for kmax <= 20
 #define KNN_KP_BIG 32      // ... for 20 < kmax <= 32 (2*KP <= 64 lanes in certify)
+#define KNN_TMARGIN 8      // screen threshold: rank KP + KNN_TMARGIN of the two half-lists' union
 #define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
 #define KNN_FB_K 32        // fallback list length (>= kmax)
 #define KNN_FB_S 64        // max reference ranges per failed row
@@ -127,6 +128,30 @@ __device__ __forceinline__ void list_insert_par(float (&lv)[KP], int (&li)[KP], 
     }
     lv[0] = keep[0] ? lv[0] : v;
     li[0] = keep[0] ? li[0] : id;
+}
+
+// R-th largest (R = KP + KNN_TMARGIN) of the union of this half-lane's list
+// and its partner's (lane ^ 32), both sorted descending: max over splits i
+// of min(mine[i-1], other[R-1-i]).  The partner's entries arrive by
+// v_permlane32_swap (no LDS).  Every ref either half has rejected or evicted
+// is <= this value, so it is a valid rejection threshold for both halves and
+// tighter than max(thr_h0, thr_h1) (about rank 2*KP of the union); the
+// margin of KNN_TMARGIN ranks above k keeps certification (excl - E > dK)
+// provable.
+template <int KP>
+__device__ __forceinline__ float union_kth(const float (&lv)[KP]) {
+    constexpr int R = KP + KNN_TMARGIN;
+    const bool lo = (threadIdx.x & 32) == 0;
+    float t = -INFINITY;
+#pragma unroll
+    for (int i = R - KP; i <= KP; ++i) {
+        // i from mine (lv[i-1]), R - i from the partner (its lv[R-1-i])
+        const unsigned x = __float_as_uint(lv[R - 1 - i]);
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        const float b = __uint_as_float(lo ? r[1] : r[0]);
+        t = fmaxf(t, i == 0 ? b : fminf(lv[i - 1], b));
+    }
+    return t;
 }
 
 template <int KS>
@@ -501,6 +526,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
     float T = -INFINITY;  // max of both halves' thresholds (see below)
     int qc = 0;           // this lane's queued candidates
+    bool tdirty = false;  // lists changed since T was last set to the union threshold
 #define KNN_FLUSH()                                                                   \
     do {                                                                              \
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
@@ -517,6 +543,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             }                                                                         \
         }                                                                             \
         qc = 0;                                                                       \
+        tdirty = true;                                                                \
     } while (0)
     KNN_STAGE_GLDS(0, chunk_at(0));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -593,16 +620,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 }
                 if (EXP == 4) atomicAdd(&g_knn_dbg[1], (unsigned long long)cnt);
             }
-            // Both halves of a query may reject anything at or below the better
-            // of their two KP-th values: the union of the lists still holds the
-            // query's overall top KP, and every rejected/evicted ref is <= the
-            // final max(thr_h0, thr_h1) that certification uses.
-            T = fmaxf(thr, __shfl_xor(thr, 32, 64));
+            // After a flush (here, with the tile's accumulators dead) both halves
+            // move to the union threshold; between flushes T only rises.
+            if (tdirty) {
+                T = union_kth<KP>(lv);
+                tdirty = false;
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (EXP != 2) __syncthreads();  // EXP 2 / 3: timing-only (no barrier / no global loads)
     }
     KNN_FLUSH();
+    T = union_kth<KP>(lv);
 #undef KNN_FLUSH
 #undef KNN_STAGE_GLDS
 #undef chunk_at
@@ -611,7 +640,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
 #pragma unroll
         for (int t = 0; t < KP; ++t) out[t] = li[t];
-        cand_thr[(int64_t)q * 2 + h] = thr;
+        cand_thr[(int64_t)q * 2 + h] = T;  // every excluded ref is <= the final union threshold
     }
 }
 
@@ -703,7 +732,8 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int idK = __shfl(id, kmax - 1, 64);
     bool ok = (idK < n);  // at least kmax real candidates
     if (tmax != -INFINITY) {
-        // An excluded ref y has approx d2 >= excl.  If it were as close as the
+        // An excluded ref y has approx d2 >= excl (tmax: the screen's final
+        // union threshold, at or above every rejected or evicted value).  If it were as close as the
         // k-th candidate (|x-y|^2 <= dK) then |y| <= |x| + sqrt(dK), so its
         // screening error is at most E = c*u*(2|x| + sqrt(dK))^2 and its approx
         // d2 at most dK + E.  excl > dK + E therefore proves it is farther
@@ -1027,7 +1057,15 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
 #define CCG_SCREEN16(KS_, KP_) \
     knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk)
-        if (KP == KNN_KP) {
+        static const int kexp = getenv("CCG_KNN_EXP") ? atoi(getenv("CCG_KNN_EXP")) : 0;  // timing experiments only
+        if (KP == KNN_KP && KSTEPS == 2 && kexp >= 1 && kexp <= 3 && !blk) {
+            if (kexp == 1)
+                knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
+            else if (kexp == 2)
+                knn_screen16_kernel<2, KNN_KP, 2><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
+            else
+                knn_screen16_kernel<2, KNN_KP, 3><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
+        } else if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
             else CCG_SCREEN16(4, KNN_KP);
