@@ -218,7 +218,7 @@ int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co,
 /* Device time of selected kernels, measured with hipEvents recorded on the
  * stream each kernel is launched on (used by bench.py for the live roofline).
  * Disabled by default; enabling adds two event records per timed launch. */
-#define CCG_KT_KNN_SCREEN 0   /* the fp32 MFMA screening kernel of ccg_knn_* */
+#define CCG_KT_KNN_SCREEN 0   /* the fp16 hi/lo MFMA screening kernel of ccg_knn_* */
 #define CCG_KT_KNN_TOTAL 1    /* prep + screen + certify + fallback */
 #define CCG_KT_SNN 2          /* whole ccg_snn_dev call */
 #define CCG_KT_SILHOUETTE 3   /* whole ccg_silhouette_dev call */
