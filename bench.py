@@ -13,8 +13,12 @@ flips, generated on the device before timing.  Inputs are resident in HBM
 when the timed region starts.  Weak scaling: B bootstraps per GPU per step
 (default 125 -> 1000 bootstraps = BASELINE config 3 at 8 GPUs).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; multi-GPU through
-torch.distributed.run (one process per GPU, RCCL).
+Usage: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1
+and no WORLD_SIZE in the environment, this process (which never touches the
+GPU) starts N ranks through torch.distributed.run (127.0.0.1) and exits with
+their status; under torch.distributed.run (WORLD_SIZE set) each rank drives
+one GPU, RCCL ("nccl") for the all-gather.  --launcher-check runs only the
+rank wiring (gloo, no GPU) and prints the world the ranks saw.
 """
 import argparse
 import json
@@ -46,12 +50,57 @@ def parse():
     ap.add_argument("--genes", type=int, default=2000)
     ap.add_argument("--boots-per-gpu", type=int, default=125)
     ap.add_argument("--boot-size", type=float, default=0.9)
-    ap.add_argument("--cpu-sample-rows", type=int, default=30000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=6000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=3,
                     help="bootstraps in flight per GPU (one engine context + HIP stream each)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """Parent of a multi-GPU run: start one rank per GPU and return their exit
+    status.  Nothing here initialises the GPU (no torch.cuda call), so no GPU
+    state is inherited or replaced; rank 0's JSON line is passed through."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_check(args):
+    """Each rank joins a gloo group and all-gathers (rank, LOCAL_RANK); rank 0
+    prints what the ranks saw.  Exercises exactly the wiring the bench uses."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    mine = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0"))], dtype=torch.int64)
+    seen = [torch.zeros_like(mine) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(seen, mine)
+    else:
+        seen = [mine]
+    if world > 1 and world != args.gpus:
+        raise SystemExit(f"world size {world} != --gpus {args.gpus}")
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_seen": [s.tolist() for s in seen], "backend": "gloo"}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def synth_pcs(torch, N, d, G, seed, dev):
@@ -106,48 +155,70 @@ def A_full_C(torch, A_local, G):
     return int(c.item())
 
 
-def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
-    """Time the CPU restatement (oracle/, C + OpenMP) on a bounded sample and
-    extrapolate to one step's work (B bootstraps + the co-cluster slab)."""
+def _cpu_boot_worker(a):
+    """One bootstrap's per-bootstrap CPU work (kNN k=20, SNN k=10/15/20, 6
+    silhouettes) on a single core, as one BiocParallel MulticoreParam worker
+    runs getClustAssignments.  Returns its seconds."""
+    X, seed = a
+    sys.path.insert(0, ROOT)
     import oracle as O
-    threads = min(16, os.cpu_count() or 1)
     rng = np.random.default_rng(seed)
-    ns = min(sample_rows, n)
-    boot = rng.integers(0, N, ns).astype(np.int32)
-    X = O.gather_rows(pcs_np, boot)
     t0 = time.perf_counter()
-    idx, _ = O.knn(X, 20, nthreads=threads)
-    t_knn = (time.perf_counter() - t0) * (n / ns) ** 2
-    t0 = time.perf_counter()
+    idx, _ = O.knn(X, 20, nthreads=1)
+    t1 = time.perf_counter()
     for k in K_NUM:
         O.snn(idx, k, "number")
-    t_snn = (time.perf_counter() - t0) * (n / ns)
-    lab = rng.integers(1, 21, (6, ns)).astype(np.int32)  # 6 of the 60 clusterings, C ~ 20
-    t0 = time.perf_counter()
-    for l_ in lab:
+    t2 = time.perf_counter()
+    for l_ in rng.integers(1, 21, (6, X.shape[0])).astype(np.int32):  # 6 of the 60 clusterings, C ~ 20
         O.silhouette(X, l_)
-    t_sil = (time.perf_counter() - t0) * (60 / 6) * (n / ns)
+    t3 = time.perf_counter()
+    return t1 - t0, t2 - t1, t3 - t2
+
+
+def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
+    """The CPU restatement (oracle/, C) timed bootstrap-parallel on the host's
+    cores, as the reference fans bootstraps over bplapply(MulticoreParam):
+    `cores` single-threaded workers each run one bootstrap sample of
+    `sample_rows` rows concurrently (so memory contention is included); the
+    per-bootstrap seconds are extrapolated to n rows (kNN n^2, SNN and
+    silhouette n, 60 clusterings) and divided over the cores.  The co-cluster
+    runs OpenMP over the same cores on 2000 cells, extrapolated by N^2."""
+    import multiprocessing as mp
+    import oracle as O
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    rng = np.random.default_rng(seed)
+    ns = min(sample_rows, n)
+    samples = [(O.gather_rows(pcs_np, rng.integers(0, N, ns).astype(np.int32)), seed + w) for w in range(cores)]
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.map(_cpu_boot_worker, samples)
+    t_knn = float(np.mean([r[0] for r in res])) * (n / ns) ** 2
+    t_snn = float(np.mean([r[1] for r in res])) * (n / ns)
+    t_sil = float(np.mean([r[2] for r in res])) * (60 / 6) * (n / ns)
     Nc = 2000
     A = rng.integers(1, 13, (B, Nc)).astype(np.int32)
     A[rng.random((B, Nc)) < 0.35] = -1
     t0 = time.perf_counter()
-    O.cocluster(A, nthreads=threads, want=("co", "both"))
+    O.cocluster(A, nthreads=cores, want=("co", "both"))
     t_coc = (time.perf_counter() - t0) * (N * (N - 1) / (Nc * (Nc - 1)))
-    t_step = B * (t_knn + t_snn + t_sil) + t_coc
+    t_step = B * (t_knn + t_snn + t_sil) / cores + t_coc
     return {
         "value": B / t_step,
         "unit": "bootstraps/s",
-        "cores": threads,
+        "cores": cores,
         "kind": "port",
-        "sample": (f"oracle (C/OpenMP) on one {ns}-row bootstrap of the same PCs: kNN x (n/{ns})^2, "
-                   f"SNN k=10/15/20 x n/{ns}, silhouette of 6 clusterings x 10 x n/{ns}; co-cluster on "
-                   f"{B} columns x {Nc} cells x (N/{Nc})^2; per-bootstrap s: knn {t_knn:.2f}, snn {t_snn:.2f}, "
-                   f"silhouette {t_sil:.2f}; co-cluster per step {t_coc:.1f}"),
+        "sample": (f"oracle (C) bootstrap-parallel: {cores} single-threaded workers, one {ns}-row bootstrap each "
+                   f"(kNN x (n/{ns})^2, SNN k=10/15/20 x n/{ns}, silhouette of 6 clusterings x 10 x n/{ns}), "
+                   f"per-bootstrap core-seconds knn {t_knn:.1f}, snn {t_snn:.2f}, silhouette {t_sil:.2f}; "
+                   f"co-cluster OpenMP x{cores} on {B} columns x {Nc} cells x (N/{Nc})^2 = {t_coc:.1f} s per step"),
     }
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.launcher_check:
+        return launcher_check(args)
     import torch
     import torch.distributed as dist
 
@@ -155,9 +226,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        if world != args.gpus:
+            raise SystemExit(f"world size {world} != --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    ranks_seen = [world]
+    if world > 1:  # the ranks RCCL actually connected: (rank, device) of each
+        mine = torch.tensor([rank, local], dtype=torch.int64, device=dev)
+        got = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        ranks_seen = [g.tolist() for g in got]
 
     from consensusclustr_amd import Engine
     from consensusclustr_amd.sharding import allgather_columns, row_slabs, slab_pairs
@@ -302,6 +382,7 @@ def main():
         "value": round(value, 3),
         "unit": "bootstraps/s",
         "n_gpus": G,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1000, 3),

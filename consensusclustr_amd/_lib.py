@@ -53,6 +53,7 @@ SIGNATURES = {
     "ccg_open": (_i, [_p, _p]),
     "ccg_close": (_i, [_p]),
     "ccg_synchronize": (_i, [_p]),
+    "ccg_check_errors": (_i, [_p]),
     "ccg_stream": (_p, [_p]),
     "ccg_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
     "ccg_gather_rows_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p]),
@@ -64,11 +65,13 @@ SIGNATURES = {
     "ccg_snn_multi_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p, _p]),
     "ccg_silhouette": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p]),
     "ccg_silhouette_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p]),
-    "ccg_select_mapback_dev": (_i, [_p, _i, _p, _p, _i64, _i, _i, _i64, _p, _p, _p, _i, _p, _i64, _p, _p]),
-    "ccg_cocluster": (_i, [_p, _p, _i64, _i64, _p, _p, _p]),
-    "ccg_cocluster_dev": (_i, [_p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "ccg_select_mapback_dev": (_i, [_p, _i, _p, _p, _i64, _i, _i, _i64, _p, _p, _p, _i, _p, _i, _i64, _p, _p]),
+    "ccg_cocluster": (_i, [_p, _p, _i, _i64, _i64, _p, _p, _p]),
+    "ccg_cocluster_dev": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),
     "ccg_consensus_knn": (_i, [_p, _p, _p, _i64, _i, _p]),
     "ccg_consensus_knn_dev": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
+    "ccg_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
+    "ccg_consensus_knn_assign_dev": (_i, [_p, _p, _i, _i64, _i64, _i, _i64, _i64, _p, _p, _p]),
     "ccg_timing_enable": (_i, [_p, _i]),
     "ccg_timing_read": (_i, [_p, _i, _p, _p]),
 }

@@ -157,27 +157,32 @@ def subcluster_bootstrap_knn(pcas, boot_idx, kmax=20, engine=None):
 
 
 def assignment_matrix(columns):
-    """do.call(cbind, ...) (:404) with NA -> -1 (:408), as the uint8 B x N
-    column-major matrix of the C ABI (0 = not sampled)."""
+    """do.call(cbind, ...) (:404) with NA -> -1 (:408), as the B x N
+    column-major matrix of the C ABI (0 = not sampled): uint8 when every code
+    fits in 1..255, else uint16 (codes up to 65535)."""
     cols = []
     for c in columns:
         c = np.asarray(c)
         cols.extend([c] if c.ndim == 1 else list(c.T))
     A = np.stack(cols).astype(np.int64)
-    if A.max() > 255:
-        raise ValueError("cluster codes above 255 are not supported by the uint8 assignment matrix")
+    if A.max() > 65535:
+        raise ValueError("cluster codes above 65535 are not supported by the assignment matrix")
     A[A < 0] = 0
-    return A.astype(np.uint8)
+    return A.astype(np.uint8 if A.max() <= 255 else np.uint16)
 
 
 def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRange=RES_RANGE, kNum=K_NUM,
-                      mode="robust", seed=123, engine=None, boot_indices=None):
+                      mode="robust", seed=123, engine=None, boot_indices=None, return_matrix=None):
     """The bootstrap + consensus core of consensusClust (R/consensusClust.R:388-456).
 
-    Returns dict(assignments=<chosen consensus labels>, jaccardDist=<packed
-    R-dist-order float64>, clustAssignments=<B x N uint8>, co, both,
-    scores=<consensus scores>, choice=<index>).  The later host stages
-    (cluster merging :459-497, null test, dendrogram) are out of scope.
+    Returns dict(assignments=<chosen consensus labels>, clustAssignments=<B x N
+    uint8/uint16>, scores=<consensus scores>, choice=<index>, candidates,
+    consensus_knn=<N x max(kNum)>) and, when return_matrix (default: N <=
+    20000), the packed R-dist-order jaccardDist, co and both.  The consensus
+    kNN (:425) comes straight from the assignment matrix through the fused
+    co-clustering top-k (ccg_consensus_knn_assign), so the N x N distance is
+    only materialised on request.  The later host stages (cluster merging
+    :459-497, null test, dendrogram) are out of scope.
     """
     eng = engine or default_engine()
     pca = np.asarray(pca, dtype=np.float64)
@@ -192,11 +197,17 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
         except Exception:  # tryCatch(..., error = rep(1, N)), :397-399
             columns.append(np.ones(N, np.int32))
     A = assignment_matrix(columns)
-    cc = eng.cocluster(A)  # 1 - parDist(customDist), :411-421
+    out = {"clustAssignments": A}
+    if return_matrix is None:
+        return_matrix = N <= 20000
+    if return_matrix:
+        cc = eng.cocluster(A)  # 1 - parDist(customDist), :411-421
+        out.update(jaccardDist=cc["dist"], co=cc["co"], both=cc["both"])
+    kmax = max(kNum)
+    cknn = eng.consensus_knn_assign(A, kmax)  # dbscan::kNN(jaccardDist, k), :425 (k < kmax: prefixes)
     finals = []
     for k in kNum:  # :423-441
-        knn = eng.consensus_knn(cc["co"], cc["both"], N, k)  # dbscan::kNN(jaccardDist, k), :425
-        ei, ej, w = eng.snn(knn, k, "rank")  # neighborsToSNNGraph(knn, "rank"), :426
+        ei, ej, w = eng.snn(np.ascontiguousarray(cknn[:, :k]), k, "rank")  # neighborsToSNNGraph(knn, "rank"), :426
         for res in resRange:
             finals.append(np.asarray(fn(N, ei, ej, w, float(res), seed), np.int32))
     lab = np.stack(finals)
@@ -206,5 +217,5 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
     means, _, _, _ = eng.silhouette(pca, codes)
     scores = np.where((nuniq > 1) & (nuniq < N / 10), means, np.where(nuniq == N, -1.0, 0.15))  # :446-452
     choice = consensus_choice(scores)
-    return {"assignments": lab[choice], "jaccardDist": cc["dist"], "clustAssignments": A, "co": cc["co"],
-            "both": cc["both"], "scores": scores, "choice": choice, "candidates": lab}
+    out.update(assignments=lab[choice], scores=scores, choice=choice, candidates=lab, consensus_knn=cknn)
+    return out

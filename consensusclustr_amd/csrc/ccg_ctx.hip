@@ -47,10 +47,18 @@ extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
     c->timing = 0;
     c->timers = nullptr;
     c->ntimers = c->cap_timers = c->used_timers = 0;
+    c->d_err = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return ccg_hip_fail(e, "hipStreamCreate", __FILE__, __LINE__);
+    }
+    e = hipMalloc(&c->d_err, 64);
+    if (e == hipSuccess) e = hipMemset(c->d_err, 0, 64);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return ccg_hip_fail(e, "hipMalloc(d_err)", __FILE__, __LINE__);
     }
     *out = c;
     return CCG_OK;
@@ -67,15 +75,35 @@ extern "C" int ccg_close(ccg_ctx* ctx) {
         (void)hipEventDestroy(ctx->timers[t].stop);
     }
     free(ctx->timers);
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return CCG_OK;
 }
 
-extern "C" int ccg_synchronize(ccg_ctx* ctx) {
+int ccg_take_device_error(ccg_ctx* ctx) {
+    int bits = 0;
     CCG_HIP(hipSetDevice(ctx->device));
     CCG_HIP(hipDeviceSynchronize());
-    return CCG_OK;
+    CCG_HIP(hipMemcpy(&bits, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (!bits) return CCG_OK;
+    CCG_HIP(hipMemset(ctx->d_err, 0, sizeof(int)));
+    if (bits & CCG_DERR_LABEL_RANGE) {
+        ccg_set_error("cluster label exceeds the assignment matrix's label width (use label_bits=16)");
+        return CCG_ERANGE;
+    }
+    ccg_set_error("SNN: neighbour index out of range or equal to the row itself");
+    return CCG_EINVAL;
+}
+
+extern "C" int ccg_synchronize(ccg_ctx* ctx) {
+    CCG_REQUIRE(ctx, "ccg_synchronize: NULL ctx");
+    return ccg_take_device_error(ctx);
+}
+
+extern "C" int ccg_check_errors(ccg_ctx* ctx) {
+    CCG_REQUIRE(ctx, "ccg_check_errors: NULL ctx");
+    return ccg_take_device_error(ctx);
 }
 
 extern "C" void* ccg_stream(ccg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

@@ -26,6 +26,7 @@ enum ccg_ws_slot {
     WS_SIL_B,        // silhouette centroids
     WS_COC_A,        // co-cluster column tables
     WS_COC_B,        // co-cluster fused-path slot tables
+    WS_COC_C,        // co-cluster partial counts between column chunks / consensus row slab
     WS_MAP_A,        // map-back first-position scratch
     WS_HOST_A,       // host-API staging 1
     WS_HOST_B,       // host-API staging 2
@@ -45,9 +46,16 @@ struct ccg_timer_rec {
     hipEvent_t start, stop;
 };
 
+// Sticky device error bits (ccg_ctx::d_err): kernels that find invalid input
+// they cannot report synchronously OR a bit in; the next ccg_synchronize /
+// ccg_check_errors / host-flavour call turns it into a status code.
+#define CCG_DERR_LABEL_RANGE 1  // map-back: a label exceeds the assignment matrix's label width
+#define CCG_DERR_SNN_INDEX 2    // SNN: neighbour index out of range or self
+
 struct ccg_ctx {
     int device;
     hipStream_t stream;
+    int* d_err;  // device word of CCG_DERR_* bits
     void* ws[WS_NSLOTS];
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
@@ -79,6 +87,10 @@ int ccg_hip_fail(hipError_t e, const char* what, const char* file, int line);
             return CCG_EINVAL;                                            \
         }                                                                 \
     } while (0)
+
+// Reads and clears ctx->d_err (synchronising the device); returns CCG_OK or
+// the status code of the first error bit with the message set.
+int ccg_take_device_error(ccg_ctx* ctx);
 
 // Returns a device buffer of at least `bytes` for `slot` (nullptr on OOM,
 // with the error message set).

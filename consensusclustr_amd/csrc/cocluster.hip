@@ -7,30 +7,28 @@
 //   jaccard = (float)overlap / (float)U  (float division), dist = 1 - jaccard.
 //
 // With H = one-hot(A) (N x sum_b C_b, unsampled rows all-zero) and
-// S = [A != 0] (N x B):  co = H H^T,  both = S S^T.  Both are computed with
-// v_mfma_i32_32x32x32_i8 on 128 x 128 output tiles of the upper triangle;
-// the one-hot K-chunks (64 positions) are expanded from the uint8 labels
-// straight into LDS, so H never exists in HBM (HBM traffic per tile is the
-// label panels, not the one-hot matrix).  Integer accumulation makes the
-// counts exact; the epilogue's division is done in fp64 and rounded once
-// to fp32, which equals the correctly rounded fp32 quotient because
-// 53 >= 2*24 + 2 (no double-rounding error), so the distances are bitwise
-// those of the reference.
+// S = [A != 0] (N x B):  co = H H^T,  both = S S^T, computed together in ONE
+// int32 accumulator by v_mfma_i32_32x32x32_i8 (see "fused one-hot path"
+// below).  Integer accumulation makes the counts exact; the epilogue's
+// division is done in fp64 and rounded once to fp32, which equals the
+// correctly rounded fp32 quotient because 53 >= 2*24 + 2 (no double-rounding
+// error), so the distances are bitwise those of the reference.
 //
-// The output is the packed upper triangle by rows == R's "dist" order.
+// Outputs: the packed upper triangle by rows (== R's "dist" order) for a row
+// slab [r0, r1), or (consensus kNN) full rows [r0, r1) x [0, N) packed as
+// co | both << 16.
 #include <algorithm>
+#include <vector>
 
 #include "ccg_internal.h"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-#define COC_BM 128
-#define COC_KC 64
-
-__global__ void coc_colmax_kernel(const uint8_t* __restrict__ A, int64_t N, int* __restrict__ colC) {
+template <typename T>
+__global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __restrict__ colC) {
     const int b = blockIdx.y;
-    const uint8_t* col = A + (int64_t)b * N;
+    const T* col = A + (int64_t)b * N;
     int mx = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -39,264 +37,84 @@ __global__ void coc_colmax_kernel(const uint8_t* __restrict__ A, int64_t N, int*
     if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(&colC[b], mx);
 }
 
-// tables layout: off[B+1] | nchunk (1) | colLo[maxch] | colHi[maxch]
-__global__ __launch_bounds__(1024) void coc_tables_kernel(const int* __restrict__ colC, int64_t B,
-                                                          int* __restrict__ off, int* __restrict__ nchunk,
-                                                          int* __restrict__ colLo, int* __restrict__ colHi) {
-    __shared__ int sh[16];
-    __shared__ int carry_s;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t == 0) carry_s = 0;
-    __syncthreads();
-    for (int64_t b0 = 0; b0 < B; b0 += 1024) {
-        const int64_t b = b0 + t;
-        const int v = b < B ? colC[b] : 0;
-        int x = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) sh[wv] = x;
-        __syncthreads();
-        int woff = 0, tot = 0;
-        for (int w = 0; w < 16; ++w) {
-            if (w < wv) woff += sh[w];
-            tot += sh[w];
-        }
-        const int carry = carry_s;
-        if (b < B) off[b] = carry + woff + x - v;
-        __syncthreads();
-        if (t == 0) carry_s = carry + tot;
-        __syncthreads();
-    }
-    const int KC = carry_s;
-    if (t == 0) {
-        off[B] = KC;
-        *nchunk = (KC + COC_KC - 1) / COC_KC;
-    }
-    const int nch = (KC + COC_KC - 1) / COC_KC;
-    for (int ch = t; ch < nch; ch += 1024) {
-        const int p0 = ch * COC_KC;
-        const int p1 = min(p0 + COC_KC - 1, KC - 1);
-        // largest b with off[b] <= p  (upper_bound - 1)
-        int lo = 0, hi = (int)B;  // off[0] = 0 <= p
-        while (hi - lo > 1) {
-            int mid = (lo + hi) >> 1;
-            if (off[mid] <= p0) lo = mid; else hi = mid;
-        }
-        colLo[ch] = lo;
-        lo = 0;
-        hi = (int)B;
-        while (hi - lo > 1) {
-            int mid = (lo + hi) >> 1;
-            if (off[mid] <= p1) lo = mid; else hi = mid;
-        }
-        colHi[ch] = lo;
-    }
-}
-
-__device__ __forceinline__ unsigned expand4(unsigned b) {
-    return (b & 1u) | ((b & 2u) << 7) | ((b & 4u) << 14) | ((b & 8u) << 21);
-}
-
-// Store a 64-position 0/1 row (bit mask) as 64 bytes, 16-B chunks swizzled.
-__device__ __forceinline__ void store_onehot_row(uint8_t* lds, int row, unsigned long long bits) {
-    const int f = (row >> 2) & 3;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const unsigned s = (unsigned)(bits >> (16 * q));
-        v4i v;
-        v[0] = (int)expand4(s & 15u);
-        v[1] = (int)expand4((s >> 4) & 15u);
-        v[2] = (int)expand4((s >> 8) & 15u);
-        v[3] = (int)expand4((s >> 12) & 15u);
-        *(v4i*)(lds + row * 64 + ((q ^ f) << 4)) = v;
-    }
-}
-
-__device__ __forceinline__ v4i load_frag(const uint8_t* lds, int row, int chunk) {
-    const int f = (row >> 2) & 3;
-    return *(const v4i*)(lds + row * 64 + ((chunk ^ f) << 4));
-}
-
-__device__ __forceinline__ void mfma_tile(const uint8_t* sA, const uint8_t* sB, int wr, int wc,
-                                          int lane, v16i (&acc)[2][2]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 2 + (lane >> 5);
-        v4i a[2], b[2];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) a[mi] = load_frag(sA, wr * 64 + mi * 32 + (lane & 31), chunk);
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) b[ni] = load_frag(sB, wc * 64 + ni * 32 + (lane & 31), chunk);
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-    }
-}
-
-__global__ __launch_bounds__(256) void coc_tile_kernel(
-    const uint8_t* __restrict__ A, int64_t N, int64_t B, int64_t r0, int64_t r1, int64_t TC,
-    int64_t I0, const int* __restrict__ off, const int* __restrict__ nchunk_p,
-    const int* __restrict__ colLo, const int* __restrict__ colHi, uint16_t* __restrict__ co,
-    uint16_t* __restrict__ both, double* __restrict__ dist) {
-    __shared__ __attribute__((aligned(16))) uint8_t sA[COC_BM * COC_KC];
-    __shared__ __attribute__((aligned(16))) uint8_t sB[COC_BM * COC_KC];
-    // tile t -> (I, J): row tiles from I0, J in [I, TC)
-    const int64_t t = blockIdx.x;
-    int64_t lo = 0, hi = ccg_cdiv(r1 - r0, COC_BM);  // relative row tile in [lo, hi)
-    // cum(Ir) = sum_{s<Ir} (TC - (I0+s)) = Ir*(TC-I0) - Ir*(Ir-1)/2
-    auto cum = [&](int64_t Ir) { return Ir * (TC - I0) - Ir * (Ir - 1) / 2; };
-    while (hi - lo > 1) {
-        int64_t mid = (lo + hi) >> 1;
-        if (cum(mid) <= t) lo = mid; else hi = mid;
-    }
-    const int64_t I = I0 + lo;
-    const int64_t J = I + (t - cum(lo));
-    const int64_t rowA0 = I * COC_BM, rowB0 = J * COC_BM;
-
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wr = wv >> 1, wc = wv & 1;
-    const int op = tid >> 7, row = tid & 127;
-    const int64_t grow = (op ? rowB0 : rowA0) + row;
-    const bool rin = grow < N;
-    uint8_t* sOp = op ? sB : sA;
-
-    v16i accC[2][2], accS[2][2];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                accC[mi][ni][r] = 0;
-                accS[mi][ni][r] = 0;
-            }
-
-    // ---- co = H H^T over one-hot chunks
-    const int nch = *nchunk_p;
-    for (int ch = 0; ch < nch; ++ch) {
-        unsigned long long bits = 0ull;
-        if (rin) {
-            const int p0 = ch * COC_KC;
-            const int b1 = colHi[ch];
-            for (int b = colLo[ch]; b <= b1; ++b) {
-                const int lab = A[(int64_t)b * N + grow];
-                if (lab) {
-                    const int pos = off[b] + lab - 1 - p0;
-                    if (pos >= 0 && pos < COC_KC) bits |= 1ull << pos;
-                }
-            }
-        }
-        store_onehot_row(sOp, row, bits);
-        __syncthreads();
-        mfma_tile(sA, sB, wr, wc, lane, accC);
-        __syncthreads();
-    }
-    // ---- both = S S^T over column chunks
-    const int nchB = (int)ccg_cdiv(B, COC_KC);
-    for (int ch = 0; ch < nchB; ++ch) {
-        unsigned long long bits = 0ull;
-        if (rin) {
-            const int64_t b0 = (int64_t)ch * COC_KC;
-            const int nb = (int)std::min<int64_t>(COC_KC, B - b0);
-            for (int kk = 0; kk < nb; ++kk)
-                if (A[(b0 + kk) * N + grow]) bits |= 1ull << kk;
-        }
-        store_onehot_row(sOp, row, bits);
-        __syncthreads();
-        mfma_tile(sA, sB, wr, wc, lane, accS);
-        __syncthreads();
-    }
-    // ---- epilogue: packed upper triangle, rows [r0, r1)
-    const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t gi = rowA0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const int64_t gj = rowB0 + wc * 64 + ni * 32 + (lane & 31);
-                if (gi < r1 && gj < N && gj > gi) {
-                    const int64_t o = gi * N - gi * (gi + 1) / 2 + (gj - gi - 1) - base;
-                    const int cv = accC[mi][ni][r], bv = accS[mi][ni][r];
-                    if (co) co[o] = (uint16_t)cv;
-                    if (both) both[o] = (uint16_t)bv;
-                    if (dist) {
-                        const float q = (float)((double)cv / (double)bv);
-                        dist[o] = 1.0 - (double)q;
-                    }
-                }
-            }
-}
-
 // ------------------------------------------------- fused one-hot path --
 // co and both in ONE int32 accumulator: every column b gets a K range of
 // S_b = ceil((C_b + 1) / 16) 16-position slots; position 0 holds the
 // "sampled" flag as int8 -128 on both sides (product 16384), positions
 // 1..C_b the one-hot label (product 1), so
-//     acc = co + 16384 * both      (co <= B <= 16383, so the fields split)
+//     acc = co + 16384 * both      (co <= B_chunk <= 16383, so the fields split)
 // and K = 16 * sum_b S_b instead of sum_b C_b + B separate positions.
-// A lane gets its 16-byte MFMA fragment for slot (b, s) from its row's uint8
-// label through a 34-entry LDS pattern table (at most two non-zero bytes), so
-// the one-hot matrix never exists -- not in HBM, not in LDS.  Labels are staged per block of
-// COF_SLOTS slots (<= COF_SLOTS columns x 384 rows: 128 A-rows + 256 B-rows) in LDS,
-// double-buffered through registers.
+// Wider matrices (granular mode, B up to 65535) run in column chunks of at
+// most 16383 whose counts are added in the epilogue of the next chunk.
+// A lane gets its 16-byte MFMA fragment for slot (b, s) from its row's label
+// through a 34-entry LDS pattern table (at most two non-zero bytes), so the
+// one-hot matrix never exists -- not in HBM, not in LDS.  Labels are staged
+// per block of COF_SLOTS slots (<= COF_SLOTS columns x 384 rows: 128 A-rows +
+// 256 B-rows) in LDS, double-buffered through registers.  Columns with no
+// label (never sampled) own no slot and are skipped: stages index the
+// compacted list of non-empty columns.
 #define COF_BM 128          // output rows per block (2 waves x 64)
 #define COF_BN 256          // output cols per block (2 waves x 128)
 #define COF_SLOTS 32        // slots per stage (16 K-steps of v_mfma_i32_32x32x32_i8)
 #define COF_ROWS (COF_BM + COF_BN)
-#define COF_LOADS (COF_SLOTS * COF_ROWS / 4 / 256)  // dwords per thread per stage
+#define COF_CHUNK 16383     // columns per accumulation chunk
+#define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
 
-// slot table: desc[k] = b << 4 | s for k < K (K padded to a multiple of
-// COF_SLOTS with -1), stage_lo[st] / stage_nc[st] = the stage's column range.
-__global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__ colC, int64_t B,
-                                                         int* __restrict__ off, int* __restrict__ nslot,
+__device__ __forceinline__ int block_excl_scan1024(int v, int* sh, int* total) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    int woff = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+        if (w < wv) woff += sh[w];
+        tot += sh[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + x - v;
+}
+
+// Slot tables of one chunk of Bc columns (colC = the chunk's column maxima):
+// ccol[c] = chunk column of the c-th non-empty column; desc[k] = c << COF_SB
+// | s for k < K (K padded to a multiple of COF_SLOTS with -1); stage_lo[st] /
+// stage_nc[st] = the stage's range of compacted columns (nc <= COF_SLOTS since
+// every non-empty column owns at least one slot).
+__global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__ colC, int64_t Bc,
+                                                         int* __restrict__ ccol, int* __restrict__ nslot,
                                                          int* __restrict__ desc, int* __restrict__ stage_lo,
                                                          int* __restrict__ stage_nc) {
     __shared__ int sh[16];
-    __shared__ int carry_s;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t == 0) carry_s = 0;
-    __syncthreads();
-    for (int64_t b0 = 0; b0 < B; b0 += 1024) {
+    const int t = threadIdx.x;
+    int kcar = 0, ccar = 0;
+    for (int64_t b0 = 0; b0 < Bc; b0 += 1024) {
         const int64_t b = b0 + t;
-        const int v = (b < B && colC[b] > 0) ? (colC[b] + 1 + 15) / 16 : 0;
-        int x = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
+        const int C = b < Bc ? colC[b] : 0;
+        const int v = C > 0 ? (C + 16) / 16 : 0;  // ceil((C + 1) / 16)
+        int ktot, ctot;
+        const int koff = kcar + block_excl_scan1024(v, sh, &ktot);
+        const int coff = ccar + block_excl_scan1024(C > 0 ? 1 : 0, sh, &ctot);
+        if (C > 0) {
+            ccol[coff] = (int)b;
+            for (int s2 = 0; s2 < v; ++s2) desc[koff + s2] = (coff << COF_SB) | s2;
         }
-        if (lane == 63) sh[wv] = x;
-        __syncthreads();
-        int woff = 0, tot = 0;
-        for (int w = 0; w < 16; ++w) {
-            if (w < wv) woff += sh[w];
-            tot += sh[w];
-        }
-        const int carry = carry_s;
-        if (b < B) off[b] = carry + woff + x - v;
-        __syncthreads();
-        if (t == 0) carry_s = carry + tot;
-        __syncthreads();
+        kcar += ktot;
+        ccar += ctot;
     }
-    const int K = carry_s;
+    const int K = kcar;
     const int Kp = (K + COF_SLOTS - 1) / COF_SLOTS * COF_SLOTS;
     if (t == 0) *nslot = Kp;
-    for (int64_t b = t; b < B; b += 1024) {
-        const int v = colC[b] > 0 ? (colC[b] + 1 + 15) / 16 : 0;
-        for (int s2 = 0; s2 < v; ++s2) desc[off[b] + s2] = (int)(b << 4) | s2;
-    }
     for (int k = K + t; k < Kp; k += 1024) desc[k] = -1;
     __syncthreads();
     for (int st = t; st < Kp / COF_SLOTS; st += 1024) {
         const int k0 = st * COF_SLOTS;
-        int k1 = min(k0 + COF_SLOTS, K) - 1;
-        const int lo = desc[k0] >> 4;
-        const int hi = desc[k1] >> 4;
+        const int k1 = min(k0 + COF_SLOTS, K) - 1;
+        const int lo = desc[k0] >> COF_SB;
+        const int hi = desc[k1] >> COF_SB;
         stage_lo[st] = lo;
         stage_nc[st] = hi - lo + 1;
     }
@@ -304,37 +122,54 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
 
 // Fragment table (LDS, 34 x 16 B): entry i < 16 = one-hot byte i; 16 + i =
 // flag (-128 in byte 0) + one-hot byte i (i >= 1); 32 = flag only; 33 = zero.
-// A fragment is one conflict-free ds_read_b128 (the 16 one-hot entries span
-// the 64 banks exactly once) after ~6 VALU to pick the entry.
+// A fragment is one ds_read_b128 after ~6 VALU to pick the entry.
 #define COF_TAB 34
 __device__ __forceinline__ int cof_entry(int lab, int sub) {
     const int pos = lab - 16 * sub;
-    const int e0 = lab < 16 ? 16 + lab : 32;      // slot 0: flag (+ label if it fits)
+    const int e0 = lab < 16 ? 16 + lab : 32;        // slot 0: flag (+ label if it fits)
     const int e1 = (unsigned)pos < 16u ? pos : 33;  // later slots: label or nothing
     return lab == 0 ? 33 : (sub == 0 ? e0 : e1);
 }
 
+// Output modes: packed upper triangle of rows [r0, r1) (R "dist" order), or
+// full rows [r0, r1) x [0, N) as one uint32 co | both << 16 per pair.
+#define COF_TRI 0
+#define COF_RECT 1
+
+// T: label type (uint8_t / uint16_t); VEC: N is a multiple of 4/sizeof(T),
+// so a dword load covers 4/sizeof(T) consecutive rows of a column.
+template <typename T, bool VEC, int MODE>
 __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
-    const uint8_t* __restrict__ A, int64_t N, int64_t r0, int64_t r1, int64_t TC, int64_t I0,
+    const T* __restrict__ A, int64_t N, int64_t r0, int64_t r1, int64_t TC, int64_t I0,
     const int* __restrict__ desc, const int* __restrict__ stage_lo, const int* __restrict__ stage_nc,
-    const int* __restrict__ nslot_p, uint16_t* __restrict__ co, uint16_t* __restrict__ both,
-    double* __restrict__ dist) {
-    __shared__ __attribute__((aligned(16))) uint8_t panel[2][COF_SLOTS][COF_ROWS];
+    const int* __restrict__ ccol, const int* __restrict__ nslot_p, const uint16_t* co_prev,
+    const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* __restrict__ dist,
+    const uint32_t* cb_prev, uint32_t* cb) {
+    constexpr int RPD = 4 / (int)sizeof(T);             // rows per dword
+    constexpr int ROWD = COF_ROWS / RPD;                // dwords per staged column
+    constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
+    __shared__ __attribute__((aligned(16))) T panel[2][COF_SLOTS][COF_ROWS];
     __shared__ __attribute__((aligned(16))) v4i ftab[COF_TAB];
     __shared__ __attribute__((aligned(16))) int sdesc[2][2][COF_SLOTS / 2];  // [buf][half][k-step]
-    // tile t -> (I, J): row tiles of 128 from I0, col tiles of 256 from J = I/2
     const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
-    // cum(Ir) = sum_{s<Ir} (TC - (I0+s)/2)
-    auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };  // sum_{s<x} s/2
-    auto cum = [&](int64_t Ir) { return Ir * TC - (fl(I0 + Ir) - fl(I0)); };
-    int64_t lo = 0, hi = TR;
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (cum(mid) <= t) lo = mid; else hi = mid;
+    int64_t I, J;
+    if (MODE == COF_TRI) {
+        // tile t -> (I, J): row tiles of 128 from I0, col tiles of 256 from J = I/2
+        // cum(Ir) = sum_{s<Ir} (TC - (I0+s)/2)
+        auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };  // sum_{s<x} s/2
+        auto cum = [&](int64_t Ir) { return Ir * TC - (fl(I0 + Ir) - fl(I0)); };
+        int64_t lo = 0, hi = TR;
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (cum(mid) <= t) lo = mid; else hi = mid;
+        }
+        I = I0 + lo;
+        J = I / 2 + (t - cum(lo));
+    } else {
+        I = I0 + t / TC;
+        J = t - (t / TC) * TC;
     }
-    const int64_t I = I0 + lo;
-    const int64_t J = I / 2 + (t - cum(lo));
     const int64_t rowA0 = I * COF_BM, rowB0 = J * COF_BN;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -349,27 +184,41 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0;
 
-    // stage loader: dword p of the panel = (column c, row dword rd); rows past N read row N-4..N-1 (masked later)
-    unsigned pf[COF_LOADS];
+    // stage loader: dword p of the panel = (column c, row dword rd); rows past
+    // N read clamped rows (their outputs are masked in the epilogue)
+    unsigned pf[LOADS];
     int pdesc = -1;
     auto issue = [&](int st) {
         const int clo = stage_lo[st], nc = stage_nc[st];
 #pragma unroll
-        for (int i = 0; i < COF_LOADS; ++i) {
+        for (int i = 0; i < LOADS; ++i) {
             const int p = i * 256 + tid;
-            const int c = p / (COF_ROWS / 4), rd = p - c * (COF_ROWS / 4);
-            int64_t row = rd < COF_BM / 4 ? rowA0 + 4 * rd : rowB0 + 4 * (rd - COF_BM / 4);
-            row = row + 4 <= N ? row : N - 4;
-            pf[i] = c < nc ? *reinterpret_cast<const unsigned*>(A + (int64_t)(clo + c) * N + row) : 0u;
+            const int c = p / ROWD, rd = p - c * ROWD;
+            int64_t row = rd < COF_BM / RPD ? rowA0 + RPD * rd : rowB0 + RPD * (rd - COF_BM / RPD);
+            unsigned v = 0u;
+            if (c < nc) {
+                const T* colp = A + (int64_t)ccol[clo + c] * N;
+                if (VEC) {
+                    row = row + RPD <= N ? row : N - RPD;
+                    v = *reinterpret_cast<const unsigned*>(colp + row);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < RPD; ++e) {
+                        const int64_t rr = row + e < N ? row + e : N - 1;
+                        v |= (unsigned)colp[rr] << (8 * sizeof(T) * e);
+                    }
+                }
+            }
+            pf[i] = v;
         }
         if (tid < COF_SLOTS) {
             const int dsc = desc[(int64_t)st * COF_SLOTS + tid];
-            pdesc = dsc < 0 ? -1 : (((dsc >> 4) - clo) << 4) | (dsc & 15);
+            pdesc = dsc < 0 ? -1 : (((dsc >> COF_SB) - clo) << COF_SB) | (dsc & ((1 << COF_SB) - 1));
         }
     };
     auto commit = [&](int bb) {
 #pragma unroll
-        for (int i = 0; i < COF_LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
+        for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
         if (tid < COF_SLOTS) sdesc[bb][tid & 1][tid >> 1] = pdesc;
     };
     if (tid < COF_TAB) {
@@ -379,8 +228,10 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         if (tid >= 16 && tid < 33) e[0] |= 0x80;  // the flag (int8 -128) in byte 0
         ftab[tid] = e;
     }
-    issue(0);
-    commit(0);
+    if (nstage > 0) {
+        issue(0);
+        commit(0);
+    }
     __syncthreads();
     const int ra = wr * 64 + (lane & 31);            // A rows ra, ra + 32 (panel rows 0..127)
     const int rb = COF_BM + wc * 128 + (lane & 31);  // B rows rb + 32*ni
@@ -404,7 +255,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         int lab[2][6];
         auto read_labels = [&](int q, int (&L)[6]) {
             const int d = dsc[q];
-            const uint8_t* col = &panel[bb][d < 0 ? 0 : d >> 4][0];
+            const T* col = &panel[bb][d < 0 ? 0 : d >> COF_SB][0];
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi) L[mi] = d < 0 ? 0 : col[ra + 32 * mi];
 #pragma unroll
@@ -412,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         };
         v4i fr[2][6];
         auto read_frags = [&](int q, const int (&L)[6], v4i (&F)[6]) {
-            const int sub = dsc[q] < 0 ? 0 : dsc[q] & 15;
+            const int sub = dsc[q] < 0 ? 0 : dsc[q] & ((1 << COF_SB) - 1);
 #pragma unroll
             for (int x = 0; x < 6; ++x) F[x] = ftab[cof_entry(L[x], sub)];
         };
@@ -437,7 +288,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             __syncthreads();
         }
     }
-    // ---- epilogue: acc = co + 16384 * both; packed upper triangle, rows [r0, r1)
+    // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts)
     const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -447,86 +298,227 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             for (int r = 0; r < 16; ++r) {
                 const int64_t gi = rowA0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int64_t gj = rowB0 + wc * 128 + ni * 32 + (lane & 31);
-                if (gi < r1 && gj < N && gj > gi) {
-                    const int64_t o = gi * N - gi * (gi + 1) / 2 + (gj - gi - 1) - base;
-                    const int a = acc[mi][ni][r];
-                    const int cv = a & 16383, bv = a >> 14;
-                    if (co) co[o] = (uint16_t)cv;
-                    if (both) both[o] = (uint16_t)bv;
-                    if (dist) {
-                        const float qv = (float)((double)cv / (double)bv);
-                        dist[o] = 1.0 - (double)qv;
+                const int a = acc[mi][ni][r];
+                int cv = a & 16383, bv = a >> 14;
+                if (MODE == COF_TRI) {
+                    if (gi < r1 && gj < N && gj > gi) {
+                        const int64_t o = gi * N - gi * (gi + 1) / 2 + (gj - gi - 1) - base;
+                        if (co_prev) {
+                            cv += co_prev[o];
+                            bv += both_prev[o];
+                        }
+                        if (co) co[o] = (uint16_t)cv;
+                        if (both) both[o] = (uint16_t)bv;
+                        if (dist) {
+                            const float qv = (float)((double)cv / (double)bv);
+                            dist[o] = 1.0 - (double)qv;
+                        }
+                    }
+                } else {
+                    if (gi < r1 && gj < N) {
+                        const int64_t o = (gi - r0) * N + gj;
+                        if (cb_prev) {
+                            const uint32_t pv = cb_prev[o];
+                            cv += (int)(pv & 0xFFFFu);
+                            bv += (int)(pv >> 16);
+                        }
+                        cb[o] = (uint32_t)cv | ((uint32_t)bv << 16);
                     }
                 }
             }
 }
 
-extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B, int64_t r0,
+// Launch state shared by the triangle and full-row drivers.
+struct CofPlan {
+    int* colC;
+    int* ccol;
+    int* nslot;
+    int* desc;
+    int* slo;
+    int* snc;
+    int64_t maxslots;
+};
+
+// Column maxima + table space.  label_bits 16 synchronises once to size the
+// slot table exactly (sum_b ceil((C_b + 1) / 16) can be large); 8 bounds it
+// by 16 slots per column.
+static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, hipStream_t st,
+                    CofPlan* pl) {
+    int* colC = (int*)ccg_ws(ctx, WS_COC_A, sizeof(int) * (B + 8));
+    if (!colC) return CCG_ENOMEM;
+    CCG_HIP(hipMemsetAsync(colC, 0, sizeof(int) * B, st));
+    const dim3 g((unsigned)std::min<int64_t>(ccg_cdiv(N, 256), 64), (unsigned)B);
+    if (label_bits == 8) coc_colmax_kernel<uint8_t><<<g, 256, 0, st>>>((const uint8_t*)A, N, colC);
+    else coc_colmax_kernel<uint16_t><<<g, 256, 0, st>>>((const uint16_t*)A, N, colC);
+    CCG_HIP(hipGetLastError());
+    const int64_t Bc = std::min<int64_t>(B, COF_CHUNK);
+    int64_t maxslots = Bc * 16 + COF_SLOTS;
+    if (label_bits == 16) {
+        std::vector<int> h(B);
+        CCG_HIP(hipMemcpyAsync(h.data(), colC, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        int64_t worst = 0;
+        for (int64_t c0 = 0; c0 < B; c0 += COF_CHUNK) {
+            int64_t s = 0;
+            for (int64_t b = c0; b < std::min<int64_t>(B, c0 + COF_CHUNK); ++b) s += h[b] > 0 ? (h[b] + 16) / 16 : 0;
+            worst = std::max(worst, s);
+        }
+        maxslots = worst + COF_SLOTS;
+    }
+    int* ft = (int*)ccg_ws(ctx, WS_COC_B, sizeof(int) * (Bc + 8 + maxslots + 2 * (maxslots / COF_SLOTS + 1)));
+    if (!ft) return CCG_ENOMEM;
+    pl->colC = colC;
+    pl->ccol = ft;
+    pl->nslot = ft + Bc;
+    pl->desc = pl->nslot + 8;
+    pl->slo = pl->desc + maxslots;
+    pl->snc = pl->slo + (maxslots / COF_SLOTS + 1);
+    pl->maxslots = maxslots;
+    return CCG_OK;
+}
+
+template <int MODE>
+static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t N, int64_t r0, int64_t r1, int64_t TC,
+                       int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
+                       const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
+                       uint32_t* cb, hipStream_t st) {
+#define COF_ARGS N, r0, r1, TC, I0, pl.desc, pl.slo, pl.snc, pl.ccol, pl.nslot, co_prev, both_prev, co, both, dist, \
+                 cb_prev, cb
+    if (label_bits == 8) {
+        const uint8_t* Ac = (const uint8_t*)A + cb0 * N;
+        if (N % 4 == 0) cof_tile_kernel<uint8_t, true, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
+        else cof_tile_kernel<uint8_t, false, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
+    } else {
+        const uint16_t* Ac = (const uint16_t*)A + cb0 * N;
+        if (N % 2 == 0) cof_tile_kernel<uint16_t, true, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
+        else cof_tile_kernel<uint16_t, false, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
+    }
+#undef COF_ARGS
+}
+
+extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int64_t r0,
                                  int64_t r1, uint16_t* co, uint16_t* both, double* dist, void* stream) {
     CCG_REQUIRE(ctx && A, "ccg_cocluster_dev: NULL argument");
+    CCG_REQUIRE(label_bits == 8 || label_bits == 16, "ccg_cocluster_dev: label_bits must be 8 or 16");
     CCG_REQUIRE(N >= 2 && N < (1LL << 31), "ccg_cocluster_dev: bad N");
     CCG_REQUIRE(B >= 1 && B <= 65535, "ccg_cocluster_dev: B=%lld must be in [1, 65535] (uint16 counts)",
                 (long long)B);
     CCG_REQUIRE(r0 >= 0 && r0 <= r1 && r1 <= N, "ccg_cocluster_dev: bad row range");
-    CCG_REQUIRE(r0 % CCG_COCLUSTER_ROW_ALIGN == 0, "ccg_cocluster_dev: r0 must be a multiple of %d",
-                CCG_COCLUSTER_ROW_ALIGN);
     hipStream_t st = ccg_pick_stream(ctx, stream);
     if (r1 == r0) return CCG_OK;
-    const int64_t maxch = ccg_cdiv(B * 255, COC_KC) + 2;
-    int* tab = (int*)ccg_ws(ctx, WS_COC_A, sizeof(int) * (B + (B + 1) + 1 + 2 * maxch + 8));
-    if (!tab) return CCG_ENOMEM;
-    int* colC = tab;
-    int* off = colC + B;
-    int* nchunk = off + (B + 1);
-    int* colLo = nchunk + 1;
-    int* colHi = colLo + maxch;
-    CCG_HIP(hipMemsetAsync(colC, 0, sizeof(int) * B, st));
-    coc_colmax_kernel<<<dim3((unsigned)std::min<int64_t>(ccg_cdiv(N, 256), 64), (unsigned)B), 256, 0, st>>>(
-        A, N, colC);
-    coc_tables_kernel<<<1, 1024, 0, st>>>(colC, B, off, nchunk, colLo, colHi);
-    static const bool legacy = getenv("CCG_COC_LEGACY") != nullptr;  // A/B switch
-    if (B <= 16383 && N % 4 == 0 && N >= 4 && !legacy) {
-        // fused one-hot path (co + 16384*both in one accumulator)
-        const int64_t maxslots = B * 16 + COF_SLOTS;
-        int* ft = (int*)ccg_ws(ctx, WS_COC_B, sizeof(int) * (B + 8 + maxslots + 2 * (maxslots / COF_SLOTS + 1)));
-        if (!ft) return CCG_ENOMEM;
-        int* foff = ft;
-        int* fnslot = foff + B;
-        int* fdesc = fnslot + 8;
-        int* fslo = fdesc + maxslots;
-        int* fsnc = fslo + (maxslots / COF_SLOTS + 1);
-        cof_slots_kernel<<<1, 1024, 0, st>>>(colC, B, foff, fnslot, fdesc, fslo, fsnc);
-        const int64_t TC = ccg_cdiv(N, COF_BN);
-        const int64_t I0 = r0 / COF_BM;
-        const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
-        auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
-        const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
-        CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_dev: too many tiles");
-        const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
-        cof_tile_kernel<<<(unsigned)ntiles, 256, 0, st>>>(A, N, r0, r1, TC, I0, fdesc, fslo, fsnc, fnslot, co,
-                                                         both, dist);
-        ccg_timer_stop(ctx, t_k, st);
-        CCG_HIP(hipGetLastError());
-        return CCG_OK;
-    }
-    const int64_t TC = ccg_cdiv(N, COC_BM);
-    const int64_t I0 = r0 / COC_BM;
-    const int64_t TR = ccg_cdiv(r1 - r0, COC_BM);
-    const int64_t ntiles = TR * (TC - I0) - TR * (TR - 1) / 2;
+    CCG_REQUIRE(r0 % CCG_COCLUSTER_ROW_ALIGN == 0, "ccg_cocluster_dev: r0 must be a multiple of %d",
+                CCG_COCLUSTER_ROW_ALIGN);
+    CofPlan pl;
+    int rc = cof_plan(ctx, A, label_bits, N, B, st, &pl);
+    if (rc) return rc;
+    const int64_t TC = ccg_cdiv(N, COF_BN);
+    const int64_t I0 = r0 / COF_BM;
+    const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
+    auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
+    const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
     CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_dev: too many tiles");
+    const int64_t nch = ccg_cdiv(B, COF_CHUNK);
+    uint16_t *pco = co, *pboth = both;  // partial counts between chunks
+    if (nch > 1 && (!co || !both)) {
+        const int64_t P = (r1 - r0) * N - (r1 * (r1 + 1) - r0 * (r0 + 1)) / 2;
+        uint16_t* scr = (uint16_t*)ccg_ws(ctx, WS_COC_C, sizeof(uint16_t) * 2 * P);
+        if (!scr) return CCG_ENOMEM;
+        if (!pco) pco = scr;
+        if (!pboth) pboth = scr + P;
+    }
     const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
-    coc_tile_kernel<<<(unsigned)ntiles, 256, 0, st>>>(A, N, B, r0, r1, TC, I0, off, nchunk, colLo, colHi,
-                                                     co, both, dist);
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t cb0 = c * COF_CHUNK, Bc = std::min<int64_t>(COF_CHUNK, B - cb0);
+        cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
+        const bool last = c == nch - 1;
+        cof_launch<COF_TRI>(label_bits, A, cb0, N, r0, r1, TC, I0, ntiles, pl, c ? pco : nullptr,
+                            c ? pboth : nullptr, nch > 1 ? pco : co, nch > 1 ? pboth : both, last ? dist : nullptr,
+                            nullptr, nullptr, st);
+    }
     ccg_timer_stop(ctx, t_k, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
 
+// Full rows [r0, r1) x [0, N) of (co, both), packed co | both << 16 into
+// cb[(i - r0) * N + j] (diagonal included).  Used by the consensus kNN on a
+// row slab so the N x N matrix never exists.
+static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int64_t r0,
+                              int64_t r1, uint32_t* cb, hipStream_t st) {
+    CofPlan pl;
+    int rc = cof_plan(ctx, A, label_bits, N, B, st, &pl);
+    if (rc) return rc;
+    const int64_t TC = ccg_cdiv(N, COF_BN);
+    const int64_t I0 = r0 / COF_BM;
+    const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
+    const int64_t ntiles = TR * TC;
+    CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_rows: too many tiles");
+    const int64_t nch = ccg_cdiv(B, COF_CHUNK);
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t cb0 = c * COF_CHUNK, Bc = std::min<int64_t>(COF_CHUNK, B - cb0);
+        cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
+        cof_launch<COF_RECT>(label_bits, A, cb0, N, r0, r1, TC, I0, ntiles, pl, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, c ? cb : nullptr, cb, st);
+    }
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
 // ------------------------------------------------------ consensus kNN --
-// One wave per row: lanes scan columns j = lane, lane+64, ...; key = the
-// fp32 similarity (larger = closer, equivalent to ascending 1 - sim), ties
-// by ascending j; self excluded; NaN (both == 0) raises the flag.
+// dbscan::kNN(jaccardDist, k)$id (R/consensusClust.R:425): per row, the k
+// smallest D = 1 - (double)(float)(co / both) over j != i, ties by ascending
+// j (R's stable order()); NaN (both == 0) makes dbscan stop().  Ascending D
+// is descending fp32 similarity, so the kernels rank by (sim desc, j asc).
+// One wave per row: lane l scans j = l, l + 64, ... (ascending per lane, so
+// an equal value never displaces an earlier j) into a sorted register list;
+// the 64 lists are merged by k rounds of wave arg-max.
 #define CKNN_K 32
+__device__ __forceinline__ void cknn_insert(float (&lv)[CKNN_K], int (&li)[CKNN_K], float s, int j) {
+    float cv = s;
+    int ci = j;
+#pragma unroll
+    for (int t = 0; t < CKNN_K; ++t) {
+        const bool sw = (cv > lv[t]) || (cv == lv[t] && ci < li[t]);
+        const float tv = lv[t];
+        const int ti = li[t];
+        lv[t] = sw ? cv : tv;
+        li[t] = sw ? ci : ti;
+        cv = sw ? tv : cv;
+        ci = sw ? ti : ci;
+    }
+}
+
+__device__ __forceinline__ void cknn_merge_out(float (&lv)[CKNN_K], int (&li)[CKNN_K], int k,
+                                               int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    for (int r = 0; r < k; ++r) {
+        float bk = lv[0];
+        int bi = li[0];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ok = __shfl_xor(bk, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ok > bk || (ok == bk && oi < bi)) {
+                bk = ok;
+                bi = oi;
+            }
+        }
+        if (lane == 0) out[r] = bi;
+        if (li[0] == bi) {
+#pragma unroll
+            for (int t = 0; t < CKNN_K - 1; ++t) {
+                lv[t] = lv[t + 1];
+                li[t] = li[t + 1];
+            }
+            lv[CKNN_K - 1] = -INFINITY;
+            li[CKNN_K - 1] = 0x7fffffff;
+        }
+    }
+}
+
+// From the packed triangle (co/both of the whole matrix).  Columns j < i come
+// from column i of the triangle (strided reads); the slab path below reads
+// rows only.
 __global__ __launch_bounds__(256) void consensus_knn_kernel(const uint16_t* __restrict__ co,
                                                             const uint16_t* __restrict__ both,
                                                             int64_t N, int k, int32_t* __restrict__ out,
@@ -553,43 +545,52 @@ __global__ __launch_bounds__(256) void consensus_knn_kernel(const uint16_t* __re
         }
         const float s = (float)((double)c / (double)u);
         if (!(s > lv[CKNN_K - 1])) continue;  // j ascending per lane: ties keep the earlier j
-        float cv = s;
-        int ci = (int)j;
+        cknn_insert(lv, li, s, (int)j);
+    }
+    if (__any(sawnan) && lane == 0) atomicOr(nan_flag, 1);
+    cknn_merge_out(lv, li, k, out + i * k);
+}
+
+// From full rows cb[(i - r0) * N + j] = co | both << 16 (rows [r0, r1)).
+__global__ __launch_bounds__(256) void consensus_knn_rows_kernel(const uint32_t* __restrict__ cb, int64_t N,
+                                                                 int64_t r0, int64_t r1, int k,
+                                                                 int32_t* __restrict__ out,
+                                                                 int* __restrict__ nan_flag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= r1) return;
+    const uint32_t* row = cb + (i - r0) * N;
+    float lv[CKNN_K];
+    int li[CKNN_K];
 #pragma unroll
-        for (int t = 0; t < CKNN_K; ++t) {
-            const bool sw = (cv > lv[t]) || (cv == lv[t] && ci < li[t]);
-            const float tv = lv[t];
-            const int ti = li[t];
-            lv[t] = sw ? cv : tv;
-            li[t] = sw ? ci : ti;
-            cv = sw ? tv : cv;
-            ci = sw ? ti : ci;
+    for (int t = 0; t < CKNN_K; ++t) {
+        lv[t] = -INFINITY;
+        li[t] = 0x7fffffff;
+    }
+    bool sawnan = false;
+    for (int64_t j0 = 0; j0 < N; j0 += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t j = j0 + 64 * e + lane;
+            v[e] = j < N ? row[j] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t j = j0 + 64 * e + lane;
+            if (j >= N || j == i) continue;
+            const unsigned c = v[e] & 0xFFFFu, u = v[e] >> 16;
+            if (u == 0) {
+                sawnan = true;
+                continue;
+            }
+            const float s = (float)((double)c / (double)u);
+            if (!(s > lv[CKNN_K - 1])) continue;
+            cknn_insert(lv, li, s, (int)j);
         }
     }
     if (__any(sawnan) && lane == 0) atomicOr(nan_flag, 1);
-    for (int r = 0; r < k; ++r) {
-        float bk = lv[0];
-        int bi = li[0];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ok = __shfl_xor(bk, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (ok > bk || (ok == bk && oi < bi)) {
-                bk = ok;
-                bi = oi;
-            }
-        }
-        if (lane == 0) out[i * k + r] = bi;
-        if (li[0] == bi) {
-#pragma unroll
-            for (int t = 0; t < CKNN_K - 1; ++t) {
-                lv[t] = lv[t + 1];
-                li[t] = li[t + 1];
-            }
-            lv[CKNN_K - 1] = -INFINITY;
-            li[CKNN_K - 1] = 0x7fffffff;
-        }
-    }
+    cknn_merge_out(lv, li, k, out + i * k);
 }
 
 extern "C" int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co, const uint16_t* both, int64_t N,
@@ -603,26 +604,89 @@ extern "C" int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co, const uin
     return CCG_OK;
 }
 
+// Rows per sub-slab of the fused consensus kNN: bounded by the packed-row
+// scratch (CKNN_SCRATCH bytes), a multiple of the co-cluster row tile.
+#define CKNN_SCRATCH (4LL << 30)
+
+extern "C" int ccg_consensus_knn_assign_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B,
+                                            int k, int64_t r0, int64_t r1, int32_t* out_idx, int32_t* d_nan_flag,
+                                            void* stream) {
+    CCG_REQUIRE(ctx && A && out_idx && d_nan_flag, "ccg_consensus_knn_assign_dev: NULL argument");
+    CCG_REQUIRE(label_bits == 8 || label_bits == 16, "ccg_consensus_knn_assign_dev: label_bits must be 8 or 16");
+    CCG_REQUIRE(N >= 2 && N < (1LL << 31) && B >= 1 && B <= 65535, "ccg_consensus_knn_assign_dev: bad sizes");
+    CCG_REQUIRE(k >= 1 && k <= CKNN_K && k <= N - 1, "ccg_consensus_knn_assign_dev: need 1 <= k <= min(32, N-1)");
+    CCG_REQUIRE(r0 >= 0 && r0 <= r1 && r1 <= N, "ccg_consensus_knn_assign_dev: bad row range");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    CCG_HIP(hipMemsetAsync(d_nan_flag, 0, sizeof(int32_t), st));
+    if (r0 == r1) return CCG_OK;
+    CCG_REQUIRE(r0 % CCG_COCLUSTER_ROW_ALIGN == 0, "ccg_consensus_knn_assign_dev: r0 must be a multiple of %d",
+                CCG_COCLUSTER_ROW_ALIGN);
+    int64_t R = (CKNN_SCRATCH / (4 * N)) / COF_BM * COF_BM;
+    R = std::max<int64_t>(R, COF_BM);
+    R = std::min<int64_t>(R, ccg_cdiv(r1 - r0, COF_BM) * COF_BM);
+    uint32_t* cb = (uint32_t*)ccg_ws(ctx, WS_COC_C, sizeof(uint32_t) * R * N);
+    if (!cb) return CCG_ENOMEM;
+    const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
+    for (int64_t a = r0; a < r1; a += R) {
+        const int64_t b = std::min(r1, a + R);
+        int rc = ccg_cocluster_rows_packed(ctx, A, label_bits, N, B, a, b, cb, st);
+        if (rc) return rc;
+        consensus_knn_rows_kernel<<<(unsigned)ccg_cdiv(b - a, 4), 256, 0, st>>>(cb, N, a, b, k, out_idx,
+                                                                                d_nan_flag);
+    }
+    ccg_timer_stop(ctx, t_k, st);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
 // ------------------------------------------------------- host flavours --
-extern "C" int ccg_cocluster(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B, uint16_t* co,
+extern "C" int ccg_cocluster(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, uint16_t* co,
                              uint16_t* both, double* dist) {
     CCG_REQUIRE(ctx && A, "ccg_cocluster: NULL argument");
     CCG_REQUIRE(N >= 2 && B >= 1, "ccg_cocluster: bad sizes");
+    CCG_REQUIRE(label_bits == 8 || label_bits == 16, "ccg_cocluster: label_bits must be 8 or 16");
     CCG_HIP(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int64_t P = N * (N - 1) / 2;
-    uint8_t* dA = (uint8_t*)ccg_ws(ctx, WS_HOST_A, (size_t)(B * N));
+    const size_t abytes = (size_t)(B * N) * (label_bits / 8);
+    void* dA = ccg_ws(ctx, WS_HOST_A, abytes);
     uint16_t* dco = co ? (uint16_t*)ccg_ws(ctx, WS_HOST_B, sizeof(uint16_t) * P) : nullptr;
     uint16_t* dboth = both ? (uint16_t*)ccg_ws(ctx, WS_HOST_C, sizeof(uint16_t) * P) : nullptr;
     double* ddist = dist ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * P) : nullptr;
     if (!dA || (co && !dco) || (both && !dboth) || (dist && !ddist)) return CCG_ENOMEM;
-    CCG_HIP(hipMemcpyAsync(dA, A, (size_t)(B * N), hipMemcpyHostToDevice, st));
-    int rc = ccg_cocluster_dev(ctx, dA, N, B, 0, N, dco, dboth, ddist, st);
+    CCG_HIP(hipMemcpyAsync(dA, A, abytes, hipMemcpyHostToDevice, st));
+    int rc = ccg_cocluster_dev(ctx, dA, label_bits, N, B, 0, N, dco, dboth, ddist, st);
     if (rc) return rc;
     if (co) CCG_HIP(hipMemcpyAsync(co, dco, sizeof(uint16_t) * P, hipMemcpyDeviceToHost, st));
     if (both) CCG_HIP(hipMemcpyAsync(both, dboth, sizeof(uint16_t) * P, hipMemcpyDeviceToHost, st));
     if (dist) CCG_HIP(hipMemcpyAsync(dist, ddist, sizeof(double) * P, hipMemcpyDeviceToHost, st));
     CCG_HIP(hipStreamSynchronize(st));
+    return CCG_OK;
+}
+
+extern "C" int ccg_consensus_knn_assign(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int k,
+                                        int32_t* out_idx) {
+    CCG_REQUIRE(ctx && A && out_idx, "ccg_consensus_knn_assign: NULL argument");
+    CCG_REQUIRE(label_bits == 8 || label_bits == 16, "ccg_consensus_knn_assign: label_bits must be 8 or 16");
+    CCG_REQUIRE(N >= 2 && B >= 1 && k >= 1, "ccg_consensus_knn_assign: bad sizes");
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const size_t abytes = (size_t)(B * N) * (label_bits / 8);
+    void* dA = ccg_ws(ctx, WS_HOST_A, abytes);
+    int32_t* dout = (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * N * k + 64);
+    if (!dA || !dout) return CCG_ENOMEM;
+    int32_t* dflag = dout + N * k;
+    CCG_HIP(hipMemcpyAsync(dA, A, abytes, hipMemcpyHostToDevice, st));
+    int rc = ccg_consensus_knn_assign_dev(ctx, dA, label_bits, N, B, k, 0, N, dout, dflag, st);
+    if (rc) return rc;
+    int flag = 0;
+    CCG_HIP(hipMemcpyAsync(&flag, dflag, sizeof(int), hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipMemcpyAsync(out_idx, dout, sizeof(int32_t) * N * k, hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
+    if (flag) {
+        ccg_set_error("ccg_consensus_knn_assign: data/distances cannot contain NAs (a pair was never co-sampled)");
+        return CCG_ENAN;
+    }
     return CCG_OK;
 }
 

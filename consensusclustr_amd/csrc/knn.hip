@@ -6,17 +6,19 @@
 // Euclidean neighbours, self excluded by row identity, ordered by the fp64
 // squared distance summed unfused in dimension order, ties by row index.
 //
-// Three stages, all on the device:
-//   1. prep     : rows64 -> refs32 image (fp32, dims permuted for the MFMA
-//                 fragment, slot d holds -|y|^2/2) and max row norm.
-//   2. screen   : v_mfma_f32_32x32x2_f32 computes v = x.y - |y|^2/2 for a
-//                 32-query x 32-reference tile per wave; each lane keeps the
-//                 KP best references of its half-tile in registers.
-//   3. certify  : one wave per query recomputes the 2*KP candidates in fp64,
-//                 bitonic-sorts them by (d2, j) across lanes and proves that
-//                 no excluded reference can enter the top k using a rigorous
-//                 fp32 error bound; rows that cannot be proven go to
-//   4. fallback : exact fp64 scan of all references for that row.
+// Stages, all on the device:
+//   1. order + prep : Morton order of the leading PCs; rows scaled by 2^e and
+//                     split into fp16 hi/lo images (knn_prep16_kernel).
+//   2. screen       : three v_mfma_f32_32x32x16_f16 per 16 dims compute
+//                     v = x.y - |y|^2/2 for a 32-query x 32-reference tile per
+//                     wave; each lane keeps the KP best references of its
+//                     half-tile in registers (knn_screen16_kernel).
+//   3. certify      : one wave per query recomputes the 2*KP candidates in
+//                     fp64, bitonic-sorts them by (d2, j) across lanes and
+//                     proves with a rigorous error bound that no excluded
+//                     reference can enter the top k; rows that cannot be
+//                     proven go to
+//   4. fallback     : exact fp64 scan of all references for that row.
 #include <math.h>
 #include <stdlib.h>
 
@@ -35,21 +37,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_FB_S 64        // max reference ranges per failed row
 #define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
 
-// Relative error budget of the fp32 screen in units of the fp32 ulp (2^-24)
-// times (|x| + max|y|)^2; see DESIGN.md "kNN certification bound".
-#define KNN_ERR_ULPS 256.0
-// fp16 hi/lo screen: 3 x 16*KSTEPS products accumulated in fp32
+// Error budget of the fp16 hi/lo screen (DESIGN.md "kNN certification bound"):
+// relative part in units of the fp32 ulp (2^-24) times (2|x| + sqrt(dK))^2 --
+// 3 x 16*KSTEPS products accumulated in fp32 -- plus an absolute part from
+// the hi/lo representation floor: hi/lo parts below KNN_F16_FLOOR (the
+// smallest normal fp16) are flushed to zero in prep, so every scaled value
+// carries an absolute error of at most 2^-14 whatever the hardware's fp16
+// denormal mode.
 #define KNN_ERR_ULPS_F16 1024.0
-
-__device__ __forceinline__ double sqdist_exact(const double* __restrict__ a,
-                                               const double* __restrict__ b, int d) {
-    double s = 0.0;
-    for (int k = 0; k < d; ++k) {
-        double t = __dsub_rn(a[k], b[k]);
-        s = __dadd_rn(s, __dmul_rn(t, t));
-    }
-    return s;
-}
+#define KNN_F16_FLOOR 0x1p-14
 
 // --------------------------------------------------------------- gather --
 __global__ void gather_rows_kernel(const double* __restrict__ pcs, int64_t N, int d,
@@ -62,53 +58,7 @@ __global__ void gather_rows_kernel(const double* __restrict__ pcs, int64_t N, in
     rows[t] = pcs[(int64_t)k * N + idx[i]];
 }
 
-// ----------------------------------------------------------------- prep --
-// refs32 row r: position h*KS + s holds dim 2s+h (fp32); dim d holds
-// -0.5*|y|^2; other pad dims 0.  Rows n..npad-1 are zero.
-__global__ void knn_prep_kernel(const double* __restrict__ rows, int64_t n, int64_t npad,
-                                int d, int KS, float* __restrict__ refs,
-                                unsigned int* __restrict__ mnorm_bits) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= npad) return;
-    float* out = refs + r * (2 * KS);
-    if (r >= n) {
-        for (int p = 0; p < 2 * KS; ++p) out[p] = 0.f;
-        return;
-    }
-    const double* y = rows + r * d;
-    double nr = 0.0;
-    for (int k = 0; k < d; ++k) nr += y[k] * y[k];
-    for (int p = 0; p < 2 * KS; ++p) {
-        int h = p / KS, s = p - h * KS;
-        int k = 2 * s + h;
-        float v = 0.f;
-        if (k < d) v = (float)y[k];
-        else if (k == d) v = (float)(-0.5 * nr);
-        out[p] = v;
-    }
-    // norm upper bound (round up by 2 ulp): non-negative float bits order as ints
-    float nf = (float)sqrt(nr);
-    nf = nextafterf(nextafterf(nf, INFINITY), INFINITY);
-    atomicMax(mnorm_bits, __float_as_uint(nf));
-}
-
 // --------------------------------------------------------------- screen --
-template <int KP>
-__device__ __forceinline__ void list_insert(float (&lv)[KP], int (&li)[KP], float v, int id) {
-    float cv = v;
-    int ci = id;
-#pragma unroll
-    for (int t = 0; t < KP; ++t) {
-        bool sw = cv > lv[t];
-        float tv = lv[t];
-        int ti = li[t];
-        lv[t] = sw ? cv : tv;
-        li[t] = sw ? ci : ti;
-        cv = sw ? tv : cv;
-        ci = sw ? ti : ci;
-    }
-}
-
 // Insert (v, id) into a descending register list (v > lv[KP-1] assumed) by
 // "position + shift": the keep-flags c_t = !(v > lv[t]) are independent
 // compares, and each slot is then a two-level select
@@ -154,91 +104,6 @@ __device__ __forceinline__ float union_kth(const float (&lv)[KP]) {
     return t;
 }
 
-template <int KS>
-__device__ __forceinline__ void load_frag(const float* __restrict__ p, float (&f)[KS]) {
-    const float4* p4 = reinterpret_cast<const float4*>(p);
-#pragma unroll
-    for (int s4 = 0; s4 < KS / 4; ++s4) {
-        float4 v = p4[s4];
-        f[4 * s4 + 0] = v.x;
-        f[4 * s4 + 1] = v.y;
-        f[4 * s4 + 2] = v.z;
-        f[4 * s4 + 3] = v.w;
-    }
-}
-
-template <int KS, int KP>
-__global__ __launch_bounds__(256) void knn_screen_kernel(const float* __restrict__ refs,
-                                                         int n, int ntiles, int d,
-                                                         int* __restrict__ cand_idx,
-                                                         float* __restrict__ cand_thr) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int col = lane & 31;
-    const int h = lane >> 5;
-    const int q = blockIdx.x * KNN_QPB + wave * 32 + col;
-    const int qrow = q < n ? q : n - 1;
-
-    float qf[KS];
-    load_frag<KS>(refs + (int64_t)qrow * (2 * KS) + h * KS, qf);
-    // query side of the norm slot is 1.0
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-        if (2 * s + h == d) qf[s] = 1.0f;
-
-    float lv[KP];
-    int li[KP];
-#pragma unroll
-    for (int t = 0; t < KP; ++t) {
-        lv[t] = -INFINITY;
-        li[t] = -1;
-    }
-    float thr = -INFINITY;
-
-    float af[KS];
-    load_frag<KS>(refs + (int64_t)col * (2 * KS) + h * KS, af);
-    for (int t = 0; t < ntiles; ++t) {
-        float an[KS];
-        const int tn = (t + 1 < ntiles) ? t + 1 : t;
-        load_frag<KS>(refs + ((int64_t)tn * 32 + col) * (2 * KS) + h * KS, an);
-
-        f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
-                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], qf[s], acc, 0, 0, 0);
-
-        const int rbase = t * 32 + 4 * h;
-        float vmax = -INFINITY;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int r = rbase + (reg & 3) + 8 * (reg >> 2);
-            float v = acc[reg];
-            v = (r < n && r != q) ? v : -INFINITY;
-            acc[reg] = v;
-            vmax = fmaxf(vmax, v);
-        }
-        if (__any(vmax > thr)) {
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const float v = acc[reg];
-                if (v > thr) {
-                    list_insert<KP>(lv, li, v, rbase + (reg & 3) + 8 * (reg >> 2));
-                    thr = lv[KP - 1];
-                }
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s) af[s] = an[s];
-    }
-    if (q < n) {
-        int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
-#pragma unroll
-        for (int t = 0; t < KP; ++t) out[t] = li[t];
-        cand_thr[(int64_t)q * 2 + h] = thr;
-    }
-}
-
 // ------------------------------------------------- fp16 hi/lo screen --
 // Each value x (scaled by sigma = 2^e so max|x| <= 2^13) is split into
 // fp16 hi = rn(x) and lo = rn(x - hi); x.y ~ hi.hi + hi.lo + lo.hi with
@@ -280,8 +145,12 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
             nr += x * x;
             xs = ldexp(x, e);
         }
-        const _Float16 hi = (_Float16)(float)xs;
-        const _Float16 lo = (_Float16)(float)(xs - (double)(float)hi);
+        // parts below the smallest normal fp16 are flushed here, explicitly,
+        // so the certification floor (KNN_F16_FLOOR) holds in any denorm mode
+        _Float16 hi = (_Float16)(float)xs;
+        if (fabs((double)(float)hi) < KNN_F16_FLOOR) hi = (_Float16)0.0f;
+        _Float16 lo = (_Float16)(float)(xs - (double)(float)hi);
+        if (fabs((double)(float)lo) < KNN_F16_FLOOR) lo = (_Float16)0.0f;
         const int s = k / 16, h = (k % 16) / 8, j = k % 8;
         hv[h * (KSTEPS * 16) + s * 8 + j] = hi;
         hv[h * (KSTEPS * 16) + KSTEPS * 8 + s * 8 + j] = lo;
@@ -428,10 +297,7 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
     return x * q + min(x, r) + i;
 }
 
-// EXP 4: product kernel plus event counters (timing experiments only)
-__device__ unsigned long long g_knn_dbg[8];
-
-template <int KSTEPS, int KP, int EXP = 0, int QC = KNN_QCAP>
+template <int KSTEPS, int KP, int QC = KNN_QCAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(const uint4* __restrict__ img,
                                                            const float* __restrict__ nrm, int n, int nchunks,
                                                            int* __restrict__ cand_idx,
@@ -530,12 +396,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #define KNN_FLUSH()                                                                   \
     do {                                                                              \
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
-            if (EXP == 4 && lane == 0) atomicAdd(&g_knn_dbg[2], 1ull);                \
             if (i_ < qc) {                                                            \
                 const uint2 e_ = qbw[i_ * 64 + lane];                                 \
                 const float v_ = __uint_as_float(e_.x);                               \
                 if (v_ > T) {                                                         \
-                    if (EXP == 4) atomicAdd(&g_knn_dbg[3], 1ull);                     \
                     list_insert_par<KP>(lv, li, v_, (int)e_.y);                       \
                     thr = lv[KP - 1];                                                 \
                     T = fmaxf(T, thr);                                                \
@@ -551,7 +415,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     for (int k = 0; k < nck; ++k) {
         const int b = k & 1;
         const int c = chunk_at(k);
-        if (k + 1 < nck && EXP != 3) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
+        if (k + 1 < nck) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
 #pragma nounroll  // unrolling the two tiles doubles live registers (248 vs 162 VGPRs)
         for (int tau = 0; tau < 2; ++tau) {
             const int row = tau * 32 + col;
@@ -590,19 +454,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             float vmax = acc[0];
 #pragma unroll
             for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
-            if (EXP == 1) {  // timing-only experiment: no insertion (results invalid)
-                T = fmaxf(T, vmax * 0.0f);
-                thr += vmax;
-                continue;
-            }
             if (__any(vmax > T)) {
-                if (EXP == 4 && lane == 0) atomicAdd(&g_knn_dbg[0], 1ull);
                 // per half-tile of 8 registers: flush first if its candidates
                 // could overflow a queue (QC >= 8), then enqueue branch-free (a
                 // write at slot qc is kept only if qc advances; slot QC absorbs
                 // the rest)
                 static_assert(QC >= 8, "queue must hold a half tile");
-                int cnt = 0;
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     int c8 = 0;
@@ -616,9 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                             make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
                         qc += v > T ? 1 : 0;
                     }
-                    cnt += c8;
                 }
-                if (EXP == 4) atomicAdd(&g_knn_dbg[1], (unsigned long long)cnt);
             }
             // After a flush (here, with the tile's accumulators dead) both halves
             // move to the union threshold; between flushes T only rises.
@@ -628,7 +483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (EXP != 2) __syncthreads();  // EXP 2 / 3: timing-only (no barrier / no global loads)
+        __syncthreads();
     }
     KNN_FLUSH();
     T = union_kth<KP>(lv);
@@ -640,7 +495,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         int* out = cand_idx + ((int64_t)q * 2 + h) * KP;
 #pragma unroll
         for (int t = 0; t < KP; ++t) out[t] = li[t];
-        cand_thr[(int64_t)q * 2 + h] = T;  // every excluded ref is <= the final union threshold
+        // Certification threshold: every ref this half excluded is at or below
+        // it.  Rejected refs were <= the T in force then (T only ever held the
+        // union value or this half's own lv[KP-1], both monotone); evicted refs
+        // are <= this half's final lv[KP-1], which can sit ABOVE the union T
+        // when this half owns most of the union's top ranks.
+        cand_thr[(int64_t)q * 2 + h] = fmaxf(T, lv[KP - 1]);
     }
 }
 
@@ -732,14 +592,19 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int idK = __shfl(id, kmax - 1, 64);
     bool ok = (idK < n);  // at least kmax real candidates
     if (tmax != -INFINITY) {
-        // An excluded ref y has approx d2 >= excl (tmax: the screen's final
-        // union threshold, at or above every rejected or evicted value).  If it were as close as the
-        // k-th candidate (|x-y|^2 <= dK) then |y| <= |x| + sqrt(dK), so its
-        // screening error is at most E = c*u*(2|x| + sqrt(dK))^2 and its approx
-        // d2 at most dK + E.  excl > dK + E therefore proves it is farther
-        // (independent of the largest norm in the data).
+        // An excluded ref y has approx d2 >= excl (tmax: each half's
+        // certification threshold, at or above every value it rejected or
+        // evicted).  If y were as close as the k-th candidate (|x-y|^2 <= dK)
+        // then |y| <= |x| + sqrt(dK), so with s = 2|x| + sqrt(dK) >= |x| + |y|
+        // its screening error is at most
+        //   E = c*2^-24*s^2                      (fp16 split + fp32 accumulation)
+        //     + 2^-12*sqrt(d)*s/sigma + 2^-26*d/sigma^2   (flushed parts < 2^-14)
+        // and its approx d2 at most dK + E.  excl > dK + E therefore proves it
+        // is farther (DESIGN.md "kNN certification bound").
         const double s = 2.0 * sqrt(nq) + sqrt(dK);
-        const double E = err_ulps * 0x1p-24 * s * s + 1e-300;
+        const double isc = sqrt(*inv_scale2);  // 1/sigma, a power of two
+        const double E = err_ulps * 0x1p-24 * s * s + 0x1p-12 * sqrt((double)d) * s * isc +
+                         0x1p-26 * (double)d * isc * isc + 1e-300;
         const double excl = nq - 2.0 * (double)tmax * (*inv_scale2);  // thresholds are in scaled units
         ok = ok && (excl - E > dK);
     }
@@ -929,38 +794,6 @@ __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
 }
 
 // --------------------------------------------------------------- driver --
-template <int KS, int KP>
-static void launch_screen(const float* refs, int n, int ntiles, int d, int* cand_idx,
-                          float* cand_thr, hipStream_t st) {
-    unsigned grid = (unsigned)ccg_cdiv(n, KNN_QPB);
-    knn_screen_kernel<KS, KP><<<grid, 256, 0, st>>>(refs, n, ntiles, d, cand_idx, cand_thr);
-}
-
-template <int KP>
-static int screen_dispatch(int KS, const float* refs, int n, int ntiles, int d, int* cand_idx,
-                           float* cand_thr, hipStream_t st) {
-    switch (KS) {
-        case 8: launch_screen<8, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
-        case 12: launch_screen<12, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
-        case 16: launch_screen<16, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
-        case 24: launch_screen<24, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
-        case 32: launch_screen<32, KP>(refs, n, ntiles, d, cand_idx, cand_thr, st); break;
-        default: ccg_set_error("ccg_knn_rows_dev: unsupported d=%d", d); return CCG_EINVAL;
-    }
-    return CCG_OK;
-}
-
-static int pick_ks(int d) {
-    // need 2*KS >= d + 1 (norm slot), KS multiple of 4
-    int need = (d + 2) / 2;
-    if (need <= 8) return 8;
-    if (need <= 12) return 12;
-    if (need <= 16) return 16;
-    if (need <= 24) return 24;
-    if (need <= 32) return 32;
-    return -1;
-}
-
 extern "C" int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                                    const int32_t* idx, int64_t n, double* rows, void* stream) {
     CCG_REQUIRE(ctx && pcs && idx && rows, "ccg_gather_rows_dev: NULL argument");
@@ -985,8 +818,7 @@ struct KnnSegs {
 static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, int32_t* out_idx,
                    double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg) {
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
-    const bool f32path = !sg && getenv("CCG_KNN_F32") != nullptr;  // A/B switch for the fp32-MFMA screen
-    const int64_t npos = sg ? sg->npos : n;                          // screening positions
+    const int64_t npos = sg ? sg->npos : n;  // screening positions
     int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * npos * 2 * KP);
     float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * npos * 2);
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
@@ -999,23 +831,9 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     CCG_HIP(hipMemsetAsync(misc, 0, 16, st));
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     int rc = CCG_OK;
-    double err_ulps;
-    const int* order_perm = nullptr;  // screening position -> bootstrap row (identity on the fp32 path)
-    if (f32path) {
-        const int KS = pick_ks(d);
-        const int64_t npad = ccg_cdiv(n, 32) * 32;
-        float* refs = (float*)ccg_ws(ctx, WS_REFS32, sizeof(float) * npad * 2 * KS);
-        if (!refs) return CCG_ENOMEM;
-        const double one = 1.0;
-        CCG_HIP(hipMemcpyAsync(inv_scale2, &one, sizeof(double), hipMemcpyHostToDevice, st));
-        knn_prep_kernel<<<(unsigned)ccg_cdiv(npad, 256), 256, 0, st>>>(rows, n, npad, d, KS, refs, mbits);
-        const int ntiles = (int)(npad / 32);
-        const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
-        rc = (KP == KNN_KP) ? screen_dispatch<KNN_KP>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st)
-                            : screen_dispatch<KNN_KP_BIG>(KS, refs, (int)n, ntiles, d, cand_idx, cand_thr, st);
-        ccg_timer_stop(ctx, t_scr, st);
-        err_ulps = KNN_ERR_ULPS;
-    } else {
+    const double err_ulps = KNN_ERR_ULPS_F16;
+    const int* order_perm = nullptr;  // screening position -> bootstrap row
+    {
         const int KSTEPS = d <= 16 ? 1 : (d <= 32 ? 2 : 4);
         const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
@@ -1057,15 +875,7 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
 #define CCG_SCREEN16(KS_, KP_) \
     knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk)
-        static const int kexp = getenv("CCG_KNN_EXP") ? atoi(getenv("CCG_KNN_EXP")) : 0;  // timing experiments only
-        if (KP == KNN_KP && KSTEPS == 2 && kexp >= 1 && kexp <= 3 && !blk) {
-            if (kexp == 1)
-                knn_screen16_kernel<2, KNN_KP, 1><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
-            else if (kexp == 2)
-                knn_screen16_kernel<2, KNN_KP, 2><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
-            else
-                knn_screen16_kernel<2, KNN_KP, 3><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk);
-        } else if (KP == KNN_KP) {
+        if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
             else CCG_SCREEN16(4, KNN_KP);
@@ -1076,9 +886,7 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         }
 #undef CCG_SCREEN16
         ccg_timer_stop(ctx, t_scr, st);
-        err_ulps = KNN_ERR_ULPS_F16;
     }
-    if (rc) return rc;
     const int64_t* seg_off = sg ? sg->seg_off : nullptr;
     const int nseg = sg ? sg->nseg : 1;
 #define CCG_CERTIFY(KP_, DM_)                                                                             \

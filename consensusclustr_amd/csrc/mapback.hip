@@ -44,34 +44,45 @@ __global__ void mapback_first_kernel(const int32_t* __restrict__ idx, int64_t n,
     if (c >= 0 && c < N) atomicMin(&first[(int64_t)b * N + c], (int)p);
 }
 
+// Writes the chosen (robust) or every (granular) clustering's label of each
+// cell's first copy; 0 = not sampled.  A label above the matrix's label width
+// (255 for uint8, 65535 for uint16) or below 1 cannot be stored: the cell is
+// written as 0 and CCG_DERR_LABEL_RANGE is raised (the host mirror raises
+// ValueError on the same input), never a clamp that would merge clusters.
+template <typename T>
 __global__ void mapback_write_kernel(int mode, const int32_t* __restrict__ labels, int64_t n, int L,
                                      int64_t N, const int* __restrict__ first,
-                                     const int32_t* __restrict__ choice, uint8_t* __restrict__ A,
-                                     int64_t col0) {
+                                     const int32_t* __restrict__ choice, T* __restrict__ A,
+                                     int64_t col0, int* __restrict__ err) {
+    constexpr int LMAX = sizeof(T) == 1 ? 255 : 65535;
     const int b = blockIdx.y;
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= N) return;
     const int f = first[(int64_t)b * N + c];
     const bool sampled = f < 0x7f7f7f7f;
-    if (mode == CCG_MODE_ROBUST) {
-        const int l = choice[b];
+    bool bad = false;
+    const int l0 = mode == CCG_MODE_ROBUST ? choice[b] : 0;
+    const int l1 = mode == CCG_MODE_ROBUST ? l0 + 1 : L;
+    for (int l = l0; l < l1; ++l) {
         int lab = sampled ? labels[((int64_t)b * L + l) * n + f] : 0;
-        A[(col0 + b) * N + c] = (uint8_t)(lab < 0 ? 0 : (lab > 255 ? 255 : lab));
-    } else {
-        for (int l = 0; l < L; ++l) {
-            int lab = sampled ? labels[((int64_t)b * L + l) * n + f] : 0;
-            A[(col0 + (int64_t)b * L + l) * N + c] = (uint8_t)(lab < 0 ? 0 : (lab > 255 ? 255 : lab));
+        if (sampled && (lab < 1 || lab > LMAX)) {
+            bad = true;
+            lab = 0;
         }
+        const int64_t colx = mode == CCG_MODE_ROBUST ? col0 + b : col0 + (int64_t)b * L + l;
+        A[colx * N + c] = (T)lab;
     }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, CCG_DERR_LABEL_RANGE);
 }
 
 extern "C" int ccg_select_mapback_dev(ccg_ctx* ctx, int mode, const int32_t* labels,
                                       const int32_t* boot_idx, int64_t n, int nb, int L, int64_t N,
                                       const double* means, const int32_t* nclust,
-                                      const int32_t* minsize, int min_size, uint8_t* A, int64_t col0,
-                                      int32_t* out_choice, void* stream) {
+                                      const int32_t* minsize, int min_size, void* A, int label_bits,
+                                      int64_t col0, int32_t* out_choice, void* stream) {
     CCG_REQUIRE(ctx && labels && boot_idx && A, "ccg_select_mapback_dev: NULL argument");
     CCG_REQUIRE(mode == CCG_MODE_ROBUST || mode == CCG_MODE_GRANULAR, "ccg_select_mapback_dev: bad mode");
+    CCG_REQUIRE(label_bits == 8 || label_bits == 16, "ccg_select_mapback_dev: label_bits must be 8 or 16");
     CCG_REQUIRE(n >= 1 && nb >= 1 && L >= 1 && N >= 1, "ccg_select_mapback_dev: bad sizes");
     CCG_REQUIRE(mode == CCG_MODE_GRANULAR || (means && nclust && minsize),
                 "ccg_select_mapback_dev: robust mode needs means/nclust/minsize");
@@ -84,8 +95,13 @@ extern "C" int ccg_select_mapback_dev(ccg_ctx* ctx, int mode, const int32_t* lab
         robust_choice_kernel<<<(unsigned)ccg_cdiv(nb, 64), 64, 0, st>>>(means, nclust, minsize, nb, L,
                                                                        min_size, choice);
     mapback_first_kernel<<<dim3((unsigned)ccg_cdiv(n, 256), nb), 256, 0, st>>>(boot_idx, n, N, first);
-    mapback_write_kernel<<<dim3((unsigned)ccg_cdiv(N, 256), nb), 256, 0, st>>>(mode, labels, n, L, N, first,
-                                                                            choice, A, col0);
+    const dim3 g((unsigned)ccg_cdiv(N, 256), nb);
+    if (label_bits == 8)
+        mapback_write_kernel<uint8_t><<<g, 256, 0, st>>>(mode, labels, n, L, N, first, choice, (uint8_t*)A, col0,
+                                                         ctx->d_err);
+    else
+        mapback_write_kernel<uint16_t><<<g, 256, 0, st>>>(mode, labels, n, L, N, first, choice, (uint16_t*)A, col0,
+                                                          ctx->d_err);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }

@@ -56,7 +56,7 @@ __global__ void snn_count_hosts(const int32_t* __restrict__ knn, int64_t n, int 
     int r = (int)(t - h * k);
     int32_t x = knn[h * kstride + r];
     if (x < 0 || x >= n || x == h) {
-        atomicOr(err, 1);
+        atomicOr(err, CCG_DERR_SNN_INDEX);
         return;
     }
     atomicAdd(&hcnt[x], 1ull);
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
     int64_t* __restrict__ cnt, const int* __restrict__ in_list, const int* __restrict__ in_count,
     int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
-    int* __restrict__ ucount, int exp) {
+    int* __restrict__ ucount) {
     __shared__ SnnWaveLds<WT> lds_all[SNN_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     SnnWaveLds<WT>& L = lds_all[wv];
@@ -395,10 +395,14 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
                 mlen = (int)(mend - mh0);
             } else {
                 mcur = knn[j * kstride + lane - 1];
-                const int q = bp[j * kmax + lane - 1];
-                mh0 = hoff[mcur] + q + 1;
-                mend = hoff[mcur + 1];
-                mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+                if ((unsigned)mcur < (unsigned)n && mcur != j) {
+                    const int q = bp[j * kmax + lane - 1];
+                    mh0 = hoff[mcur] + q + 1;
+                    mend = hoff[mcur + 1];
+                    mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+                } else {
+                    mcur = (int)j;  // invalid input (reported via CCG_DERR_SNN_INDEX): no items
+                }
             }
         }
         int incl = mlen;
@@ -426,14 +430,9 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
                 ii = mi;
                 const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
                 if (q < L.u.g.hend[mi]) {
-                    if (exp & 2) {
-                        p = (int)(j + 1 + (q * 7919) % (n - j));
-                        rp = (int)(q & 15) + 1;
-                    } else {
-                        const int2 hr = hosts_s[q];
-                        p = hr.x;
-                        rp = hr.y;
-                    }
+                    const int2 hr = hosts_s[q];
+                    p = hr.x;
+                    rp = hr.y;
                 } else {
                     p = L.u.g.cur[mi];
                 }
@@ -446,7 +445,7 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
             int np, nrp, nii;
             fetch(t0 + 64 + lane, np, nrp, nii);
             bool ok = true;
-            if (p >= 0 && !(exp & 1)) {
+            if (p >= 0) {
                 const unsigned c = snn_contrib(sp, ii, rp);
                 if (c != sp.init) ok = table_insert64(tab, p, c, sp, snn_log2<WT>(), WT);
             }
@@ -486,7 +485,7 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
         const int R = (u + 63) >> 6;
         int* hist = L.u.s.hist;
         int* bst = L.u.s.bst;
-        if (u == 0 || (exp & 4)) {
+        if (u == 0) {
         } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, dst);
         else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, dst);
         else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, dst);
@@ -568,10 +567,14 @@ __global__ __launch_bounds__(64 * SNN_WAVES, SI <= 1024 ? 4 : 2) void snn_sort_b
                 mlen = (int)(mend - mh0);
             } else {
                 mcur = knn[j * kstride + lane - 1];
-                const int q = bp[j * kmax + lane - 1];
-                mh0 = hoff[mcur] + q + 1;
-                mend = hoff[mcur + 1];
-                mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+                if ((unsigned)mcur < (unsigned)n && mcur != j) {
+                    const int q = bp[j * kmax + lane - 1];
+                    mh0 = hoff[mcur] + q + 1;
+                    mend = hoff[mcur + 1];
+                    mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
+                } else {
+                    mcur = (int)j;  // invalid input (reported via CCG_DERR_SNN_INDEX): no items
+                }
             }
         }
         int incl = mlen;
@@ -817,6 +820,7 @@ __global__ __launch_bounds__(256) void snn_block_kernel(
         __syncthreads();
         for (int i = 0; i <= kmax; ++i) {
             const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
+            if ((unsigned)cur >= (unsigned)n || (i > 0 && cur == j)) continue;  // invalid (CCG_DERR_SNN_INDEX)
             const int64_t h0 = hoff[cur];
             const int64_t len = hoff[cur + 1] - h0 + 1;
             for (int64_t o = tid; o < len; o += 256) {
@@ -973,6 +977,7 @@ __global__ __launch_bounds__(256) void snn_dense_kernel(
         __syncthreads();
         for (int i = 0; i <= kmax; ++i) {
             const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
+            if ((unsigned)cur >= (unsigned)n || (i > 0 && cur == j)) continue;  // invalid (CCG_DERR_SNN_INDEX)
             const int64_t h0 = hoff[cur];
             const int64_t len = hoff[cur + 1] - h0 + 1;
             for (int64_t o = threadIdx.x; o < len; o += 256) {
@@ -1086,7 +1091,7 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     int* split = bp + n * kmax;
     int* ucount = (int*)(scratch + n * SNN_WCAP);
     unsigned long long* cursor = (unsigned long long*)(hoff + (n + 1));
-    int* err = (int*)(hoff + 2 * (n + 1));
+    int* err = ctx->d_err;
     int* ov_list = ov;  // nodes for the block path (overflowed both wave tiers)
     int* ov2_list = ov + n;
     int* flag1 = ov + 2 * n;
@@ -1098,7 +1103,6 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     const int64_t nkk = (int64_t)n * kmax;
     const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
     CCG_HIP(hipMemsetAsync(hoff, 0, sizeof(int64_t) * (n + 1), st));
-    CCG_HIP(hipMemsetAsync(err, 0, sizeof(int) * 4, st));
     CCG_HIP(hipMemsetAsync(flag1, 0, sizeof(int) * 2 * n, st));
     CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
     CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * nk * (n + 1), st));
@@ -1111,7 +1115,6 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     snn_sort_hosts<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(hoff, n, kmax, hosts,
                                                                                       hosts_s, bp, split);
     const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
-    static const int snn_exp = getenv("CCG_SNN_EXP") ? atoi(getenv("CCG_SNN_EXP")) : 0;  // timing experiments only
     // pass 1: per-graph counts (sort tier for nodes with <= 1024 items, 2048-slot hash tables,
     // then block tables, then dense)
     snn_sort_build_kernel<1024><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
@@ -1120,7 +1123,7 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     const unsigned nblk2 = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 1024);
     snn_wave_build_kernel<2048><<<nblk2, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
                                                                   ova_list, ova_count, ov_list, ov_count, scratch,
-                                                                  ucount, snn_exp);
+                                                                  ucount);
     snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, ov_list, ov_count,
                                                  ov2_list, ov2_count, flag2, out);
     snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,

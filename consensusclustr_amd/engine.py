@@ -64,7 +64,12 @@ class Engine:
         return torch.cuda.ExternalStream(self.lib.ccg_stream(self.ctx))
 
     def synchronize(self):
+        """Synchronise the device; raises CcgError for a sticky device error
+        (a label wider than the assignment matrix, an invalid SNN index)."""
         check(self.lib.ccg_synchronize(self.ctx))
+
+    def check_errors(self):
+        check(self.lib.ccg_check_errors(self.ctx))
 
     def timing(self, enable=True):
         """Enable per-kernel hipEvent timing (ccg_timing_enable)."""
@@ -162,15 +167,18 @@ class Engine:
     def cocluster(self, A, want=("co", "both", "dist")):
         """Co-clustering counts/distance (ccg_cocluster), packed R "dist" order.
 
-        A: B x N uint8 column-major assignment matrix (0 = not sampled).
+        A: B x N uint8 or uint16 column-major assignment matrix (0 = not sampled).
         """
-        A = np.ascontiguousarray(A, dtype=np.uint8)
+        A = np.ascontiguousarray(A)
+        if A.dtype not in (np.uint8, np.uint16):
+            A = A.astype(np.uint8)
+        bits = 8 * A.dtype.itemsize
         B, N = A.shape
         P = N * (N - 1) // 2
         co = np.empty(P, np.uint16) if "co" in want else None
         both = np.empty(P, np.uint16) if "both" in want else None
         dist = np.empty(P, np.float64) if "dist" in want else None
-        check(self.lib.ccg_cocluster(self.ctx, _ptr(A), N, B, _ptr(co), _ptr(both), _ptr(dist)))
+        check(self.lib.ccg_cocluster(self.ctx, _ptr(A), bits, N, B, _ptr(co), _ptr(both), _ptr(dist)))
         return {"co": co, "both": both, "dist": dist}
 
     def consensus_knn(self, co, both, N, k):
@@ -179,6 +187,20 @@ class Engine:
         both = np.ascontiguousarray(both, dtype=np.uint16)
         out = np.empty((N, k), np.int32)
         rc = self.lib.ccg_consensus_knn(self.ctx, _ptr(co), _ptr(both), N, k, _ptr(out))
+        if rc == _lib.CCG_ENAN:
+            raise ValueError("data/distances cannot contain NAs for kNN")
+        check(rc)
+        return out
+
+    def consensus_knn_assign(self, A, k):
+        """The same kNN straight from the assignment matrix, fused with the
+        co-clustering GEMM (ccg_consensus_knn_assign; N x N never stored)."""
+        A = np.ascontiguousarray(A)
+        if A.dtype not in (np.uint8, np.uint16):
+            A = A.astype(np.uint8)
+        B, N = A.shape
+        out = np.empty((N, k), np.int32)
+        rc = self.lib.ccg_consensus_knn_assign(self.ctx, _ptr(A), 8 * A.dtype.itemsize, N, B, k, _ptr(out))
         if rc == _lib.CCG_ENAN:
             raise ValueError("data/distances cannot contain NAs for kNN")
         check(rc)
@@ -242,17 +264,31 @@ class Engine:
 
     def select_mapback_t(self, mode, labels, boot_idx, N, A, col0, means=None, nclust=None, minsize=None,
                          min_size=0, out_choice=None):
+        """A: (B, N) uint8 or uint16 tensor (label width from its dtype)."""
+        import torch
         nb, L, n = labels.shape
         md = {"robust": _lib.CCG_MODE_ROBUST, "granular": _lib.CCG_MODE_GRANULAR}[mode]
+        bits = 8 if A.dtype == torch.uint8 else 16
         check(self.lib.ccg_select_mapback_dev(self.ctx, md, _ptr(labels), _ptr(boot_idx), n, nb, L, N,
-                                              _ptr(means), _ptr(nclust), _ptr(minsize), min_size, _ptr(A),
+                                              _ptr(means), _ptr(nclust), _ptr(minsize), min_size, _ptr(A), bits,
                                               col0, _ptr(out_choice), _stream()))
 
     def cocluster_t(self, A, r0, r1, co=None, both=None, dist=None):
+        """A: (B, N) uint8 or uint16 tensor; outputs are row-slab tensors."""
+        import torch
         B, N = A.shape
-        check(self.lib.ccg_cocluster_dev(self.ctx, _ptr(A), N, B, r0, r1, _ptr(co), _ptr(both), _ptr(dist),
+        bits = 8 if A.dtype == torch.uint8 else 16
+        check(self.lib.ccg_cocluster_dev(self.ctx, _ptr(A), bits, N, B, r0, r1, _ptr(co), _ptr(both), _ptr(dist),
                                          _stream()))
 
     def consensus_knn_t(self, co, both, N, k, out_idx, d_flag):
         check(self.lib.ccg_consensus_knn_dev(self.ctx, _ptr(co), _ptr(both), N, k, _ptr(out_idx),
                                              _ptr(d_flag), _stream()))
+
+    def consensus_knn_assign_t(self, A, k, r0, r1, out_idx, d_flag):
+        """Rows [r0, r1) of the consensus kNN from the (B, N) assignment tensor."""
+        import torch
+        B, N = A.shape
+        bits = 8 if A.dtype == torch.uint8 else 16
+        check(self.lib.ccg_consensus_knn_assign_dev(self.ctx, _ptr(A), bits, N, B, k, r0, r1, _ptr(out_idx),
+                                                    _ptr(d_flag), _stream()))

@@ -21,11 +21,12 @@ def row_slabs(N, G, align=128):
     counts need r_g = N(1 - sqrt(1 - g/G)).  Interior cuts are rounded to
     multiples of `align` (the co-cluster tile height).
     """
+    top = (N // align) * align  # interior cuts stay aligned (a cut at N would be an unaligned r0)
     cuts = [0]
     for g in range(1, G):
         r = N * (1.0 - math.sqrt(1.0 - g / G))
         r = int(round(r / align)) * align
-        cuts.append(min(max(r, cuts[-1]), N))
+        cuts.append(min(max(r, cuts[-1]), top))
     cuts.append(N)
     return cuts
 

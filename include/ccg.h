@@ -31,7 +31,11 @@
  *   ccg_cocluster                   : the RcppXPtrUtils customDist plugin passed
  *       to parallelDist::parDist(method="custom") and 1 - parDist(...)
  *       (:411-421).
- *   ccg_consensus_knn               : dbscan::kNN(jaccardDist, k)$id (:425).
+ *   ccg_consensus_knn[_assign]      : dbscan::kNN(jaccardDist, k)$id (:425).
+ *
+ * Errors found by a kernel on the device (a label wider than the assignment
+ * matrix, an invalid SNN neighbour index) are sticky in the context and are
+ * returned by the next ccg_synchronize / ccg_check_errors call.
  */
 #ifndef CCG_H
 #define CCG_H
@@ -42,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 1
+#define CCG_ABI_VERSION 2
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -75,7 +79,10 @@ int ccg_abi_version(void);
 const char* ccg_last_error(void);
 int ccg_open(const ccg_config* cfg, ccg_ctx** out);
 int ccg_close(ccg_ctx* ctx);
+/* Synchronises the device; returns the sticky device error if one was
+ * raised since the last check (CCG_ERANGE / CCG_EINVAL), else CCG_OK. */
 int ccg_synchronize(ccg_ctx* ctx);
+int ccg_check_errors(ccg_ctx* ctx);
 /* The context's default stream (hipStream_t). */
 void* ccg_stream(ccg_ctx* ctx);
 
@@ -171,38 +178,43 @@ int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
 
 /* ----------------------------------------------- selection + map-back -- */
 /* For nb bootstraps with L clusterings each (labels nb x L x n int32,
- * codes 1..255), map labels back to the N cells (first copy in sample
- * order wins; unsampled -> 0) and write uint8 columns of the column-major
- * assignment matrix A (B x N) starting at column col0.
+ * codes 1..2^label_bits - 1), map labels back to the N cells (first copy in
+ * sample order wins; unsampled -> 0) and write columns of the column-major
+ * assignment matrix A (B x N, uint8 for label_bits 8, uint16 for 16) starting
+ * at column col0.
  *   ROBUST  : one column per bootstrap, the clustering chosen by the
  *             per-bootstrap score rules (:662-670) and rank(ties="first")
  *             (:685-686) from means/nclust/minsize (nb x L);
  *             out_choice (nb, nullable) receives the chosen index.
- *   GRANULAR: L columns per bootstrap (:688). */
+ *   GRANULAR: L columns per bootstrap (:688).
+ * A label outside [1, 2^label_bits - 1] is stored as 0 and raises the sticky
+ * CCG_ERANGE (reported by ccg_synchronize / ccg_check_errors). */
 int ccg_select_mapback_dev(ccg_ctx* ctx, int mode, const int32_t* labels,
                            const int32_t* boot_idx, int64_t n, int nb, int L,
                            int64_t N, const double* means,
                            const int32_t* nclust, const int32_t* minsize,
-                           int min_size, uint8_t* A, int64_t col0,
+                           int min_size, void* A, int label_bits, int64_t col0,
                            int32_t* out_choice, void* stream);
 
 /* ------------------------------------------------------- co-clustering -- */
-/* A: B x N uint8 column-major assignment matrix, 0 = not sampled (R's -1),
- * 1..255 = cluster code.  For the rows [r0, r1) of the packed upper
- * triangle (row i holds j = i+1..N-1; this is exactly the order of R's
- * "dist" object) writes
- *   co   : #{b : A_bi == A_bj != 0}         (uint16, B <= 65535)
+/* A: B x N column-major assignment matrix of uint8 (label_bits 8) or uint16
+ * (label_bits 16) codes, 0 = not sampled (R's -1), 1.. = cluster code.
+ * B <= 65535 (uint16 counts; columns are accumulated in chunks of 16383).
+ * For the rows [r0, r1) of the packed upper triangle (row i holds
+ * j = i+1..N-1; this is exactly the order of R's "dist" object) writes
+ *   co   : #{b : A_bi == A_bj != 0}         (uint16)
  *   both : #{b : A_bi != 0 and A_bj != 0}   (uint16)
  *   dist : 1 - (double)((float)co / (float)both)  (NaN when both == 0)
  * Any output may be NULL.  Slab element (i, j) lives at
  * i*N - i*(i+1)/2 + (j-i-1) - (r0*N - r0*(r0+1)/2).
- * r0 must be a multiple of 128 (CCG_COCLUSTER_ROW_ALIGN) or r0 == 0. */
+ * r0 must be a multiple of 128 (CCG_COCLUSTER_ROW_ALIGN) unless r0 == r1.
+ * label_bits 16 synchronises the stream once (slot-table sizing). */
 #define CCG_COCLUSTER_ROW_ALIGN 128
-int ccg_cocluster(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B,
-                  uint16_t* co, uint16_t* both, double* dist);
-int ccg_cocluster_dev(ccg_ctx* ctx, const uint8_t* A, int64_t N, int64_t B,
-                      int64_t r0, int64_t r1, uint16_t* co, uint16_t* both,
-                      double* dist, void* stream);
+int ccg_cocluster(ccg_ctx* ctx, const void* A, int label_bits, int64_t N,
+                  int64_t B, uint16_t* co, uint16_t* both, double* dist);
+int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N,
+                      int64_t B, int64_t r0, int64_t r1, uint16_t* co,
+                      uint16_t* both, double* dist, void* stream);
 
 /* --------------------------------------------------- consensus kNN -- */
 /* kNN on the co-clustering distance from packed (full, r0 = 0) co/both:
@@ -213,6 +225,18 @@ int ccg_consensus_knn(ccg_ctx* ctx, const uint16_t* co, const uint16_t* both,
 int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co,
                           const uint16_t* both, int64_t N, int k,
                           int32_t* out_idx, int32_t* d_nan_flag, void* stream);
+/* The same kNN straight from the assignment matrix, fused with the
+ * co-clustering GEMM: rows [r0, r1) (r0 a multiple of 128) are processed in
+ * sub-slabs whose full rows of (co, both) live only in a bounded workspace
+ * (<= 4 GB), so the N x N matrix is never stored.  out_idx rows r0..r1-1 of
+ * an N x k int32 matrix (0-based).  *d_nan_flag (device) is set to 1 if any
+ * pair in those rows was never co-sampled. */
+int ccg_consensus_knn_assign(ccg_ctx* ctx, const void* A, int label_bits,
+                             int64_t N, int64_t B, int k, int32_t* out_idx);
+int ccg_consensus_knn_assign_dev(ccg_ctx* ctx, const void* A, int label_bits,
+                                 int64_t N, int64_t B, int k, int64_t r0,
+                                 int64_t r1, int32_t* out_idx,
+                                 int32_t* d_nan_flag, void* stream);
 
 /* ------------------------------------------------------ kernel timing -- */
 /* Device time of selected kernels, measured with hipEvents recorded on the

@@ -37,6 +37,13 @@
  *  - orc_consensus_knn: dbscan::kNN(jaccardDist, k)$id            :425
  *                      per-row stable order() of the distance row with the
  *                      diagonal set to +Inf; NaN distances are an error.
+ *  - orc_knn_queries : orc_knn restricted to selected query rows (same
+ *                      semantics; for parity checks at BASELINE sizes where
+ *                      the full O(n^2 d) scan would take too long).
+ *  - orc_cocluster_rows: customDist counts for selected rows i against every
+ *                      j (full rows, j = i included), from the engine's
+ *                      encoding of clustAssignments (:404-408): uint8/uint16
+ *                      codes with 0 = NA.
  */
 #include <math.h>
 #include <stdint.h>
@@ -120,6 +127,52 @@ int orc_knn(const double* X, int64_t n, int d, int K, int32_t* out_idx,
                 for (int t = 0; t < K; ++t) {
                     out_idx[i * K + t] = bi[t];
                     if (out_dist) out_dist[i * K + t] = sqrt(bd[t]);
+                }
+            }
+        }
+        free(bd);
+        free(bi);
+    }
+    return err ? ORC_ENOMEM : ORC_OK;
+}
+
+/* The same search for the nq rows qidx[] only: out rows t = 0..nq-1. */
+int orc_knn_queries(const double* X, int64_t n, int d, int K, const int32_t* qidx, int64_t nq,
+                    int32_t* out_idx, double* out_dist, int nthreads) {
+    if (K < 1 || K > n - 1 || d < 1) return ORC_EINVAL;
+    for (int64_t t = 0; t < nq; ++t)
+        if (qidx[t] < 0 || qidx[t] >= n) return ORC_EINVAL;
+    set_threads(nthreads);
+    int err = 0;
+#pragma omp parallel
+    {
+        double* bd = (double*)malloc(sizeof(double) * (size_t)K);
+        int32_t* bi = (int32_t*)malloc(sizeof(int32_t) * (size_t)K);
+        if (!bd || !bi) {
+#pragma omp atomic write
+            err = 1;
+        } else {
+#pragma omp for schedule(dynamic, 4)
+            for (int64_t t = 0; t < nq; ++t) {
+                const int64_t i = qidx[t];
+                int cnt = 0;
+                const double* xi = X + i * d;
+                for (int64_t j = 0; j < n; ++j) {
+                    if (j == i) continue;
+                    double s = sqdist(xi, X + j * d, d);
+                    if (cnt == K && !(s < bd[K - 1])) continue;
+                    int p = (cnt < K) ? cnt++ : K - 1;
+                    while (p > 0 && s < bd[p - 1]) {
+                        bd[p] = bd[p - 1];
+                        bi[p] = bi[p - 1];
+                        --p;
+                    }
+                    bd[p] = s;
+                    bi[p] = (int32_t)j;
+                }
+                for (int u = 0; u < K; ++u) {
+                    out_idx[t * K + u] = bi[u];
+                    if (out_dist) out_dist[t * K + u] = sqrt(bd[u]);
                 }
             }
         }
@@ -479,4 +532,49 @@ int orc_consensus_knn(const double* dist, int64_t N, int k, int32_t* out_idx,
         free(bi);
     }
     return err ? ORC_ENOMEM : ORC_OK;
+}
+
+/* ---- customDist counts for selected full rows ------------------------- */
+/* A: B x N column-major codes, uint8 (label_bits 8) or uint16 (16), 0 = NA.
+ * For each of the nr rows rows[t]: co[t*N + j] = #{b: A_bi == A_bj != 0},
+ * both[t*N + j] = #{b: A_bi != 0, A_bj != 0} for every j (j = i included). */
+int orc_cocluster_rows(const void* A, int label_bits, int64_t N, int64_t B, const int32_t* rows, int64_t nr,
+                       uint32_t* co, uint32_t* both, int nthreads) {
+    if (N < 1 || B < 1 || (label_bits != 8 && label_bits != 16)) return ORC_EINVAL;
+    for (int64_t t = 0; t < nr; ++t)
+        if (rows[t] < 0 || rows[t] >= N) return ORC_EINVAL;
+    set_threads(nthreads);
+    const uint8_t* A8 = (const uint8_t*)A;
+    const uint16_t* A16 = (const uint16_t*)A;
+    const int64_t JB = 4096;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t j0 = 0; j0 < N; j0 += JB) {
+        const int64_t j1 = j0 + JB < N ? j0 + JB : N;
+        for (int64_t t = 0; t < nr; ++t) {
+            uint32_t* cr = co + t * N;
+            uint32_t* br = both + t * N;
+            for (int64_t j = j0; j < j1; ++j) cr[j] = br[j] = 0;
+            const int64_t i = rows[t];
+            for (int64_t b = 0; b < B; ++b) {
+                if (label_bits == 8) {
+                    const uint8_t* col = A8 + b * N;
+                    const uint8_t a = col[i];
+                    if (!a) continue;
+                    for (int64_t j = j0; j < j1; ++j) {
+                        cr[j] += col[j] == a;
+                        br[j] += col[j] != 0;
+                    }
+                } else {
+                    const uint16_t* col = A16 + b * N;
+                    const uint16_t a = col[i];
+                    if (!a) continue;
+                    for (int64_t j = j0; j < j1; ++j) {
+                        cr[j] += col[j] == a;
+                        br[j] += col[j] != 0;
+                    }
+                }
+            }
+        }
+    }
+    return ORC_OK;
 }

@@ -16,7 +16,7 @@ __all__ = [
     "build", "lib", "gather_rows", "knn", "snn", "silhouette", "mapback",
     "cocluster", "consensus_knn", "robust_choice", "consensus_choice",
     "py_knn", "py_snn", "py_cocluster", "packed_index", "RES_RANGE", "K_NUM",
-    "robust_score", "consensus_score",
+    "robust_score", "consensus_score", "knn_queries", "cocluster_rows",
 ]
 
 # consensusClust defaults, R/consensusClust.R:126-127
@@ -44,8 +44,11 @@ def lib():
         L.orc_mapback.argtypes = [p, i64, p, i64, p]
         L.orc_cocluster.argtypes = [p, i64, i64, p, p, p, i32]
         L.orc_consensus_knn.argtypes = [p, i64, i32, p, i32]
+        L.orc_knn_queries.argtypes = [p, i64, i32, i32, p, i64, p, p, i32]
+        L.orc_cocluster_rows.argtypes = [p, i32, i64, i64, p, i64, p, p, i32]
         for f in (L.orc_gather_rows, L.orc_knn, L.orc_snn, L.orc_silhouette,
-                  L.orc_mapback, L.orc_cocluster, L.orc_consensus_knn):
+                  L.orc_mapback, L.orc_cocluster, L.orc_consensus_knn,
+                  L.orc_knn_queries, L.orc_cocluster_rows):
             f.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -79,6 +82,34 @@ def knn(X, k, nthreads=0):
     dist = np.empty((n, k), dtype=np.float64)
     _check(lib().orc_knn(_ptr(X), n, d, k, _ptr(idx), _ptr(dist), nthreads), "knn")
     return idx, dist
+
+
+def knn_queries(X, k, qidx, nthreads=0):
+    """orc_knn for the rows qidx only: (idx, dist) of shape (len(qidx), k)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    q = np.ascontiguousarray(qidx, dtype=np.int32)
+    n, d = X.shape
+    idx = np.empty((q.size, k), dtype=np.int32)
+    dist = np.empty((q.size, k), dtype=np.float64)
+    _check(lib().orc_knn_queries(_ptr(X), n, d, k, _ptr(q), q.size, _ptr(idx), _ptr(dist), nthreads), "knn_queries")
+    return idx, dist
+
+
+def cocluster_rows(A, rows, nthreads=0):
+    """customDist counts of selected rows against every column j.
+
+    A: B x N uint8/uint16 codes (0 = NA).  Returns (co, both) uint32 arrays of
+    shape (len(rows), N); entry j = i is included.
+    """
+    A = np.ascontiguousarray(A)
+    assert A.dtype in (np.uint8, np.uint16)
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    B, N = A.shape
+    co = np.empty((r.size, N), np.uint32)
+    both = np.empty((r.size, N), np.uint32)
+    _check(lib().orc_cocluster_rows(_ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(r), r.size, _ptr(co), _ptr(both),
+                                    nthreads), "cocluster_rows")
+    return co, both
 
 
 def snn(knn_idx, k, type="number"):

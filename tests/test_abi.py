@@ -13,7 +13,7 @@ def test_header_declares_expected_entry_points():
     syms = _lib.header_symbols()
     for s in ("ccg_open", "ccg_knn_boot", "ccg_knn_rows_dev", "ccg_snn", "ccg_snn_dev", "ccg_silhouette",
               "ccg_select_mapback_dev", "ccg_cocluster", "ccg_cocluster_dev", "ccg_consensus_knn",
-              "ccg_timing_read"):
+              "ccg_consensus_knn_assign", "ccg_consensus_knn_assign_dev", "ccg_check_errors", "ccg_timing_read"):
         assert s in syms
 
 
@@ -33,7 +33,7 @@ def test_nm_exports_are_extern_c():
 
 def test_abi_version_and_error_path():
     lib = _lib.load()
-    assert lib.ccg_abi_version() == 1
+    assert lib.ccg_abi_version() == 2
     # NULL out-pointer: rejected before any device work, message set
     assert lib.ccg_open(None, None) == _lib.CCG_EINVAL
     assert b"NULL" in lib.ccg_last_error()

@@ -18,3 +18,18 @@ def test_sharded_cocluster_matches_single_process(tmp_path, world):
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert out.read_text() == "ok"
+
+
+def test_bench_launcher_starts_the_requested_ranks():
+    """bench.py --gpus 2 (no WORLD_SIZE) starts 2 ranks via torch.distributed.run;
+    --launcher-check wires them over gloo without touching a GPU."""
+    import json
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2
+    assert sorted(x[0] for x in out["ranks_seen"]) == [0, 1]

@@ -1,0 +1,244 @@
+"""Adversarial and boundary cases of the HIP engine (round-2 review items).
+
+kNN certification: a lane-half owning a query's whole top-k with a tie at
+rank k (the evicted-ref bound), near-origin points beside a huge outlier (the
+fp16 representation floor), kmax = 32 (the KP_BIG screen).  Co-clustering:
+all-zero columns inside a slot stage, uint16 labels, B > 16383 (column
+chunks), odd N.  Boundary: labels wider than the assignment matrix, invalid
+SNN input through the device ABI, the fused consensus kNN.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _mixture(rng, N, d, C=8, spread=3.0):
+    centers = rng.normal(scale=spread, size=(C, d))
+    return centers[rng.integers(0, C, N)] + rng.normal(size=(N, d))
+
+
+def _unit(rng, d):
+    v = rng.normal(size=d)
+    return v / np.linalg.norm(v)
+
+
+# ----------------------------------------------------------------- kNN --
+def _half_owner_rows(seed=0):
+    """Segment positions are rows (identity order), 64-row chunks, 32-row
+    tiles; a ref at tile offset r % 8 < 4 lands in lane-half 0.  Query 130
+    (block 1, scanned chunk order 2, 3, 1, 4, 0) gets its 19 nearest refs and
+    a duplicated pair (rows 136 and 0, identical) at rank 20, all in half 0.
+    Row 136 is seen in the first chunk, row 0 in the last: the screen keeps
+    136 and drops 0, so only a correct bound sends the query to the exact
+    path, which returns row 0 (the lower index) at rank 20."""
+    rng = np.random.default_rng(seed)
+    n, d = 320, 4
+    X = np.empty((n, d))
+    for i in range(n):
+        X[i] = (10.0 + 0.37 * i) * _unit(rng, d)  # far, distinct radii
+    X[130] = 0.0
+    near = [128, 129, 131, 137, 138, 139, 144, 145, 146, 147, 152, 153, 154, 155, 160, 161, 162, 163, 168]
+    for t, r in enumerate(near):
+        X[r] = 0.1 * (t + 1) * _unit(rng, d)
+    X[136] = 2.0 * _unit(rng, d)
+    X[0] = X[136]
+    return X
+
+
+@pytest.mark.parametrize("kmax", [20, 10])
+def test_knn_certify_half_owns_topk_with_tie(engine, kmax):
+    X = _half_owner_rows()
+    if kmax == 10:  # move the duplicated pair to rank 10
+        X = X.copy()
+        rng = np.random.default_rng(9)
+        near = [128, 129, 131, 137, 138, 139, 144, 145, 146]
+        for t, r in enumerate(near):
+            X[r] = 0.1 * (t + 1) * _unit(rng, 4)
+        for r in [147, 152, 153, 154, 155, 160, 161, 162, 163, 168]:
+            X[r] = (3.0 + 0.05 * r) * _unit(rng, 4)
+        X[136] = 0.95 * _unit(rng, 4)
+        X[0] = X[136]
+    oi, od = O.knn(X, kmax)
+    assert oi[130, kmax - 1] == 0  # the tie resolves to the lower row index
+    (idx, dist), = engine.knn_segments([X], kmax=kmax)
+    assert np.array_equal(idx, oi)
+    np.testing.assert_allclose(dist, od, rtol=RTOL, atol=1e-12)
+    idx2, _ = engine.knn_boot(X, np.arange(X.shape[0]), kmax=kmax)  # Morton-ordered path
+    assert np.array_equal(idx2[0], oi)
+
+
+def test_knn_near_origin_cluster_beside_huge_outlier(engine):
+    """Scaled coordinates of the near-origin points fall below the fp16 normal
+    range (2^-14): the screen cannot rank them, so the certification's
+    absolute term must refuse them and the exact path must answer."""
+    rng = np.random.default_rng(12)
+    X = rng.normal(scale=1e-6, size=(2000, 10))
+    X[0, 0] = 1e4
+    X[1:40] += rng.normal(scale=3.0, size=(39, 10))  # a few ordinary-scale rows
+    idx, dist = engine.knn_boot(X, np.arange(2000), kmax=20)
+    oi, od = O.knn(X, 20)
+    assert np.array_equal(idx[0], oi)
+    np.testing.assert_allclose(dist[0], od, rtol=RTOL, atol=0)
+    assert engine.last_knn_stats[1] >= 1900  # the tiny rows went to the exact fallback
+
+
+@pytest.mark.parametrize("kmax,d", [(32, 20), (25, 30), (32, 7), (21, 40)])
+def test_knn_kp_big_vs_oracle(engine, kmax, d):
+    rng = np.random.default_rng(kmax * 100 + d)
+    N = 3000
+    pcs = _mixture(rng, N, d)
+    boot = rng.integers(0, N, int(0.9 * N)).astype(np.int32)
+    idx, dist = engine.knn_boot(pcs, boot, kmax=kmax)
+    oi, od = O.knn(O.gather_rows(pcs, boot), kmax)
+    assert np.array_equal(idx[0], oi)
+    np.testing.assert_allclose(dist[0], od, rtol=RTOL, atol=1e-12)
+
+
+# -------------------------------------------------------- co-clustering --
+def _to_oracle(A):
+    A = np.array(A, np.int64)
+    A[A == 0] = -1
+    return A.astype(np.int32)
+
+
+def _check_cocluster(engine, A):
+    r = engine.cocluster(A)
+    o = O.cocluster(_to_oracle(A))
+    assert np.array_equal(r["co"], o["co"].astype(np.uint16))
+    assert np.array_equal(r["both"], o["both"].astype(np.uint16))
+    assert np.array_equal(r["dist"], o["dist"], equal_nan=True)
+
+
+def test_cocluster_zero_columns_inside_a_stage(engine):
+    """Never-sampled columns own no K slot; 20 one-slot columns interleaved
+    with all-zero ones span 39 columns in one 32-slot stage."""
+    rng = np.random.default_rng(20)
+    B, N = 40, 512
+    A = rng.integers(1, 4, (B, N)).astype(np.uint8)
+    A[1::2] = 0
+    A[rng.random((B, N)) < 0.1] = 0
+    _check_cocluster(engine, A)
+
+
+@pytest.mark.parametrize("B,N,C", [(50, 600, 1000), (33, 257, 300), (7, 130, 65535)])
+def test_cocluster_uint16_labels(engine, B, N, C):
+    rng = np.random.default_rng(B + N)
+    A = rng.integers(1, C + 1, (B, N)).astype(np.uint16)
+    A[:, ::5] = rng.integers(1, 4, (B, (N + 4) // 5))  # frequent co-assignment too
+    A[rng.random((B, N)) < 0.1] = 0
+    _check_cocluster(engine, A)
+
+
+@pytest.mark.parametrize("B,N,dtype", [(20000, 260, np.uint8), (16500, 257, np.uint16), (16384, 128, np.uint8)])
+def test_cocluster_column_chunks(engine, B, N, dtype):
+    """B > 16383 (granular mode): counts of 16383-column chunks are added."""
+    rng = np.random.default_rng(B)
+    Cb = rng.integers(2, 8, B)
+    A = (rng.random((B, N)) * Cb[:, None]).astype(dtype) + 1
+    A[rng.random((B, N)) < 0.1] = 0
+    _check_cocluster(engine, A)
+
+
+def test_cocluster_chunks_dist_only_matches(engine):
+    import torch
+    rng = np.random.default_rng(77)
+    B, N = 17000, 384
+    A = rng.integers(0, 5, (B, N)).astype(np.uint8)
+    full = engine.cocluster(A)
+    At = torch.from_numpy(A).cuda()
+    P = N * (N - 1) // 2
+    dist = torch.empty(P, dtype=torch.float64, device="cuda")
+    engine.cocluster_t(At, 0, N, dist=dist)  # co/both NULL: chunk partials in scratch
+    torch.cuda.synchronize()
+    assert np.array_equal(dist.cpu().numpy(), full["dist"], equal_nan=True)
+
+
+# ---------------------------------------------------- selection + map-back --
+def test_mapback_label_range_raises_and_uint16_holds(engine):
+    import torch
+    from consensusclustr_amd import CcgError
+    from consensusclustr_amd.consensus import mapback
+    rng = np.random.default_rng(5)
+    N, n, nb, L = 400, 360, 2, 3
+    boots = torch.from_numpy(rng.integers(0, N, (nb, n)).astype(np.int32)).cuda()
+    lab_np = rng.integers(1, 700, (nb, L, n)).astype(np.int32)
+    labels = torch.from_numpy(lab_np).cuda()
+    A8 = torch.zeros((nb * L, N), dtype=torch.uint8, device="cuda")
+    engine.select_mapback_t("granular", labels, boots, N, A8, 0)
+    with pytest.raises(CcgError) as e:
+        engine.synchronize()
+    assert e.value.code == -6  # CCG_ERANGE, never a silent clamp
+    engine.check_errors()  # the sticky error was cleared
+    A16 = torch.zeros((nb * L, N), dtype=torch.int16, device="cuda")  # uint16 storage (non-uint8 = 16-bit labels)
+    engine.select_mapback_t("granular", labels, boots, N, A16, 0)
+    engine.synchronize()
+    got = A16.cpu().numpy().view(np.uint16)
+    bn = boots.cpu().numpy()
+    for b in range(nb):
+        for l_ in range(L):
+            col = mapback(bn[b], lab_np[b, l_], N)
+            col[col < 0] = 0
+            assert np.array_equal(got[b * L + l_], col.astype(np.uint16))
+
+
+# ----------------------------------------------------------------- SNN --
+def test_snn_dev_invalid_index_is_reported(engine):
+    import torch
+    from consensusclustr_amd import CcgError
+    n, k = 500, 10
+    rng = np.random.default_rng(3)
+    idx = np.stack([rng.choice(np.setdiff1d(np.arange(n), [i]), k, replace=False) for i in range(n)]).astype(np.int32)
+    idx[7, 3] = n + 5  # out of range
+    knn_t = torch.from_numpy(idx).cuda()
+    cap = n * 200
+    out = (torch.empty(cap, dtype=torch.int32, device="cuda"), torch.empty(cap, dtype=torch.int32, device="cuda"),
+           torch.empty(cap, dtype=torch.float64, device="cuda"))
+    ne = torch.zeros(1, dtype=torch.int64, device="cuda")
+    engine.snn_multi_t(knn_t, (k,), "number", [out], ne)
+    with pytest.raises(CcgError):
+        engine.synchronize()
+    engine.check_errors()
+
+
+# ------------------------------------------------------ consensus kNN --
+@pytest.mark.parametrize("B,N,dtype", [(100, 1100, np.uint8), (60, 700, np.uint16), (300, 1025, np.uint8)])
+def test_consensus_knn_fused_vs_oracle(engine, B, N, dtype):
+    """dbscan::kNN(jaccardDist) from the assignment matrix without the N x N
+    matrix, vs the oracle's stable order() over the full distance."""
+    rng = np.random.default_rng(B * 7 + N)
+    C = rng.integers(2, 12, B)
+    A = ((rng.random((B, N)) * C[:, None]).astype(np.int64) + 1)
+    A[rng.random((B, N)) < 0.1] = 0
+    A = A.astype(dtype)
+    o = O.cocluster(_to_oracle(A), want=("dist",))
+    got = engine.consensus_knn_assign(A, 20)
+    for k in (10, 15, 20):  # kNum: k < 20 are prefixes of the stable order
+        assert np.array_equal(got[:, :k], O.consensus_knn(o["dist"], N, k))
+
+
+def test_consensus_knn_fused_row_ranges(engine):
+    import torch
+    rng = np.random.default_rng(8)
+    B, N, k = 80, 900, 15
+    A = rng.integers(1, 6, (B, N)).astype(np.uint8)
+    ref = engine.consensus_knn_assign(A, k)
+    At = torch.from_numpy(A).cuda()
+    out = torch.full((N, k), -1, dtype=torch.int32, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for r0, r1 in ((0, 128), (128, 512), (512, 900)):
+        engine.consensus_knn_assign_t(At, k, r0, r1, out, flag)
+    torch.cuda.synchronize()
+    assert flag.item() == 0
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_consensus_knn_fused_nan_raises(engine):
+    A = np.zeros((3, 5), np.uint8)
+    A[:, :3] = 1  # cells 3, 4 never sampled
+    with pytest.raises(ValueError):
+        engine.consensus_knn_assign(A, 2)

@@ -45,8 +45,10 @@ def test_assignment_matrix():
     A = C.assignment_matrix(cols)
     assert A.dtype == np.uint8 and A.shape == (3, 3)
     assert A.tolist() == [[1, 0, 3], [2, 0, 4], [1, 5, 4]]
+    wide = C.assignment_matrix([np.array([1, 300]), np.array([-1, 2])])  # codes > 255: uint16 matrix
+    assert wide.dtype == np.uint16 and wide.tolist() == [[1, 300], [0, 2]]
     with pytest.raises(ValueError):
-        C.assignment_matrix([np.array([1, 300])])
+        C.assignment_matrix([np.array([1, 70000])])
 
 
 @pytest.mark.parametrize("N,G", [(100000, 8), (100000, 2), (250000, 8), (1000, 4), (130, 8)])
@@ -88,3 +90,11 @@ def test_louvain_recovers_two_cliques():
     lab = louvain(20, np.array(ei), np.array(ej), np.ones(len(ei)), resolution=1.0, seed=0)
     assert len(set(lab[:10])) == 1 and len(set(lab[10:])) == 1 and lab[0] != lab[10]
     assert lab.min() == 1
+
+
+@pytest.mark.parametrize("N,G", [(300, 8), (1000, 3), (129, 2), (257, 4)])
+def test_row_slabs_small_n_cuts_stay_aligned(N, G):
+    """A cut must never equal an unaligned N (it would be the next rank's r0)."""
+    cuts = row_slabs(N, G)
+    assert all(c % 128 == 0 for c in cuts[:-1])
+    assert cuts[-1] == N

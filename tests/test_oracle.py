@@ -108,3 +108,34 @@ def test_collision_fixture_has_fp32_collisions(golden):
     assert g["dist"][0] == g["dist"][1]
     r = O.cocluster(g["A"].astype(np.int32))
     assert np.array_equal(r["dist"], g["dist"])
+
+
+def test_knn_queries_equals_full_search_rows():
+    rng = np.random.default_rng(31)
+    X = rng.normal(size=(700, 6))
+    X[100:140] = X[0:40]  # duplicates
+    full_i, full_d = O.knn(X, 15)
+    q = np.array([0, 5, 100, 139, 699], np.int32)
+    qi, qd = O.knn_queries(X, 15, q)
+    assert np.array_equal(qi, full_i[q])
+    assert np.array_equal(qd, full_d[q])
+    assert np.array_equal(qi[:, :10], O.py_knn(X, 10)[q])
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16])
+def test_cocluster_rows_equals_packed_triangle(dtype):
+    rng = np.random.default_rng(32)
+    B, N = 40, 150
+    A = rng.integers(0, 300 if dtype == np.uint16 else 6, (B, N)).astype(dtype)
+    Ao = A.astype(np.int32)
+    Ao[Ao == 0] = -1
+    ref = O.py_cocluster(Ao)
+    rows = np.array([0, 7, 149], np.int32)
+    co, both = O.cocluster_rows(A, rows)
+    for t, i in enumerate(rows):
+        for j in range(N):
+            if j == i:
+                continue
+            o = O.packed_index(min(i, j), max(i, j), N)
+            assert co[t, j] == ref["co"][o] and both[t, j] == ref["both"][o]
+        assert both[t, i] == B - (A[:, i] == 0).sum()  # the diagonal: sampled count
