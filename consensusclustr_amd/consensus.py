@@ -212,10 +212,13 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
             finals.append(np.asarray(fn(N, ei, ej, w, float(res), seed), np.int32))
     lab = np.stack(finals)
     nuniq = np.array([np.unique(l_).size for l_ in finals])
-    # silhouette on the full pca for every candidate (only used where 1 < C < N/10)
-    codes = np.stack([np.unique(l_, return_inverse=True)[1] + 1 for l_ in finals]).astype(np.int32)
-    means, _, _, _ = eng.silhouette(pca, codes)
-    scores = np.where((nuniq > 1) & (nuniq < N / 10), means, np.where(nuniq == N, -1.0, 0.15))  # :446-452
+    # approxSilhouette on the full pca only where it is used, 1 < C < N/10 (:446-452)
+    scored = np.flatnonzero((nuniq > 1) & (nuniq < N / 10))
+    means = np.zeros(len(finals))
+    if scored.size:
+        codes = np.stack([np.unique(finals[t], return_inverse=True)[1] + 1 for t in scored]).astype(np.int32)
+        means[scored] = eng.silhouette(pca, codes)[0]
+    scores = np.where((nuniq > 1) & (nuniq < N / 10), means, np.where(nuniq == N, -1.0, 0.15))
     choice = consensus_choice(scores)
     out.update(assignments=lab[choice], scores=scores, choice=choice, candidates=lab, consensus_knn=cknn)
     return out

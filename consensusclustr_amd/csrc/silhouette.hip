@@ -52,8 +52,10 @@ __device__ __forceinline__ void load_row(const double* __restrict__ x, int64_t r
     for (int k = 0; k < DMAX; ++k) xr[k] = (k < d) ? x[r * d + k] : 0.0;
 }
 
-// K1: fixed-point cluster sums and counts.
-template <int DMAX>
+// K1: fixed-point cluster sums and counts, staged in LDS when (cmax + 1) x d
+// accumulators fit (SIL_LDS_CAP), else added straight to the global sums.
+#define SIL_LDS_CAP 65536
+template <int DMAX, bool LDS>
 __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__ x, int64_t m,
                                                       int d, const int32_t* __restrict__ labels,
                                                       int L, int cmax,
@@ -72,27 +74,55 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
     const int nacc = (cmax + 1) * d;
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
-        for (int t = threadIdx.x; t < nacc; t += SIL_T) acc[t] = 0ull;
-        for (int t = threadIdx.x; t <= cmax; t += SIL_T) cnt[t] = 0u;
-        __syncthreads();
+        unsigned long long* gs = gsum + (int64_t)l * nacc;
+        unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
+        if (LDS) {
+            for (int t = threadIdx.x; t < nacc; t += SIL_T) acc[t] = 0ull;
+            for (int t = threadIdx.x; t <= cmax; t += SIL_T) cnt[t] = 0u;
+            __syncthreads();
+        }
         if (in) {
             const int lab = labels[(int64_t)l * m + r];
             if (lab >= 1 && lab <= cmax) {
 #pragma unroll
                 for (int k = 0; k < DMAX; ++k)
-                    if (k < d) atomicAdd(&acc[lab * d + k], (unsigned long long)__double2ll_rn(xr[k] * sc));
-                atomicAdd(&cnt[lab], 1u);
+                    if (k < d) {
+                        const unsigned long long q = (unsigned long long)__double2ll_rn(xr[k] * sc);
+                        if (LDS) atomicAdd(&acc[lab * d + k], q);
+                        else atomicAdd(&gs[(int64_t)lab * d + k], q);
+                    }
+                if (LDS) atomicAdd(&cnt[lab], 1u);
+                else atomicAdd(&gc[lab], 1ull);
             }
         }
-        __syncthreads();
-        unsigned long long* gs = gsum + (int64_t)l * nacc;
-        unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
-        for (int t = threadIdx.x; t < nacc; t += SIL_T)
-            if (acc[t]) atomicAdd(&gs[t], acc[t]);
-        for (int t = threadIdx.x; t <= cmax; t += SIL_T)
-            if (cnt[t]) atomicAdd(&gc[t], (unsigned long long)cnt[t]);
-        __syncthreads();
+        if (LDS) {
+            __syncthreads();
+            for (int t = threadIdx.x; t < nacc; t += SIL_T)
+                if (acc[t]) atomicAdd(&gs[t], acc[t]);
+            for (int t = threadIdx.x; t <= cmax; t += SIL_T)
+                if (cnt[t]) atomicAdd(&gc[t], (unsigned long long)cnt[t]);
+            __syncthreads();
+        }
     }
+}
+
+__device__ __forceinline__ int sil_block_excl_scan(int v, int* sh, int* total) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    int woff = 0, tot = 0;
+    for (int w = 0; w < SIL_T / 64; ++w) {
+        if (w < wv) woff += sh[w];
+        tot += sh[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + x - v;
 }
 
 // K2: per labeling, the present codes (ascending = sort(unique(clusters)))
@@ -106,44 +136,48 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
                                                 int* __restrict__ npres, int* __restrict__ codes,
                                                 int* __restrict__ pos, double* __restrict__ mu,
                                                 double* __restrict__ muc, double* __restrict__ auxc) {
-    __shared__ int pos_s[257];
+    __shared__ int sh[SIL_T / 64];
     const int l = blockIdx.x;
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
     const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
     const unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
     const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
-    if (threadIdx.x == 0) {
-        int np = 0;
-        pos_s[0] = -1;
-        for (int c = 1; c <= cmax; ++c) {
-            pos_s[c] = gc[c] ? np : -1;
-            if (gc[c]) codes[(int64_t)l * cmax + np++] = c;
-        }
-        npres[l] = np;
+    int* pl = pos + (int64_t)l * (cmax + 1);
+    int carry = 0;
+    for (int c0 = 0; c0 <= cmax; c0 += SIL_T) {
+        const int c = c0 + threadIdx.x;
+        const bool present = c >= 1 && c <= cmax && gc[c] != 0ull;
+        int tot;
+        const int ex = carry + sil_block_excl_scan(present ? 1 : 0, sh, &tot);
+        if (c <= cmax) pl[c] = present ? ex : -1;
+        if (present) codes[(int64_t)l * cmax + ex] = c;
+        carry += tot;
     }
+    if (threadIdx.x == 0) npres[l] = carry;
     __syncthreads();
     double* ml = mu + (int64_t)l * (cmax + 1) * DMAX;
     double* mcl = muc + (int64_t)l * cmax * DMAX;
-    for (int t = threadIdx.x; t < (cmax + 1) * DMAX; t += SIL_T) {
-        const int c = t / DMAX, k = t - c * DMAX;
+    for (int64_t t = threadIdx.x; t < (int64_t)(cmax + 1) * DMAX; t += SIL_T) {
+        const int c = (int)(t / DMAX), k = (int)(t - (int64_t)c * DMAX);
         const unsigned long long n = gc[c];
-        const double v = (n && k < d) ? ((double)(long long)gs[c * d + k] * inv_sc) / (double)n : 0.0;
+        const double v = (n && k < d) ? ((double)(long long)gs[(int64_t)c * d + k] * inv_sc) / (double)n : 0.0;
         ml[t] = v;
-        if (pos_s[c] >= 0) mcl[pos_s[c] * DMAX + k] = v;
+        const int pc = pl[c];
+        if (pc >= 0) mcl[(int64_t)pc * DMAX + k] = v;
     }
-    for (int c = threadIdx.x; c <= cmax; c += SIL_T) pos[(int64_t)l * (cmax + 1) + c] = pos_s[c];
     __syncthreads();
     for (int c = threadIdx.x; c <= cmax; c += SIL_T) {
-        if (pos_s[c] < 0) continue;
+        const int pc = pl[c];
+        if (pc < 0) continue;
         double s = 0.0;
-        for (int k = 0; k < d; ++k) s = fma(ml[c * DMAX + k], ml[c * DMAX + k], s);
-        auxc[((int64_t)l * cmax + pos_s[c]) * 2] = s;
+        for (int k = 0; k < d; ++k) s = fma(ml[(int64_t)c * DMAX + k], ml[(int64_t)c * DMAX + k], s);
+        auxc[((int64_t)l * cmax + pc) * 2] = s;
     }
 }
 
 // K3: fixed-point within-cluster sum of squared distances to the centroid
 // (the exact difference form, as colMeans(sweep(x, 2, centroid)^2)).
-template <int DMAX>
+template <int DMAX, bool LDS>
 __global__ __launch_bounds__(SIL_T) void sil_var(const double* __restrict__ x, int64_t m, int d,
                                                  const int32_t* __restrict__ labels, int L, int cmax,
                                                  const unsigned* __restrict__ maxabs_bits,
@@ -162,13 +196,16 @@ __global__ __launch_bounds__(SIL_T) void sil_var(const double* __restrict__ x, i
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
         const double* ml = mu + (int64_t)l * (cmax + 1) * DMAX;
-        for (int t = threadIdx.x; t < (cmax + 1) * DMAX; t += SIL_T) mus[t] = ml[t];
-        for (int t = threadIdx.x; t <= cmax; t += SIL_T) vacc[t] = 0ull;
-        __syncthreads();
+        unsigned long long* gv = gvar + (int64_t)l * (cmax + 1);
+        if (LDS) {
+            for (int t = threadIdx.x; t < (cmax + 1) * DMAX; t += SIL_T) mus[t] = ml[t];
+            for (int t = threadIdx.x; t <= cmax; t += SIL_T) vacc[t] = 0ull;
+            __syncthreads();
+        }
         if (in) {
             const int lab = labels[(int64_t)l * m + r];
             if (lab >= 1 && lab <= cmax) {
-                const double* mc = mus + lab * DMAX;
+                const double* mc = LDS ? mus + lab * DMAX : ml + (int64_t)lab * DMAX;
                 double s = 0.0;
 #pragma unroll
                 for (int k = 0; k < DMAX; ++k)
@@ -176,14 +213,17 @@ __global__ __launch_bounds__(SIL_T) void sil_var(const double* __restrict__ x, i
                         const double t = xr[k] - mc[k];
                         s += t * t;
                     }
-                atomicAdd(&vacc[lab], (unsigned long long)__double2ll_rn(s * vsc));
+                const unsigned long long q = (unsigned long long)__double2ll_rn(s * vsc);
+                if (LDS) atomicAdd(&vacc[lab], q);
+                else atomicAdd(&gv[lab], q);
             }
         }
-        __syncthreads();
-        unsigned long long* gv = gvar + (int64_t)l * (cmax + 1);
-        for (int t = threadIdx.x; t <= cmax; t += SIL_T)
-            if (vacc[t]) atomicAdd(&gv[t], vacc[t]);
-        __syncthreads();
+        if (LDS) {
+            __syncthreads();
+            for (int t = threadIdx.x; t <= cmax; t += SIL_T)
+                if (vacc[t]) atomicAdd(&gv[t], vacc[t]);
+            __syncthreads();
+        }
     }
 }
 
@@ -231,6 +271,12 @@ __device__ __forceinline__ void sil_row_width(const double (&xr)[DMAX], double s
     }
 }
 
+// centroids per LDS stage of sil_width: [CH][DMAX] f64 + [CH][2] f64 + [CH] int within 64 KB
+template <int DMAX>
+constexpr int sil_chunk() {
+    return DMAX <= 16 ? 256 : (DMAX <= 32 ? 224 : 112);
+}
+
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x, int64_t m, int d,
                                                    const int32_t* __restrict__ labels, int L, int cmax,
@@ -243,9 +289,10 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
                                                    unsigned long long* __restrict__ wcnt,
                                                    double* __restrict__ out_width) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* smu = (double*)smem;                  // [np][DMAX]
-    double* sau = smu + (int64_t)cmax * DMAX;     // [np][2]
-    int* scode = (int*)(sau + 2 * (int64_t)cmax); // [np]
+    constexpr int CH = sil_chunk<DMAX>();          // centroids staged per pass
+    double* smu = (double*)smem;                  // [CH][DMAX]
+    double* sau = smu + (int64_t)CH * DMAX;       // [CH][2]
+    int* scode = (int*)(sau + 2 * (int64_t)CH);   // [CH]
     const int64_t ra = (int64_t)blockIdx.x * (2 * SIL_T) + threadIdx.x, rb = ra + SIL_T;
     const bool ina = ra < m, inb = rb < m;
     double xa[DMAX], xb[DMAX];
@@ -261,56 +308,60 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
         const int np = npres[l];
-        {
-            const double* ml = muc + (int64_t)l * cmax * DMAX;
-            for (int t = threadIdx.x; t < np * DMAX; t += SIL_T) smu[t] = ml[t];
-            const double* al = auxc + (int64_t)l * cmax * 2;
-            for (int t = threadIdx.x; t < 2 * np; t += SIL_T) sau[t] = al[t];
-            for (int t = threadIdx.x; t < np; t += SIL_T) scode[t] = codes[(int64_t)l * cmax + t];
-        }
-        __syncthreads();
         const int laba = ina ? labels[(int64_t)l * m + ra] : 0;
         const int labb = inb ? labels[(int64_t)l * m + rb] : 0;
+        const double* ml = muc + (int64_t)l * cmax * DMAX;
+        const double* al = auxc + (int64_t)l * cmax * 2;
         double otha = INFINITY, othb = INFINITY;
-        for (int pi = 0; pi < np; ++pi) {
-            const double2* mc = reinterpret_cast<const double2*>(smu + pi * DMAX);
-            double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+        for (int p0 = 0; p0 < np; p0 += CH) {
+            const int nc = min(CH, np - p0);
+            for (int t = threadIdx.x; t < nc * DMAX; t += SIL_T) smu[t] = ml[(int64_t)p0 * DMAX + t];
+            for (int t = threadIdx.x; t < 2 * nc; t += SIL_T) sau[t] = al[2 * (int64_t)p0 + t];
+            for (int t = threadIdx.x; t < nc; t += SIL_T) scode[t] = codes[(int64_t)l * cmax + p0 + t];
+            __syncthreads();
+            for (int pi = 0; pi < nc; ++pi) {
+                const double2* mc = reinterpret_cast<const double2*>(smu + pi * DMAX);
+                double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
 #pragma unroll
-            for (int k2 = 0; k2 < DMAX / 2; ++k2) {
-                const double2 mv = mc[k2];
-                a0 = fma(xa[2 * k2], mv.x, a0);
-                a1 = fma(xa[2 * k2 + 1], mv.y, a1);
-                b0 = fma(xb[2 * k2], mv.x, b0);
-                b1 = fma(xb[2 * k2 + 1], mv.y, b1);
+                for (int k2 = 0; k2 < DMAX / 2; ++k2) {
+                    const double2 mv = mc[k2];
+                    a0 = fma(xa[2 * k2], mv.x, a0);
+                    a1 = fma(xa[2 * k2 + 1], mv.y, a1);
+                    b0 = fma(xb[2 * k2], mv.x, b0);
+                    b1 = fma(xb[2 * k2 + 1], mv.y, b1);
+                }
+                const double mm = sau[2 * pi], vc = sau[2 * pi + 1];
+                const int c = scode[pi];
+                const double sa = fmax(fma(-2.0, a0 + a1, xxa + mm), 0.0) + vc;
+                const double sb = fmax(fma(-2.0, b0 + b1, xxb + mm), 0.0) + vc;
+                if (c != laba && sa < otha) otha = sa;
+                if (c != labb && sb < othb) othb = sb;
             }
-            const double mm = sau[2 * pi], vc = sau[2 * pi + 1];
-            const int c = scode[pi];
-            const double sa = fmax(fma(-2.0, a0 + a1, xxa + mm), 0.0) + vc;
-            const double sb = fmax(fma(-2.0, b0 + b1, xxb + mm), 0.0) + vc;
-            if (c != laba && sa < otha) otha = sa;
-            if (c != labb && sb < othb) othb = sb;
+            __syncthreads();  // before the next chunk (or labeling) overwrites the stage
         }
         // own cluster in the difference form: exact 0 for a singleton, as in R
         double selfa = INFINITY, selfb = INFINITY;
         if (ina && laba >= 1 && laba <= cmax) {
             const int p = pos[(int64_t)l * (cmax + 1) + laba];
+            const double* mcp = ml + (int64_t)p * DMAX;
             double s = 0.0;
 #pragma unroll
             for (int k = 0; k < DMAX; ++k) {
-                const double t = xa[k] - smu[p * DMAX + k];
+                const double t = xa[k] - mcp[k];
                 s = fma(t, t, s);
             }
-            selfa = s + sau[2 * p + 1];
+            selfa = s + al[2 * (int64_t)p + 1];
         }
         if (inb && labb >= 1 && labb <= cmax) {
             const int p = pos[(int64_t)l * (cmax + 1) + labb];
+            const double* mcp = ml + (int64_t)p * DMAX;
             double s = 0.0;
 #pragma unroll
             for (int k = 0; k < DMAX; ++k) {
-                const double t = xb[k] - smu[p * DMAX + k];
+                const double t = xb[k] - mcp[k];
                 s = fma(t, t, s);
             }
-            selfb = s + sau[2 * p + 1];
+            selfb = s + al[2 * (int64_t)p + 1];
         }
         long long wq = 0;
         unsigned wn = 0;
@@ -327,7 +378,6 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
             if (wq) atomicAdd(&wsum[l], (unsigned long long)wq);
             if (wn) atomicAdd(&wcnt[l], (unsigned long long)wn);
         }
-        __syncthreads();  // before the next labeling overwrites the centroids
     }
 }
 
@@ -359,15 +409,22 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
                        int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc,
                        double* out_width, hipStream_t st) {
     dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
-    size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
-    size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
-    sil_centroid<DMAX><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+    const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
+    const size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
+    if (lds1 <= SIL_LDS_CAP)
+        sil_centroid<DMAX, true><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+    else
+        sil_centroid<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
     sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gcnt, npres, codes, pos, mu, muc, auxc);
-    sil_var<DMAX><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
+    if (lds2 <= SIL_LDS_CAP)
+        sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
+    else
+        sil_var<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
     sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
                                                                                 gvar, pos, auxc);
     dim3 grid2((unsigned)ccg_cdiv(m, 2 * SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
-    size_t lds5 = (size_t)cmax * DMAX * 8 + (size_t)cmax * 16 + (size_t)cmax * 4;
+    constexpr int CH = sil_chunk<DMAX>();
+    const size_t lds5 = (size_t)CH * DMAX * 8 + (size_t)CH * 16 + (size_t)CH * 4;
     sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, pos, muc, auxc, wsum,
                                             wcnt, out_width);
 }
@@ -379,7 +436,7 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     CCG_REQUIRE(ctx && x && labels, "ccg_silhouette_dev: NULL argument");
     CCG_REQUIRE(m >= 1 && m < (1LL << 31) && d >= 1 && d <= 64 && L >= 1,
                 "ccg_silhouette_dev: bad sizes m=%lld d=%d L=%d", (long long)m, d, L);
-    CCG_REQUIRE(cmax >= 1 && cmax <= 256, "ccg_silhouette_dev: cmax=%d must be in [1, 256]", cmax);
+    CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_dev: cmax=%d must be in [1, 2^24]", cmax);
     hipStream_t st = ccg_pick_stream(ctx, stream);
     const int64_t nacc = (int64_t)(cmax + 1) * d;
     const int64_t words = (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L + 8;

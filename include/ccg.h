@@ -164,7 +164,7 @@ int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n,
 /* --------------------------------------------------------- silhouette -- */
 /* mean(approxSilhouette(x, labels_l)[,3], na.rm=TRUE) for L label vectors
  * over the same m x d float64 row-major matrix.  labels: L x m int32 codes
- * in [1, cmax], cmax <= 256.  Outputs (length L): mean width (NaN if every
+ * in [1, cmax], cmax <= 2^24 (workspace grows with L x cmax x d).  Outputs (length L): mean width (NaN if every
  * width is NaN), number of distinct clusters, smallest cluster size.
  * out_width (L x m) may be NULL. */
 int ccg_silhouette(ccg_ctx* ctx, const double* x, int64_t m, int d,

@@ -242,3 +242,23 @@ def test_consensus_knn_fused_nan_raises(engine):
     A[:, :3] = 1  # cells 3, 4 never sampled
     with pytest.raises(ValueError):
         engine.consensus_knn_assign(A, 2)
+
+
+# ---------------------------------------------------------- silhouette --
+@pytest.mark.parametrize("m,d,C", [(6000, 30, 1000), (4000, 50, 200), (3000, 12, 2900), (5000, 64, 300)])
+def test_silhouette_many_clusters_vs_oracle(engine, m, d, C):
+    """More than 256 clusters (high-resolution clusterings are scored too,
+    R/consensusClust.R:663-664): global accumulation and chunked centroid
+    staging instead of the LDS fast path."""
+    rng = np.random.default_rng(m + C)
+    X = _mixture(rng, m, d, C=16)
+    labs = np.stack([rng.integers(1, C + 1, m), rng.integers(1, 9, m)]).astype(np.int32)
+    labs[0, :5] = C  # make sure the top code is present
+    mean, nc, ms, w = engine.silhouette(X, labs, want_width=True)
+    for l_ in range(2):
+        ow, om, oC = O.silhouette(X, labs[l_])
+        np.testing.assert_allclose(mean[l_], om, rtol=RTOL)
+        assert nc[l_] == oC
+        ok = ~np.isnan(ow)
+        assert np.array_equal(np.isnan(w[l_]), ~ok)
+        np.testing.assert_allclose(w[l_][ok], ow[ok], rtol=RTOL, atol=1e-9)
