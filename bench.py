@@ -264,12 +264,14 @@ def main():
     rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(S)]
     knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(S)]
     rows, knn = rows_s[0], knn_s[0]
-    caps = [120 * n, 240 * n, 400 * n]  # SNN edges per node ~ 90 / 190 / 320 at k = 10 / 15 / 20
+    rcap = 700 * n  # SNN row entries (items per node ~ 560 at cfg3); grown once after the warmup if short
 
-    def alloc_snn(caps):
-        return [[(torch.empty(c, dtype=torch.int32, device=dev), torch.empty(c, dtype=torch.int32, device=dev),
-                  torch.empty(c, dtype=torch.float64, device=dev)) for c in caps] for _ in range(S)]
-    snn_out = alloc_snn(caps)
+    def alloc_snn(rcap):
+        # per stream: the union-graph rows of ccg_snn_rows_dev (row offsets, lengths, partners, packed weights)
+        return [(torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),
+                 torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
+                for _ in range(S)]
+    snn_out = alloc_snn(rcap)
     if os.environ.get("CCG_BENCH_TORCH_STREAMS"):
         streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     else:
@@ -299,7 +301,7 @@ def main():
             with torch.cuda.stream(streams[si]):
                 e.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[si])
                 e.knn_rows_t(rows_s[si], 20, knn_s[si])
-                e.snn_multi_t(knn_s[si], K_NUM, "number", snn_out[si], nedges[j])
+                e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
                 e.silhouette_t(rows_s[si], labels[j], cmax, means[j], nclust[j], minsize[j])
         for st_ in streams:
             cur.wait_stream(st_)
@@ -316,15 +318,15 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    need = nedges.max(0).values.tolist()
-    if any(e > c for e, c in zip(need, caps)):  # grow once and redo the warmup
-        caps = [int(max(e * 1.25, c)) for e, c in zip(need, caps)]
-        snn_out = alloc_snn(caps)
+    short = int(nedges.min().item())
+    if short < 0:  # rows did not fit: -short entries needed; grow once and redo the warmup
+        rcap = int(-short * 1.25)
+        snn_out = alloc_snn(rcap)
         step()
         torch.cuda.synchronize()
-        need = nedges.max(0).values.tolist()
-        if any(e > c for e, c in zip(need, caps)):
-            raise RuntimeError(f"SNN edge capacity too small: need {need}, have {caps}")
+        if int(nedges.min().item()) < 0:
+            raise RuntimeError(f"SNN row capacity too small: {rcap}")
+    need = nedges.max(0).values.tolist()
     fb = eng.knn_rows_t(rows, 20, knn, stats=True)  # certification statistics of the last bootstrap
 
     # ---------------- timed region

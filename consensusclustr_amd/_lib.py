@@ -63,6 +63,8 @@ SIGNATURES = {
     "ccg_snn": (_i, [_p, _p, _i64, _i, _i, _i, _p, _p, _p, _i64, _p]),
     "ccg_snn_dev": (_i, [_p, _p, _i64, _i, _i, _i, _p, _p, _p, _i64, _p, _p]),
     "ccg_snn_multi_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p, _p]),
+    "ccg_snn_rows_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _i64, _p, _p]),
+    "ccg_snn_reserve": (_i, [_p, _i64]),
     "ccg_silhouette": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p]),
     "ccg_silhouette_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p]),
     "ccg_select_mapback_dev": (_i, [_p, _i, _p, _p, _i64, _i, _i, _i64, _p, _p, _p, _i, _p, _i, _i64, _p, _p]),

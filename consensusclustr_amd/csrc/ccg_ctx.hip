@@ -48,6 +48,7 @@ extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
     c->timers = nullptr;
     c->ntimers = c->cap_timers = c->used_timers = 0;
     c->d_err = nullptr;
+    c->snn_row_reserve = 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

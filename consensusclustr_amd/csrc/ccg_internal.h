@@ -38,6 +38,8 @@ enum ccg_ws_slot {
     WS_FB_D,         // kNN fallback per-range lists (keys)
     WS_FB_I,         // kNN fallback per-range lists (ids)
     WS_SEGS,         // kNN batched-segment plan (offsets, blocks, positions)
+    WS_SORT,         // device radix sort temporary storage
+    WS_SNN_ROWS,     // SNN per-node partner rows (padded CSR of the per-graph API)
     WS_NSLOTS
 };
 
@@ -56,6 +58,7 @@ struct ccg_ctx {
     int device;
     hipStream_t stream;
     int* d_err;  // device word of CCG_DERR_* bits
+    int64_t snn_row_reserve;  // SNN row entries reserved by the per-graph API (0 = default)
     void* ws[WS_NSLOTS];
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
@@ -104,5 +107,10 @@ static inline hipStream_t ccg_pick_stream(ccg_ctx* ctx, void* s) {
 // total goes to out[n].  in may alias out.  Uses WS_SCAN.
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n,
                  hipStream_t st);
+
+// Stable device radix sort of (key, value) int32 pairs on the low key_bits
+// bits of the keys (hipCUB; temporary storage in WS_SORT).
+int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
+                       int32_t* vals_out, int64_t n, int key_bits, hipStream_t st);
 
 __host__ __device__ static inline int64_t ccg_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

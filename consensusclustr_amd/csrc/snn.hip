@@ -13,13 +13,20 @@
 // (rj, rp) belongs to graph k iff max(rj, rp) <= k.  Per graph t the value
 // lives in byte t of a 32-bit word (counts <= 33, rank sums <= 64).
 //
-// Each undirected edge is emitted by its smaller endpoint (partners p > j).
-// Per node one wave builds an LDS open-addressing hash table of its
-// partners (key p, packed per-graph values), then (pass 2) compacts it,
-// bitonic-sorts by p and emits each graph's edges in (i, j) order at offsets
-// from a device scan of pass-1 counts -- deterministic and sorted, no
-// scratch.  Nodes with more partners than the wave table holds use a
-// 256-thread table of 16K slots; beyond that an exact O(n) dense path.
+// Pipeline (every step deterministic):
+//   1. host lists: the kNN entries radix-sorted (stable) by neighbour, so
+//      every hosts(s) is in ascending host order; back-pointers bp (where h
+//      sits in hosts(knn[h][r])) and split[x] (hosts of x below x).
+//   2. capacity: per node the number M_j of (partner, member) items with
+//      partner p > j; a scan gives every node a row of M_j slots.
+//   3. build, one wave per node: the items are gathered, ordered by partner
+//      and merged (sum for NUMBER, bytewise min for RANK) into the node's row
+//      of (partner, packed per-graph values), ascending partner -- the union
+//      graph (the largest k) in CSR form with per-graph counts.  Tiers by
+//      size: register/LDS bucket sort (<= 1024 items), a 2048-slot LDS hash
+//      table, a 16K-slot block table, an exact O(n) dense pass.
+//   4. per-graph edge lists (i < j sorted by (i, j)) are streamed from the
+//      rows when the caller wants them (ccg_snn_multi_dev).
 #include <algorithm>
 #include <cstdlib>
 
@@ -28,8 +35,8 @@
 #define WAVE_LDS_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
 
 #define SNN_MAXK 4           // graphs per pass (|kNum| <= 4)
-#define SNN_WT 2048          // wave table slots
-#define SNN_WAVES 4          // waves per block in the wave kernel
+#define SNN_WT 2048          // wave hash-table slots
+#define SNN_WAVES 4          // waves per block in the wave kernels
 #define SNN_BT 16384         // block table slots (overflow path)
 #define SNN_DENSE_BLOCKS 64  // concurrent dense-path nodes
 #define SNN_EMPTY (-1)
@@ -41,6 +48,7 @@ struct SnnSpec {
     unsigned init;     // empty value word (0 for NUMBER, 0xFFFFFFFF for RANK)
 };
 
+// Per-graph edge outputs (ccg_snn_multi_dev).
 struct SnnOut {
     int32_t* oi[SNN_MAXK];
     int32_t* oj[SNN_MAXK];
@@ -48,70 +56,15 @@ struct SnnOut {
     int64_t cap[SNN_MAXK];
 };
 
-__global__ void snn_count_hosts(const int32_t* __restrict__ knn, int64_t n, int kstride, int k,
-                                unsigned long long* __restrict__ hcnt, int* __restrict__ err) {
-    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * k) return;
-    int64_t h = t / k;
-    int r = (int)(t - h * k);
-    int32_t x = knn[h * kstride + r];
-    if (x < 0 || x >= n || x == h) {
-        atomicOr(err, CCG_DERR_SNN_INDEX);
-        return;
-    }
-    atomicAdd(&hcnt[x], 1ull);
-}
-
-__global__ void snn_fill_hosts(const int32_t* __restrict__ knn, int64_t n, int kstride, int k,
-                               unsigned long long* __restrict__ cursor, int2* __restrict__ hosts) {
-    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * k) return;
-    int64_t h = t / k;
-    int r = (int)(t - h * k);
-    int32_t x = knn[h * kstride + r];
-    if (x < 0 || x >= n || x == h) return;
-    unsigned long long p = atomicAdd(&cursor[x], 1ull);
-    hosts[p] = make_int2((int)h, r + 1);
-}
-
-// Sort every host list by host id (one wave per list; rank of each entry =
-// number of smaller ids, ids in a list are distinct) into hosts_s, and record
-// where each kNN entry landed: bp[h * kmax + r - 1] = position of h in
-// hosts_s(knn[h][r - 1]), split[x] = number of hosts of x below x.  The
-// build then starts member s of node j at the entry after j itself, so it
-// only ever fetches partners p > j.
-#define SNN_SORT_LDS 512
-__global__ __launch_bounds__(256) void snn_sort_hosts(const int64_t* __restrict__ hoff, int64_t n, int kmax,
-                                                      const int2* __restrict__ hosts, int2* __restrict__ hosts_s,
-                                                      int* __restrict__ bp, int* __restrict__ split) {
-    __shared__ int buf_all[4][SNN_SORT_LDS];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int* buf = buf_all[wv];
-    for (int64_t x = (int64_t)blockIdx.x * 4 + wv; x < n; x += (int64_t)gridDim.x * 4) {
-        const int64_t h0 = hoff[x];
-        const int len = (int)(hoff[x + 1] - h0);
-        const int2* src = hosts + h0;
-        const bool in_lds = len <= SNN_SORT_LDS;
-        if (in_lds)
-            for (int c = lane; c < len; c += 64) buf[c] = src[c].x;
-        WAVE_LDS_SYNC();
-        int below = 0;
-        for (int c = lane; c < len; c += 64) {
-            const int2 e = src[c];
-            int rank = 0;
-            if (in_lds)
-                for (int i = 0; i < len; ++i) rank += buf[i] < e.x;
-            else
-                for (int i = 0; i < len; ++i) rank += src[i].x < e.x;
-            hosts_s[h0 + rank] = e;
-            bp[(int64_t)e.x * kmax + e.y - 1] = rank;
-            below += e.x < x;
-        }
-        for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
-        if (lane == 0) split[x] = below;
-        WAVE_LDS_SYNC();
-    }
-}
+// Node rows: row j = [roff[j], roff[j] + rlen[j]) of (nbr, wpk), capacity
+// roff[j+1] - roff[j]; written only when roff[n] <= cap.
+struct SnnRows {
+    const int64_t* roff;
+    int32_t* rlen;
+    int32_t* nbr;
+    uint32_t* wpk;
+    int64_t cap;
+};
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     const int lane = threadIdx.x & 63;
@@ -140,6 +93,10 @@ __device__ __forceinline__ unsigned bytewise_min(unsigned a, unsigned b) {
     return r;
 }
 
+__device__ __forceinline__ unsigned snn_combine(int type, unsigned a, unsigned b) {
+    return type == CCG_SNN_NUMBER ? a + b : bytewise_min(a, b);  // per-byte counts never carry
+}
+
 template <typename V>
 __device__ __forceinline__ void snn_update(const SnnSpec& sp, V* v, unsigned c) {
     if (sp.type == CCG_SNN_NUMBER) {
@@ -160,31 +117,6 @@ __device__ __forceinline__ unsigned snn_hash(int p, int bits) {
     return ((unsigned)p * 2654435761u) >> (32 - bits);
 }
 
-// Insert partner p with contribution c; returns false when the table is full.
-template <int T>
-__device__ __forceinline__ bool table_insert(int* keys, unsigned* vals, int* count, int p, unsigned c,
-                                             const SnnSpec& sp, int bits) {
-    unsigned s = snn_hash(p, bits);
-    for (int probe = 0; probe < T; ++probe) {
-        int k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (k == SNN_EMPTY) {
-            const int prev = atomicCAS(&keys[s], SNN_EMPTY, p);
-            if (prev == SNN_EMPTY) {
-                atomicAdd(count, 1);
-                k = p;
-            } else {
-                k = prev;
-            }
-        }
-        if (k == p) {
-            snn_update(sp, &vals[s], c);
-            return true;
-        }
-        s = (s + 1) & (T - 1);
-    }
-    return false;
-}
-
 __device__ __forceinline__ bool graph_has(const SnnSpec& sp, unsigned v, int t) {
     const unsigned b = (v >> (8 * t)) & 0xFFu;
     return sp.type == CCG_SNN_NUMBER ? b != 0u : b != 0xFFu;
@@ -197,15 +129,331 @@ __device__ __forceinline__ double graph_weight(const SnnSpec& sp, unsigned v, in
     return w < 1e-6 ? 1e-6 : w;
 }
 
-// ---------------------------------------------------------------- wave path --
-// Pass 1 (build): one wave per node builds an LDS hash table of 64-bit slots
-// (partner p << 32 | packed per-graph values): a new partner costs one CAS, a
-// repeat one add.  The table is compacted, sorted by p and parked in a
-// fixed-capacity scratch row; per-graph edge counts go to cnt[t][j].  It
-// serves the nodes the sort path below cannot stage (more than 1024 items);
-// nodes beyond its capacity go to the block path.
-// Pass 2 (emit) streams the sorted rows into the caller's edge arrays.
-#define SNN_WCAP (SNN_WT * 3 / 4)
+// --------------------------------------------------------- host lists --
+// Entry t = h*kmax + r of the kNN (h lists x at rank r+1) becomes the pair
+// (x, t); invalid neighbours (out of range, self) get key n, sort to the end
+// and raise CCG_DERR_SNN_INDEX.
+__global__ void snn_pairs_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride, int kmax,
+                                 int32_t* __restrict__ keys, int32_t* __restrict__ vals, int* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kmax) return;
+    const int64_t h = t / kmax;
+    const int r = (int)(t - h * kmax);
+    const int32_t x = knn[h * kstride + r];
+    const bool ok = x >= 0 && x < n && x != h;
+    if (!ok) atomicOr(err, CCG_DERR_SNN_INDEX);
+    keys[t] = ok ? x : (int32_t)n;
+    vals[t] = (int32_t)t;
+}
+
+// hoff[x] = first sorted position with key >= x (x = 0..n).
+__global__ void snn_hoff_kernel(const int32_t* __restrict__ skey, int64_t total, int64_t n,
+                                int64_t* __restrict__ hoff) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x > n) return;
+    int64_t lo = 0, hi = total;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (skey[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    hoff[x] = lo;
+}
+
+// hosts_s[p] = (host, rank); bp[t] = position of the host in its list.
+__global__ void snn_hosts_kernel(const int32_t* __restrict__ skey, const int32_t* __restrict__ sval, int kmax,
+                                 const int64_t* __restrict__ hoff, int64_t n, int2* __restrict__ hosts_s,
+                                 int* __restrict__ bp) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hoff[n]) return;
+    const int32_t x = skey[p], t = sval[p];
+    const int h = t / kmax, r = t - h * kmax;
+    hosts_s[p] = make_int2(h, r + 1);
+    bp[t] = (int)(p - hoff[x]);
+}
+
+// split[x] = number of hosts of x below x (hosts are ascending).
+__global__ void snn_split_kernel(const int64_t* __restrict__ hoff, const int2* __restrict__ hosts_s, int64_t n,
+                                 int* __restrict__ split) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    int64_t lo = hoff[x], hi = hoff[x + 1];
+    const int64_t base = lo;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (hosts_s[mid].x < x) lo = mid + 1; else hi = mid;
+    }
+    split[x] = (int)(lo - base);
+}
+
+// ------------------------------------------------------------- members --
+// Member i of node j (lane i <= kmax): i = 0 is j itself, starting at its
+// first host above j; i >= 1 is s = knn[j][i-1], starting at the entry
+// after j in hosts(s), plus s itself (rank 0) when s > j.  Items are the
+// partners p > j only.
+struct SnnMember {
+    int cur;
+    int len;
+    long long h0, hend;
+};
+
+__device__ __forceinline__ SnnMember snn_member(const int32_t* __restrict__ knn, int64_t n, int kstride, int kmax,
+                                                int64_t j, int lane, const int64_t* __restrict__ hoff,
+                                                const int* __restrict__ bp, const int* __restrict__ split) {
+    SnnMember m{0, 0, 0, 0};
+    if (lane > kmax) return m;
+    if (lane == 0) {
+        m.cur = (int)j;
+        m.h0 = hoff[j] + split[j];
+        m.hend = hoff[j + 1];
+        m.len = (int)(m.hend - m.h0);
+    } else {
+        const int c = knn[j * kstride + lane - 1];
+        if ((unsigned)c < (unsigned)n && c != j) {
+            const int q = bp[j * kmax + lane - 1];
+            m.cur = c;
+            m.h0 = hoff[c] + q + 1;
+            m.hend = hoff[c + 1];
+            m.len = (int)(m.hend - m.h0) + (c > j ? 1 : 0);
+        } else {
+            m.cur = (int)j;  // invalid input (reported via CCG_DERR_SNN_INDEX): no items
+        }
+    }
+    return m;
+}
+
+// Items M_j of every node: the row capacities.
+__global__ __launch_bounds__(256) void snn_items_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                        int kmax, const int64_t* __restrict__ hoff,
+                                                        const int* __restrict__ bp, const int* __restrict__ split,
+                                                        int64_t* __restrict__ cap) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        int v = m.len;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) cap[j] = v;
+    }
+}
+
+// Write the per-graph counts of a finished row.
+__device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[SNN_MAXK], int64_t n, int64_t j,
+                                               int lane, int64_t* __restrict__ cnt) {
+#pragma unroll
+    for (int t = 0; t < SNN_MAXK; ++t) {
+        int64_t v = c4[t];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
+    }
+}
+
+// ------------------------------------------------------- sort (ESC) tier --
+// Nodes with at most 64*R items: the items are gathered to registers (all
+// host loads of the node in flight at once), bucketed by partner into an LDS
+// stage (histogram, wave scan, scatter), ranked inside their bucket by
+// (partner, stage slot) and rewritten in order; one pass over the sorted
+// stage merges equal partners and writes the row.  R is chosen per node
+// (4, 8, 12 or 16 rounds of 64 items) so a node pays for its own size only.
+#define SNN_SNB 240   // buckets
+#define SNN_SI 1024   // items staged per wave
+
+struct SnnSortLds {
+    unsigned long long stage[SNN_SI];
+    union {
+        struct {  // gather phase: member headers
+            long long h0[64];
+            long long hend[64];
+            int cur[64];
+            int pre[65];
+        } g;
+        struct {  // bucket phase
+            int hist[SNN_SNB];
+            int bst[SNN_SNB + 1];
+        } s;
+    } u;
+};
+
+template <int R>
+__device__ __forceinline__ void snn_sort_node(SnnSortLds& L, const SnnSpec& sp, int64_t n, int64_t j, int M,
+                                              int lane, const int2* __restrict__ hosts_s, const SnnRows& rows,
+                                              int64_t* __restrict__ cnt) {
+    unsigned long long* stage = L.stage;
+    // gather: every host load of the node is issued before any is used
+    int2 hr[R];
+    int im[R];
+    int mi = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int t = 64 * r + lane;
+        im[r] = -1;
+        hr[r] = make_int2(-1, 0);
+        if (t < M) {
+            while (L.u.g.pre[mi + 1] <= t) ++mi;
+            im[r] = mi;
+            const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
+            if (q < L.u.g.hend[mi]) hr[r] = hosts_s[q];
+            else hr[r] = make_int2(L.u.g.cur[mi], 0);
+        }
+    }
+    WAVE_LDS_SYNC();
+    int* hist = L.u.s.hist;
+    int* bst = L.u.s.bst;
+    for (int b = lane; b < SNN_SNB; b += 64) hist[b] = 0;
+    WAVE_LDS_SYNC();
+    const float inv = (float)SNN_SNB / (float)(n - j);
+    unsigned long long e[R];
+    int bk[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        e[r] = ~0ull;
+        bk[r] = -1;
+        if (im[r] >= 0) {
+            const unsigned c = snn_contrib(sp, im[r], hr[r].y);
+            if (c != sp.init) {
+                e[r] = ((unsigned long long)(unsigned)hr[r].x << 32) | c;
+                bk[r] = min(SNN_SNB - 1, (int)((float)(hr[r].x - (int)j - 1) * inv));
+                atomicAdd(&hist[bk[r]], 1);
+            }
+        }
+    }
+    WAVE_LDS_SYNC();
+    // bucket starts: lane owns buckets 4*lane .. 4*lane+3
+    int hv[4], hs = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int b = 4 * lane + i;
+        hv[i] = b < SNN_SNB ? hist[b] : 0;
+        hs += hv[i];
+    }
+    int sc = hs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(sc, o);
+        if (lane >= o) sc += y;
+    }
+    const int V = __shfl(sc, 63);
+    int run = sc - hs;
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int b = 4 * lane + i;
+        if (b < SNN_SNB) {
+            bst[b] = run;
+            hist[b] = run;  // scatter cursor
+        }
+        run += hv[i];
+    }
+    if (lane == 0) bst[SNN_SNB] = V;
+    WAVE_LDS_SYNC();
+    int pos[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        pos[r] = 0;
+        if (bk[r] >= 0) {
+            pos[r] = atomicAdd(&hist[bk[r]], 1);
+            stage[pos[r]] = e[r];
+        }
+    }
+    WAVE_LDS_SYNC();
+    // rank inside the bucket by (p, slot)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (bk[r] >= 0) {
+            const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
+            const unsigned key = (unsigned)(e[r] >> 32);
+            int rank = 0;
+            for (int q = b0; q < b1; ++q) {
+                const unsigned kq = (unsigned)(stage[q] >> 32);
+                rank += (kq < key || (kq == key && q < pos[r])) ? 1 : 0;
+            }
+            pos[r] = b0 + rank;
+        }
+    }
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (bk[r] >= 0) stage[pos[r]] = e[r];
+    WAVE_LDS_SYNC();
+    // unique partners: the first of each run of equal keys merges the run
+    const bool write = rows.roff[n] <= rows.cap;
+    const int64_t ro = rows.roff[j];
+    int u = 0;
+    int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+    for (int q0 = 0; q0 < V; q0 += 64) {
+        const int q = q0 + lane;
+        unsigned key = 0, agg = 0;
+        bool first = false;
+        if (q < V) {
+            const unsigned long long x = stage[q];
+            key = (unsigned)(x >> 32);
+            first = q == 0 || (unsigned)(stage[q - 1] >> 32) != key;
+            if (first) {
+                agg = (unsigned)x;
+                for (int q2 = q + 1; q2 < V; ++q2) {
+                    const unsigned long long y = stage[q2];
+                    if ((unsigned)(y >> 32) != key) break;
+                    agg = snn_combine(sp.type, agg, (unsigned)y);
+                }
+            }
+        }
+        const unsigned long long m = __ballot(first);
+        if (first) {
+            if (write) {
+                const int64_t o = ro + u + __popcll(m & lanemask_lt());
+                rows.nbr[o] = (int32_t)key;
+                rows.wpk[o] = agg;
+            }
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t)
+                if (t < sp.nk && graph_has(sp, agg, t)) ++c4[t];
+        }
+        u += __popcll(m);
+    }
+    snn_row_counts(sp, c4, n, j, lane, cnt);
+    if (lane == 0) rows.rlen[j] = u;
+}
+
+__global__ __launch_bounds__(64 * SNN_WAVES, 4) void snn_sort_build_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
+    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
+    int64_t* __restrict__ cnt, SnnRows rows, int* __restrict__ ov_list, int* __restrict__ ov_count) {
+    __shared__ SnnSortLds lds_all[SNN_WAVES];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    SnnSortLds& L = lds_all[wv];
+    const int kmax = sp.kk[sp.nk - 1];
+    for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
+        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        int incl = m.len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int M = __shfl(incl, 63);
+        if (M > SNN_SI) {
+            if (lane == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
+            continue;
+        }
+        if (lane <= kmax) {
+            L.u.g.pre[lane] = incl - m.len;
+            L.u.g.h0[lane] = m.h0;
+            L.u.g.hend[lane] = m.hend;
+            L.u.g.cur[lane] = m.cur;
+        }
+        if (lane == 0) L.u.g.pre[kmax + 1] = M;
+        WAVE_LDS_SYNC();
+        if (M <= 256) snn_sort_node<4>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else if (M <= 512) snn_sort_node<8>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else if (M <= 768) snn_sort_node<12>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else snn_sort_node<16>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        WAVE_LDS_SYNC();
+    }
+}
+
+// ---------------------------------------------------------- hash tier --
+// Nodes with more items: one wave per node builds an LDS hash table of
+// 64-bit slots (partner p << 32 | packed per-graph values): a new partner
+// costs one CAS, a repeat one add.  The table is compacted, sorted by p and
+// written to the row.  Nodes beyond its capacity go to the block tier.
 #define SNN_EMPTY64 (~0ull)
 
 __device__ __forceinline__ bool table_insert64(unsigned long long* tab, int p, unsigned c, const SnnSpec& sp,
@@ -246,49 +494,8 @@ constexpr int snn_log2() {
     return b;
 }
 
-// One item per active lane into a WT-slot table, probing with CAS only (a
-// CAS on an empty slot inserts, a returned equal key means the partner is
-// already there).  The loop runs while any lane still has its item, so the
-// control flow stays wave-uniform.  Returns false on lanes that found no slot.
-template <int WT>
-__device__ __forceinline__ bool wave_insert64(unsigned long long* tab, int p, unsigned c, bool active, int type) {
-    unsigned s = snn_hash(p, snn_log2<WT>());
-    const unsigned long long want = ((unsigned long long)(unsigned)p << 32) | c;
-    int probes = 0;
-    bool ok = true;
-    while (__any(active)) {
-        if (active) {
-            unsigned long long old = atomicCAS(&tab[s], SNN_EMPTY64, want);
-            if (old == SNN_EMPTY64) {
-                active = false;
-            } else if ((unsigned)(old >> 32) == (unsigned)p) {
-                if (type == CCG_SNN_NUMBER) {
-                    atomicAdd(&tab[s], (unsigned long long)c);  // per-byte counts never carry
-                } else {
-                    while (true) {
-                        const unsigned nv = bytewise_min((unsigned)old, c);
-                        if (nv == (unsigned)old) break;
-                        const unsigned long long nw = (old & 0xFFFFFFFF00000000ull) | nv;
-                        const unsigned long long prev = atomicCAS(&tab[s], old, nw);
-                        if (prev == old) break;
-                        old = prev;
-                    }
-                }
-                active = false;
-            } else {
-                s = (s + 1) & (WT - 1);
-                if (++probes == WT) {
-                    active = false;
-                    ok = false;
-                }
-            }
-        }
-    }
-    return ok;
-}
-
 // Sort a node's u compacted entries (tab[0..u), distinct partners p in (j, n))
-// by p and store them to dst[0..u).  Each lane holds entries c = r*64 + lane
+// by p and store them to the row.  Each lane holds entries c = r*64 + lane
 // in registers; a 128-bucket split on p (monotone in p) gives every entry its
 // bucket's start by a histogram + wave scan, the entries are scattered into
 // bucket order in tab, and each entry's final place is its bucket start plus
@@ -296,7 +503,8 @@ __device__ __forceinline__ bool wave_insert64(unsigned long long* tab, int p, un
 #define SNN_NB 128
 template <int RMAX>
 __device__ __forceinline__ void snn_bucket_store(unsigned long long* tab, int u, int lane, int64_t j, int64_t n,
-                                                 int* hist, int* bst, unsigned long long* __restrict__ dst) {
+                                                 int* hist, int* bst, int32_t* __restrict__ nbr,
+                                                 uint32_t* __restrict__ wpk, bool write) {
     unsigned long long e[RMAX];
     int bk[RMAX];
     const float inv = (float)SNN_NB / (float)(n - j - 1);
@@ -338,7 +546,10 @@ __device__ __forceinline__ void snn_bucket_store(unsigned long long* tab, int u,
             const unsigned p = (unsigned)(e[r] >> 32);
             int rank = 0;
             for (int i = b0; i < b1; ++i) rank += (unsigned)(tab[i] >> 32) < p;
-            dst[b0 + rank] = e[r];
+            if (write) {
+                nbr[b0 + rank] = (int32_t)p;
+                wpk[b0 + rank] = (uint32_t)e[r];
+            }
         }
     }
 }
@@ -360,52 +571,27 @@ struct SnnWaveLds {
     } u;
 };
 
-// Tier kernel: WT-slot tables (WT = 1024: 4 waves/SIMD, fits ~96% of nodes at
-// cfg3; WT = 2048 for the overflow list of the first tier).  in_list = nullptr
-// walks every node, else the in_count nodes of in_list.
 template <int WT>
-__global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_build_kernel(
+__global__ __launch_bounds__(64 * SNN_WAVES, 2) void snn_wave_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, const int* __restrict__ in_list, const int* __restrict__ in_count,
-    int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
-    int* __restrict__ ucount) {
+    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ in_list, const int* __restrict__ in_count,
+    int* __restrict__ ov_list, int* __restrict__ ov_count) {
     __shared__ SnnWaveLds<WT> lds_all[SNN_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     SnnWaveLds<WT>& L = lds_all[wv];
     unsigned long long* tab = L.tab;
     const int kmax = sp.kk[sp.nk - 1];
     constexpr int CAP = WT * 3 / 4;
-    const int64_t nn = in_list ? (int64_t)*in_count : n;
+    const int64_t nn = *in_count;
+    const bool write = rows.roff[n] <= rows.cap;
     for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
-        const int64_t j = in_list ? (int64_t)in_list[f] : f;
+        const int64_t j = in_list[f];
         for (int s = lane; s < WT; s += 64) tab[s] = SNN_EMPTY64;
-        // Flat gather over the partners p > j only: member 0 (j itself) from
-        // its first host above j, member i (s = knn[j][i-1]) from the entry
-        // after j in the sorted hosts(s), plus s itself (rank 0) when s > j.
-        // Item t of M = sum of member lengths; host entries are fetched one
+        // Flat gather over the partners p > j; host entries are fetched one
         // round ahead so their latency hides behind the current LDS inserts.
-        int mcur = 0, mlen = 0;
-        long long mh0 = 0, mend = 0;
-        if (lane <= kmax) {
-            if (lane == 0) {
-                mcur = (int)j;
-                mh0 = hoff[j] + split[j];
-                mend = hoff[j + 1];
-                mlen = (int)(mend - mh0);
-            } else {
-                mcur = knn[j * kstride + lane - 1];
-                if ((unsigned)mcur < (unsigned)n && mcur != j) {
-                    const int q = bp[j * kmax + lane - 1];
-                    mh0 = hoff[mcur] + q + 1;
-                    mend = hoff[mcur + 1];
-                    mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
-                } else {
-                    mcur = (int)j;  // invalid input (reported via CCG_DERR_SNN_INDEX): no items
-                }
-            }
-        }
-        int incl = mlen;
+        const SnnMember mem = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        int incl = mem.len;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(incl, o);
@@ -413,10 +599,10 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
         }
         const int M = __shfl(incl, 63);
         if (lane <= kmax) {
-            L.u.g.pre[lane] = incl - mlen;
-            L.u.g.h0[lane] = mh0;
-            L.u.g.hend[lane] = mend;
-            L.u.g.cur[lane] = mcur;
+            L.u.g.pre[lane] = incl - mem.len;
+            L.u.g.h0[lane] = mem.h0;
+            L.u.g.hend[lane] = mem.hend;
+            L.u.g.cur[lane] = mem.cur;
         }
         if (lane == 0) L.u.g.pre[kmax + 1] = M;
         WAVE_LDS_SYNC();
@@ -474,22 +660,18 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
             WAVE_LDS_SYNC();
         }
         if (full || u > CAP) {
-            if (lane == 0) {
-                const int q = atomicAdd(ov_count, 1);
-                ov_list[q] = (int)j;
-            }
+            if (lane == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
             continue;
         }
-        // Sort by partner and park the row in scratch (bucket split + in-bucket rank).
-        unsigned long long* dst = scratch + j * SNN_WCAP;
+        const int64_t ro = rows.roff[j];
         const int R = (u + 63) >> 6;
         int* hist = L.u.s.hist;
         int* bst = L.u.s.bst;
         if (u == 0) {
-        } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, dst);
-        else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, dst);
-        else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, dst);
-        else if constexpr (CAP > 768) snn_bucket_store<CAP / 64>(tab, u, lane, j, n, hist, bst, dst);
+        } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
+        else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
+        else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
+        else snn_bucket_store<CAP / 64>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
         WAVE_LDS_SYNC();
         int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
         for (int c = lane; c < u; c += 64) {
@@ -498,301 +680,46 @@ __global__ __launch_bounds__(64 * SNN_WAVES, WT <= 1024 ? 4 : 2) void snn_wave_b
             for (int t = 0; t < SNN_MAXK; ++t)
                 if (t < sp.nk && graph_has(sp, v, t)) ++c4[t];
         }
-#pragma unroll
-        for (int t = 0; t < SNN_MAXK; ++t) {
-            int64_t v = c4[t];
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
-        }
-        if (lane == 0) ucount[j] = u;
+        snn_row_counts(sp, c4, n, j, lane, cnt);
+        if (lane == 0) rows.rlen[j] = u;
         WAVE_LDS_SYNC();
     }
 }
 
-// ------------------------------------------------------- sort (ESC) path --
-// Nodes with at most SI items (partners p > j, with multiplicity) skip the
-// hash table: the items are gathered to registers (all host loads in flight
-// at once), bucketed by p into an LDS stage (histogram, scan, scatter),
-// ranked inside their bucket by (p, stage slot) and rewritten in sorted
-// order; one pass over the sorted stage then merges equal partners (sum for
-// NUMBER, bytewise min for RANK) and writes the row.  Every item costs a
-// fixed handful of LDS operations instead of a probe sequence.
-#define SNN_SNB 240  // buckets: SI*8 + 2*SNN_SNB*4 + 4 bytes of LDS per wave
-
-template <int SI>
-struct SnnSortLds {
-    unsigned long long stage[SI];
-    union {
-        struct {  // gather phase: member headers
-            long long h0[64];
-            long long hend[64];
-            int cur[64];
-            int pre[65];
-        } g;
-        struct {  // bucket phase
-            int hist[SNN_SNB];
-            int bst[SNN_SNB + 1];
-        } s;
-    } u;
-};
-
-__device__ __forceinline__ unsigned snn_combine(int type, unsigned a, unsigned b) {
-    return type == CCG_SNN_NUMBER ? a + b : bytewise_min(a, b);  // per-byte counts never carry
-}
-
-template <int SI>
-__global__ __launch_bounds__(64 * SNN_WAVES, SI <= 1024 ? 4 : 2) void snn_sort_build_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
-    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, const int* __restrict__ in_list, const int* __restrict__ in_count,
-    int* __restrict__ ov_list, int* __restrict__ ov_count, unsigned long long* __restrict__ scratch,
-    int* __restrict__ ucount) {
-    constexpr int R = SI / 64;
-    __shared__ SnnSortLds<SI> lds_all[SNN_WAVES];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    SnnSortLds<SI>& L = lds_all[wv];
-    unsigned long long* stage = L.stage;
-    const int kmax = sp.kk[sp.nk - 1];
-    const int64_t nn = in_list ? (int64_t)*in_count : n;
-    for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
-        const int64_t j = in_list ? (int64_t)in_list[f] : f;
-        // members: as in snn_wave_build_kernel (partners p > j only)
-        int mcur = 0, mlen = 0;
-        long long mh0 = 0, mend = 0;
-        if (lane <= kmax) {
-            if (lane == 0) {
-                mcur = (int)j;
-                mh0 = hoff[j] + split[j];
-                mend = hoff[j + 1];
-                mlen = (int)(mend - mh0);
+// --------------------------------------------------------- block tier --
+// Same algorithm with one 256-thread block and a 16K-slot table per node,
+// for the overflow list of the hash tier; the table is compacted and
+// bitonic-sorted by partner in LDS.  Nodes that overflow here too are
+// appended to ov2 for the dense tier.
+__device__ __forceinline__ bool table_insert_blk(int* keys, unsigned* vals, int* count, int p, unsigned c,
+                                                 const SnnSpec& sp, int bits) {
+    unsigned s = snn_hash(p, bits);
+    for (int probe = 0; probe < SNN_BT; ++probe) {
+        int k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == SNN_EMPTY) {
+            const int prev = atomicCAS(&keys[s], SNN_EMPTY, p);
+            if (prev == SNN_EMPTY) {
+                atomicAdd(count, 1);
+                k = p;
             } else {
-                mcur = knn[j * kstride + lane - 1];
-                if ((unsigned)mcur < (unsigned)n && mcur != j) {
-                    const int q = bp[j * kmax + lane - 1];
-                    mh0 = hoff[mcur] + q + 1;
-                    mend = hoff[mcur + 1];
-                    mlen = (int)(mend - mh0) + (mcur > j ? 1 : 0);
-                } else {
-                    mcur = (int)j;  // invalid input (reported via CCG_DERR_SNN_INDEX): no items
-                }
+                k = prev;
             }
         }
-        int incl = mlen;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
+        if (k == p) {
+            snn_update(sp, &vals[s], c);
+            return true;
         }
-        const int M = __shfl(incl, 63);
-        if (M > SI) {
-            if (lane == 0) {
-                const int q = atomicAdd(ov_count, 1);
-                ov_list[q] = (int)j;
-            }
-            continue;
-        }
-        if (lane <= kmax) {
-            L.u.g.pre[lane] = incl - mlen;
-            L.u.g.h0[lane] = mh0;
-            L.u.g.hend[lane] = mend;
-            L.u.g.cur[lane] = mcur;
-        }
-        if (lane == 0) L.u.g.pre[kmax + 1] = M;
-        WAVE_LDS_SYNC();
-        // gather: every host load of the node is issued before any is used
-        int2 hr[R];
-        int im[R];
-        int mi = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int t = 64 * r + lane;
-            im[r] = -1;
-            hr[r] = make_int2(-1, 0);
-            if (t < M) {
-                while (L.u.g.pre[mi + 1] <= t) ++mi;
-                im[r] = mi;
-                const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
-                if (q < L.u.g.hend[mi]) hr[r] = hosts_s[q];
-                else hr[r] = make_int2(L.u.g.cur[mi], 0);
-            }
-        }
-        WAVE_LDS_SYNC();
-        int* hist = L.u.s.hist;
-        int* bst = L.u.s.bst;
-        for (int b = lane; b < SNN_SNB; b += 64) hist[b] = 0;
-        WAVE_LDS_SYNC();
-        const float inv = (float)SNN_SNB / (float)(n - j);
-        unsigned long long e[R];
-        int bk[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            e[r] = SNN_EMPTY64;
-            bk[r] = -1;
-            if (im[r] >= 0) {
-                const unsigned c = snn_contrib(sp, im[r], hr[r].y);
-                if (c != sp.init) {
-                    e[r] = ((unsigned long long)(unsigned)hr[r].x << 32) | c;
-                    bk[r] = min(SNN_SNB - 1, (int)((float)(hr[r].x - (int)j - 1) * inv));
-                    atomicAdd(&hist[bk[r]], 1);
-                }
-            }
-        }
-        WAVE_LDS_SYNC();
-        // bucket starts: lane owns buckets 4*lane .. 4*lane+3
-        int hv[4], hs = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = 4 * lane + i;
-            hv[i] = b < SNN_SNB ? hist[b] : 0;
-            hs += hv[i];
-        }
-        int sc = hs;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(sc, o);
-            if (lane >= o) sc += y;
-        }
-        const int V = __shfl(sc, 63);
-        int run = sc - hs;
-        WAVE_LDS_SYNC();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = 4 * lane + i;
-            if (b < SNN_SNB) {
-                bst[b] = run;
-                hist[b] = run;  // scatter cursor
-            }
-            run += hv[i];
-        }
-        if (lane == 0) bst[SNN_SNB] = V;
-        WAVE_LDS_SYNC();
-        int pos[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            pos[r] = 0;
-            if (bk[r] >= 0) {
-                pos[r] = atomicAdd(&hist[bk[r]], 1);
-                stage[pos[r]] = e[r];
-            }
-        }
-        WAVE_LDS_SYNC();
-        // rank inside the bucket by (p, slot)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (bk[r] >= 0) {
-                const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
-                const unsigned key = (unsigned)(e[r] >> 32);
-                int rank = 0;
-                for (int q = b0; q < b1; ++q) {
-                    const unsigned kq = (unsigned)(stage[q] >> 32);
-                    rank += (kq < key || (kq == key && q < pos[r])) ? 1 : 0;
-                }
-                pos[r] = b0 + rank;
-            }
-        }
-        WAVE_LDS_SYNC();
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (bk[r] >= 0) stage[pos[r]] = e[r];
-        WAVE_LDS_SYNC();
-        // unique partners: first of each run of equal keys
-        auto is_first = [&](int q, unsigned& key) {
-            const unsigned long long x = stage[q];
-            key = (unsigned)(x >> 32);
-            return q == 0 || (unsigned)(stage[q - 1] >> 32) != key;
-        };
-        if constexpr (SI > SNN_WCAP) {
-            int uu = 0;
-            for (int q0 = 0; q0 < V; q0 += 64) {
-                unsigned key;
-                const bool first = q0 + lane < V && is_first(q0 + lane, key);
-                uu += __popcll(__ballot(first));
-            }
-            if (uu > SNN_WCAP) {
-                if (lane == 0) {
-                    const int q = atomicAdd(ov_count, 1);
-                    ov_list[q] = (int)j;
-                }
-                WAVE_LDS_SYNC();
-                continue;
-            }
-        }
-        unsigned long long* dst = scratch + j * SNN_WCAP;
-        int u = 0;
-        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
-        for (int q0 = 0; q0 < V; q0 += 64) {
-            const int q = q0 + lane;
-            unsigned key = 0, agg = 0;
-            const bool first = q < V && is_first(q, key);
-            if (first) {
-                agg = (unsigned)stage[q];
-                for (int q2 = q + 1; q2 < V; ++q2) {
-                    const unsigned long long y = stage[q2];
-                    if ((unsigned)(y >> 32) != key) break;
-                    agg = snn_combine(sp.type, agg, (unsigned)y);
-                }
-            }
-            const unsigned long long m = __ballot(first);
-            if (first) {
-                dst[u + __popcll(m & lanemask_lt())] = ((unsigned long long)key << 32) | agg;
-#pragma unroll
-                for (int t = 0; t < SNN_MAXK; ++t)
-                    if (t < sp.nk && graph_has(sp, agg, t)) ++c4[t];
-            }
-            u += __popcll(m);
-        }
-#pragma unroll
-        for (int t = 0; t < SNN_MAXK; ++t) {
-            int64_t v = c4[t];
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = v;
-        }
-        if (lane == 0) ucount[j] = u;
-        WAVE_LDS_SYNC();
+        s = (s + 1) & (SNN_BT - 1);
     }
+    return false;
 }
 
-__global__ __launch_bounds__(256) void snn_wave_emit_kernel(int64_t n, SnnSpec sp, const int64_t* __restrict__ off,
-                                                            const int* __restrict__ ov_flag,
-                                                            const unsigned long long* __restrict__ scratch,
-                                                            const int* __restrict__ ucount, SnnOut out) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
-        if (ov_flag[j]) continue;
-        const int u = ucount[j];
-        const unsigned long long* src = scratch + j * SNN_WCAP;
-        for (int t = 0; t < sp.nk; ++t) {
-            int64_t e = off[(int64_t)t * (n + 1) + j];
-            for (int c0 = 0; c0 < u; c0 += 64) {
-                const int c = c0 + lane;
-                const unsigned long long x = c < u ? src[c] : 0ull;
-                const unsigned v = (unsigned)x;
-                const bool has = c < u && graph_has(sp, v, t);
-                const unsigned long long m = __ballot(has);
-                if (has) {
-                    const int64_t pos = e + __popcll(m & lanemask_lt());
-                    if (pos < out.cap[t]) {
-                        out.oi[t][pos] = (int32_t)j;
-                        out.oj[t][pos] = (int32_t)(x >> 32);
-                        out.ow[t][pos] = graph_weight(sp, v, t);
-                    }
-                }
-                e += __popcll(m);
-            }
-        }
-    }
-}
-
-// --------------------------------------------------------------- block path --
-// Same algorithm with one 256-thread block and a 16K-slot table per node, for
-// the overflow list of the wave path.  Nodes that overflow here too are
-// appended to ov2 for the dense path.
-template <bool EMIT>
-__global__ __launch_bounds__(256) void snn_block_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
-    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
-    const int* __restrict__ ov_list, const int* __restrict__ ov_count, int* __restrict__ ov2_list,
-    int* __restrict__ ov2_count, const int* __restrict__ ov2_flag, SnnOut out) {
+__global__ __launch_bounds__(256) void snn_block_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                        SnnSpec sp, const int64_t* __restrict__ hoff,
+                                                        const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
+                                                        SnnRows rows, const int* __restrict__ ov_list,
+                                                        const int* __restrict__ ov_count, int* __restrict__ ov2_list,
+                                                        int* __restrict__ ov2_count) {
     __shared__ int keys[SNN_BT];
     __shared__ unsigned vals[SNN_BT];
     __shared__ int count;
@@ -806,9 +733,9 @@ __global__ __launch_bounds__(256) void snn_block_kernel(
     constexpr int PER = SNN_BT / 256;  // slots owned per thread during compaction
     const int cap_entries = SNN_BT * 3 / 4;
     const int nov = *ov_count;
+    const bool write = rows.roff[n] <= rows.cap;
     for (int f = blockIdx.x; f < nov; f += gridDim.x) {
         const int64_t j = ov_list[f];
-        if (EMIT && ov2_flag[j]) continue;  // uniform across the block
         for (int s = tid; s < SNN_BT; s += 256) {
             keys[s] = SNN_EMPTY;
             vals[s] = sp.init;
@@ -835,37 +762,13 @@ __global__ __launch_bounds__(256) void snn_block_kernel(
                 }
                 if (p > j) {
                     const unsigned c = snn_contrib(sp, i, rp);
-                    if (c != sp.init && !table_insert<SNN_BT>(keys, vals, &count, p, c, sp, BITS)) full_s = 1;
+                    if (c != sp.init && !table_insert_blk(keys, vals, &count, p, c, sp, BITS)) full_s = 1;
                 }
             }
         }
         __syncthreads();
         if (full_s || count > cap_entries) {
-            if (!EMIT && tid == 0) {
-                const int q = atomicAdd(ov2_count, 1);
-                ov2_list[q] = (int)j;
-            }
-            __syncthreads();
-            continue;
-        }
-        if (!EMIT) {
-            int64_t c[SNN_MAXK] = {0, 0, 0, 0};
-            for (int s = tid; s < SNN_BT; s += 256)
-                if (keys[s] != SNN_EMPTY) {
-                    const unsigned v = vals[s];
-#pragma unroll
-                    for (int t = 0; t < SNN_MAXK; ++t)
-                        if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
-                }
-#pragma unroll
-            for (int t = 0; t < SNN_MAXK; ++t) {
-                int64_t v = c[t];
-                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                if (lane == 0) wsum[wv][t] = v;
-            }
-            __syncthreads();
-            if (tid < sp.nk)
-                cnt[(int64_t)tid * (n + 1) + j] = wsum[0][tid] + wsum[1][tid] + wsum[2][tid] + wsum[3][tid];
+            if (tid == 0) ov2_list[atomicAdd(ov2_count, 1)] = (int)j;
             __syncthreads();
             continue;
         }
@@ -925,51 +828,47 @@ __global__ __launch_bounds__(256) void snn_block_kernel(
                 __syncthreads();
             }
         }
-        for (int t = 0; t < sp.nk; ++t) {
-            int64_t e = cnt[(int64_t)t * (n + 1) + j];
-            for (int c0 = 0; c0 < u; c0 += 256) {
-                const int c = c0 + tid;
-                const bool in = c < u;
-                const unsigned v = in ? vals[c] : sp.init;
-                const bool has = in && graph_has(sp, v, t);
-                const unsigned long long m = __ballot(has);
-                if (lane == 0) wsum[wv][0] = __popcll(m);
-                __syncthreads();
-                int64_t before = 0, tot = 0;
-                for (int w = 0; w < 4; ++w) {
-                    if (w < wv) before += wsum[w][0];
-                    tot += wsum[w][0];
-                }
-                if (has) {
-                    const int64_t pos = e + before + __popcll(m & lanemask_lt());
-                    if (pos < out.cap[t]) {
-                        out.oi[t][pos] = (int32_t)j;
-                        out.oj[t][pos] = keys[c];
-                        out.ow[t][pos] = graph_weight(sp, v, t);
-                    }
-                }
-                e += tot;
-                __syncthreads();
+        const int64_t ro = rows.roff[j];
+        int64_t c[SNN_MAXK] = {0, 0, 0, 0};
+        for (int q = tid; q < u; q += 256) {
+            const unsigned v = vals[q];
+            if (write) {
+                rows.nbr[ro + q] = keys[q];
+                rows.wpk[ro + q] = v;
             }
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t)
+                if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
         }
+#pragma unroll
+        for (int t = 0; t < SNN_MAXK; ++t) {
+            int64_t v = c[t];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) wsum[wv][t] = v;
+        }
+        __syncthreads();
+        if (tid < sp.nk) cnt[(int64_t)tid * (n + 1) + j] = wsum[0][tid] + wsum[1][tid] + wsum[2][tid] + wsum[3][tid];
+        if (tid == 0) rows.rlen[j] = u;
         __syncthreads();
     }
 }
 
-// --------------------------------------------------------------- dense path --
+// --------------------------------------------------------- dense tier --
 // Exact O(n) per node with a dense word per partner.  Reads/writes go
 // through agent-scope atomics so the block never sees stale L1 lines.
-template <bool EMIT>
-__global__ __launch_bounds__(256) void snn_dense_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp,
-    const int64_t* __restrict__ hoff, const int2* __restrict__ hosts, const int* __restrict__ ov_list,
-    const int* __restrict__ ov_count, unsigned* __restrict__ dense_all, int64_t* __restrict__ cnt,
-    SnnOut out) {
+__global__ __launch_bounds__(256) void snn_dense_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                        SnnSpec sp, const int64_t* __restrict__ hoff,
+                                                        const int2* __restrict__ hosts,
+                                                        const int* __restrict__ ov_list,
+                                                        const int* __restrict__ ov_count,
+                                                        unsigned* __restrict__ dense_all, int64_t* __restrict__ cnt,
+                                                        SnnRows rows) {
     __shared__ int64_t wsum[4];
     unsigned* dense = dense_all + (int64_t)blockIdx.x * n;
     const int nov = *ov_count;
     const int kmax = sp.kk[sp.nk - 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bool write = rows.roff[n] <= rows.cap;
     for (int f = blockIdx.x; f < nov; f += gridDim.x) {
         const int64_t j = ov_list[f];
         for (int64_t p = j + 1 + threadIdx.x; p < n; p += 256)
@@ -997,52 +896,174 @@ __global__ __launch_bounds__(256) void snn_dense_kernel(
             }
         }
         __syncthreads();
-        for (int t = 0; t < sp.nk; ++t) {
-            int64_t base = EMIT ? cnt[(int64_t)t * (n + 1) + j] : 0;
-            int64_t total = 0;
-            for (int64_t p0 = j + 1; p0 < n; p0 += 256) {
-                const int64_t p = p0 + threadIdx.x;
-                const unsigned v = (p < n) ? __hip_atomic_load(&dense[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : sp.init;
-                const bool hit = (p < n) && graph_has(sp, v, t);
-                const unsigned long long m = __ballot(hit);
-                if (lane == 0) wsum[wv] = __popcll(m);
-                __syncthreads();
-                int64_t before = 0, tot = 0;
-                for (int w = 0; w < 4; ++w) {
-                    if (w < wv) before += wsum[w];
-                    tot += wsum[w];
+        // the row: partners of the union graph (the largest k) in ascending p
+        const int64_t ro = rows.roff[j];
+        const int tu = sp.nk - 1;
+        int64_t total = 0;
+        int64_t c[SNN_MAXK] = {0, 0, 0, 0};
+        for (int64_t p0 = j + 1; p0 < n; p0 += 256) {
+            const int64_t p = p0 + threadIdx.x;
+            const unsigned v = (p < n) ? __hip_atomic_load(&dense[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : sp.init;
+            const bool hit = (p < n) && graph_has(sp, v, tu);
+            const unsigned long long m = __ballot(hit);
+            if (lane == 0) wsum[wv] = __popcll(m);
+            __syncthreads();
+            int64_t before = 0, tot = 0;
+            for (int w = 0; w < 4; ++w) {
+                if (w < wv) before += wsum[w];
+                tot += wsum[w];
+            }
+            if (hit) {
+                const int64_t e = ro + total + before + __popcll(m & lanemask_lt());
+                if (write) {
+                    rows.nbr[e] = (int32_t)p;
+                    rows.wpk[e] = v;
                 }
-                if (EMIT && hit) {
-                    const int64_t e = base + total + before + __popcll(m & lanemask_lt());
-                    if (e < out.cap[t]) {
-                        out.oi[t][e] = (int32_t)j;
-                        out.oj[t][e] = (int32_t)p;
-                        out.ow[t][e] = graph_weight(sp, v, t);
+#pragma unroll
+                for (int t = 0; t < SNN_MAXK; ++t)
+                    if (t < sp.nk && graph_has(sp, v, t)) ++c[t];
+            }
+            total += tot;
+            __syncthreads();
+        }
+#pragma unroll
+        for (int t = 0; t < SNN_MAXK; ++t) {
+            int64_t v = c[t];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) wsum[wv] = v;
+            __syncthreads();
+            if (threadIdx.x == 0 && t < sp.nk) cnt[(int64_t)t * (n + 1) + j] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) rows.rlen[j] = (int32_t)total;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------- per-graph edge lists --
+// Graph t's edges of node j are the row entries with byte t present, already
+// in ascending partner order; off_t = exclusive scan of the per-graph counts.
+__global__ __launch_bounds__(256) void snn_emit_kernel(int64_t n, SnnSpec sp, const int64_t* __restrict__ off,
+                                                       SnnRows rows, SnnOut out) {
+    const int lane = threadIdx.x & 63;
+    if (rows.roff[n] > rows.cap) return;  // rows were not written (reported through the totals)
+    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+        const int u = rows.rlen[j];
+        const int64_t ro = rows.roff[j];
+        for (int t = 0; t < sp.nk; ++t) {
+            if (out.cap[t] <= 0) continue;
+            int64_t e = off[(int64_t)t * (n + 1) + j];
+            for (int c0 = 0; c0 < u; c0 += 64) {
+                const int c = c0 + lane;
+                const unsigned v = c < u ? rows.wpk[ro + c] : sp.init;
+                const bool has = c < u && graph_has(sp, v, t);
+                const unsigned long long m = __ballot(has);
+                if (has) {
+                    const int64_t pos = e + __popcll(m & lanemask_lt());
+                    if (pos < out.cap[t]) {
+                        out.oi[t][pos] = (int32_t)j;
+                        out.oj[t][pos] = rows.nbr[ro + c];
+                        out.ow[t][pos] = graph_weight(sp, v, t);
                     }
                 }
-                total += tot;
-                __syncthreads();
+                e += __popcll(m);
             }
-            if (!EMIT && threadIdx.x == 0) cnt[(int64_t)t * (n + 1) + j] = total;
-            __syncthreads();
         }
     }
 }
 
-__global__ void snn_mark_kernel(const int* __restrict__ list, const int* __restrict__ count,
-                                int* __restrict__ flag) {
-    const int nl = *count;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) flag[list[i]] = 1;
-}
-
-__global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int nk, int64_t* d0, int64_t* d1,
-                                int64_t* d2, int64_t* d3) {
+// Totals per graph; -(required row capacity) when the rows did not fit.
+__global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int nk, const int64_t* __restrict__ roff,
+                                int64_t rcap, int64_t* d0, int64_t* d1, int64_t* d2, int64_t* d3) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int64_t* ds[4] = {d0, d1, d2, d3};
+    const bool fit = roff[n] <= rcap;
     for (int t = 0; t < nk; ++t)
-        if (ds[t]) *ds[t] = cnt[(int64_t)t * (n + 1) + n];
+        if (ds[t]) *ds[t] = fit ? cnt[(int64_t)t * (n + 1) + n] : -roff[n];
 }
+
+// --------------------------------------------------------------- driver --
+static int snn_spec(const int* ks, int nk, int type, int kstride, SnnSpec* sp) {
+    CCG_REQUIRE(ks, "SNN: NULL ks");
+    CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "SNN: 1 <= nk <= %d", SNN_MAXK);
+    CCG_REQUIRE(type == CCG_SNN_NUMBER || type == CCG_SNN_RANK, "SNN: bad type");
+    sp->nk = nk;
+    sp->type = type;
+    sp->init = type == CCG_SNN_NUMBER ? 0u : 0xFFFFFFFFu;
+    for (int t = 0; t < SNN_MAXK; ++t) sp->kk[t] = t < nk ? ks[t] : 0;
+    for (int t = 0; t < nk; ++t)
+        CCG_REQUIRE(ks[t] >= 1 && ks[t] <= kstride && ks[t] <= 32 && (t == 0 || ks[t] > ks[t - 1]),
+                    "SNN: ks must be ascending in [1, min(kstride, 32)]");
+    return CCG_OK;
+}
+
+// Builds the node rows (union graph) and per-graph counts; on return
+// cnt[t][0..n] holds their exclusive scans (graph t's edge offsets and total).
+// roff: n+1 row offsets (capacity-based), from the workspace when NULL.
+static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const SnnSpec& sp, hipStream_t st,
+                     int32_t* nbr, uint32_t* wpk, int64_t cap, int64_t* roff, int32_t* rlen, int64_t** cnt_out,
+                     const int64_t** roff_out) {
+    const int kmax = sp.kk[sp.nk - 1];
+    const int64_t nkk = n * kmax;
+    CCG_REQUIRE(nkk < (1LL << 31) - 1, "SNN: n*kmax too large");
+    int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
+    int2* hosts_s = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (nkk + 1));
+    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * sp.nk * (n + 1));
+    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (3 * n + 64));
+    unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
+    int32_t* pairs = (int32_t*)ccg_ws(ctx, WS_SNN_F, sizeof(int32_t) * 4 * (nkk + 16));
+    int* bp = (int*)ccg_ws(ctx, WS_SNN_G, sizeof(int) * (nkk + n + 64));
+    if (!hoff || !hosts_s || !cnt || !ov || !dense || !pairs || !bp) return CCG_ENOMEM;
+    int* split = bp + nkk;
+    int32_t* keys = pairs;
+    int32_t* vals = pairs + (nkk + 16);
+    int32_t* skey = vals + (nkk + 16);
+    int32_t* sval = skey + (nkk + 16);
+    int* ova_list = ov;
+    int* ov_list = ov + n;
+    int* ov2_list = ov + 2 * n;
+    int* ov_count = ov + 3 * n;  // [0] hash tier, [1] block tier, [2] dense tier
+    if (!roff) roff = hoff + (n + 1);
+    // 1. host lists
+    int bits = 1;
+    while ((1LL << bits) <= n) ++bits;
+    snn_pairs_kernel<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, keys, vals, ctx->d_err);
+    int rc = ccg_sort_pairs_i32(ctx, keys, skey, vals, sval, nkk, bits, st);
+    if (rc) return rc;
+    snn_hoff_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(skey, nkk, n, hoff);
+    snn_hosts_kernel<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(skey, sval, kmax, hoff, n, hosts_s, bp);
+    snn_split_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(hoff, hosts_s, n, split);
+    // 2. row capacities
+    const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
+    snn_items_kernel<<<nblk, 256, 0, st>>>(knn, n, kstride, kmax, hoff, bp, split, roff);
+    rc = ccg_scan_i64(ctx, roff, roff, n, st);
+    if (rc) return rc;
+    // 3. build: sort tier -> hash tier -> block tier -> dense tier
+    SnnRows rows{roff, rlen, nbr, wpk, cap};
+    CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
+    CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * sp.nk * (n + 1), st));
+    snn_sort_build_kernel<<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
+                                                          ova_list, ov_count);
+    snn_wave_build_kernel<SNN_WT><<<1024, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split,
+                                                                   cnt, rows, ova_list, ov_count, ov_list,
+                                                                   ov_count + 1);
+    snn_block_kernel<<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list, ov_count + 1,
+                                          ov2_list, ov_count + 2);
+    snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,
+                                                       dense, cnt, rows);
+    for (int t = 0; t < sp.nk; ++t) {
+        rc = ccg_scan_i64(ctx, cnt + (int64_t)t * (n + 1), cnt + (int64_t)t * (n + 1), n, st);
+        if (rc) return rc;
+    }
+    *cnt_out = cnt;
+    *roff_out = roff;
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+// Default row reservation of the per-graph API: entries per node per (kmax + 1).
+#define SNN_ROW_RESERVE 40
 
 extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks,
                                  int nk, int type, int32_t* const* out_i, int32_t* const* out_j,
@@ -1050,23 +1071,17 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
                                  void* stream) {
     CCG_REQUIRE(ctx && knn && ks && d_nedges, "ccg_snn_multi_dev: NULL argument");
     CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1, "ccg_snn_multi_dev: bad n");
-    CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "ccg_snn_multi_dev: 1 <= nk <= %d", SNN_MAXK);
-    CCG_REQUIRE(type == CCG_SNN_NUMBER || type == CCG_SNN_RANK, "ccg_snn_multi_dev: bad type");
     SnnSpec sp;
-    sp.nk = nk;
-    sp.type = type;
-    sp.init = type == CCG_SNN_NUMBER ? 0u : 0xFFFFFFFFu;
+    int rc = snn_spec(ks, nk, type, kstride, &sp);
+    if (rc) return rc;
     SnnOut out;
     for (int t = 0; t < SNN_MAXK; ++t) {
-        sp.kk[t] = t < nk ? ks[t] : 0;
         out.cap[t] = 0;
         out.oi[t] = nullptr;
         out.oj[t] = nullptr;
         out.ow[t] = nullptr;
     }
     for (int t = 0; t < nk; ++t) {
-        CCG_REQUIRE(ks[t] >= 1 && ks[t] <= kstride && ks[t] <= 32 && (t == 0 || ks[t] > ks[t - 1]),
-                    "ccg_snn_multi_dev: ks must be ascending in [1, min(kstride, 32)]");
         out.cap[t] = caps ? caps[t] : 0;
         if (out.cap[t] > 0) {
             CCG_REQUIRE(out_i && out_j && out_w && out_i[t] && out_j[t] && out_w[t],
@@ -1078,76 +1093,57 @@ extern "C" int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, in
     }
     const int kmax = ks[nk - 1];
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
-    int2* hosts = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * 2 * (n * kmax + 1));
-    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * nk * (n + 1));
-    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (5 * n + 64));
-    unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
-    unsigned long long* scratch =
-        (unsigned long long*)ccg_ws(ctx, WS_SNN_F, sizeof(unsigned long long) * n * SNN_WCAP + sizeof(int) * (n + 64));
-    int* bp = (int*)ccg_ws(ctx, WS_SNN_G, sizeof(int) * (n * kmax + n + 64));
-    if (!hoff || !hosts || !cnt || !ov || !dense || !scratch || !bp) return CCG_ENOMEM;
-    int2* hosts_s = hosts + (n * kmax + 1);
-    int* split = bp + n * kmax;
-    int* ucount = (int*)(scratch + n * SNN_WCAP);
-    unsigned long long* cursor = (unsigned long long*)(hoff + (n + 1));
-    int* err = ctx->d_err;
-    int* ov_list = ov;  // nodes for the block path (overflowed both wave tiers)
-    int* ov2_list = ov + n;
-    int* flag1 = ov + 2 * n;
-    int* flag2 = ov + 3 * n;
-    int* ova_list = ov + 4 * n;  // more than 1024 items -> 2048-slot hash tier
-    int* ov_count = ov + 5 * n;
-    int* ov2_count = ov_count + 1;
-    int* ova_count = ov_count + 2;
-    const int64_t nkk = (int64_t)n * kmax;
     const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
-    CCG_HIP(hipMemsetAsync(hoff, 0, sizeof(int64_t) * (n + 1), st));
-    CCG_HIP(hipMemsetAsync(flag1, 0, sizeof(int) * 2 * n, st));
-    CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
-    CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * nk * (n + 1), st));
-    snn_count_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax,
-                                                                  (unsigned long long*)hoff, err);
-    int rc = ccg_scan_i64(ctx, hoff, hoff, n, st);
+    const int64_t rcap =
+        ctx->snn_row_reserve > 0 ? ctx->snn_row_reserve : (int64_t)SNN_ROW_RESERVE * n * (kmax + 1);
+    char* rbuf =
+        (char*)ccg_ws(ctx, WS_SNN_ROWS, (sizeof(int32_t) + sizeof(uint32_t)) * rcap + sizeof(int32_t) * (n + 64));
+    if (!rbuf) return CCG_ENOMEM;
+    int32_t* nbr = (int32_t*)rbuf;
+    uint32_t* wpk = (uint32_t*)(nbr + rcap);
+    int32_t* rlen = (int32_t*)(wpk + rcap);
+    int64_t* cnt = nullptr;
+    const int64_t* roff = nullptr;
+    rc = snn_build(ctx, knn, n, kstride, sp, st, nbr, wpk, rcap, nullptr, rlen, &cnt, &roff);
     if (rc) return rc;
-    CCG_HIP(hipMemcpyAsync(cursor, hoff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
-    snn_fill_hosts<<<(unsigned)ccg_cdiv(nkk, 256), 256, 0, st>>>(knn, n, kstride, kmax, cursor, hosts);
-    snn_sort_hosts<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(hoff, n, kmax, hosts,
-                                                                                      hosts_s, bp, split);
-    const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
-    // pass 1: per-graph counts (sort tier for nodes with <= 1024 items, 2048-slot hash tables,
-    // then block tables, then dense)
-    snn_sort_build_kernel<1024><<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
-                                                                 nullptr, nullptr, ova_list, ova_count, scratch,
-                                                                 ucount);
-    const unsigned nblk2 = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 1024);
-    snn_wave_build_kernel<2048><<<nblk2, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt,
-                                                                  ova_list, ova_count, ov_list, ov_count, scratch,
-                                                                  ucount);
-    snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, ov_list, ov_count,
-                                                 ov2_list, ov2_count, flag2, out);
-    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
-                                                             ov2_count, dense, cnt, out);
-    snn_mark_kernel<<<64, 256, 0, st>>>(ov_list, ov_count, flag1);
-    snn_mark_kernel<<<64, 256, 0, st>>>(ov2_list, ov2_count, flag2);
-    for (int t = 0; t < nk; ++t) {
-        rc = ccg_scan_i64(ctx, cnt + (int64_t)t * (n + 1), cnt + (int64_t)t * (n + 1), n, st);
-        if (rc) return rc;
-    }
     bool any_cap = false;
     for (int t = 0; t < nk; ++t) any_cap |= out.cap[t] > 0;
     if (any_cap) {
-        snn_wave_emit_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(
-            n, sp, cnt, flag1, scratch, ucount, out);
-        snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, ov_list, ov_count,
-                                                    ov2_list, ov2_count, flag2, out);
-        snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
-                                                                ov2_count, dense, cnt, out);
+        SnnRows rows{roff, rlen, nbr, wpk, rcap};
+        snn_emit_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384), 256, 0, st>>>(n, sp, cnt, rows, out);
     }
-    snn_copy_totals<<<1, 64, 0, st>>>(cnt, n, nk, d_nedges[0], nk > 1 ? d_nedges[1] : nullptr,
+    snn_copy_totals<<<1, 64, 0, st>>>(cnt, n, nk, roff, rcap, d_nedges[0], nk > 1 ? d_nedges[1] : nullptr,
                                       nk > 2 ? d_nedges[2] : nullptr, nk > 3 ? d_nedges[3] : nullptr);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+extern "C" int ccg_snn_rows_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk,
+                                int type, int64_t* row_off, int32_t* row_len, int32_t* nbr, uint32_t* wpk,
+                                int64_t cap, int64_t* d_nedges, void* stream) {
+    CCG_REQUIRE(ctx && knn && ks && row_off && row_len && d_nedges, "ccg_snn_rows_dev: NULL argument");
+    CCG_REQUIRE(cap == 0 || (nbr && wpk), "ccg_snn_rows_dev: NULL rows with cap > 0");
+    CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1, "ccg_snn_rows_dev: bad n");
+    SnnSpec sp;
+    int rc = snn_spec(ks, nk, type, kstride, &sp);
+    if (rc) return rc;
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
+    int64_t* cnt = nullptr;
+    const int64_t* roff = nullptr;
+    rc = snn_build(ctx, knn, n, kstride, sp, st, nbr, wpk, cap, row_off, row_len, &cnt, &roff);
+    if (rc) return rc;
+    snn_copy_totals<<<1, 64, 0, st>>>(cnt, n, nk, roff, cap, d_nedges, nk > 1 ? d_nedges + 1 : nullptr,
+                                      nk > 2 ? d_nedges + 2 : nullptr, nk > 3 ? d_nedges + 3 : nullptr);
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+extern "C" int ccg_snn_reserve(ccg_ctx* ctx, int64_t entries) {
+    CCG_REQUIRE(ctx && entries >= 0, "ccg_snn_reserve: bad argument");
+    ctx->snn_row_reserve = entries;
     return CCG_OK;
 }
 
@@ -1179,11 +1175,16 @@ extern "C" int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
     double* dw = cap > 0 ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * cap) : nullptr;
     if (!dknn || !dne || (cap > 0 && (!di || !dj || !dw))) return CCG_ENOMEM;
     CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
-    int rc = ccg_snn_dev(ctx, dknn, n, kstride, k, type, di, dj, dw, cap, dne, st);
-    if (rc) return rc;
     int64_t ne = 0;
-    CCG_HIP(hipMemcpyAsync(&ne, dne, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    CCG_HIP(hipStreamSynchronize(st));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        int rc = ccg_snn_dev(ctx, dknn, n, kstride, k, type, di, dj, dw, cap, dne, st);
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(&ne, dne, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        if (ne >= 0) break;
+        ctx->snn_row_reserve = -ne + (-ne) / 8;  // rows did not fit the reservation: grow and rerun
+    }
+    CCG_REQUIRE(ne >= 0, "ccg_snn: row reservation could not be satisfied");
     *nedges = ne;
     if (ne > cap) {
         ccg_set_error("ccg_snn: capacity %lld < required %lld edges", (long long)cap, (long long)ne);

@@ -256,6 +256,21 @@ class Engine:
         check(self.lib.ccg_snn_multi_dev(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, oi, oj, ow, caps, dn,
                                          _stream()))
 
+    def snn_rows_t(self, knn_idx, ks, type, row_off, row_len, nbr, wpk, d_nedges):
+        """All graphs of ks as rows of the union graph (ccg_snn_rows_dev):
+        row_off (n+1,) int64, row_len (n,) int32, nbr / wpk (cap,) int32 /
+        uint32-as-int32 tensors, d_nedges (len(ks),) int64 (negative =
+        -required capacity)."""
+        n, kst = knn_idx.shape
+        nk = len(ks)
+        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        karr = (ctypes.c_int * nk)(*ks)
+        check(self.lib.ccg_snn_rows_dev(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, _ptr(row_off), _ptr(row_len),
+                                        _ptr(nbr), _ptr(wpk), nbr.numel(), _ptr(d_nedges), _stream()))
+
+    def snn_reserve(self, entries):
+        check(self.lib.ccg_snn_reserve(self.ctx, entries))
+
     def silhouette_t(self, x, labels, cmax, out_mean, out_nclust, out_minsize, out_width=None):
         m, d = x.shape
         L = labels.shape[0]

@@ -146,7 +146,8 @@ int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k,
 
 /* Device flavour: writes min(E, cap) edges and E to *d_nedges (device
  * int64); no host synchronisation.  If E > cap the caller re-runs with a
- * larger cap. */
+ * larger cap; a negative *d_nedges means the row reservation
+ * (ccg_snn_reserve) was too small. */
 int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                 int k, int type, int32_t* out_i, int32_t* out_j,
                 double* out_w, int64_t cap, int64_t* d_nedges, void* stream);
@@ -160,6 +161,27 @@ int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n,
                       int32_t* const* out_i, int32_t* const* out_j,
                       double* const* out_w, const int64_t* caps,
                       int64_t* const* d_nedges, void* stream);
+
+/* The same graphs as rows (CSR of the union graph = the largest k, built in
+ * one pass): row j = partners p > j of node j in ascending order,
+ * nbr[row_off[j] .. row_off[j] + row_len[j]) with wpk = per-graph packed
+ * values (byte t: NUMBER count / RANK rank sum r of graph ks[t]; absent =
+ * 0 / 0xFF; weight = count or max(ks[t] - r/2, 1e-6)).  Row capacities are
+ * the node's item counts, so row_off (device int64, n+1) is capacity-based
+ * and row_len (device int32, n) gives the used length.  d_nedges[t] (device
+ * int64, nk entries) receives graph t's edge count, or -(required row
+ * capacity) when it exceeds cap (rows are then not written; rerun with a
+ * larger cap).  No host synchronisation.  This is the compact form a caller
+ * hands to host clustering (8 B per union edge instead of 16 B per edge per
+ * graph). */
+int ccg_snn_rows_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
+                     const int* ks, int nk, int type, int64_t* row_off,
+                     int32_t* row_len, int32_t* nbr, uint32_t* wpk, int64_t cap,
+                     int64_t* d_nedges, void* stream);
+/* Row entries the per-graph functions reserve in the context workspace
+ * (0 = the default 40 n (kmax+1)); ccg_snn grows it on demand, the _dev
+ * functions report -(required) in d_nedges instead. */
+int ccg_snn_reserve(ccg_ctx* ctx, int64_t entries);
 
 /* --------------------------------------------------------- silhouette -- */
 /* mean(approxSilhouette(x, labels_l)[,3], na.rm=TRUE) for L label vectors

@@ -262,3 +262,66 @@ def test_silhouette_many_clusters_vs_oracle(engine, m, d, C):
         ok = ~np.isnan(ow)
         assert np.array_equal(np.isnan(w[l_]), ~ok)
         np.testing.assert_allclose(w[l_][ok], ow[ok], rtol=RTOL, atol=1e-9)
+
+
+# ------------------------------------------------------------ SNN rows --
+def _rows_to_graphs(off, ln, nbr, wpk, ks, t):
+    out = []
+    for g, k in enumerate(ks):
+        ei, ej, w = [], [], []
+        for j in range(ln.size):
+            for c in range(off[j], off[j] + ln[j]):
+                b = (int(wpk[c]) >> (8 * g)) & 0xFF
+                if (b != 0) if t == "number" else (b != 0xFF):
+                    ei.append(j)
+                    ej.append(nbr[c])
+                    w.append(float(b) if t == "number" else max(k - 0.5 * b, 1e-6))
+        out.append((np.array(ei, np.int32), np.array(ej, np.int32), np.array(w)))
+    return out
+
+
+@pytest.mark.parametrize("t", ["number", "rank"])
+def test_snn_rows_match_per_graph_edges(engine, t):
+    """The compact union-graph rows (ccg_snn_rows_dev) carry every graph of
+    kNum with the same edges and weights as the per-graph lists."""
+    import torch
+    rng = np.random.default_rng(33)
+    X = _mixture(rng, 6000, 12)
+    X[:600] = X[600:1200]  # duplicates
+    idx, _ = engine.knn_boot(X, np.arange(6000), kmax=20)
+    n = idx.shape[1]
+    knn_t = torch.from_numpy(idx[0]).cuda()
+    ks = (10, 15, 20)
+    off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    ln = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cap = n * 400
+    nbr = torch.empty(cap, dtype=torch.int32, device="cuda")
+    wpk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    ne = torch.zeros(3, dtype=torch.int64, device="cuda")
+    engine.snn_rows_t(knn_t, ks, t, off, ln, nbr, wpk, ne)
+    torch.cuda.synchronize()
+    got = _rows_to_graphs(off.cpu().numpy(), ln.cpu().numpy(), nbr.cpu().numpy(),
+                          wpk.cpu().numpy().view(np.uint32), ks, t)
+    for g, k in enumerate(ks):
+        ref = O.snn(idx[0], k, t)
+        assert ne[g].item() == ref[0].size
+        for a, b in zip(got[g], ref):
+            assert np.array_equal(a, b)
+    # too small a capacity: rows are not written, the totals report -(required)
+    ne2 = torch.zeros(3, dtype=torch.int64, device="cuda")
+    engine.snn_rows_t(knn_t, ks, t, off, ln, nbr[:100], wpk[:100], ne2)
+    torch.cuda.synchronize()
+    assert ne2[0].item() < 0 and -ne2[0].item() == off[-1].item()
+
+
+def test_snn_host_flavour_grows_row_reservation(engine):
+    rng = np.random.default_rng(34)
+    X = _mixture(rng, 3000, 8)
+    idx, _ = engine.knn_boot(X, np.arange(3000), kmax=20)
+    engine.snn_reserve(1000)  # far too small for the default-sized per-graph path...
+    try:
+        a = engine.snn(idx[0], 20, "number")  # ...the host flavour grows it and reruns
+    finally:
+        engine.snn_reserve(0)
+    for x, y in zip(a, O.snn(idx[0], 20, "number")):
+        assert np.array_equal(x, y)
