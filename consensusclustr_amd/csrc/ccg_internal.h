@@ -22,6 +22,7 @@ enum ccg_ws_slot {
     WS_SNN_E,        // SNN per-node counts / flags
     WS_SNN_F,        // SNN sorted per-node partner rows (scratch)
     WS_SNN_G,        // SNN host back-pointers and per-node splits
+    WS_SNN_H,        // SNN node size classes (scan)
     WS_SIL_A,        // silhouette accumulators
     WS_SIL_B,        // silhouette centroids
     WS_COC_A,        // co-cluster column tables

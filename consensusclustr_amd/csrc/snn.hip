@@ -254,10 +254,11 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
 // stage merges equal partners and writes the row.  R is chosen per node
 // (4, 8, 12 or 16 rounds of 64 items) so a node pays for its own size only.
 #define SNN_SNB 240   // buckets
-#define SNN_SI 1024   // items staged per wave
+#define SNN_SI 1024   // items staged per wave (largest sort-tier node)
 
+template <int SI>
 struct SnnSortLds {
-    unsigned long long stage[SNN_SI];
+    unsigned long long stage[SI];
     union {
         struct {  // gather phase: member headers
             long long h0[64];
@@ -272,26 +273,30 @@ struct SnnSortLds {
     } u;
 };
 
-template <int R>
-__device__ __forceinline__ void snn_sort_node(SnnSortLds& L, const SnnSpec& sp, int64_t n, int64_t j, int M,
-                                              int lane, const int2* __restrict__ hosts_s, const SnnRows& rows,
-                                              int64_t* __restrict__ cnt) {
+template <int R, int SI>
+__device__ __forceinline__ void snn_sort_node(SnnSortLds<SI>& L, const SnnSpec& sp, int64_t n, int64_t j, int M,
+                                              int lane, const int2* __restrict__ hosts_s,
+                                              const SnnRows& rows, int64_t* __restrict__ cnt) {
     unsigned long long* stage = L.stage;
-    // gather: every host load of the node is issued before any is used
-    int2 hr[R];
-    int im[R];
+    // gather: every host load of the node is issued before any is used;
+    // item r is held as (p << 32 | member << 8 | host rank) until its
+    // contribution is known, then as (p << 32 | packed contribution)
+    unsigned long long e[R];
     int mi = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int t = 64 * r + lane;
-        im[r] = -1;
-        hr[r] = make_int2(-1, 0);
+        e[r] = ~0ull;
         if (t < M) {
             while (L.u.g.pre[mi + 1] <= t) ++mi;
-            im[r] = mi;
             const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
-            if (q < L.u.g.hend[mi]) hr[r] = hosts_s[q];
-            else hr[r] = make_int2(L.u.g.cur[mi], 0);
+            int p = L.u.g.cur[mi], rp = 0;
+            if (q < L.u.g.hend[mi]) {
+                const int2 h = hosts_s[q];
+                p = h.x;
+                rp = h.y;
+            }
+            e[r] = ((unsigned long long)(unsigned)p << 32) | (unsigned)(mi << 8) | (unsigned)rp;
         }
     }
     WAVE_LDS_SYNC();
@@ -300,18 +305,20 @@ __device__ __forceinline__ void snn_sort_node(SnnSortLds& L, const SnnSpec& sp, 
     for (int b = lane; b < SNN_SNB; b += 64) hist[b] = 0;
     WAVE_LDS_SYNC();
     const float inv = (float)SNN_SNB / (float)(n - j);
-    unsigned long long e[R];
     int bk[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        e[r] = ~0ull;
         bk[r] = -1;
-        if (im[r] >= 0) {
-            const unsigned c = snn_contrib(sp, im[r], hr[r].y);
+        if (e[r] != ~0ull) {
+            const unsigned lo = (unsigned)e[r];
+            const unsigned c = snn_contrib(sp, (int)(lo >> 8), (int)(lo & 0xFFu));
+            const int p = (int)(e[r] >> 32);
             if (c != sp.init) {
-                e[r] = ((unsigned long long)(unsigned)hr[r].x << 32) | c;
-                bk[r] = min(SNN_SNB - 1, (int)((float)(hr[r].x - (int)j - 1) * inv));
+                e[r] = ((unsigned long long)(unsigned)p << 32) | c;
+                bk[r] = min(SNN_SNB - 1, (int)((float)(p - (int)j - 1) * inv));
                 atomicAdd(&hist[bk[r]], 1);
+            } else {
+                e[r] = ~0ull;
             }
         }
     }
@@ -412,41 +419,86 @@ __device__ __forceinline__ void snn_sort_node(SnnSortLds& L, const SnnSpec& sp, 
     if (lane == 0) rows.rlen[j] = u;
 }
 
-__global__ __launch_bounds__(64 * SNN_WAVES, 4) void snn_sort_build_kernel(
+// Three size classes, each its own kernel over its own node list (built by a
+// scan, so in ascending node order): CLS 0 sorts the nodes with <= 320 items
+// (R = 3 or 5), CLS 1 those with 321..640 (R = 8 or 10), CLS 2 641..1024
+// (R = 12 or 16).  The LDS stage is sized to the class, so small nodes --
+// the majority -- run at more waves per SIMD to hide the gather latency.  One
+// node per wave: no node loop whose invariants the compiler would hoist into
+// the item registers.
+template <int CLS>
+__global__ __launch_bounds__(64 * SNN_WAVES, CLS == 0 ? 8 : (CLS == 1 ? 6 : 4)) void snn_sort_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, SnnRows rows, int* __restrict__ ov_list, int* __restrict__ ov_count) {
-    __shared__ SnnSortLds lds_all[SNN_WAVES];
+    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ list, const int64_t* __restrict__ count) {
+    constexpr int SI = CLS == 0 ? 320 : (CLS == 1 ? 640 : 1024);
+    __shared__ SnnSortLds<SI> lds_all[SNN_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    SnnSortLds& L = lds_all[wv];
+    SnnSortLds<SI>& L = lds_all[wv];
     const int kmax = sp.kk[sp.nk - 1];
-    for (int64_t j = (int64_t)blockIdx.x * SNN_WAVES + wv; j < n; j += (int64_t)gridDim.x * SNN_WAVES) {
-        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
-        int incl = m.len;
+    const int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv;
+    if (f >= *count) return;
+    const int64_t j = list[f];
+    const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+    int incl = m.len;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        const int M = __shfl(incl, 63);
-        if (M > SNN_SI) {
-            if (lane == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
-            continue;
-        }
-        if (lane <= kmax) {
-            L.u.g.pre[lane] = incl - m.len;
-            L.u.g.h0[lane] = m.h0;
-            L.u.g.hend[lane] = m.hend;
-            L.u.g.cur[lane] = m.cur;
-        }
-        if (lane == 0) L.u.g.pre[kmax + 1] = M;
-        WAVE_LDS_SYNC();
-        if (M <= 256) snn_sort_node<4>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else if (M <= 512) snn_sort_node<8>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else if (M <= 768) snn_sort_node<12>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else snn_sort_node<16>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        WAVE_LDS_SYNC();
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
     }
+    const int M = __shfl(incl, 63);
+    if (lane <= kmax) {
+        L.u.g.pre[lane] = incl - m.len;
+        L.u.g.h0[lane] = m.h0;
+        L.u.g.hend[lane] = m.hend;
+        L.u.g.cur[lane] = m.cur;
+    }
+    if (lane == 0) L.u.g.pre[kmax + 1] = M;
+    WAVE_LDS_SYNC();
+    if (CLS == 0) {
+        if (M <= 192) snn_sort_node<3>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else snn_sort_node<5>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+    } else if (CLS == 1) {
+        if (M <= 512) snn_sort_node<8>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else snn_sort_node<10>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+    } else {
+        if (M <= 768) snn_sort_node<12>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+        else snn_sort_node<16>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
+    }
+}
+
+// Size class of every node from its capacity (items): packed one-hot counts
+// (class c in bits 21c..21c+20) for one scan that ranks every class at once.
+// Classes 0..2 in 21-bit fields (n < 2^21); class 3's rank is the node index
+// minus the other three.
+#define SNN_CLS_BITS 21
+__global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, int64_t* __restrict__ cls) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t M = roff[j + 1] - roff[j];
+    const int c = M <= 320 ? 0 : (M <= 640 ? 1 : (M <= SNN_SI ? 2 : 3));
+    cls[j] = c < 3 ? 1LL << (SNN_CLS_BITS * c) : 0;
+}
+
+// Lists of each class in node order; counts[c] = class size.
+__global__ void snn_class_scatter_kernel(const int64_t* __restrict__ cls_scan, int64_t n, int* __restrict__ lists,
+                                         int64_t* __restrict__ counts) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > n) return;
+    const int64_t mask = (1LL << SNN_CLS_BITS) - 1;
+    const int64_t v = cls_scan[j];
+    int64_t r[4];
+    r[0] = v & mask;
+    r[1] = (v >> SNN_CLS_BITS) & mask;
+    r[2] = (v >> (2 * SNN_CLS_BITS)) & mask;
+    r[3] = j - r[0] - r[1] - r[2];
+    if (j == n) {
+        for (int c = 0; c < 4; ++c) counts[c] = r[c];
+        return;
+    }
+    const int64_t d = cls_scan[j + 1] - v;  // this node's one-hot class (0 for class 3)
+    const int c = d == 1 ? 0 : (d == (1LL << SNN_CLS_BITS) ? 1 : (d == (1LL << (2 * SNN_CLS_BITS)) ? 2 : 3));
+    lists[c * n + r[c]] = (int)j;
 }
 
 // ---------------------------------------------------------- hash tier --
@@ -575,7 +627,7 @@ template <int WT>
 __global__ __launch_bounds__(64 * SNN_WAVES, 2) void snn_wave_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ in_list, const int* __restrict__ in_count,
+    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ in_list, const int64_t* __restrict__ in_count,
     int* __restrict__ ov_list, int* __restrict__ ov_count) {
     __shared__ SnnWaveLds<WT> lds_all[SNN_WAVES];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -583,8 +635,8 @@ __global__ __launch_bounds__(64 * SNN_WAVES, 2) void snn_wave_build_kernel(
     unsigned long long* tab = L.tab;
     const int kmax = sp.kk[sp.nk - 1];
     constexpr int CAP = WT * 3 / 4;
-    const int64_t nn = *in_count;
     const bool write = rows.roff[n] <= rows.cap;
+    const int64_t nn = *in_count;
     for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
         const int64_t j = in_list[f];
         for (int s = lane; s < WT; s += 64) tab[s] = SNN_EMPTY64;
@@ -1010,7 +1062,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
     int2* hosts_s = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (nkk + 1));
     int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * sp.nk * (n + 1));
-    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (3 * n + 64));
+    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (5 * n + 64));
     unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
     int32_t* pairs = (int32_t*)ccg_ws(ctx, WS_SNN_F, sizeof(int32_t) * 4 * (nkk + 16));
     int* bp = (int*)ccg_ws(ctx, WS_SNN_G, sizeof(int) * (nkk + n + 64));
@@ -1020,10 +1072,9 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     int32_t* vals = pairs + (nkk + 16);
     int32_t* skey = vals + (nkk + 16);
     int32_t* sval = skey + (nkk + 16);
-    int* ova_list = ov;
-    int* ov_list = ov + n;
-    int* ov2_list = ov + 2 * n;
-    int* ov_count = ov + 3 * n;  // [0] hash tier, [1] block tier, [2] dense tier
+    int* ov_list = ov + 3 * n;
+    int* ov2_list = ov + 4 * n;
+    int* ov_count = ov + 5 * n;  // [1] block tier, [2] dense tier
     if (!roff) roff = hoff + (n + 1);
     // 1. host lists
     int bits = 1;
@@ -1043,11 +1094,25 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     SnnRows rows{roff, rlen, nbr, wpk, cap};
     CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
     CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * sp.nk * (n + 1), st));
-    snn_sort_build_kernel<<<nblk, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
-                                                          ova_list, ov_count);
-    snn_wave_build_kernel<SNN_WT><<<1024, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split,
-                                                                   cnt, rows, ova_list, ov_count, ov_list,
-                                                                   ov_count + 1);
+    // size classes -> node lists (scan of packed one-hot class counts)
+    CCG_REQUIRE(n < (1LL << SNN_CLS_BITS), "SNN: n must be below 2^%d", SNN_CLS_BITS);
+    int64_t* cls = (int64_t*)ccg_ws(ctx, WS_SNN_H, sizeof(int64_t) * (n + 1 + 8) + sizeof(int) * 4 * n);
+    if (!cls) return CCG_ENOMEM;
+    int64_t* ccount = cls + (n + 1);
+    int* lists = (int*)(ccount + 8);
+    snn_class_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(roff, n, cls);
+    rc = ccg_scan_i64(ctx, cls, cls, n, st);
+    if (rc) return rc;
+    snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
+    const unsigned nsb = (unsigned)ccg_cdiv(n, SNN_WAVES);
+    snn_sort_build_kernel<0><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
+                                                             lists, ccount);
+    snn_sort_build_kernel<1><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
+                                                             lists + n, ccount + 1);
+    snn_sort_build_kernel<2><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
+                                                             lists + 2 * n, ccount + 2);
+    snn_wave_build_kernel<SNN_WT><<<(unsigned)std::min<int64_t>(nsb, 1024), 64 * SNN_WAVES, 0, st>>>(
+        knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + 3 * n, ccount + 3, ov_list, ov_count + 1);
     snn_block_kernel<<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list, ov_count + 1,
                                           ov2_list, ov_count + 2);
     snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,

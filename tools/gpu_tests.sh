@@ -4,7 +4,7 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 180 --timeout-method thread \
-    -rf ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+    -rf -k "${PYTEST_K:-not nothing}" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

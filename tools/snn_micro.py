@@ -14,6 +14,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from consensusclustr_amd import _lib  # noqa: E402
+if len(sys.argv) > 2 and sys.argv[1] == "--lib":  # tools only: time a variant build of libccg
+    _lib.LIB_PATH = os.path.abspath(sys.argv[2])
 import bench  # noqa: E402
 from consensusclustr_amd import Engine  # noqa: E402
 
