@@ -105,30 +105,47 @@ __device__ __forceinline__ float union_kth(const float (&lv)[KP]) {
 }
 
 // ------------------------------------------------- fp16 hi/lo screen --
-// Each value x (scaled by sigma = 2^e so max|x| <= 2^13) is split into
+// Each value x (scaled by sigma = 2^e so max|x| < 2^12) is split into
 // fp16 hi = rn(x) and lo = rn(x - hi); x.y ~ hi.hi + hi.lo + lo.hi with
 // |error| <= ~2^-22 |x||y| per product plus fp32 accumulation, i.e. fp32-class
-// accuracy from three v_mfma_f32_32x32x16_f16 (16 cycles/K-block each at
-// 16x the fp32 MFMA rate).  -|y|^2/2 enters as the accumulator init.
+// accuracy from three v_mfma_f32_32x32x16_f16 per 16 dims.  The reference
+// norm term rides in dimension d (the first padding dimension): the image
+// holds -|y|^2/2 / 2^KNN_NORM_SHIFT there (hi/lo split like any value) and the
+// query side 2^KNN_NORM_SHIFT, so the MFMA chain alone yields
+// v = x.y - |y|^2/2 from a zero accumulator (16 * KSTEPS >= d + 1).
 // Row image (64*KSTEPS bytes): for lane-half h in {0,1}: KSTEPS hi chunks
 // then KSTEPS lo chunks of 8 halves (dims 16s + 8h .. +7), so a lane reads
 // one contiguous 32*KSTEPS-byte run.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
-#define KNN_CHUNK 64   // refs per LDS stage (2 MFMA tiles)
-#define KNN_QCAP 12    // per-lane insertion queue slots (flush before a tile that would overflow)
+#define KNN_CHUNK 64        // refs per LDS stage (2 MFMA tiles)
+#define KNN_NBUF 3          // LDS stages in flight (prefetch distance 2 chunks)
+#define KNN_QCAP 12         // per-lane insertion queue slots (flush before a half tile that could overflow)
+#ifndef KNN_ENQ_BRANCHY
+#define KNN_ENQ_BRANCHY 0   // per-register exec-masked enqueue (1) or branch-free per half tile (0)
+#endif
+#define KNN_NORM_SHIFT 15   // the query's norm-dimension value 2^15 (exact in fp16)
+#define KNN_PAD_NORM (-65504.0f)  // padding rows: below every real value (|v| < 1.6e9 < 2^31)
 
 __device__ __forceinline__ int knn_scale_exp(const unsigned* maxabs_bits) {
     const float m = __uint_as_float(*maxabs_bits);
     if (!(m > 0.f)) return 0;
-    return 13 - (ilogbf(m) + 1);  // max|x| * 2^e < 2^13
+    return 12 - (ilogbf(m) + 1);  // max|x| * 2^e < 2^12, so |y|^2/2 / 2^15 < 2^14 for d <= 63
+}
+
+__device__ __forceinline__ void knn_split16(double xs, _Float16& hi, _Float16& lo) {
+    // parts below the smallest normal fp16 are flushed here, explicitly,
+    // so the certification floor (KNN_F16_FLOOR) holds in any denorm mode
+    hi = (_Float16)(float)xs;
+    if (fabs((double)(float)hi) < KNN_F16_FLOOR) hi = (_Float16)0.0f;
+    lo = (_Float16)(float)(xs - (double)(float)hi);
+    if (fabs((double)(float)lo) < KNN_F16_FLOOR) lo = (_Float16)0.0f;
 }
 
 template <int KSTEPS>
 __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, int64_t npad, int d,
                                   const unsigned* __restrict__ maxabs_bits, const int* __restrict__ perm,
-                                  uint4* __restrict__ img, float* __restrict__ nrm,
-                                  double* __restrict__ inv_scale2) {
+                                  uint4* __restrict__ img, double* __restrict__ inv_scale2) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in spatial order
     if (r >= npad) return;
     const int64_t src = r < n ? perm[r] : -1;  // -1: padding position (segment padding or r >= n)
@@ -137,20 +154,17 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
     if (r == 0) *inv_scale2 = ldexp(1.0, -2 * e);
     _Float16 hv[KSTEPS * 32];  // [h][hi s..][lo s..] flattened below
     double nr = 0.0;
+    for (int k = 0; k < d; ++k) {
+        const double x = valid ? rows[src * d + k] : 0.0;
+        nr += x * x;
+    }
 #pragma unroll
     for (int k = 0; k < KSTEPS * 16; ++k) {
         double xs = 0.0;
-        if (valid && k < d) {
-            const double x = rows[src * d + k];
-            nr += x * x;
-            xs = ldexp(x, e);
-        }
-        // parts below the smallest normal fp16 are flushed here, explicitly,
-        // so the certification floor (KNN_F16_FLOOR) holds in any denorm mode
-        _Float16 hi = (_Float16)(float)xs;
-        if (fabs((double)(float)hi) < KNN_F16_FLOOR) hi = (_Float16)0.0f;
-        _Float16 lo = (_Float16)(float)(xs - (double)(float)hi);
-        if (fabs((double)(float)lo) < KNN_F16_FLOOR) lo = (_Float16)0.0f;
+        if (k < d) xs = valid ? ldexp(rows[src * d + k], e) : 0.0;
+        else if (k == d) xs = valid ? -0.5 * ldexp(nr, 2 * e - KNN_NORM_SHIFT) : (double)KNN_PAD_NORM;
+        _Float16 hi, lo;
+        knn_split16(xs, hi, lo);
         const int s = k / 16, h = (k % 16) / 8, j = k % 8;
         hv[h * (KSTEPS * 16) + s * 8 + j] = hi;
         hv[h * (KSTEPS * 16) + KSTEPS * 8 + s * 8 + j] = lo;
@@ -158,7 +172,6 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
     uint4* out = img + r * (KSTEPS * 4);
 #pragma unroll
     for (int c = 0; c < KSTEPS * 4; ++c) out[c] = *reinterpret_cast<const uint4*>(&hv[c * 8]);
-    nrm[r] = valid ? (float)(-0.5 * ldexp(nr, 2 * e)) : -INFINITY;
 }
 
 template <int KSTEPS>
@@ -297,35 +310,41 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
     return x * q + min(x, r) + i;
 }
 
+// s_waitcnt vmcnt(N) for a compile-time N (the LDS-DMA is issued as inline
+// asm, so the compiler does not track it).
+template <int N>
+__device__ __forceinline__ void knn_wait_vmcnt() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else static_assert(N == 0, "unsupported vmcnt");
+}
+
 template <int KSTEPS, int KP, int QC = KNN_QCAP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(const uint4* __restrict__ img,
-                                                           const float* __restrict__ nrm, int n, int nchunks,
-                                                           int* __restrict__ cand_idx,
-                                                           float* __restrict__ cand_thr,
-                                                           const int4* __restrict__ blk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(
+    const uint4* __restrict__ img, int n, int nchunks, int d, int* __restrict__ cand_idx,
+    float* __restrict__ cand_thr, const int4* __restrict__ blk) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
     constexpr int ROWB = KSTEPS * 64;               // bytes per row
-    constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage (no norms)
-    constexpr int LOADS = (KNN_CHUNK * C16) / 256;  // uint4 loads per thread per stage
-    // ALL of the kernel's LDS is this one array (two staging buffers, then the
+    constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage
+    constexpr int LOADS = (KNN_CHUNK * C16) / 256;  // LDS-DMA instructions per thread per stage
+    // ALL of the kernel's LDS is this one array (the staging buffers, then the
     // queues): with a second __shared__ object beside the LDS-DMA target,
     // hipcc waits vmcnt(0) before the first ds_read of every tile, which
-    // serialises the next chunk's DMA with this chunk's compute.
-    constexpr int SBUF = STAGE + KNN_CHUNK * 4;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SBUF + 4 * (QC + 1) * 64 * 8];
-#define lds(bb_) (smem + (bb_) * SBUF)
-    // Per-lane insertion queues (slot-major, so a wave's enqueue is one
-    // conflict-free ds_write_b64).  Candidates above the running threshold are
-    // queued per tile and inserted in batches: a flush costs max-queue-length
-    // insertion rounds for the whole wave instead of one round per (tile,
-    // register) that any lane touched.
-    // per-wave queues [slot][lane] (slot QC takes the discarded branchless writes)
-    uint2* const qbw = reinterpret_cast<uint2*>(smem + 2 * SBUF) + (threadIdx.x >> 6) * (QC + 1) * 64;
+    // serialises the staging with the compute.
+    __shared__ __attribute__((aligned(16))) unsigned char smem[KNN_NBUF * STAGE + 4 * (QC + 1) * 64 * 8];
+#define lds(bb_) (smem + (bb_) * STAGE)
+    // Per-lane insertion queues (slot-major [slot][lane]; slot QC is spare).
+    // Candidates above the running threshold are queued per tile and inserted
+    // in batches: a flush costs max-queue-length insertion rounds for the
+    // whole wave instead of one round per (tile, register) any lane touched.
+    uint2* const qbw = reinterpret_cast<uint2*>(smem + KNN_NBUF * STAGE) + (threadIdx.x >> 6) * (QC + 1) * 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
     const int bx = xcd_block(blockIdx.x, gridDim.x);
-    // the block's reference chunks [cl, ch) and query limit qhi: the whole
-    // image, or (batched segments) its own segment
+    // the block's reference chunks [cl, ch), query limit qhi (= the last valid
+    // reference position + 1): the whole image, or (batched segments) its own
     int cl = 0, ch = nchunks, qhi = n;
     if (blk) {
         const int4 bi = blk[bx];
@@ -350,6 +369,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             qh[s] = *reinterpret_cast<h8*>(&a);
             ql[s] = *reinterpret_cast<h8*>(&b);
         }
+        // the query side of the norm dimension d is 2^KNN_NORM_SHIFT (exact, no lo part)
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (16 * s + 8 * h + e == d) {
+                    qh[s][e] = (_Float16)(float)(1 << KNN_NORM_SHIFT);
+                    ql[s][e] = (_Float16)0.0f;
+                }
     }
     float lv[KP];
     int li[KP];
@@ -363,11 +391,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // Staging by LDS-DMA (global_load_lds_dwordx4): the LDS image is written
     // lane-linearly, so the row swizzle goes on the per-lane SOURCE address
     // (swz_chunk is an involution) and the same swizzle on the fragment reads.
-    // Issued as inline asm: hipcc would otherwise wait vmcnt(0) before the
-    // first ds_read of every tile (it cannot tell the DMA target from the
-    // buffer being read), serialising the next chunk's DMA with this chunk's
-    // compute.  The explicit vmcnt(0) before each chunk's closing barrier is
-    // the only wait the DMA needs.
 #define KNN_STAGE_GLDS(bb, cidx)                                                                   \
     do {                                                                                           \
         const unsigned char* src_ = reinterpret_cast<const unsigned char*>(img) +                 \
@@ -378,9 +401,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             glds16(src_, (unsigned)(row_ * ROWB + swz_chunk<KSTEPS>(row_, cs_) * 16),             \
                    lds_addr(lds(bb) + (i_ * 256 + wave * 64) * 16));                              \
         }                                                                                          \
-        if (wave == 0 && lane < KNN_CHUNK / 4)                                                     \
-            glds16(reinterpret_cast<const unsigned char*>(nrm) + (int64_t)(cidx) * (KNN_CHUNK * 4), \
-                   (unsigned)(lane * 16), lds_addr(lds(bb) + STAGE));                              \
     } while (0)
     // Rows are in spatial (Morton) order, so scan ref chunks outward from the
     // block's own position: near neighbours arrive first, the threshold tightens
@@ -390,7 +410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int Lc = c0 - cl, Rc = ch - 1 - c0, Mc = min(Lc, Rc);
     const int nck = ch - cl;
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
-    float T = -INFINITY;  // max of both halves' thresholds (see below)
+    float T = -INFINITY;  // rejection threshold (see below)
     int qc = 0;           // this lane's queued candidates
     bool tdirty = false;  // lists changed since T was last set to the union threshold
 #define KNN_FLUSH()                                                                   \
@@ -409,14 +429,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         qc = 0;                                                                       \
         tdirty = true;                                                                \
     } while (0)
+    // Pipeline: chunks k+1 and k+2 are in flight while chunk k is computed; at
+    // the top of iteration k the wave waits for its own part of chunk k
+    // (vmcnt: the younger chunk k+1 may stay outstanding), the barrier makes
+    // every wave's part visible and frees buffer (k+2) % 3 (last read in k-1).
     KNN_STAGE_GLDS(0, chunk_at(0));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (nck > 1) KNN_STAGE_GLDS(1, chunk_at(1));
     for (int k = 0; k < nck; ++k) {
-        const int b = k & 1;
+        const int b = k % KNN_NBUF;
         const int c = chunk_at(k);
-        if (k + 1 < nck) KNN_STAGE_GLDS(b ^ 1, chunk_at(k + 1));
-#pragma nounroll  // unrolling the two tiles doubles live registers (248 vs 162 VGPRs)
+        if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
+        else knn_wait_vmcnt<0>();
+        __syncthreads();
+        if (k + 2 < nck) KNN_STAGE_GLDS((k + 2) % KNN_NBUF, chunk_at(k + 2));
+#pragma nounroll  // unrolling the two tiles doubles live registers
         for (int tau = 0; tau < 2; ++tau) {
             const int row = tau * 32 + col;
             h8 ah[KSTEPS], al[KSTEPS];
@@ -429,37 +455,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 ah[s] = *reinterpret_cast<h8*>(&a);
                 al[s] = *reinterpret_cast<h8*>(&bb);
             }
-            f32x16 acc;
-            const float* nb = reinterpret_cast<const float*>(lds(b) + STAGE) + tau * 32 + 4 * h;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 v = *reinterpret_cast<const float4*>(nb + 8 * g);
-                acc[4 * g + 0] = v.x;
-                acc[4 * g + 1] = v.y;
-                acc[4 * g + 2] = v.z;
-                acc[4 * g + 3] = v.w;
-            }
-            const int rbase = c * KNN_CHUNK + tau * 32;
-            if (rbase == q0) {  // diagonal tile: exclude self (wave-uniform branch)
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg)
-                    if ((reg & 3) + 8 * (reg >> 2) + 4 * h == col) acc[reg] = -INFINITY;
-            }
+            f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KSTEPS; ++s) {
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], qh[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], ql[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], qh[s], acc, 0, 0, 0);
             }
+            const int rbase = c * KNN_CHUNK + tau * 32;
+            if (rbase == q0 || rbase + 32 > qhi) {  // diagonal tile (self) or padding refs (wave-uniform)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int r = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    if (r == q || r >= qhi) acc[reg] = -INFINITY;
+                }
+            }
+            // per half-tile of 8 registers: flush first if its candidates could
+            // overflow a queue, then enqueue each register's candidates under
+            // its own exec mask (a register no lane beats costs one compare)
+            static_assert(QC >= 8, "queue must hold a half tile");
+#if KNN_ENQ_BRANCHY
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                if (__any(qc > QC - 8)) KNN_FLUSH();
+#pragma unroll
+                for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
+                    const float v = acc[reg];
+                    if (v > T) {
+                        qbw[qc * 64 + lane] = make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
+                        ++qc;
+                    }
+                }
+            }
+#else
             float vmax = acc[0];
 #pragma unroll
             for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
             if (__any(vmax > T)) {
-                // per half-tile of 8 registers: flush first if its candidates
-                // could overflow a queue (QC >= 8), then enqueue branch-free (a
-                // write at slot qc is kept only if qc advances; slot QC absorbs
-                // the rest)
-                static_assert(QC >= 8, "queue must hold a half tile");
+                // branch-free: a write at slot qc is kept only if qc advances
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     int c8 = 0;
@@ -475,6 +508,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     }
                 }
             }
+#endif
             // After a flush (here, with the tile's accumulators dead) both halves
             // move to the union threshold; between flushes T only rises.
             if (tdirty) {
@@ -482,8 +516,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 tdirty = false;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
     KNN_FLUSH();
     T = union_kth<KP>(lv);
@@ -599,12 +631,13 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
         // its screening error is at most
         //   E = c*2^-24*s^2                      (fp16 split + fp32 accumulation)
         //     + 2^-12*sqrt(d)*s/sigma + 2^-26*d/sigma^2   (flushed parts < 2^-14)
+        //     + 8/sigma^2      (the norm dimension: 2^15 x a flushed part < 2^-14)
         // and its approx d2 at most dK + E.  excl > dK + E therefore proves it
         // is farther (DESIGN.md "kNN certification bound").
         const double s = 2.0 * sqrt(nq) + sqrt(dK);
         const double isc = sqrt(*inv_scale2);  // 1/sigma, a power of two
         const double E = err_ulps * 0x1p-24 * s * s + 0x1p-12 * sqrt((double)d) * s * isc +
-                         0x1p-26 * (double)d * isc * isc + 1e-300;
+                         (0x1p-26 * (double)d + 8.0) * isc * isc + 1e-300;
         const double excl = nq - 2.0 * (double)tmax * (*inv_scale2);  // thresholds are in scaled units
         ok = ok && (excl - E > dK);
     }
@@ -834,11 +867,10 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     const double err_ulps = KNN_ERR_ULPS_F16;
     const int* order_perm = nullptr;  // screening position -> bootstrap row
     {
-        const int KSTEPS = d <= 16 ? 1 : (d <= 32 ? 2 : 4);
+        const int KSTEPS = d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4);  // d data dims + the norm dimension
         const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
-        uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
+        uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + 256);
         if (!img) return CCG_ENOMEM;
-        float* nrm = (float*)((char*)img + (size_t)npad * 64 * KSTEPS);
         unsigned* bnd = misc + 8;
         CCG_HIP(hipMemsetAsync(bnd, 0xff, 3 * sizeof(unsigned), st));
         CCG_HIP(hipMemsetAsync(bnd + 3, 0, 3 * sizeof(unsigned), st));
@@ -864,17 +896,17 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         }
         const unsigned pg = (unsigned)ccg_cdiv(npad, 256);
         if (KSTEPS == 1)
-            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
         else if (KSTEPS == 2)
-            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
         else
-            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, nrm, inv_scale2);
+            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
         const int nch = (int)(npad / KNN_CHUNK);
         const unsigned grid = (unsigned)ccg_cdiv(npos, KNN_QPB);
         const int4* blk = sg ? sg->blk : nullptr;
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
 #define CCG_SCREEN16(KS_, KP_) \
-    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, nrm, (int)npos, nch, cand_idx, cand_thr, blk)
+    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk)
         if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
