@@ -145,16 +145,6 @@ def synth_labels(torch, pop_boot, L, dev, seed):
     return torch.where(flip, rnd, lab).to(torch.int32)
 
 
-def A_full_C(torch, A_local, G):
-    """sum over all G*B columns of C_b (= max label per column), via one
-    all-reduce of the per-rank sums (labels are codes 1..C_b)."""
-    c = A_local.max(dim=1).values.to(torch.int64).sum()
-    if G > 1:
-        import torch.distributed as dist
-        dist.all_reduce(c)
-    return int(c.item())
-
-
 def _cpu_boot_worker(a):
     """One bootstrap's per-bootstrap CPU work (kNN k=20, SNN k=10/15/20, 6
     silhouettes) on a single core, as one BiocParallel MulticoreParam worker
@@ -240,10 +230,16 @@ def main():
         ranks_seen = [g.tolist() for g in got]
 
     from consensusclustr_amd import Engine
-    from consensusclustr_amd.sharding import allgather_columns, row_slabs, slab_pairs
+    from consensusclustr_amd.sharding import DeviceGroup, exchange_group_id, row_slabs, slab_pairs
 
+    # libccg's device group: this rank's context + an RCCL communicator over
+    # all ranks (the all-gather and the slab split run inside libccg)
+    if world > 1:
+        grp = DeviceGroup.open_rank(local, world, rank, exchange_group_id())
+    else:
+        grp = DeviceGroup.open([local])
     S = max(1, args.streams)
-    engs = [Engine(local) for _ in range(S)]  # own workspaces per in-flight bootstrap
+    engs = [grp.engines[0]] + [Engine(local) for _ in range(S - 1)]  # own workspaces per in-flight bootstrap
     eng = engs[0]
     N, d, B = args.cells, args.pcs, args.boots_per_gpu
     n = int(args.boot_size * N)
@@ -281,7 +277,8 @@ def main():
     nclust = torch.empty((B, L), dtype=torch.int32, device=dev)
     minsize = torch.empty((B, L), dtype=torch.int32, device=dev)
     choice = torch.empty(B, dtype=torch.int32, device=dev)
-    A_local = torch.zeros((B, N), dtype=torch.uint8, device=dev)
+    A_full = torch.zeros((G * B, N), dtype=torch.uint8, device=dev)  # all ranks' columns
+    A_local = A_full[rank * B:(rank + 1) * B]  # this rank's block, all-gathered in place
     cuts = row_slabs(N, G)
     r0, r1 = cuts[rank], cuts[rank + 1]
     P = max(slab_pairs(N, r0, r1), 1)
@@ -307,8 +304,8 @@ def main():
             cur.wait_stream(st_)
         eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
                              minsize=minsize, out_choice=choice)
-        A = allgather_columns(A_local) if G > 1 else A_local
-        eng.cocluster_t(A, r0, r1, co=co, both=both)
+        grp.allgather_columns_t([A_local], [B] * G, [A_full])
+        grp.cocluster_sharded_t([A_full], co=[co], both=[both])
 
     def barrier():
         if G > 1:
@@ -371,7 +368,7 @@ def main():
     # per 16-dim block, d padded to 16*ceil(d/16)
     mfma_exec = 3 * 2.0 * n * n * (16 * ((d + 15) // 16))
     # co-cluster roofline: OPS = 2 * P * (sum_b C_b + B) over this rank's slab
-    colC = A_full_C(torch, A_local, G)
+    colC = int(A_full.max(dim=1).values.to(torch.int64).sum().item())  # sum_b C_b over all ranks' columns
     coc_ops = 2.0 * P * (colC + G * B)
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -440,6 +437,9 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
+    for e in engs[1:]:
+        e.close()
+    grp.close()
     if G > 1:
         dist.destroy_process_group()
 

@@ -25,6 +25,7 @@ CCG_SNN_RANK = 1
 CCG_MODE_ROBUST = 0
 CCG_MODE_GRANULAR = 1
 COCLUSTER_ROW_ALIGN = 128
+GROUP_ID_BYTES = 128
 
 _ERRNAMES = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAP", -5: "ENAN", -6: "ERANGE"}
 
@@ -55,6 +56,7 @@ SIGNATURES = {
     "ccg_synchronize": (_i, [_p]),
     "ccg_check_errors": (_i, [_p]),
     "ccg_stream": (_p, [_p]),
+    "ccg_ctx_device": (_i, [_p, _p]),
     "ccg_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
     "ccg_gather_rows_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p]),
     "ccg_knn_rows_dev": (_i, [_p, _p, _i64, _i, _i, _p, _p, _p, _p]),
@@ -74,6 +76,22 @@ SIGNATURES = {
     "ccg_consensus_knn_dev": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "ccg_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
     "ccg_consensus_knn_assign_dev": (_i, [_p, _p, _i, _i64, _i64, _i, _i64, _i64, _p, _p, _p]),
+    "ccg_row_slabs": (_i, [_i64, _i, _p]),
+    "ccg_rect_slabs": (_i, [_i64, _i, _p]),
+    "ccg_boot_shard": (_i, [_i64, _i, _i, _p, _p]),
+    "ccg_group_open": (_i, [_p, _i, _p]),
+    "ccg_group_unique_id": (_i, [_p]),
+    "ccg_group_open_rank": (_i, [_i, _i, _i, _p, _p]),
+    "ccg_group_close": (_i, [_p]),
+    "ccg_group_info": (_i, [_p, _p, _p, _p]),
+    "ccg_group_ctx": (_i, [_p, _i, _p]),
+    "ccg_group_synchronize": (_i, [_p]),
+    "ccg_allgather_columns": (_i, [_p, _p, _p, _i64, _i, _p]),
+    "ccg_cocluster_sharded_dev": (_i, [_p, _p, _i, _i64, _i64, _p, _p, _p, _p]),
+    "ccg_consensus_knn_sharded_dev": (_i, [_p, _p, _i, _i64, _i64, _i, _p, _p]),
+    "ccg_group_cocluster": (_i, [_p, _p, _i, _i64, _i64, _p, _p, _p]),
+    "ccg_group_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
+    "ccg_group_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
     "ccg_timing_enable": (_i, [_p, _i]),
     "ccg_timing_read": (_i, [_p, _i, _p, _p]),
 }

@@ -109,6 +109,12 @@ extern "C" int ccg_check_errors(ccg_ctx* ctx) {
 
 extern "C" void* ccg_stream(ccg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+extern "C" int ccg_ctx_device(const ccg_ctx* ctx, int* device) {
+    CCG_REQUIRE(ctx && device, "ccg_ctx_device: NULL argument");
+    *device = ctx->device;
+    return CCG_OK;
+}
+
 void* ccg_ws(ccg_ctx* ctx, int slot, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (ctx->ws_bytes[slot] >= bytes) return ctx->ws[slot];

@@ -39,12 +39,26 @@ class Engine:
         ctx = _vp()
         check(self.lib.ccg_open(ctypes.byref(cfg), ctypes.byref(ctx)))
         self.ctx = ctx
+        self.owned = True
         self.last_knn_stats = None
 
+    @classmethod
+    def from_ctx(cls, ctx):
+        """A non-owning Engine over a context owned elsewhere (a device group's)."""
+        e = cls.__new__(cls)
+        e.lib = _lib.load()
+        e.ctx = ctx
+        e.owned = False
+        e.last_knn_stats = None
+        dev = ctypes.c_int()
+        check(e.lib.ccg_ctx_device(ctx, ctypes.byref(dev)))
+        e.device = dev.value
+        return e
+
     def close(self):
-        if self.ctx:
+        if self.ctx and self.owned:
             self.lib.ccg_close(self.ctx)
-            self.ctx = None
+        self.ctx = None
 
     def __enter__(self):
         return self

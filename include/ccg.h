@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 2
+#define CCG_ABI_VERSION 3
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -85,6 +85,8 @@ int ccg_synchronize(ccg_ctx* ctx);
 int ccg_check_errors(ccg_ctx* ctx);
 /* The context's default stream (hipStream_t). */
 void* ccg_stream(ccg_ctx* ctx);
+/* The HIP device ordinal the context runs on. */
+int ccg_ctx_device(const ccg_ctx* ctx, int* device);
 
 /* ---------------------------------------------------------------- kNN -- */
 /* Exact Euclidean kNN of every bootstrap row among the other rows of the
@@ -219,8 +221,10 @@ int ccg_select_mapback_dev(ccg_ctx* ctx, int mode, const int32_t* labels,
                            int32_t* out_choice, void* stream);
 
 /* ------------------------------------------------------- co-clustering -- */
-/* A: B x N column-major assignment matrix of uint8 (label_bits 8) or uint16
- * (label_bits 16) codes, 0 = not sampled (R's -1), 1.. = cluster code.
+/* A: the assignment matrix as R holds it (N cells x B bootstraps,
+ * column-major: bootstrap b's N labels are contiguous at A + b*N), uint8
+ * (label_bits 8) or uint16 (label_bits 16) codes, 0 = not sampled (R's -1),
+ * 1.. = cluster code.
  * B <= 65535 (uint16 counts; columns are accumulated in chunks of 16383).
  * For the rows [r0, r1) of the packed upper triangle (row i holds
  * j = i+1..N-1; this is exactly the order of R's "dist" object) writes
@@ -259,6 +263,76 @@ int ccg_consensus_knn_assign_dev(ccg_ctx* ctx, const void* A, int label_bits,
                                  int64_t N, int64_t B, int k, int64_t r0,
                                  int64_t r1, int32_t* out_idx,
                                  int32_t* d_nan_flag, void* stream);
+
+/* ------------------------------------------------------------ multi-GPU -- */
+/* A device group: one context (stream + workspaces) per device and one RCCL
+ * communicator per device over xGMI.  The reference runs bootstraps on
+ * BiocParallel workers and parDist on RcppParallel threads of one node
+ * (R/consensusClust.R:391-421); the group is that fan-out across GPUs:
+ *   bootstraps  -> contiguous blocks per rank (ccg_boot_shard), no traffic;
+ *   co-cluster  -> one all-gather of the assignment columns, then row slabs
+ *                  of the packed triangle balanced by pair count
+ *                  (ccg_row_slabs), each kept by its device;
+ *   consensus kNN -> equal full-row slabs (ccg_rect_slabs), then an
+ *                  all-gather of the N x k neighbour matrix.
+ * Arrays indexed by "local device" l have one entry per device this process
+ * drives (ccg_group_info nlocal); rank of local l = first_rank + l. */
+#define CCG_GROUP_ID_BYTES 128
+typedef struct ccg_group ccg_group;
+
+/* Host-only planning (no device work): cuts[0..G] with cuts[0] = 0,
+ * cuts[G] = N and interior cuts multiples of CCG_COCLUSTER_ROW_ALIGN.
+ * ccg_row_slabs: cut g ~ N (1 - sqrt(1 - g/G)) (equal packed-triangle pairs);
+ * ccg_rect_slabs: cut g ~ N g / G (equal full rows). */
+int ccg_row_slabs(int64_t N, int G, int64_t* cuts);
+int ccg_rect_slabs(int64_t N, int G, int64_t* cuts);
+/* Bootstrap block [*b0, *b1) of `rank` among G (sizes differ by <= 1). */
+int ccg_boot_shard(int64_t nboots, int G, int rank, int64_t* b0, int64_t* b1);
+
+/* One process, several devices (ncclCommInitAll over `devices`). */
+int ccg_group_open(const int* devices, int ndev, ccg_group** out);
+/* One process per device: rank 0 calls ccg_group_unique_id, the caller
+ * broadcasts the CCG_GROUP_ID_BYTES bytes to every rank (any channel), then
+ * every rank calls ccg_group_open_rank (collective; blocks until all join). */
+int ccg_group_unique_id(uint8_t* id);
+int ccg_group_open_rank(int device, int nranks, int rank, const uint8_t* id, ccg_group** out);
+int ccg_group_close(ccg_group* g);
+int ccg_group_info(const ccg_group* g, int* nlocal, int* nranks, int* first_rank);
+/* The engine context of local device `local` (owned by the group). */
+int ccg_group_ctx(ccg_group* g, int local, ccg_ctx** out);
+/* ccg_synchronize on every local context; first sticky error wins. */
+int ccg_group_synchronize(ccg_group* g);
+
+/* All-gather of assignment columns (device pointers, enqueued on each local
+ * context's stream, no host synchronisation).  Rank r contributes counts[r]
+ * bootstrap columns of N labels (local_A[l]: counts[first_rank+l] x N, each
+ * column contiguous); every local device receives the sum(counts) x N matrix
+ * A[l] with rank r's columns after rank r-1's.  local_A[l] may alias its own
+ * block of A[l].  counts: host array of nranks entries. */
+int ccg_allgather_columns(ccg_group* g, const void* const* local_A, const int64_t* counts, int64_t N,
+                          int label_bits, void* const* A);
+/* Each local device computes its rank's row slab [cuts[r], cuts[r+1]) of the
+ * packed co/both/dist (ccg_row_slabs cuts) from its full copy A[l]; slab
+ * layout as ccg_cocluster_dev with r0 = cuts[r].  co/both/dist may be NULL
+ * (or hold NULL entries).  cuts (host, nranks+1) may be NULL. */
+int ccg_cocluster_sharded_dev(ccg_group* g, const void* const* A, int label_bits, int64_t N, int64_t B,
+                              uint16_t* const* co, uint16_t* const* both, double* const* dist,
+                              int64_t* cuts);
+/* Fused consensus kNN over the group: each device computes rows
+ * [cuts[r], cuts[r+1]) (ccg_rect_slabs) of its N x k out_idx[l], then the
+ * rows are all-gathered so every device holds the whole matrix, and
+ * d_nan_flag[l] (device int32) holds the OR over ranks. */
+int ccg_consensus_knn_sharded_dev(ccg_group* g, const void* const* A, int label_bits, int64_t N, int64_t B,
+                                  int k, int32_t* const* out_idx, int32_t* const* d_nan_flag);
+/* Host flavours for a single-process group (nlocal == nranks): A is uploaded
+ * once and broadcast over xGMI; outputs as ccg_cocluster /
+ * ccg_consensus_knn_assign / ccg_knn_boot (bootstraps split over devices). */
+int ccg_group_cocluster(ccg_group* g, const void* A, int label_bits, int64_t N, int64_t B, uint16_t* co,
+                        uint16_t* both, double* dist);
+int ccg_group_consensus_knn_assign(ccg_group* g, const void* A, int label_bits, int64_t N, int64_t B, int k,
+                                   int32_t* out_idx);
+int ccg_group_knn_boot(ccg_group* g, const double* pcs, int64_t N, int d, const int32_t* boot_idx, int64_t n,
+                       int nb, int kmax, int32_t* out_idx, double* out_dist, ccg_knn_stats* stats);
 
 /* ------------------------------------------------------ kernel timing -- */
 /* Device time of selected kernels, measured with hipEvents recorded on the

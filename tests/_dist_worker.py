@@ -1,6 +1,9 @@
-"""Worker for tests/test_distributed.py (gloo, CPU): the multi-GPU sharding
-plumbing -- bootstrap blocks per rank, all-gather of assignment columns,
-pair-balanced row slabs -- checked against the single-process oracle."""
+"""Worker for tests/test_distributed.py (gloo, CPU): the multi-GPU plan of
+libccg's device group rehearsed across processes -- the group-id hand-off
+from rank 0 (sharding.exchange_group_id), bootstrap blocks (ccg_boot_shard),
+the rank-ordered column all-gather (emulated with gloo; on GPUs it is
+ccg_allgather_columns over RCCL) and pair-balanced row slabs
+(ccg_row_slabs) -- checked against the single-process oracle."""
 import os
 import sys
 
@@ -14,7 +17,7 @@ sys.path.insert(0, ROOT)
 
 def packed_slab_numpy(A, r0, r1):
     """co/both of rows [r0, r1) of the packed upper triangle (CPU, test only)."""
-    A = A.numpy().astype(np.int64)
+    A = A.astype(np.int64)
     B, N = A.shape
     co, both = [], []
     for i in range(r0, r1):
@@ -31,24 +34,39 @@ def main(rank, world, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from consensusclustr_amd.sharding import boot_shard, sharded_cocluster, slab_pairs
+    from consensusclustr_amd.sharding import boot_shard, exchange_group_id, row_slabs, slab_pairs
     import oracle as O
+    # the RCCL id every rank passes to ccg_group_open_rank comes from rank 0
+    gid = exchange_group_id(make_id=lambda: np.random.default_rng(99).integers(0, 256, 128, dtype=np.uint8))
+    ids = [None] * world
+    dist.all_gather_object(ids, gid)
+    assert all(x == ids[0] for x in ids) and len(gid) == 128
     N, nboots = 300, 10
     rng = np.random.default_rng(7)
     full = rng.integers(0, 6, (nboots, N)).astype(np.uint8)  # the assignment columns of all bootstraps
-    b0, b1 = boot_shard(nboots, world, rank)
-    local = torch.from_numpy(full[b0:b1].copy())
-    (co, both), (r0, r1), A = sharded_cocluster(local, N, packed_slab_numpy)
-    assert np.array_equal(A.numpy(), full), "all-gathered columns differ from the single-process matrix"
+    spans = [boot_shard(nboots, world, r) for r in range(world)]
+    b0, b1 = spans[rank]
+    counts = [s[1] - s[0] for s in spans]
+    # rank-ordered all-gather of unequal blocks (pad to the largest, trim)
+    bmax = max(counts)
+    mine = np.zeros((bmax, N), np.uint8)
+    mine[:b1 - b0] = full[b0:b1]
+    parts = [torch.zeros((bmax, N), dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(mine))
+    A = np.concatenate([parts[r].numpy()[:counts[r]] for r in range(world)])
+    assert np.array_equal(A, full), "all-gathered columns differ from the single-process matrix"
+    cuts = row_slabs(N, world)
+    r0, r1 = cuts[rank], cuts[rank + 1]
+    co, both = packed_slab_numpy(A, r0, r1)
     assert co.size == slab_pairs(N, r0, r1)
-    parts = [None] * world
-    dist.all_gather_object(parts, (co, both))
+    got = [None] * world
+    dist.all_gather_object(got, (co, both))
     if rank == 0:
         Ao = full.astype(np.int32)
         Ao[Ao == 0] = -1
         ref = O.cocluster(Ao)
-        co_all = np.concatenate([p[0] for p in parts])
-        both_all = np.concatenate([p[1] for p in parts])
+        co_all = np.concatenate([p[0] for p in got])
+        both_all = np.concatenate([p[1] for p in got])
         assert np.array_equal(co_all, ref["co"].astype(np.int64)), "sharded co counts differ"
         assert np.array_equal(both_all, ref["both"].astype(np.int64)), "sharded both counts differ"
         with open(out_path, "w") as f:

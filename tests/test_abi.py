@@ -13,7 +13,9 @@ def test_header_declares_expected_entry_points():
     syms = _lib.header_symbols()
     for s in ("ccg_open", "ccg_knn_boot", "ccg_knn_rows_dev", "ccg_snn", "ccg_snn_dev", "ccg_silhouette",
               "ccg_select_mapback_dev", "ccg_cocluster", "ccg_cocluster_dev", "ccg_consensus_knn",
-              "ccg_consensus_knn_assign", "ccg_consensus_knn_assign_dev", "ccg_check_errors", "ccg_timing_read"):
+              "ccg_consensus_knn_assign", "ccg_consensus_knn_assign_dev", "ccg_check_errors", "ccg_timing_read",
+              "ccg_group_open", "ccg_group_open_rank", "ccg_group_unique_id", "ccg_allgather_columns",
+              "ccg_cocluster_sharded_dev", "ccg_consensus_knn_sharded_dev", "ccg_row_slabs", "ccg_boot_shard"):
         assert s in syms
 
 
@@ -33,7 +35,7 @@ def test_nm_exports_are_extern_c():
 
 def test_abi_version_and_error_path():
     lib = _lib.load()
-    assert lib.ccg_abi_version() == 2
+    assert lib.ccg_abi_version() == 3
     # NULL out-pointer: rejected before any device work, message set
     assert lib.ccg_open(None, None) == _lib.CCG_EINVAL
     assert b"NULL" in lib.ccg_last_error()
@@ -57,3 +59,8 @@ def test_consts_match_header():
     for name in ("CCG_EINVAL", "CCG_ECAP", "CCG_ENAN", "CCG_SNN_RANK", "CCG_MODE_GRANULAR"):
         assert name in text
     assert f"CCG_COCLUSTER_ROW_ALIGN {_lib.COCLUSTER_ROW_ALIGN}" in text
+
+
+def test_library_links_rccl():
+    out = subprocess.check_output(["readelf", "-d", _lib.LIB_PATH]).decode()
+    assert "librccl.so" in out  # the device group's collectives are RCCL, inside the library

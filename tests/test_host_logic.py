@@ -98,3 +98,22 @@ def test_row_slabs_small_n_cuts_stay_aligned(N, G):
     cuts = row_slabs(N, G)
     assert all(c % 128 == 0 for c in cuts[:-1])
     assert cuts[-1] == N
+
+
+@pytest.mark.parametrize("N,G", [(1000, 3), (250000, 8), (300, 8), (100, 2)])
+def test_rect_slabs_cover_evenly(N, G):
+    from consensusclustr_amd.sharding import rect_slabs
+    cuts = rect_slabs(N, G)
+    assert cuts[0] == 0 and cuts[-1] == N and all(a <= b for a, b in zip(cuts, cuts[1:]))
+    assert all(c % 128 == 0 for c in cuts[1:-1])
+    if N >= 128 * G * 4:
+        sizes = np.diff(cuts)
+        assert sizes.max() - sizes.min() <= 2 * 128
+
+
+def test_row_slabs_formula():
+    """ccg_row_slabs (libccg, host-only) = the closed form r_g = N(1 - sqrt(1 - g/G)) rounded to 128."""
+    import math
+    N, G = 100000, 8
+    want = [0] + [int(round(N * (1 - math.sqrt(1 - g / G)) / 128)) * 128 for g in range(1, G)] + [N]
+    assert row_slabs(N, G) == want
