@@ -76,6 +76,12 @@ SIGNATURES = {
     "ccg_consensus_knn_dev": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "ccg_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
     "ccg_consensus_knn_assign_dev": (_i, [_p, _p, _i, _i64, _i64, _i, _i64, _i64, _p, _p, _p]),
+    "ccg_cluster_block_sums": (_i, [_p, _p, _i, _i64, _i64, _p, _i, _p, _p]),
+    "ccg_cluster_block_sums_dev": (_i, [_p, _p, _i, _i64, _i64, _p, _i, _p, _p, _p]),
+    "ccg_cluster_block_means": (_i, [_i, _p, _p, _p]),
+    "ccg_contingency": (_i, [_p, _p, _i, _i64, _i64, _p, _i, _i, _p]),
+    "ccg_contingency_dev": (_i, [_p, _p, _i, _i64, _i64, _p, _i, _i, _p, _p]),
+    "ccg_pairwise_rand_ratio": (_i, [_i, _i, _p, _i, _p]),
     "ccg_row_slabs": (_i, [_i64, _i, _p]),
     "ccg_rect_slabs": (_i, [_i64, _i, _p]),
     "ccg_boot_shard": (_i, [_i64, _i, _i, _p, _p]),

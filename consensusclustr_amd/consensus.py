@@ -172,7 +172,8 @@ def assignment_matrix(columns):
 
 
 def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRange=RES_RANGE, kNum=K_NUM,
-                      mode="robust", seed=123, engine=None, boot_indices=None, return_matrix=None):
+                      mode="robust", seed=123, engine=None, boot_indices=None, return_matrix=None,
+                      merge=False, minStability=0.175):
     """The bootstrap + consensus core of consensusClust (R/consensusClust.R:388-456).
 
     Returns dict(assignments=<chosen consensus labels>, clustAssignments=<B x N
@@ -181,8 +182,8 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
     20000), the packed R-dist-order jaccardDist, co and both.  The consensus
     kNN (:425) comes straight from the assignment matrix through the fused
     co-clustering top-k (ccg_consensus_knn_assign), so the N x N distance is
-    only materialised on request.  The later host stages (cluster merging
-    :459-497, null test, dendrogram) are out of scope.
+    only materialised on request.  merge=True adds the cluster merging of
+    :458-497 (merge_unstable_clusters) as final_assignments / stability.
     """
     eng = engine or default_engine()
     pca = np.asarray(pca, dtype=np.float64)
@@ -221,4 +222,152 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
     scores = np.where((nuniq > 1) & (nuniq < N / 10), means, np.where(nuniq == N, -1.0, 0.15))
     choice = consensus_choice(scores)
     out.update(assignments=lab[choice], scores=scores, choice=choice, candidates=lab, consensus_knn=cknn)
+    if merge:
+        m = merge_unstable_clusters(lab[choice], A, kNum, minStability, eng)
+        out.update(final_assignments=m["assignments"], stability=m["stability"])
     return out
+
+
+# ------------------------------------------- after the consensus choice --
+# R/consensusClust.R:458-497.  finalAssignments starts as cluster_leiden's
+# integer membership; the first small-cluster merge assigns a character
+# (colnames(clustDist)[...]), which turns the whole vector into character, so
+# from then on table()/factor level order is the lexicographic order of the
+# decimal labels.  Labels stay integers here; `is_char` tracks that order.
+def _level_order(values, is_char):
+    vals = sorted(set(int(v) for v in values))
+    return sorted(vals, key=str) if is_char else vals
+
+
+def _unique_order(values):
+    _, first = np.unique(values, return_index=True)
+    return [int(values[i]) for i in np.sort(first)]
+
+
+def _exact_block_sums(simsum, npairs):
+    """(K, K, 2) uint64 words -> exact Python-int sums (object array)."""
+    K = npairs.shape[0]
+    S = np.empty((K, K), dtype=object)
+    for p in range(K):
+        for q in range(K):
+            S[p, q] = (int(simsum[p, q, 1]) << 64) + int(simsum[p, q, 0])
+    return S, npairs.astype(object)
+
+
+def merge_small_clusters(final, A, kNum=K_NUM, engine=None, max_iter=100000):
+    """while (min(table(f)) < max(kNum[1], 20)) merge the smallest cluster into
+    its nearest by determineHierachy(as.matrix(jaccardDist), f) (:462-467).
+
+    The block sums come from the assignment matrix in one GPU pass
+    (ccg_cluster_block_sums); merges add exact sums, so every iteration's
+    distance row is the exact block mean, correctly rounded (R: long-double
+    two-pass mean).  Returns (labels, is_char)."""
+    from fractions import Fraction
+    eng = engine or default_engine()
+    f = np.asarray(final).astype(np.int64).copy()
+    thr = max(int(kNum[0]), 20)
+    base = sorted(set(f.tolist()))
+    pos = {v: t for t, v in enumerate(base)}
+    S, Np = _exact_block_sums(*eng.cluster_block_sums(A, np.array([pos[v] for v in f], np.int32), len(base)))
+    members = {v: [pos[v]] for v in base}  # current label -> original clusters
+    is_char = False
+    for _ in range(max_iter):
+        levels = _level_order(f, is_char)
+        counts = {v: int((f == v).sum()) for v in levels}
+        small = min(levels, key=lambda v: (counts[v], levels.index(v)))  # which.min(table(f))
+        if counts[small] >= thr:
+            return f, is_char
+        best, bestd = None, None
+        for v in _unique_order(f):  # which.min over clustDist[small, ] in unique() order
+            if v == small:
+                d = Fraction(1)  # diag(clustDist) = 1
+            else:
+                s = sum(S[p, q] + S[q, p] for p in members[small] for q in members[v])
+                n = sum(Np[p, q] + Np[q, p] for p in members[small] for q in members[v])
+                if n == 0:
+                    continue  # NaN: which.min skips NA
+                d = 1 - Fraction(s, n << 39)
+            if bestd is None or d < bestd:
+                best, bestd = v, d
+        if best == small:
+            raise RuntimeError("merge target is the cluster itself (the reference loops forever here)")
+        f[f == small] = best
+        members[best] = members[best] + members.pop(small)
+        is_char = True
+    raise RuntimeError("small-cluster merging did not converge")
+
+
+def stability_matrix(final, A, is_char=False, engine=None):
+    """apply(simplify2array(lapply(boots, pairwiseRand(f[mask], A[, b][mask],
+    mode="ratio", adjusted=TRUE))), 2, rowMeans2, na.rm=TRUE) (:470-481).
+
+    Contingency tables of every bootstrap column come from one GPU pass
+    (ccg_contingency); the ratio is host arithmetic (ccg_pairwise_rand_ratio).
+    Returns None where the reference's tryCatch returns NULL (per-bootstrap
+    matrices of different sizes), else the K x K matrix in level order with
+    diag 1 and NA -> 1 (:485-487)."""
+    import math
+    from .engine import pairwise_rand_ratio
+    eng = engine or default_engine()
+    f = np.asarray(final).astype(np.int64)
+    levels = _level_order(f, is_char)
+    pos = {v: t for t, v in enumerate(levels)}
+    K = len(levels)
+    tab = eng.contingency(A, np.array([pos[v] for v in f], np.int32), K)
+    mats = []
+    for b in range(tab.shape[0]):
+        t = tab[b]
+        present = np.flatnonzero(t[:, 1:].sum(1) > 0)  # ref levels in f[mask]
+        mats.append(pairwise_rand_ratio(t[present]))
+    if len({m.shape for m in mats}) != 1:
+        return None  # simplify2array cannot stack -> apply() errors -> NULL
+    arr = np.stack(mats)
+    Kb = arr.shape[1]
+    out = np.empty((Kb, Kb))
+    for i in range(Kb):
+        for j in range(Kb):
+            v = arr[:, i, j]
+            v = v[~np.isnan(v)]
+            out[i, j] = math.fsum(v) / v.size if v.size else np.nan
+    np.fill_diagonal(out, 1.0)
+    out[np.isnan(out)] = 1.0
+    return out
+
+
+def stability_merge(final, A, stab, minStability=0.175, max_iter=100000):
+    """while (min(stabilityMat) < minStability) (:489-495): clustersToMerge =
+    as.numeric(which(stab == min, arr.ind=TRUE)) -- 1-based positions, whose
+    first two entries are the rows of the first two matches in column-major
+    order -- and labels EQUAL to those positions are relabelled (the
+    reference compares labels with matrix indices)."""
+    f = np.asarray(final).astype(np.int64).copy()
+    A = np.array(A, copy=True)
+    stab = np.array(stab, dtype=np.float64, copy=True)
+    for _ in range(max_iter):
+        m = stab.min()
+        if not m < minStability:
+            return f, A, stab
+        rows, cols = np.nonzero((stab == m).T)  # column-major scan: (col, row) pairs
+        hits = list(zip(cols, rows))  # (row, col) in column-major order
+        flat = [r + 1 for r, _ in hits] + [c + 1 for _, c in hits]
+        c1, c2 = flat[0], flat[1]
+        f[f == c2] = c1
+        A[A == c2] = c1
+        stab[c1 - 1, c2 - 1] = 1.0
+        stab[c2 - 1, c1 - 1] = 1.0
+    raise RuntimeError("stability merging did not converge (the reference loops forever here)")
+
+
+def merge_unstable_clusters(final, A, kNum=K_NUM, minStability=0.175, engine=None):
+    """R/consensusClust.R:458-497 as one step: small-cluster merging by the
+    co-clustering block distances, then bootstrap-stability merging.
+    Returns dict(assignments, stability (or None), clustAssignments)."""
+    f = np.asarray(final).astype(np.int64)
+    if np.unique(f).size <= 1:
+        return {"assignments": f, "stability": None, "clustAssignments": A}
+    f, is_char = merge_small_clusters(f, A, kNum, engine)
+    stab = stability_matrix(f, A, is_char, engine)
+    if stab is None:
+        return {"assignments": np.ones_like(f), "stability": None, "clustAssignments": A}
+    f, A2, stab = stability_merge(f, A, stab, minStability)
+    return {"assignments": f, "stability": stab, "clustAssignments": A2}

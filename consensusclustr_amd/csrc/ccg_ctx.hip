@@ -93,6 +93,10 @@ int ccg_take_device_error(ccg_ctx* ctx) {
         ccg_set_error("cluster label exceeds the assignment matrix's label width (use label_bits=16)");
         return CCG_ERANGE;
     }
+    if (bits & CCG_DERR_CLUSTER_INDEX) {
+        ccg_set_error("cluster position outside [0, K)");
+        return CCG_EINVAL;
+    }
     ccg_set_error("SNN: neighbour index out of range or equal to the row itself");
     return CCG_EINVAL;
 }

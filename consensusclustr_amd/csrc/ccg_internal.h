@@ -41,6 +41,7 @@ enum ccg_ws_slot {
     WS_SEGS,         // kNN batched-segment plan (offsets, blocks, positions)
     WS_SORT,         // device radix sort temporary storage
     WS_SNN_ROWS,     // SNN per-node partner rows (padded CSR of the per-graph API)
+    WS_HIER,         // cluster block sums: co/both row sub-slab
     WS_NSLOTS
 };
 
@@ -54,6 +55,7 @@ struct ccg_timer_rec {
 // ccg_check_errors / host-flavour call turns it into a status code.
 #define CCG_DERR_LABEL_RANGE 1  // map-back: a label exceeds the assignment matrix's label width
 #define CCG_DERR_SNN_INDEX 2    // SNN: neighbour index out of range or self
+#define CCG_DERR_CLUSTER_INDEX 4  // block sums / contingency: cluster position outside [0, K)
 
 struct ccg_ctx {
     int device;

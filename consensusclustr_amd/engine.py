@@ -220,6 +220,33 @@ class Engine:
         check(rc)
         return out
 
+    def cluster_block_sums(self, A, f, K):
+        """Exact determineHierachy block sums (ccg_cluster_block_sums):
+        simsum (K, K, 2) uint64 (lo, hi words of sum sim * 2^39 over pairs
+        i < j with f_i = p, f_j = q, both > 0), npairs (K, K) int64."""
+        A = np.ascontiguousarray(A)
+        if A.dtype not in (np.uint8, np.uint16):
+            A = A.astype(np.uint8)
+        B, N = A.shape
+        f = np.ascontiguousarray(f, dtype=np.int32)
+        simsum = np.empty((K, K, 2), np.uint64)
+        npairs = np.empty((K, K), np.int64)
+        check(self.lib.ccg_cluster_block_sums(self.ctx, _ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(f), K,
+                                              _ptr(simsum), _ptr(npairs)))
+        return simsum, npairs
+
+    def contingency(self, A, f, K, C=None):
+        """table(f, A[b, ]) of every bootstrap column (ccg_contingency): (B, K, C+1) int32."""
+        A = np.ascontiguousarray(A)
+        if A.dtype not in (np.uint8, np.uint16):
+            A = A.astype(np.uint8)
+        B, N = A.shape
+        C = int(A.max()) if C is None else int(C)
+        f = np.ascontiguousarray(f, dtype=np.int32)
+        tab = np.empty((B, K, C + 1), np.int32)
+        check(self.lib.ccg_contingency(self.ctx, _ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(f), K, C, _ptr(tab)))
+        return tab
+
     # ---------------------------------------------------------- device API
     def gather_rows_t(self, pcs_cm, N, d, idx, rows):
         """rows[i, :] = pcs[idx[i], :]; pcs_cm is a column-major (d, N) tensor."""
@@ -321,3 +348,23 @@ class Engine:
         bits = 8 if A.dtype == torch.uint8 else 16
         check(self.lib.ccg_consensus_knn_assign_dev(self.ctx, _ptr(A), bits, N, B, k, r0, r1, _ptr(out_idx),
                                                     _ptr(d_flag), _stream()))
+
+
+# ----------------------------------------------------- host-only arithmetic
+def cluster_block_means(simsum, npairs):
+    """ccg_cluster_block_means: the K x K determineHierachy distance matrix."""
+    simsum = np.ascontiguousarray(simsum, dtype=np.uint64)
+    npairs = np.ascontiguousarray(npairs, dtype=np.int64)
+    K = npairs.shape[0]
+    out = np.empty((K, K), np.float64)
+    check(_lib.load().ccg_cluster_block_means(K, _ptr(simsum), _ptr(npairs), _ptr(out)))
+    return out
+
+
+def pairwise_rand_ratio(tab, adjusted=True):
+    """ccg_pairwise_rand_ratio: pairwiseRand(mode="ratio") from a K x (C+1) table."""
+    tab = np.ascontiguousarray(tab, dtype=np.int32)
+    K, W = tab.shape
+    out = np.empty((K, K), np.float64)
+    check(_lib.load().ccg_pairwise_rand_ratio(K, W - 1, _ptr(tab), 1 if adjusted else 0, _ptr(out)))
+    return out

@@ -33,6 +33,11 @@
  *       (:411-421).
  *   ccg_consensus_knn[_assign]      : dbscan::kNN(jaccardDist, k)$id (:425).
  *
+ *   ccg_cluster_block_sums          : determineHierachy(as.matrix(jaccardDist), ...)
+ *       block means (:463, :699-721).
+ *   ccg_contingency                 : the counting of bluster::pairwiseRand
+ *       (:470-474).
+ *
  * Errors found by a kernel on the device (a label wider than the assignment
  * matrix, an invalid SNN neighbour index) are sticky in the context and are
  * returned by the next ccg_synchronize / ccg_check_errors call.
@@ -263,6 +268,39 @@ int ccg_consensus_knn_assign_dev(ccg_ctx* ctx, const void* A, int label_bits,
                                  int64_t N, int64_t B, int k, int64_t r0,
                                  int64_t r1, int32_t* out_idx,
                                  int32_t* d_nan_flag, void* stream);
+
+/* ------------------------------------- cluster distances and stability -- */
+/* determineHierachy(as.matrix(jaccardDist), f, return="distance")
+ * (R/consensusClust.R:463, :585, :621, :699-721) without the N x N matrix.
+ * f: N cluster positions in [0, K) (device for _dev).  For every packed pair
+ * i < j with both_ij > 0 (NaN pairs are dropped, na.rm=TRUE):
+ *   simsum[2 (f_i K + f_j) + {0, 1}] += sim_ij * 2^39 as a 128-bit (lo, hi)
+ *       integer, sim_ij = (float)co_ij / (float)both_ij (exact: every such
+ *       ratio is a multiple of 2^-39);
+ *   npairs[f_i K + f_j] += 1.
+ * The sums are exact, so merging clusters is adding entries.  N < 2^24. */
+int ccg_cluster_block_sums(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B,
+                           const int32_t* f, int K, uint64_t* simsum, int64_t* npairs);
+int ccg_cluster_block_sums_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B,
+                               const int32_t* f, int K, uint64_t* simsum, int64_t* npairs, void* stream);
+/* Host-only: the K x K determineHierachy matrix from the sums: diagonal 0,
+ * out[p][q] = mean of D = 1 - sim over the pairs between p and q (both
+ * orientations), NaN if there are none. */
+int ccg_cluster_block_means(int K, const uint64_t* simsum, const int64_t* npairs, double* out);
+/* Contingency of every bootstrap column against a clustering -- the counting
+ * inside bluster::pairwiseRand(f[mask], A[, b][mask]) (:470-474):
+ * tab[(b K + p)(C + 1) + a] = #{i : f_i = p, A_bi = a}, a = 0..C (0 = not
+ * sampled).  A label above C raises the sticky CCG_ERANGE. */
+int ccg_contingency(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, const int32_t* f,
+                    int K, int C, int32_t* tab);
+int ccg_contingency_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B,
+                        const int32_t* f, int K, int C, int32_t* tab, void* stream);
+/* Host-only: pairwiseRand(mode="ratio", adjusted) from one K x (C+1) table
+ * (column 0 ignored): diagonal = fraction of the pairs inside ref cluster p
+ * that share an alt cluster, off-diagonal = fraction of the pairs across p
+ * and q that alt splits; adjusted: (obs - E) / (total - E) with E under
+ * random alt labels.  0/0 -> NaN. */
+int ccg_pairwise_rand_ratio(int K, int C, const int32_t* tab, int adjusted, double* out);
 
 /* ------------------------------------------------------------ multi-GPU -- */
 /* A device group: one context (stream + workspaces) per device and one RCCL

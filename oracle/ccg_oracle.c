@@ -44,6 +44,12 @@
  *                      j (full rows, j = i included), from the engine's
  *                      encoding of clustAssignments (:404-408): uint8/uint16
  *                      codes with 0 = NA.
+ *  - orc_block_means : determineHierachy(as.matrix(jaccardDist), f,
+ *                      return="distance")                      :463, :699-721
+ *                      mean(distanceMatrix[c1, c2], na.rm=TRUE) with R's
+ *                      two-pass long-double mean, once per unordered pair.
+ *  - orc_contingency : table(ref, alt) per bootstrap column -- the counting
+ *                      inside bluster::pairwiseRand(ref, alt)      :473-474
  */
 #include <math.h>
 #include <stdint.h>
@@ -576,5 +582,88 @@ int orc_cocluster_rows(const void* A, int label_bits, int64_t N, int64_t B, cons
             }
         }
     }
+    return ORC_OK;
+}
+
+/* ---- determineHierachy block means (R/consensusClust.R:699-721) -------- */
+/* dist packed as orc_cocluster.  f: N cluster positions 0..K-1 in
+ * unique(assignments) order.  out (K x K, row-major): diagonal 0 (the matrix
+ * starts at 0 and the diagonal is never written, :702-704); for p < q
+ * (clust1 = p visited first, :707-716) out[p][q] = out[q][p] =
+ * mean(distanceMatrix[which(f == p), which(f == q)], na.rm = TRUE): the
+ * submatrix in column-major order, NaN dropped, R's mean (long-double sum,
+ * divide, one long-double correction pass; summary.c).  Empty -> NaN. */
+int orc_block_means(const double* dist, int64_t N, const int32_t* f, int K, double* out, int nthreads) {
+    if (N < 1 || K < 1) return ORC_EINVAL;
+    for (int64_t i = 0; i < N; ++i)
+        if (f[i] < 0 || f[i] >= K) return ORC_EINVAL;
+    int64_t* cnt = (int64_t*)calloc((size_t)K, sizeof(int64_t));
+    int64_t* start = (int64_t*)calloc((size_t)K + 1, sizeof(int64_t));
+    int64_t* members = (int64_t*)malloc(sizeof(int64_t) * (size_t)N);
+    if (!cnt || !start || !members) {
+        free(cnt); free(start); free(members);
+        return ORC_ENOMEM;
+    }
+    for (int64_t i = 0; i < N; ++i) cnt[f[i]]++;
+    for (int c = 0; c < K; ++c) start[c + 1] = start[c] + cnt[c];
+    for (int c = 0; c < K; ++c) cnt[c] = 0;
+    for (int64_t i = 0; i < N; ++i) members[start[f[i]] + cnt[f[i]]++] = i;  /* which(): ascending */
+    for (int64_t t = 0; t < (int64_t)K * K; ++t) out[t] = 0.0;
+    set_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) collapse(2)
+    for (int p = 0; p < K; ++p)
+        for (int q = 0; q < K; ++q) {
+            if (q <= p) continue;
+            const int64_t* rp = members + start[p];
+            const int64_t* rq = members + start[q];
+            const int64_t np_ = start[p + 1] - start[p], nq = start[q + 1] - start[q];
+#define ORC_D(i, j) dist[((i) < (j) ? (i) : (j)) * N - ((i) < (j) ? (i) : (j)) * (((i) < (j) ? (i) : (j)) + 1) / 2 + \
+                         ((i) < (j) ? (j) : (i)) - ((i) < (j) ? (i) : (j)) - 1]
+            long double s = 0.0L;
+            int64_t n = 0;
+            for (int64_t b = 0; b < nq; ++b)      /* columns: clust2 samples */
+                for (int64_t a = 0; a < np_; ++a) {  /* rows: clust1 samples */
+                    double v = ORC_D(rp[a], rq[b]);
+                    if (isnan(v)) continue;
+                    s += v;
+                    ++n;
+                }
+            double m;
+            if (n == 0) {
+                m = NAN;
+            } else {
+                s /= (long double)n;
+                if (isfinite((double)s)) {
+                    long double t = 0.0L;
+                    for (int64_t b = 0; b < nq; ++b)
+                        for (int64_t a = 0; a < np_; ++a) {
+                            double v = ORC_D(rp[a], rq[b]);
+                            if (!isnan(v)) t += (v - s);
+                        }
+                    s += t / (long double)n;
+                }
+                m = (double)s;
+            }
+#undef ORC_D
+            out[(int64_t)p * K + q] = m;
+            out[(int64_t)q * K + p] = m;
+        }
+    free(cnt); free(start); free(members);
+    return ORC_OK;
+}
+
+/* ---- contingency tables of each bootstrap column vs a clustering ------ */
+/* A: B x N codes (uint8/uint16, 0 = NA); f: N reference positions 0..K-1.
+ * tab[(b*K + p)*(C+1) + a] = #{i : f_i = p, A_bi = a}, a = 0..C. */
+int orc_contingency(const void* A, int label_bits, int64_t N, int64_t B, const int32_t* f, int K, int C,
+                    int32_t* tab) {
+    if (N < 1 || B < 1 || K < 1 || C < 0 || (label_bits != 8 && label_bits != 16)) return ORC_EINVAL;
+    memset(tab, 0, sizeof(int32_t) * (size_t)(B * K * (C + 1)));
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t i = 0; i < N; ++i) {
+            int a = label_bits == 8 ? ((const uint8_t*)A)[b * N + i] : ((const uint16_t*)A)[b * N + i];
+            if (a > C || f[i] < 0 || f[i] >= K) return ORC_EINVAL;
+            tab[(b * K + f[i]) * (C + 1) + a]++;
+        }
     return ORC_OK;
 }

@@ -17,6 +17,7 @@ __all__ = [
     "cocluster", "consensus_knn", "robust_choice", "consensus_choice",
     "py_knn", "py_snn", "py_cocluster", "packed_index", "RES_RANGE", "K_NUM",
     "robust_score", "consensus_score", "knn_queries", "cocluster_rows",
+    "block_means", "contingency", "pairwise_rand_ratio",
 ]
 
 # consensusClust defaults, R/consensusClust.R:126-127
@@ -46,9 +47,11 @@ def lib():
         L.orc_consensus_knn.argtypes = [p, i64, i32, p, i32]
         L.orc_knn_queries.argtypes = [p, i64, i32, i32, p, i64, p, p, i32]
         L.orc_cocluster_rows.argtypes = [p, i32, i64, i64, p, i64, p, p, i32]
+        L.orc_block_means.argtypes = [p, i64, p, i32, p, i32]
+        L.orc_contingency.argtypes = [p, i32, i64, i64, p, i32, i32, p]
         for f in (L.orc_gather_rows, L.orc_knn, L.orc_snn, L.orc_silhouette,
                   L.orc_mapback, L.orc_cocluster, L.orc_consensus_knn,
-                  L.orc_knn_queries, L.orc_cocluster_rows):
+                  L.orc_knn_queries, L.orc_cocluster_rows, L.orc_block_means, L.orc_contingency):
             f.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -286,3 +289,56 @@ def py_cocluster(A):
             dist[o] = 1.0 - float(q)
             o += 1
     return {"co": co, "both": both, "dist": dist}
+
+
+def block_means(dist, N, f, K, nthreads=0):
+    """determineHierachy(as.matrix(jaccardDist), assignments, return="distance")
+    (:699-721) with f = positions 0..K-1 in unique(assignments) order."""
+    dist = np.ascontiguousarray(dist, dtype=np.float64)
+    f = np.ascontiguousarray(f, dtype=np.int32)
+    out = np.empty((K, K), np.float64)
+    _check(lib().orc_block_means(_ptr(dist), N, _ptr(f), K, _ptr(out), nthreads), "block_means")
+    return out
+
+
+def contingency(A, f, K, C=None):
+    """table(f, A[b, ]) for every bootstrap column b: (B, K, C+1) int32."""
+    A = np.ascontiguousarray(A)
+    B, N = A.shape
+    C = int(A.max()) if C is None else C
+    f = np.ascontiguousarray(f, dtype=np.int32)
+    tab = np.empty((B, K, C + 1), np.int32)
+    _check(lib().orc_contingency(_ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(f), K, C, _ptr(tab)), "contingency")
+    return tab
+
+
+def pairwise_rand_ratio(tab, adjusted=True):
+    """bluster::pairwiseRand(ref, alt, mode="ratio", adjusted) from the
+    contingency table(ref, alt) (K ref levels x alt levels), :470-474.
+
+    PARITY UNPINNED: bluster is absent; restated from its documented
+    definition -- diagonal: fraction of the C(n_p, 2) pairs inside ref cluster
+    p that share an alt cluster; off-diagonal: fraction of the n_p n_q pairs
+    across p and q that are split in alt; adjusted: (obs - E)/(total - E)
+    with E the expectation under random alt labels (p_same = sum_a C(n_a, 2) /
+    C(n, 2)).  0/0 -> NaN."""
+    t = np.asarray(tab, dtype=np.float64)
+    c2 = lambda x: x * (x - 1.0) / 2.0
+    n_p = t.sum(1)
+    n_a = t.sum(0)
+    n = t.sum()
+    p_same = c2(n_a).sum() / c2(n) if n > 1 else np.nan
+    K = t.shape[0]
+    out = np.empty((K, K))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        for p in range(K):
+            for q in range(K):
+                if p == q:
+                    obs, tot = c2(t[p]).sum(), c2(n_p[p])
+                    exp = tot * p_same
+                else:
+                    tot = n_p[p] * n_p[q]
+                    obs = tot - (t[p] * t[q]).sum()
+                    exp = tot * (1.0 - p_same)
+                out[p, q] = (obs - exp) / (tot - exp) if adjusted else obs / tot
+    return out

@@ -1,0 +1,178 @@
+"""Cluster distances and bootstrap stability after the consensus choice
+(R/consensusClust.R:458-497) on the GPU, against the
+oracle: determineHierachy block means from exact block sums, pairwiseRand
+contingency tables, and the whole merge step against a literal restatement
+of the reference's R loop on the materialised distance matrix."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _A(rng, B, N, C=6, na=0.25, dtype=np.uint8):
+    A = rng.integers(1, C + 1, (B, N)).astype(dtype)
+    A[rng.random((B, N)) < na] = 0
+    return A
+
+
+def _oracle_dist(A):
+    Ao = A.astype(np.int32)
+    Ao[Ao == 0] = -1
+    return O.cocluster(Ao, want=("co", "both", "dist"))
+
+
+def _exact_sums_from_counts(co, both, f, N, K):
+    """sum of sim * 2^39 per (f_i, f_j), i < j, from the oracle counts (exact in
+    int64 at these sizes: < 2^40 per pair, < 2^17 pairs)."""
+    iu, ju = np.triu_indices(N, 1)
+    ok = both > 0
+    sim = (co[ok].astype(np.float32) / both[ok].astype(np.float32)).astype(np.float32)
+    fx = (sim.astype(np.float64) * 2.0 ** 39).astype(np.int64)
+    key = f[iu[ok]].astype(np.int64) * K + f[ju[ok]]
+    S = np.zeros(K * K, np.int64)
+    np.add.at(S, key, fx)
+    n = np.bincount(key, minlength=K * K).astype(np.int64)
+    return S.reshape(K, K), n.reshape(K, K)
+
+
+@pytest.mark.parametrize("B,N,K,dtype", [(40, 700, 5, np.uint8), (25, 513, 300, np.uint8),
+                                         (17000, 300, 4, np.uint8), (30, 640, 9, np.uint16)])
+def test_block_sums_exact_and_means_match_oracle(engine, B, N, K, dtype):
+    from consensusclustr_amd.engine import cluster_block_means
+    rng = np.random.default_rng(B + N + K)
+    A = _A(rng, B, N, C=300 if dtype == np.uint16 else 6, dtype=dtype)
+    f = rng.integers(0, K, N).astype(np.int32)
+    simsum, npairs = engine.cluster_block_sums(A, f, K)
+    ref = _oracle_dist(A)
+    S, n = _exact_sums_from_counts(ref["co"], ref["both"], f, N, K)
+    assert np.array_equal(npairs, n)
+    assert not simsum[:, :, 1].any()  # high words: sums stay below 2^64 at these sizes
+    assert np.array_equal(simsum[:, :, 0].astype(np.int64), S)  # exact integer sums
+    if K <= 12:
+        means = cluster_block_means(simsum, npairs)
+        want = O.block_means(ref["dist"], N, f, K)
+        assert np.allclose(means, want, rtol=4e-16, atol=0, equal_nan=True)
+
+
+def test_block_sums_bad_cluster_index_is_reported(engine):
+    from consensusclustr_amd._lib import CcgError
+    rng = np.random.default_rng(3)
+    A = _A(rng, 10, 300)
+    f = np.zeros(300, np.int32)
+    f[7] = 9
+    with pytest.raises(CcgError, match="EINVAL"):
+        engine.cluster_block_sums(A, f, 4)
+
+
+@pytest.mark.parametrize("B,N,K,C,dtype", [(50, 3000, 6, 8, np.uint8), (7, 1000, 40, 400, np.uint16),
+                                           (300, 257, 3, 2, np.uint8)])
+def test_contingency_matches_oracle(engine, B, N, K, C, dtype):
+    rng = np.random.default_rng(B * K)
+    A = _A(rng, B, N, C=C, dtype=dtype)
+    f = rng.integers(0, K, N).astype(np.int32)
+    assert np.array_equal(engine.contingency(A, f, K, C), O.contingency(A, f, K, C))
+
+
+def test_contingency_label_above_C_is_reported(engine):
+    from consensusclustr_amd._lib import CcgError
+    A = np.array([[1, 2, 5, 1]], np.uint8)
+    with pytest.raises(CcgError, match="ERANGE"):
+        engine.contingency(A, np.zeros(4, np.int32), 1, 3)
+
+
+# ------------------------------------------- literal restatement of :458-497
+def _r_table_levels(lab, is_char):
+    vals = sorted(set(lab))
+    return sorted(vals, key=str) if is_char else vals
+
+
+def _literal_merge(final, A, D, N, kNum, minStability):
+    """R/consensusClust.R:458-497 statement by statement on the materialised
+    distance (oracle block means, oracle contingency, oracle ratio)."""
+    f = [int(v) for v in final]
+    is_char = False
+    if len(set(f)) <= 1:
+        return np.array(f), None
+    while True:  # :462-467
+        levels = _r_table_levels(f, is_char)
+        counts = [f.count(v) for v in levels]
+        if min(counts) >= max(kNum[0], 20):
+            break
+        small = levels[counts.index(min(counts))]
+        uniq = list(dict.fromkeys(f))
+        fpos = np.array([uniq.index(v) for v in f], np.int32)
+        cd = O.block_means(D, N, fpos, len(uniq))
+        np.fill_diagonal(cd, 1.0)
+        row = cd[uniq.index(small)]
+        j = int(np.nanargmin(row))
+        f = [uniq[j] if v == small else v for v in f]
+        is_char = True
+    levels = _r_table_levels(f, is_char)  # :470-481
+    mats = []
+    for b in range(A.shape[0]):
+        mask = A[b] != 0
+        ref = [v for v, m in zip(f, mask) if m]
+        present = [v for v in levels if v in set(ref)]
+        alt = A[b][mask]
+        tab = np.array([[sum(1 for r, a in zip(ref, alt) if r == p and a == c) for c in range(1, int(A.max()) + 1)]
+                        for p in present])
+        mats.append(O.pairwise_rand_ratio(tab))
+    if len({m.shape for m in mats}) != 1:
+        return np.ones(len(f), np.int64), None
+    arr = np.stack(mats)
+    K = arr.shape[1]
+    stab = np.empty((K, K))
+    for i in range(K):
+        for j in range(K):
+            v = arr[:, i, j][~np.isnan(arr[:, i, j])]
+            stab[i, j] = math.fsum(v) / v.size if v.size else np.nan
+    np.fill_diagonal(stab, 1.0)
+    stab[np.isnan(stab)] = 1.0
+    f = np.array(f)
+    while stab.min() < minStability:  # :489-495
+        hits = np.argwhere(stab.T == stab.min())[:, ::-1]  # (row, col) in column-major order
+        flat = list(hits[:, 0] + 1) + list(hits[:, 1] + 1)
+        c1, c2 = flat[0], flat[1]
+        f[f == c2] = c1
+        stab[c1 - 1, c2 - 1] = stab[c2 - 1, c1 - 1] = 1.0
+    return f, stab
+
+
+def _blocky(rng, N, B, C, flip):
+    """Assignments with C true groups (two of them small) and per-bootstrap noise."""
+    truth = rng.integers(0, C, N)
+    truth[:12] = C        # a 12-cell group -> small-cluster merge
+    truth[12:20] = C + 1  # an 8-cell group
+    A = np.zeros((B, N), np.uint8)
+    for b in range(B):
+        perm = rng.permutation(C + 2) + 1
+        lab = perm[truth]
+        noisy = rng.random(N) < flip
+        lab[noisy] = rng.integers(1, C + 3, noisy.sum())
+        lab[rng.random(N) < 0.3] = 0
+        A[b] = lab
+    return truth, A
+
+
+@pytest.mark.parametrize("seed,flip", [(1, 0.05), (2, 0.3), (3, 0.6)])
+def test_merge_unstable_clusters_matches_literal_restatement(engine, seed, flip):
+    from consensusclustr_amd.consensus import merge_unstable_clusters
+    rng = np.random.default_rng(seed)
+    N, B, C = 400, 40, 5
+    truth, A = _blocky(rng, N, B, C, flip)
+    final = truth + 1
+    # some leiden-like relabelling: membership ids by first appearance
+    _, inv = np.unique(final, return_inverse=True)
+    final = inv + 1
+    D = _oracle_dist(A)["dist"]
+    got = merge_unstable_clusters(final, A, (10, 15, 20), 0.175, engine)
+    want_f, want_stab = _literal_merge(final, A, D, N, (10, 15, 20), 0.175)
+    assert np.array_equal(got["assignments"], want_f)
+    if want_stab is None:
+        assert got["stability"] is None
+    else:
+        assert np.allclose(got["stability"], want_stab, rtol=1e-14, atol=0)

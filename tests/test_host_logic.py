@@ -117,3 +117,79 @@ def test_row_slabs_formula():
     N, G = 100000, 8
     want = [0] + [int(round(N * (1 - math.sqrt(1 - g / G)) / 128)) * 128 for g in range(1, G)] + [N]
     assert row_slabs(N, G) == want
+
+
+def test_pairwise_rand_ratio_matches_oracle_restatement():
+    """libccg's host ratio (ccg_pairwise_rand_ratio) == the oracle's numpy restatement, bitwise."""
+    import oracle as O
+    from consensusclustr_amd.engine import pairwise_rand_ratio
+    rng = np.random.default_rng(5)
+    for K, C in [(2, 3), (5, 9), (7, 1), (3, 12)]:
+        tab = rng.integers(0, 40, (K, C + 1)).astype(np.int32)
+        tab[rng.integers(0, K), 1:] = 0  # a ref cluster with no sampled cells -> NaN entries
+        for adj in (True, False):
+            got = pairwise_rand_ratio(tab, adj)
+            want = O.pairwise_rand_ratio(tab[:, 1:], adj)
+            assert np.array_equal(got, want, equal_nan=True)
+
+
+def test_pairwise_rand_ratio_known_values():
+    """Hand-computed: ref {0: 4 cells, 1: 2 cells}; alt puts 3 of cluster 0 together."""
+    from consensusclustr_amd.engine import pairwise_rand_ratio
+    tab = np.array([[0, 3, 1], [0, 0, 2]], np.int32)  # column 0 = unsampled
+    r = pairwise_rand_ratio(tab, adjusted=False)
+    assert r[0, 0] == 3 / 6          # C(3,2) of C(4,2) pairs stay together
+    assert r[1, 1] == 1.0            # the 2 cells of cluster 1 stay together
+    assert r[0, 1] == (8 - 2) / 8    # 8 cross pairs, 2 share alt cluster 2
+    assert r[0, 1] == r[1, 0]
+
+
+def test_cluster_block_means_exact():
+    """ccg_cluster_block_means from 128-bit sums: symmetrised, diag 0, NaN when empty,
+    equal to the correctly rounded rational mean."""
+    from fractions import Fraction
+    from consensusclustr_amd.engine import cluster_block_means
+    rng = np.random.default_rng(9)
+    K = 4
+    sims = {}
+    simsum = np.zeros((K, K, 2), np.uint64)
+    npairs = np.zeros((K, K), np.int64)
+    for p in range(K):
+        for q in range(K):
+            if p == 3 or q == 3:
+                continue  # cluster 3 has no co-sampled pairs
+            co = rng.integers(0, 50, 200)
+            both = rng.integers(50, 60000, 200)
+            s = [int(np.float32(np.float32(c) / np.float32(b)) * np.float32(2.0 ** 39)) for c, b in zip(co, both)]
+            tot = sum(s) * 3000  # large totals exercise the high word
+            simsum[p, q, 0] = tot & ((1 << 64) - 1)
+            simsum[p, q, 1] = tot >> 64
+            npairs[p, q] = 200 * 3000
+            sims[p, q] = (tot, 200 * 3000)
+    out = cluster_block_means(simsum, npairs)
+    assert np.all(np.diag(out) == 0)
+    assert np.isnan(out[0, 3]) and np.isnan(out[3, 1])
+    for p in range(3):
+        for q in range(3):
+            if p == q:
+                continue
+            s = sims[p, q][0] + sims[q, p][0]
+            n = sims[p, q][1] + sims[q, p][1]
+            want = float(1 - Fraction(s, n << 39))
+            assert abs(out[p, q] - want) <= np.spacing(want)
+            assert out[p, q] == out[q, p]
+
+
+def test_stability_merge_follows_the_reference_index_rule():
+    """which(stab == min, arr.ind=TRUE) -> rows of the first two column-major matches;
+    labels EQUAL to those 1-based positions are merged (R/consensusClust.R:489-495)."""
+    from consensusclustr_amd.consensus import stability_merge
+    stab = np.ones((3, 3))
+    stab[0, 2] = stab[2, 0] = 0.1
+    f = np.array([1, 1, 2, 3, 3, 2])
+    A = np.array([[1, 3, 3, 2, 0, 1]], np.uint8)
+    f2, A2, s2 = stability_merge(f, A, stab, 0.175)
+    # matches in column-major order: (3,1) then (1,3) -> merge label 1 into label 3
+    assert f2.tolist() == [3, 3, 2, 3, 3, 2]
+    assert A2.tolist() == [[3, 3, 3, 2, 0, 3]]
+    assert s2.min() == 1.0

@@ -139,3 +139,39 @@ def test_cocluster_rows_equals_packed_triangle(dtype):
             o = O.packed_index(min(i, j), max(i, j), N)
             assert co[t, j] == ref["co"][o] and both[t, j] == ref["both"][o]
         assert both[t, i] == B - (A[:, i] == 0).sum()  # the diagonal: sampled count
+
+
+def test_block_means_vs_literal_restatement():
+    """orc_block_means == determineHierachy(as.matrix(D), f, "distance") restated
+    with numpy on the square matrix (within an ulp: R's two-pass long-double mean)."""
+    from fractions import Fraction
+    rng = np.random.default_rng(11)
+    B, N = 30, 160
+    A = rng.integers(-1, 5, (B, N)).astype(np.int32)
+    D = O.cocluster(A, want=("dist",))["dist"]
+    sq = np.zeros((N, N))
+    iu = np.triu_indices(N, 1)
+    sq[iu] = D
+    sq = sq + sq.T
+    f = rng.integers(0, 6, N).astype(np.int32)
+    got = O.block_means(D, N, f, 6)
+    for p in range(6):
+        assert got[p, p] == 0
+        for q in range(6):
+            if p == q:
+                continue
+            blk = sq[np.ix_(f == p, f == q)].ravel()
+            blk = blk[~np.isnan(blk)]
+            want = float(sum(Fraction(x) for x in blk) / len(blk))
+            assert abs(got[p, q] - want) <= np.spacing(want)
+
+
+def test_contingency_vs_numpy():
+    rng = np.random.default_rng(12)
+    A = rng.integers(0, 7, (9, 300)).astype(np.uint8)
+    f = rng.integers(0, 4, 300).astype(np.int32)
+    tab = O.contingency(A, f, 4, 6)
+    for b in range(9):
+        for p in range(4):
+            for a in range(7):
+                assert tab[b, p, a] == np.sum((f == p) & (A[b] == a))
