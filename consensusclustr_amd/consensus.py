@@ -371,3 +371,53 @@ def merge_unstable_clusters(final, A, kNum=K_NUM, minStability=0.175, engine=Non
         return {"assignments": np.ones_like(f), "stability": None, "clustAssignments": A}
     f, A2, stab = stability_merge(f, A, stab, minStability)
     return {"assignments": f, "stability": stab, "clustAssignments": A2}
+
+
+# ------------------------------------------------ null-simulation test --
+# testSplits / generateNullStatistic (R/consensusClust.R:759-814, :891-964).
+# The null count matrices come from scDesign3 (R, host) and their PCA from
+# prcomp_irlba; the engine clusters all null PC matrices of one test together:
+# ONE batched kNN over the simulations (ccg_knn_segments), then per
+# simulation the SNN graphs, host clustering and one batched silhouette over
+# the 3 x 19 candidate clusterings.
+NULL_RES_RANGE = np.concatenate([np.arange(0.01, 0.3 + 1e-12, 0.03), np.arange(0.3, 2 + 1e-12, 0.2)])  # :803
+
+
+def null_statistics(pca_nulls, kNum=K_NUM, clusterFun="leiden", resRange=NULL_RES_RANGE, minSize=5, seed=123,
+                    engine=None):
+    """generateNullStatistic (:796-813) for every null PC matrix: the mean
+    approxSilhouette of getClustAssignments(pcaNull, robust, minSize=5), 0 if
+    the PCA failed (None / all NaN) or one cluster was chosen."""
+    eng = engine or default_engine()
+    fn = _cluster_fn(clusterFun)
+    kmax = max(kNum)
+    ok = [t for t, p in enumerate(pca_nulls) if p is not None and not np.all(np.isnan(np.asarray(p, np.float64)))]
+    out = np.zeros(len(pca_nulls))
+    if not ok:
+        return out
+    mats = [np.asarray(pca_nulls[t], np.float64) for t in ok]
+    knns = eng.knn_segments(mats, kmax=kmax, want_dist=False)  # every simulation in one set of launches
+    for t, X, (knn, _) in zip(ok, mats, knns):
+        n = X.shape[0]
+        labels = []
+        for k in kNum:  # getClustAssignments' k-outer / resolution-inner loop (:653-654)
+            ei, ej, w = eng.snn(np.ascontiguousarray(knn), k, "number")
+            for res in resRange:
+                labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
+        lab = np.stack(labels)
+        means, nclust, minsize, _ = eng.silhouette(X, lab)
+        choice = robust_choice(robust_scores(means, nclust, minsize, minSize))
+        out[t] = 0.0 if nclust[choice] < 2 else means[choice]  # :806-811 (same labels, same mean)
+    return out
+
+
+def null_test_pvalue(silhouette, null_scores):
+    """fitdistr(nullDist, 'normal') (MLE: mean, sd with divisor n) and
+    1 - pnorm(silhouette, mean, sd) (:939-940)."""
+    import math
+    x = np.asarray(null_scores, np.float64)
+    mu = math.fsum(x) / x.size
+    sd = math.sqrt(math.fsum((x - mu) ** 2) / x.size)
+    if sd == 0.0:
+        return 0.0 if silhouette > mu else 1.0
+    return 1.0 - 0.5 * math.erfc(-((silhouette - mu) / sd) / math.sqrt(2.0))

@@ -120,3 +120,34 @@ def test_consensus_cluster_matches_oracle_pipeline(engine, pca):
     choice = O.consensus_choice(scores)
     assert got["choice"] == choice
     assert np.array_equal(got["assignments"], finals[choice])
+
+
+def test_null_statistics_match_oracle_pipeline(engine):
+    """generateNullStatistic's clustering + silhouette (:796-813) for a batch of
+    null PC matrices (one batched kNN) vs the oracle run per simulation."""
+    from consensusclustr_amd.consensus import NULL_RES_RANGE, null_statistics, null_test_pvalue
+    rng = np.random.default_rng(77)
+    nulls = [rng.normal(size=(int(n), d)) for n, d in [(600, 5), (750, 5), (420, 8), (900, 3)]]
+    nulls.insert(2, None)  # a failed prcomp_irlba -> score 0
+    got = null_statistics(nulls, kNum=KNUM, clusterFun=components, engine=engine)
+    want = []
+    for X in nulls:
+        if X is None:
+            want.append(0.0)
+            continue
+        idx, _ = O.knn(X, max(KNUM))
+        labs, scores, means, ncl = [], [], [], []
+        for k in KNUM:
+            ei, ej, w = O.snn(idx, k, "number")
+            for res in NULL_RES_RANGE:
+                lab = components(X.shape[0], ei, ej, w, float(res), 123)
+                _, m, C = O.silhouette(X, lab)
+                ok = np.bincount(lab)[1:].min() > 5
+                scores.append(O.robust_score(C, m, ok))
+                means.append(m)
+                ncl.append(C)
+        c = O.robust_choice(scores)
+        want.append(0.0 if ncl[c] < 2 else means[c])
+    assert np.allclose(got, want, rtol=1e-5, atol=0)
+    p = null_test_pvalue(0.5, got)
+    assert 0.0 <= p <= 1.0

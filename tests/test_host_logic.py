@@ -193,3 +193,13 @@ def test_stability_merge_follows_the_reference_index_rule():
     assert f2.tolist() == [3, 3, 2, 3, 3, 2]
     assert A2.tolist() == [[3, 3, 3, 2, 0, 3]]
     assert s2.min() == 1.0
+
+
+def test_null_test_pvalue_is_normal_mle_tail():
+    """fitdistr(x, 'normal') (MLE sd, divisor n) + 1 - pnorm (:939-940)."""
+    from scipy.stats import norm
+    from consensusclustr_amd.consensus import null_test_pvalue
+    x = np.array([0.21, 0.25, 0.19, 0.3, 0.22, 0.27, 0.24, 0.2, 0.26, 0.23])
+    mu, sd = x.mean(), x.std()  # numpy std: divisor n
+    for s in (0.1, 0.24, 0.31, 0.5):
+        assert abs(null_test_pvalue(s, x) - norm.sf(s, mu, sd)) < 1e-12
