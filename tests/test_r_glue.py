@@ -1,0 +1,77 @@
+"""Structural checks of the R binding (src/ccg_r.c + R/ccg.R), which cannot be
+run here (no R): the glue type-checks against include/ccg.h and an R-API
+declaration stub, every libccg function it calls is declared in ccg.h, every
+.Call entry point is registered with its true arity, and every C_ symbol the
+R code uses is registered with the number of arguments it passes."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from consensusclustr_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GLUE = os.path.join(ROOT, "src", "ccg_r.c")
+RCODE = os.path.join(ROOT, "R", "ccg.R")
+
+
+def _glue():
+    return open(GLUE).read()
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc missing")
+def test_glue_type_checks_against_header():
+    r = subprocess.run(["gcc", "-fsyntax-only", "-std=c11", "-Wall", "-Werror", "-Wno-cast-function-type",
+                        "-I", os.path.join(ROOT, "tests", "r_stub"), "-I", os.path.join(ROOT, "include"), GLUE],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_glue_calls_only_declared_entry_points():
+    declared = set(_lib.header_symbols())
+    called = set(re.findall(r"\b(ccg_(?!r_)\w+)\s*\(", _glue()))
+    called -= {"ccg_ctx", "ccg_group", "ccg_config", "ccg_knn_stats"}
+    assert called, "no libccg calls found"
+    assert called <= declared, sorted(called - declared)
+
+
+def _registered():
+    return {m.group(1): int(m.group(2))
+            for m in re.finditer(r'\{"(ccg_r_\w+)",\s*\(DL_FUNC\)&\1,\s*(\d+)\}', _glue())}
+
+
+def test_every_call_entry_point_is_registered_with_its_arity():
+    text = _glue()
+    defs = {m.group(1): m.group(2) for m in re.finditer(r"^SEXP (ccg_r_\w+)\(([^)]*)\)", text, re.M)}
+    reg = _registered()
+    assert set(defs) == set(reg)
+    for name, args in defs.items():
+        n = 0 if args.strip() in ("", "void") else args.count(",") + 1
+        assert reg[name] == n, name
+
+
+def test_r_code_uses_registered_symbols_with_matching_arity():
+    reg = _registered()
+    code = open(RCODE).read()
+    calls = re.findall(r"\.Call\(C_(ccg_r_\w+)((?:[^()]|\([^()]*(?:\([^()]*\)[^()]*)*\))*)\)", code)
+    assert calls
+    for name, rest in calls:
+        assert name in reg, name
+        depth, nargs = 0, 0
+        for ch in rest:
+            if ch in "([":
+                depth += 1
+            elif ch in ")]":
+                depth -= 1
+            elif ch == "," and depth == 0:
+                nargs += 1
+        assert nargs == reg[name], (name, nargs, reg[name])
+
+
+def test_r_code_covers_the_replaced_seams():
+    code = open(RCODE).read()
+    for fn in ("getClustAssignments", "ccgConsensusCore", "ccgConsensusKNN", "ccgJaccardDist",
+               "ccgClusterDistance", "ccgStabilityMatrix", "ccgSilhouetteMeans", "ccgNullStatistics"):
+        assert re.search(rf"^{fn} <- function\(", code, re.M), fn
