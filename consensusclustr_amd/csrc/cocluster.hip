@@ -120,15 +120,16 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
     }
 }
 
-// Fragment table (LDS, 34 x 16 B): entry i < 16 = one-hot byte i; 16 + i =
-// flag (-128 in byte 0) + one-hot byte i (i >= 1); 32 = flag only; 33 = zero.
-// A fragment is one ds_read_b128 after ~6 VALU to pick the entry.
-#define COF_TAB 34
-__device__ __forceinline__ int cof_entry(int lab, int sub) {
-    const int pos = lab - 16 * sub;
-    const int e0 = lab < 16 ? 16 + lab : 32;        // slot 0: flag (+ label if it fits)
-    const int e1 = (unsigned)pos < 16u ? pos : 33;  // later slots: label or nothing
-    return lab == 0 ? 33 : (sub == 0 ? e0 : e1);
+// Fragment table (LDS, 36 x 16 B), indexed by off + med3(lab - 16 sub, -1, 16):
+//   slots sub >= 1 (off 1):  entry 0 / 17 = zero (label below / above the
+//       slot), 1 + x = one-hot byte x (x = 0..15);
+//   slot 0 (off 19):  entry 19 = zero (lab 0, not sampled), 19 + lab = flag
+//       (-128 in byte 0) + one-hot byte lab (lab = 1..15), 35 = flag only.
+// A fragment is one ds_read_b128 after 3 VALU (sub, med3, shift-add); the
+// per-slot 16 sub and entry offset are computed once per K-step.
+#define COF_TAB 36
+__device__ __forceinline__ int cof_entry(int lab, int sub16, int off) {
+    return off + min(max(lab - sub16, -1), 16);
 }
 
 // Output modes: packed upper triangle of rows [r0, r1) (R "dist" order), or
@@ -185,52 +186,81 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0;
 
     // stage loader: dword p of the panel = (column c, row dword rd); rows past
-    // N read clamped rows (their outputs are masked in the epilogue)
+    // N read clamped rows (their outputs are masked in the epilogue).  The
+    // column indices of stage st+1 are fetched while stage st is issued, so
+    // a stage's label loads never wait on the column table; every load is
+    // unconditional (ccol has >= COF_SLOTS readable entries past any stage
+    // start; columns c >= nc are zeroed after the load).
+    // Stage loader.  Every value loaded in an iteration is first used at that
+    // iteration's commit, after the stage's MFMAs: the labels of stage st+1
+    // (from the column list scol[(st+1) & 1] in LDS) and the column list of
+    // stage st+2 (a 32-entry slice of ccol, masked to the stage's nc at
+    // commit; ccol has >= COF_SLOTS readable entries past any stage start).
+    // Dword p of the panel = (column c, row dword rd); rows past N read
+    // clamped rows (their outputs are masked in the epilogue); panel columns
+    // c >= nc hold column 0's labels and are never read by a descriptor.
+    __shared__ int scol[2][COF_SLOTS];
     unsigned pf[LOADS];
-    int pdesc = -1;
+    int pdesc = -1, pclo = 0, pcol = 0, pcolok = 0;
     auto issue = [&](int st) {
-        const int clo = stage_lo[st], nc = stage_nc[st];
+        const int* sc = scol[st & 1];
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) {
             const int p = i * 256 + tid;
             const int c = p / ROWD, rd = p - c * ROWD;
             int64_t row = rd < COF_BM / RPD ? rowA0 + RPD * rd : rowB0 + RPD * (rd - COF_BM / RPD);
+            const T* colp = A + (int64_t)sc[c] * N;
             unsigned v = 0u;
-            if (c < nc) {
-                const T* colp = A + (int64_t)ccol[clo + c] * N;
-                if (VEC) {
-                    row = row + RPD <= N ? row : N - RPD;
-                    v = *reinterpret_cast<const unsigned*>(colp + row);
-                } else {
+            if (VEC) {
+                row = row + RPD <= N ? row : N - RPD;
+                v = *reinterpret_cast<const unsigned*>(colp + row);
+            } else {
 #pragma unroll
-                    for (int e = 0; e < RPD; ++e) {
-                        const int64_t rr = row + e < N ? row + e : N - 1;
-                        v |= (unsigned)colp[rr] << (8 * sizeof(T) * e);
-                    }
+                for (int e = 0; e < RPD; ++e) {
+                    const int64_t rr = row + e < N ? row + e : N - 1;
+                    v |= (unsigned)colp[rr] << (8 * sizeof(T) * e);
                 }
             }
             pf[i] = v;
         }
+        pclo = stage_lo[st];
+        if (tid < COF_SLOTS) pdesc = desc[(int64_t)st * COF_SLOTS + tid];
+    };
+    auto fetch_cols = [&](int st) {
         if (tid < COF_SLOTS) {
-            const int dsc = desc[(int64_t)st * COF_SLOTS + tid];
-            pdesc = dsc < 0 ? -1 : (((dsc >> COF_SB) - clo) << COF_SB) | (dsc & ((1 << COF_SB) - 1));
+            pcol = ccol[stage_lo[st] + tid];
+            pcolok = tid < stage_nc[st];
         }
     };
-    auto commit = [&](int bb) {
+    auto commit = [&](int bb, int stc) {
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
-        if (tid < COF_SLOTS) sdesc[bb][tid & 1][tid >> 1] = pdesc;
+        if (tid < COF_SLOTS) {
+            const int dsc = pdesc;
+            sdesc[bb][tid & 1][tid >> 1] =
+                dsc < 0 ? -1 : (((dsc >> COF_SB) - pclo) << COF_SB) | (dsc & ((1 << COF_SB) - 1));
+            if (stc >= 0) scol[stc & 1][tid] = pcolok ? pcol : 0;
+        }
     };
     if (tid < COF_TAB) {
         v4i e = {0, 0, 0, 0};
-        const int i = tid < 16 ? tid : (tid < 32 ? tid - 16 : -1);
-        if (tid < 33 && i >= 0 && !(tid >= 16 && i == 0)) e[i >> 2] = 1 << (8 * (i & 3));
-        if (tid >= 16 && tid < 33) e[0] |= 0x80;  // the flag (int8 -128) in byte 0
+        if (tid >= 1 && tid <= 16) {  // later slots: one-hot byte tid - 1
+            const int x = tid - 1;
+            e[x >> 2] = 1 << (8 * (x & 3));
+        } else if (tid >= 20) {  // slot 0, label tid - 19 (35: >= 16, flag only)
+            const int x = tid - 19;
+            if (x < 16) e[x >> 2] = 1 << (8 * (x & 3));
+            e[0] |= 0x80;  // the flag (int8 -128) in byte 0
+        }
         ftab[tid] = e;
     }
     if (nstage > 0) {
+        fetch_cols(0);
+        if (tid < COF_SLOTS) scol[0][tid] = pcolok ? pcol : 0;
+        __syncthreads();
         issue(0);
-        commit(0);
+        if (nstage > 1) fetch_cols(1);
+        commit(0, nstage > 1 ? 1 : -1);
     }
     __syncthreads();
     const int ra = wr * 64 + (lane & 31);            // A rows ra, ra + 32 (panel rows 0..127)
@@ -239,6 +269,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     for (int st = 0; st < nstage; ++st) {
         const int bb = st & 1;
         if (st + 1 < nstage) issue(st + 1);
+        if (st + 2 < nstage) fetch_cols(st + 2);
         // software pipeline over the stage's K-steps: labels of step q+2 and
         // the fragment-table reads of step q+1 are in flight while the MFMAs
         // of step q run
@@ -253,19 +284,23 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             dsc[4 * q4 + 3] = v.w;
         }
         int lab[2][6];
+        // branch-free: a padding slot (desc -1) reads column 0's labels and
+        // maps every label to the zero entry (sub16 above any label)
         auto read_labels = [&](int q, int (&L)[6]) {
-            const int d = dsc[q];
-            const T* col = &panel[bb][d < 0 ? 0 : d >> COF_SB][0];
+            const T* col = &panel[bb][max(dsc[q], 0) >> COF_SB][0];
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi) L[mi] = d < 0 ? 0 : col[ra + 32 * mi];
+            for (int mi = 0; mi < 2; ++mi) L[mi] = col[ra + 32 * mi];
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) L[2 + ni] = d < 0 ? 0 : col[rb + 32 * ni];
+            for (int ni = 0; ni < 4; ++ni) L[2 + ni] = col[rb + 32 * ni];
         };
         v4i fr[2][6];
         auto read_frags = [&](int q, const int (&L)[6], v4i (&F)[6]) {
-            const int sub = dsc[q] < 0 ? 0 : dsc[q] & ((1 << COF_SB) - 1);
+            const int d = dsc[q];
+            const int sub = d & ((1 << COF_SB) - 1);
+            const int sub16 = d < 0 ? (1 << 20) : 16 * sub;
+            const int off = (d >= 0 && sub == 0) ? 19 : 1;
 #pragma unroll
-            for (int x = 0; x < 6; ++x) F[x] = ftab[cof_entry(L[x], sub)];
+            for (int x = 0; x < 6; ++x) F[x] = ftab[cof_entry(L[x], sub16, off)];
         };
         read_labels(0, lab[0]);
         read_labels(1, lab[1]);
@@ -284,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         }
         if (st + 1 < nstage) {
             __syncthreads();  // every wave is done with buffer bb^1 (read in stage st-1)
-            commit(bb ^ 1);
+            commit(bb ^ 1, st + 2 < nstage ? st + 2 : -1);
             __syncthreads();
         }
     }
