@@ -118,9 +118,15 @@ __device__ __forceinline__ float union_kth(const float (&lv)[KP]) {
 // one contiguous 32*KSTEPS-byte run.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
-#define KNN_CHUNK 64        // refs per LDS stage (2 MFMA tiles)
-#define KNN_NBUF 3          // LDS stages in flight (prefetch distance 2 chunks)
-#define KNN_QCAP 12         // per-lane insertion queue slots (flush before a half tile that could overflow)
+// LDS staging of the reference image: chunks of knn_chunk(KSTEPS) refs
+// (chunk / 32 MFMA tiles per barrier) in knn_nbuf(KSTEPS) buffers (prefetch
+// distance nbuf - 1).  128-ref chunks in 2 buffers halve the barriers of 64 x 3
+// at the same LDS (3 blocks per CU); d > 31 rows are twice as wide and keep
+// 64 x 3 so that 2 blocks still fit.
+__host__ __device__ constexpr int knn_chunk(int ksteps) { return ksteps == 4 ? 64 : 128; }
+__host__ __device__ constexpr int knn_nbuf(int ksteps) { return ksteps == 4 ? 3 : 2; }
+static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4); }  // d dims + the norm dim
+#define KNN_QCAP 8          // per-lane insertion queue slots (flush before a half tile that could overflow)
 #ifndef KNN_ENQ_BRANCHY
 #define KNN_ENQ_BRANCHY 0   // per-register exec-masked enqueue (1) or branch-free per half tile (0)
 #endif
@@ -318,6 +324,7 @@ __device__ __forceinline__ void knn_wait_vmcnt() {
     else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -327,6 +334,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     float* __restrict__ cand_thr, const int4* __restrict__ blk) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
     constexpr int ROWB = KSTEPS * 64;               // bytes per row
+    constexpr int KNN_CHUNK = knn_chunk(KSTEPS);
+    constexpr int KNN_NBUF = knn_nbuf(KSTEPS);
     constexpr int STAGE = KNN_CHUNK * ROWB;         // bytes of one stage
     constexpr int LOADS = (KNN_CHUNK * C16) / 256;  // LDS-DMA instructions per thread per stage
     // ALL of the kernel's LDS is this one array (the staging buffers, then the
@@ -433,17 +442,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // the top of iteration k the wave waits for its own part of chunk k
     // (vmcnt: the younger chunk k+1 may stay outstanding), the barrier makes
     // every wave's part visible and frees buffer (k+2) % 3 (last read in k-1).
+    static_assert(KNN_NBUF == 2 || KNN_NBUF == 3, "2 or 3 staging buffers");
     KNN_STAGE_GLDS(0, chunk_at(0));
-    if (nck > 1) KNN_STAGE_GLDS(1, chunk_at(1));
+    if (KNN_NBUF == 3 && nck > 1) KNN_STAGE_GLDS(1, chunk_at(1));
     for (int k = 0; k < nck; ++k) {
         const int b = k % KNN_NBUF;
         const int c = chunk_at(k);
-        if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
-        else knn_wait_vmcnt<0>();
+        if constexpr (knn_nbuf(KSTEPS) == 3) {
+            if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
+            else knn_wait_vmcnt<0>();
+        } else {
+            knn_wait_vmcnt<0>();
+        }
         __syncthreads();
-        if (k + 2 < nck) KNN_STAGE_GLDS((k + 2) % KNN_NBUF, chunk_at(k + 2));
-#pragma nounroll  // unrolling the two tiles doubles live registers
-        for (int tau = 0; tau < 2; ++tau) {
+        if (k + KNN_NBUF - 1 < nck) KNN_STAGE_GLDS((k + KNN_NBUF - 1) % KNN_NBUF, chunk_at(k + KNN_NBUF - 1));
+#pragma nounroll  // unrolling the tiles multiplies live registers
+        for (int tau = 0; tau < KNN_CHUNK / 32; ++tau) {
             const int row = tau * 32 + col;
             h8 ah[KSTEPS], al[KSTEPS];
 #pragma unroll
@@ -867,7 +881,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     const double err_ulps = KNN_ERR_ULPS_F16;
     const int* order_perm = nullptr;  // screening position -> bootstrap row
     {
-        const int KSTEPS = d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4);  // d data dims + the norm dimension
+        const int KSTEPS = knn_ksteps(d);
+        const int KNN_CHUNK = knn_chunk(KSTEPS);
         const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + 256);
         if (!img) return CCG_ENOMEM;
@@ -994,6 +1009,7 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
     const int64_t npos = po[nseg];
     CCG_REQUIRE(npos < (1LL << 30), "ccg_knn_segments_dev: too many positions");
     const int64_t nblk = npos / KNN_QPB;
+    const int KNN_CHUNK = knn_chunk(knn_ksteps(d));
     std::vector<int> hperm(npos, -1);
     std::vector<int4> hblk(nblk);
     for (int s = 0; s < nseg; ++s) {

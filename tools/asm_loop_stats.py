@@ -13,9 +13,15 @@ def main(path, ksub):
     lines = open(path).read().splitlines()
     start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and ksub in l and l.rstrip().endswith(":")
                  or (l.startswith("_Z") and ksub in l.split(":")[0]))
-    end = next(i for i in range(start, len(lines)) if lines[i].strip().startswith("s_endpgm"))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
     body = lines[start:end + 1]
-    heads = [(i, l.split(":")[0]) for i, l in enumerate(body) if "Loop Header" in l and l.startswith(".LBB")]
+    heads = []
+    for i, l in enumerate(body):
+        if "Loop Header" not in l:
+            continue
+        j = i if l.startswith(".LBB") else i - 1  # the label may sit on the line above the comment
+        if body[j].startswith(".LBB"):
+            heads.append((j, body[j].split(":")[0]))
     for hi, lab in heads:
         back = [i for i, l in enumerate(body) if re.search(r"s_(c)?branch\w*\s+" + re.escape(lab) + r"\s*$", l)]
         back = [i for i in back if i > hi]

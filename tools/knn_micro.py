@@ -3,8 +3,8 @@
 Times the screen kernel and the whole kNN with the library's hipEvent timers.
 Data: one 90k-row bootstrap of bench.py's synthetic NB-count PCs (KM_DATA=gauss:
 a 12-component Gaussian mixture instead).
-Variants come from environment variables read by libccg (CCG_KNN_F32,
-CCG_KNN_EXP); run each in its own process.
+Variants are separate builds of libccg (tools/build_variant.sh, --lib);
+run each in its own process.
 """
 import json
 import os
