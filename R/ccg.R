@@ -223,3 +223,20 @@ ccgNullStatistics <- function(pcaNulls, kNum, clusterFun = "leiden", minSize = 5
   }
   out
 }
+
+#' The PC matrix of a cell subset (:287, :337-382): log1p(counts / sf) on the
+#' variable genes, prcomp_irlba with per-gene centring and scaling -- on the
+#' GPU, exact (signs: each component's largest-|loading| gene positive).
+#' pcNum = "find" (or > 30) takes 50 components and applies the :356 rule.
+ccgSubsetPCs <- function(counts, sizeFactors, genes, cells = seq_len(ncol(counts)), pcNum = "find", pcVar = 0.2) {
+  eng <- ccgEngine()
+  find <- identical(pcNum, "find") || pcNum > 30
+  k <- if (find) 50L else as.integer(pcNum)
+  if (is.logical(genes)) genes <- which(genes)
+  p <- .Call(C_ccg_r_pca, eng, as.matrix(counts) + 0, as.numeric(sizeFactors), as.integer(genes),
+             as.integer(cells), k)
+  if (find) k <- max(which(cumsum(p$sdev[1:50]) / sum(p$sdev[1:50]) > pcVar)[1], 5)
+  x <- p$x[, seq_len(k), drop = FALSE]
+  rownames(x) <- colnames(counts)[cells]
+  list(pca = x, sdev = p$sdev, pcNum = k)
+}

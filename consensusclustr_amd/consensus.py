@@ -421,3 +421,29 @@ def null_test_pvalue(silhouette, null_scores):
     if sd == 0.0:
         return 0.0 if silhouette > mu else 1.0
     return 1.0 - 0.5 * math.erfc(-((silhouette - mu) / sd) / math.sqrt(2.0))
+
+
+# ------------------------------------------------------- PCs of a subset --
+def choose_pc_num(sdev, pcVar=0.2):
+    """pcNum = max(which(cumsum(sdev[1:50]) / sum(sdev) > pcVar)[1], 5) (:356):
+    the first (1-based) component count whose share of the summed sdev of
+    the top 50 exceeds pcVar, at least 5."""
+    s = np.asarray(sdev, np.float64)[:50]
+    frac = np.cumsum(s) / s.sum()
+    hit = np.flatnonzero(frac > pcVar)
+    return max(int(hit[0]) + 1 if hit.size else 5, 5)
+
+
+def subset_pcs(counts, sf, genes=None, cells=None, pcNum="find", pcVar=0.2, engine=None):
+    """The PC matrix of a (sub)cluster (:287, :337-382, iterate=TRUE at :562):
+    log1p(counts / sf) on the variable genes, prcomp_irlba with per-gene
+    centring and scaling (ccg_pca on the GPU); pcNum "find" (or > 30) takes
+    50 components and keeps the first choose_pc_num(sdev, pcVar).
+    Returns (pca: n_cells x pcNum, sdev)."""
+    eng = engine or default_engine()
+    if pcNum == "find" or int(pcNum) > 30:
+        x, sdev = eng.pca(counts, sf, genes, cells, npc=50)
+        k = choose_pc_num(sdev, pcVar)
+        return x[:, :k], sdev
+    x, sdev = eng.pca(counts, sf, genes, cells, npc=int(pcNum))
+    return x, sdev

@@ -42,6 +42,7 @@ enum ccg_ws_slot {
     WS_SORT,         // device radix sort temporary storage
     WS_SNN_ROWS,     // SNN per-node partner rows (padded CSR of the per-graph API)
     WS_HIER,         // cluster block sums: co/both row sub-slab
+    WS_PCA,          // PCA: standardised cells x genes, covariance, subspace blocks
     WS_NSLOTS
 };
 

@@ -247,6 +247,24 @@ class Engine:
         check(self.lib.ccg_contingency(self.ctx, _ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(f), K, C, _ptr(tab)))
         return tab
 
+    def pca(self, counts, sf, genes=None, cells=None, npc=50):
+        """Normalisation + PCA of a cell subset (ccg_pca): log1p(counts/sf) on
+        the selected genes, centred and scaled per gene, top npc components.
+
+        counts: G x N gene-by-cell array; sf: N size factors; genes / cells:
+        0-based index arrays (None = all).  Returns (x: nc x npc scores,
+        sdev: npc)."""
+        C = np.asfortranarray(counts, dtype=np.float64)
+        G, N = C.shape
+        g = np.arange(G, dtype=np.int32) if genes is None else np.ascontiguousarray(genes, dtype=np.int32)
+        c = np.arange(N, dtype=np.int32) if cells is None else np.ascontiguousarray(cells, dtype=np.int32)
+        sf = np.ascontiguousarray(sf, dtype=np.float64)
+        x = np.empty((npc, c.size), np.float64)  # column-major nc x npc
+        sdev = np.empty(npc, np.float64)
+        check(self.lib.ccg_pca(self.ctx, _ptr(C), G, N, _ptr(sf), _ptr(g), g.size, _ptr(c), c.size, npc, _ptr(x),
+                               _ptr(sdev)))
+        return x.T.copy(), sdev
+
     # ---------------------------------------------------------- device API
     def gather_rows_t(self, pcs_cm, N, d, idx, rows):
         """rows[i, :] = pcs[idx[i], :]; pcs_cm is a column-major (d, N) tensor."""

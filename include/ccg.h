@@ -37,6 +37,8 @@
  *       block means (:463, :699-721).
  *   ccg_contingency                 : the counting of bluster::pairwiseRand
  *       (:470-474).
+ *   ccg_pca                         : shifted_log_transform + prcomp_irlba
+ *       (:287, :339, :369, :790).
  *
  * Errors found by a kernel on the device (a label wider than the assignment
  * matrix, an invalid SNN neighbour index) are sticky in the context and are
@@ -301,6 +303,29 @@ int ccg_contingency_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, 
  * and q that alt splits; adjusted: (obs - E) / (total - E) with E under
  * random alt labels.  0/0 -> NaN. */
 int ccg_pairwise_rand_ratio(int K, int C, const int32_t* tab, int adjusted, double* out);
+
+/* ---------------------------------------------- normalisation + PCA -- */
+/* The producer of a (sub)cluster's PC matrix (R/consensusClust.R:287, :339,
+ * :369, :790; iterate=TRUE re-runs it per cluster):
+ *   norm = log1p(counts[genes, cells] / sf[cells])   shifted_log_transform
+ *                                                     with pseudo_count 1
+ *   pca  = prcomp_irlba(t(norm), npc, center = rowMeans2(norm),
+ *                       scale = rowSds(norm))
+ * counts: G x N column-major doubles (R's gene x cell matrix); sf: N size
+ * factors; genes: ng 0-based rows (the variable features); cells: nc 0-based
+ * columns.  Outputs: x (nc x npc, column-major = pca$x) and sdev (npc,
+ * descending; a HOST array in both flavours).  The PCA is exact (subspace
+ * iteration to a 1e-11 relative eigen-residual; irlba stops at 1e-5).  Each
+ * component's sign puts its largest-|loading| gene positive (irlba's signs
+ * follow its random start).  CCG_ENAN if a selected gene has zero variance
+ * among the cells (prcomp_irlba fails there; the reference then returns one
+ * cluster, :371-378).  Requires 1 <= npc < min(ng, nc). */
+int ccg_pca(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
+            const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
+            double* sdev);
+int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
+                const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
+                double* sdev, void* stream);
 
 /* ------------------------------------------------------------ multi-GPU -- */
 /* A device group: one context (stream + workspaces) per device and one RCCL

@@ -413,6 +413,40 @@ SEXP ccg_r_stability(SEXP e, SEXP A, SEXP f, SEXP K, SEXP adjusted) {
     return out;
 }
 
+/* ------------------------------------------------ normalisation + PCA -- */
+/* The PC matrix of a cell subset (:287, :339, :369, :790): counts G x N
+ * double matrix (dense), sf size factors (N), genes / cells 1-based index
+ * vectors, npc components.  Returns list(x = ncells x npc, sdev).  A gene
+ * with zero variance raises the error the reference's tryCatch(prcomp_irlba)
+ * turns into NA (:368-378). */
+SEXP ccg_r_pca(SEXP e, SEXP counts, SEXP sf, SEXP genes, SEXP cells, SEXP npc) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    const int64_t G = Rf_nrows(counts), N = Rf_ncols(counts), nc = XLENGTH(cells);
+    const int ng = Rf_length(genes), k = Rf_asInteger(npc);
+    int32_t* g0 = (int32_t*)R_alloc((size_t)ng, sizeof(int32_t));
+    int32_t* c0 = (int32_t*)R_alloc((size_t)nc, sizeof(int32_t));
+    for (int t = 0; t < ng; ++t) g0[t] = INTEGER(genes)[t] - 1;
+    for (int64_t t = 0; t < nc; ++t) c0[t] = INTEGER(cells)[t] - 1;
+    SEXP x = PROTECT(Rf_allocMatrix(REALSXP, (int)nc, k));
+    SEXP sd = PROTECT(Rf_allocVector(REALSXP, k));
+    int rc = ccg_pca(ctx, REAL(counts), G, N, REAL(sf), g0, ng, c0, nc, k, REAL(x), REAL(sd));
+    if (rc != CCG_OK) {
+        UNPROTECT(2);
+        fail("ccg_pca", rc);
+    }
+    SEXP res = PROTECT(Rf_allocVector(VECSXP, 2));
+    SET_VECTOR_ELT(res, 0, x);
+    SET_VECTOR_ELT(res, 1, sd);
+    SEXP nm = PROTECT(Rf_allocVector(STRSXP, 2));
+    SET_STRING_ELT(nm, 0, Rf_mkChar("x"));
+    SET_STRING_ELT(nm, 1, Rf_mkChar("sdev"));
+    Rf_setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(4);
+    return res;
+}
+
 /* ------------------------------------------------------- registration -- */
 static const R_CallMethodDef call_methods[] = {
     {"ccg_r_open", (DL_FUNC)&ccg_r_open, 1},
@@ -428,6 +462,7 @@ static const R_CallMethodDef call_methods[] = {
     {"ccg_r_consensus_knn", (DL_FUNC)&ccg_r_consensus_knn, 3},
     {"ccg_r_block_dist", (DL_FUNC)&ccg_r_block_dist, 4},
     {"ccg_r_stability", (DL_FUNC)&ccg_r_stability, 5},
+    {"ccg_r_pca", (DL_FUNC)&ccg_r_pca, 6},
     {NULL, NULL, 0}};
 
 void R_init_consensusClustR(DllInfo* dll) {

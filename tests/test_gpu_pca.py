@@ -1,0 +1,73 @@
+"""Normalisation + PCA of a cell subset (ccg_pca; R/consensusClust.R:287,
+:339, :369, :790) against numpy's exact eigen-decomposition of the same
+standardised matrix.  prcomp_irlba is approximate (tol 1e-5) and its signs
+follow a random start, so the contract is the exact PCA with each
+component's largest-|loading| gene positive."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _counts(rng, G, N, pops=4):
+    base = rng.lognormal(-0.5, 1.2, G)
+    fc = np.exp(rng.normal(0, 1.0, (pops, G)) * (rng.random((pops, G)) < 0.15))
+    lab = rng.integers(0, pops, N)
+    sf = rng.lognormal(0, 0.3, N)
+    mu = base[None, :] * fc[lab] * sf[:, None]
+    return rng.poisson(mu).T.astype(np.float64), sf  # G x N
+
+
+def _reference(counts, sf, genes, cells, npc):
+    Y = np.log1p(counts[np.ix_(genes, cells)] / sf[cells][None, :]).T  # cells x genes
+    Z = (Y - Y.mean(0)) / Y.std(0, ddof=1)
+    C = Z.T @ Z / (Z.shape[0] - 1)
+    w, V = np.linalg.eigh(C)
+    w, V = w[::-1][:npc], V[:, ::-1][:, :npc]
+    for j in range(npc):
+        if V[np.argmax(np.abs(V[:, j])), j] < 0:
+            V[:, j] = -V[:, j]
+    return Z @ V, np.sqrt(w), w
+
+
+@pytest.mark.parametrize("G,N,ng,nc,npc", [(300, 900, 200, 700, 20), (120, 400, 120, 400, 10)])
+def test_pca_matches_exact_eigendecomposition(engine, G, N, ng, nc, npc):
+    rng = np.random.default_rng(G + nc)
+    counts, sf = _counts(rng, G, N)
+    genes = np.sort(rng.choice(G, ng, replace=False)).astype(np.int32)
+    cells = rng.choice(N, nc, replace=False).astype(np.int32)
+    keep = counts[np.ix_(genes, cells)].std(1) > 0
+    genes = genes[keep]
+    x, sdev = engine.pca(counts, sf, genes, cells, npc)
+    xr, sr, w = _reference(counts, sf, genes, cells, npc)
+    assert x.shape == (cells.size, npc)
+    assert np.allclose(sdev, sr, rtol=1e-10, atol=0)
+    for j in range(npc):  # vectors are determined where the eigenvalue is separated
+        gap = min(abs(w[j] - w[j - 1]) if j else np.inf, abs(w[j] - w[j + 1]) if j + 1 < npc else np.inf) / w[0]
+        if gap > 1e-3:
+            assert np.linalg.norm(x[:, j] - xr[:, j]) <= 1e-6 * np.linalg.norm(xr[:, j]), j
+
+
+def test_pca_zero_variance_gene_is_reported(engine):
+    from consensusclustr_amd._lib import CcgError
+    rng = np.random.default_rng(5)
+    counts, sf = _counts(rng, 50, 200)
+    counts[7] = 0.0
+    with pytest.raises(CcgError, match="ENAN"):
+        engine.pca(counts, sf, None, None, 5)
+
+
+def test_subset_pcs_find_rule_and_scale(engine):
+    """pcNum = 'find': 50 components, then the :356 rule, at a subcluster's size."""
+    from consensusclustr_amd.consensus import choose_pc_num, subset_pcs
+    rng = np.random.default_rng(9)
+    counts, sf = _counts(rng, 2000, 6000, pops=6)
+    genes = np.flatnonzero(counts.std(1) > 0)[:1500].astype(np.int32)
+    t0 = time.perf_counter()
+    pcs, sdev = subset_pcs(counts, sf, genes, None, "find", 0.2, engine)
+    dt = time.perf_counter() - t0
+    print(f"ccg_pca 1500 genes x 6000 cells, 50 PCs: {dt:.2f} s")
+    assert pcs.shape == (6000, choose_pc_num(sdev, 0.2))
+    assert np.all(np.diff(sdev) <= 0)

@@ -203,3 +203,13 @@ def test_null_test_pvalue_is_normal_mle_tail():
     mu, sd = x.mean(), x.std()  # numpy std: divisor n
     for s in (0.1, 0.24, 0.31, 0.5):
         assert abs(null_test_pvalue(s, x) - norm.sf(s, mu, sd)) < 1e-12
+
+
+def test_choose_pc_num_rule():
+    """pcNum = max(which(cumsum(sdev)/sum(sdev) > pcVar)[1], 5) (:356)."""
+    from consensusclustr_amd.consensus import choose_pc_num
+    sdev = np.array([10.0, 5, 3] + [1.0] * 47)
+    # cumulative shares: 10/65 = 0.154, 15/65 = 0.23 -> first above 0.2 is component 2 -> max(2, 5) = 5
+    assert choose_pc_num(sdev, 0.2) == 5
+    assert choose_pc_num(sdev, 0.5) == 1 + int(np.flatnonzero(np.cumsum(sdev) / sdev.sum() > 0.5)[0])
+    assert choose_pc_num(sdev, 0.5) == 18  # 33/65 = 0.508 at component 18

@@ -73,5 +73,6 @@ def test_r_code_uses_registered_symbols_with_matching_arity():
 def test_r_code_covers_the_replaced_seams():
     code = open(RCODE).read()
     for fn in ("getClustAssignments", "ccgConsensusCore", "ccgConsensusKNN", "ccgJaccardDist",
-               "ccgClusterDistance", "ccgStabilityMatrix", "ccgSilhouetteMeans", "ccgNullStatistics"):
+               "ccgClusterDistance", "ccgStabilityMatrix", "ccgSilhouetteMeans", "ccgNullStatistics",
+               "ccgSubsetPCs"):
         assert re.search(rf"^{fn} <- function\(", code, re.M), fn
