@@ -209,6 +209,12 @@ def main():
         sys.exit(launch_ranks(args))
     if args.launcher_check:
         return launcher_check(args)
+    # The result is ONE JSON line on stdout.  Native libraries print banners
+    # to fd 1 (RCCL announces its version on communicator init), so fd 1 goes
+    # to stderr for the run and the JSON line is written to the saved stdout.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -436,7 +442,7 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     for e in engs[1:]:
         e.close()
     grp.close()

@@ -46,7 +46,7 @@ def main():
     scr = eng.timing_read("knn_screen")
     tot = eng.timing_read("knn_total")
     st = eng.knn_rows_t(rows, 20, idx, stats=True)
-    out = {"variant": {k: os.environ.get(k) for k in ("CCG_KNN_F32", "CCG_KNN_EXP", "CCG_KNN_QF")},
+    out = {"lib": os.path.basename(_lib.LIB_PATH),
            "screen_ms": scr[0] / scr[1], "knn_total_ms": tot[0] / tot[1], "fallback": st[1]}
     print(json.dumps(out))
 
