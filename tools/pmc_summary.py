@@ -64,9 +64,10 @@ def main():
                 if c in m:
                     print(f"| {c}/SQ_WAVE_CYCLES | {m[c] / m['SQ_WAVE_CYCLES']:.3f} |")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE"):
-            # busy cycles are summed over 256 CUs x 4 SIMDs (gfx94x convention)
-            print(f"| MFMA busy frac (MFMA_BUSY / (GUI_ACTIVE*1024)) | "
-                  f"{m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] * 1024):.3f} |")
+            # busy cycles are summed over 256 CUs x 4 SIMDs; GRBM_GUI_ACTIVE is
+            # summed over the 8 XCDs, so the kernel's cycles are GUI_ACTIVE / 8
+            print(f"| MFMA busy frac (MFMA_BUSY / (GUI_ACTIVE/8 * 1024)) | "
+                  f"{m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] / 8 * 1024):.3f} |")
         print()
     if a.traffic_json:
         out = {}

@@ -2,8 +2,8 @@
 
 Same synthetic PCs as bench.py (100k cells x 30 PCs, 90k-row bootstrap),
 exact kNN at k=20, then `reps` passes of the k = 10/15/20 NUMBER graphs,
-timed with the library's hipEvent timers.  CCG_SNN_EXP (read by libccg)
-selects timing-only variants of the build kernel; run each in its own process.
+timed with the library's hipEvent timers.  Variants are separate builds of libccg
+(tools/build_variant.sh, --lib); run each in its own process.
 """
 import json
 import os
@@ -43,8 +43,19 @@ def main():
     for _ in range(reps):
         eng.snn_multi_t(knn, (10, 15, 20), "number", outs, ne)
     ms, cnt = eng.timing_read("snn")
-    # partner-count profile: edges per node of the k=20 graph (each edge once)
-    print(json.dumps({"variant": os.environ.get("CCG_SNN_EXP"), "snn_ms": ms / cnt,
+    # the bench's form: union-graph rows only (ccg_snn_rows_dev, no per-graph emit)
+    rcap = 700 * n
+    ro = (torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),
+          torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
+    ne2 = torch.zeros(3, dtype=torch.int64, device=dev)
+    eng.snn_rows_t(knn, (10, 15, 20), "number", *ro, ne2)
+    torch.cuda.synchronize()
+    eng.timing_read("snn")
+    for _ in range(reps):
+        eng.snn_rows_t(knn, (10, 15, 20), "number", *ro, ne2)
+    ms2, cnt2 = eng.timing_read("snn")
+    assert ne2.tolist() == ne.tolist()
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "snn_multi_ms": ms / cnt, "snn_rows_ms": ms2 / cnt2,
                       "edges": [int(x) for x in ne.tolist()]}))
 
 
