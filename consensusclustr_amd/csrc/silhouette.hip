@@ -20,7 +20,9 @@
 #include "ccg_internal.h"
 
 #define SIL_T 256
+#ifndef SIL_LG
 #define SIL_LG 10
+#endif
 
 __device__ __forceinline__ int scale_exp(double bound) {
     // largest e with bound * 2^e <= 2^61
