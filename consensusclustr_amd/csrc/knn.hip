@@ -34,8 +34,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_TMARGIN 8      // screen threshold: rank KP + KNN_TMARGIN of the two half-lists' union
 #define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
 #define KNN_FB_K 32        // fallback list length (>= kmax)
+#ifndef KNN_FB_S
 #define KNN_FB_S 64        // max reference ranges per failed row
+#endif
 #define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
+#define KNN_FB_UNITS 448   // target (failed row, range) blocks
 
 // Error budget of the fp16 hi/lo screen (DESIGN.md "kNN certification bound"):
 // relative part in units of the fp32 ulp (2^-24) times (2|x| + sqrt(dK))^2 --
@@ -687,10 +690,15 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
 __device__ __forceinline__ int knn_fb_splits(int nfail, int slots) {
     if (nfail <= 0) return 1;
     int S = slots / nfail;
+    // about KNN_FB_UNITS (row, range) blocks in all: more ranges only add merge
+    // rounds once the failed rows' scans fill the GPU (16 ranges x ~22 rows: 102 us
+    // at cfg3; 64 ranges: 139 us; 8 ranges: 132 us)
+    const int T = KNN_FB_UNITS / nfail;
+    S = T < S ? T : S;
     return S < 1 ? 1 : (S > KNN_FB_S ? KNN_FB_S : S);
 }
 
-template <int DMAX>
+template <int DMAX, int FBK>
 __global__ __launch_bounds__(256) void knn_fallback_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
@@ -714,10 +722,10 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
         double xq[DMAX];
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
-        double lv[KNN_FB_K];
-        int li[KNN_FB_K];
+        double lv[FBK];
+        int li[FBK];
 #pragma unroll
-        for (int t = 0; t < KNN_FB_K; ++t) {
+        for (int t = 0; t < FBK; ++t) {
             lv[t] = INFINITY;
             li[t] = 0x7fffffff;
         }
@@ -743,11 +751,11 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
                     const double t = __dsub_rn(xq[k], yv[k]);
                     s = __dadd_rn(s, __dmul_rn(t, t));
                 }
-            if (j == q || !(s < lv[KNN_FB_K - 1])) continue;  // j ascending per thread
+            if (j == q || !(s < lv[FBK - 1])) continue;  // j ascending per thread
             double cv = s;
             int ci = j;
 #pragma unroll
-            for (int t = 0; t < KNN_FB_K; ++t) {
+            for (int t = 0; t < FBK; ++t) {
                 bool sw = key_less(cv, ci, lv[t], li[t]);
                 double tv = lv[t];
                 int ti = li[t];
@@ -776,12 +784,12 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
             }
             if (bi != 0x7fffffff && li[0] == bi) {  // the winning thread pops its head (ids are unique)
 #pragma unroll
-                for (int t = 0; t < KNN_FB_K - 1; ++t) {
+                for (int t = 0; t < FBK - 1; ++t) {
                     lv[t] = lv[t + 1];
                     li[t] = li[t + 1];
                 }
-                lv[KNN_FB_K - 1] = INFINITY;
-                li[KNN_FB_K - 1] = 0x7fffffff;
+                lv[FBK - 1] = INFINITY;
+                li[FBK - 1] = 0x7fffffff;
             }
         }
         __syncthreads();
@@ -974,15 +982,19 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
     if (!fb_d || !fb_i) return CCG_ENOMEM;
-    if (d <= 16)
-        knn_fallback_kernel<16><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i, seg_off, nseg);
-    else if (d <= 32)
-        knn_fallback_kernel<32><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i, seg_off, nseg);
-    else
-        knn_fallback_kernel<64><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots,
-                                                      fb_d, fb_i, seg_off, nseg);
+#define CCG_FALLBACK(DM_, FK_)                                                                            \
+    knn_fallback_kernel<DM_, FK_><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots, \
+                                                        fb_d, fb_i, seg_off, nseg)
+    if (kmax <= KNN_KP) {  // per-thread lists of kmax <= 20 entries
+        if (d <= 16) CCG_FALLBACK(16, KNN_KP);
+        else if (d <= 32) CCG_FALLBACK(32, KNN_KP);
+        else CCG_FALLBACK(64, KNN_KP);
+    } else {
+        if (d <= 16) CCG_FALLBACK(16, KNN_FB_K);
+        else if (d <= 32) CCG_FALLBACK(32, KNN_FB_K);
+        else CCG_FALLBACK(64, KNN_FB_K);
+    }
+#undef CCG_FALLBACK
     knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
                                                    out_dist, seg_off, nseg);
     ccg_timer_stop(ctx, t_all, st);
