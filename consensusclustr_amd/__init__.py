@@ -12,7 +12,8 @@ from .consensus import (  # noqa: F401
     K_NUM, RES_RANGE, assignment_matrix, bootstrap_indices, consensus_choice, consensus_cluster,
     getClustAssignments, mapback, robust_choice, robust_scores)
 from .sharding import boot_shard, row_slabs  # noqa: F401
+from .pipeline import consensusClust  # noqa: F401
 
 __all__ = ["Engine", "CcgError", "load", "getClustAssignments", "consensus_cluster", "bootstrap_indices",
            "mapback", "assignment_matrix", "robust_choice", "consensus_choice", "robust_scores", "row_slabs",
-           "boot_shard", "K_NUM", "RES_RANGE"]
+           "boot_shard", "K_NUM", "RES_RANGE", "consensusClust"]
