@@ -253,7 +253,9 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
 // (partner, stage slot) and rewritten in order; one pass over the sorted
 // stage merges equal partners and writes the row.  R is chosen per node
 // (4, 8, 12 or 16 rounds of 64 items) so a node pays for its own size only.
+#ifndef SNN_SNB
 #define SNN_SNB 240   // buckets
+#endif
 #define SNN_SI 1024   // items staged per wave (largest sort-tier node)
 
 template <int SI>
@@ -323,11 +325,12 @@ __device__ __forceinline__ void snn_sort_node(SnnSortLds<SI>& L, const SnnSpec& 
         }
     }
     WAVE_LDS_SYNC();
-    // bucket starts: lane owns buckets 4*lane .. 4*lane+3
-    int hv[4], hs = 0;
+    // bucket starts: lane owns buckets BPL*lane .. BPL*lane+BPL-1
+    constexpr int BPL = (SNN_SNB + 63) / 64;
+    int hv[BPL], hs = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int b = 4 * lane + i;
+    for (int i = 0; i < BPL; ++i) {
+        const int b = BPL * lane + i;
         hv[i] = b < SNN_SNB ? hist[b] : 0;
         hs += hv[i];
     }
@@ -341,8 +344,8 @@ __device__ __forceinline__ void snn_sort_node(SnnSortLds<SI>& L, const SnnSpec& 
     int run = sc - hs;
     WAVE_LDS_SYNC();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int b = 4 * lane + i;
+    for (int i = 0; i < BPL; ++i) {
+        const int b = BPL * lane + i;
         if (b < SNN_SNB) {
             bst[b] = run;
             hist[b] = run;  // scatter cursor
