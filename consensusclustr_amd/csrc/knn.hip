@@ -130,9 +130,6 @@ __host__ __device__ constexpr int knn_chunk(int ksteps) { return ksteps == 4 ? 6
 __host__ __device__ constexpr int knn_nbuf(int ksteps) { return ksteps == 4 ? 3 : 2; }
 static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4); }  // d dims + the norm dim
 #define KNN_QCAP 8          // per-lane insertion queue slots (flush before a half tile that could overflow)
-#ifndef KNN_ENQ_BRANCHY
-#define KNN_ENQ_BRANCHY 0   // per-register exec-masked enqueue (1) or branch-free per half tile (0)
-#endif
 #define KNN_NORM_SHIFT 15   // the query's norm-dimension value 2^15 (exact in fp16)
 #define KNN_PAD_NORM (-65504.0f)  // padding rows: below every real value (|v| < 1.6e9 < 2^31)
 
@@ -319,6 +316,41 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
     return x * q + min(x, r) + i;
 }
 
+// Timing attribution for tools only (tools/build_variant.sh stamps
+// "-DKNN_STAMPS=1"): s_memtime stamps split each screen wave's cycles into
+// chunk DMA issue (0), tile MFMA + max-reduce (1), enqueue (2), flushes (3),
+// union thresholds (4), the chunk's vmcnt wait (5) and barrier (6);
+// ccg_debug_knn_stamps reads the sums.  The stamps' own waits inflate the
+// tile share.
+#ifdef KNN_STAMPS
+__device__ unsigned long long knn_stamp_acc[8];
+#define KST_DECL                                                \
+    unsigned long long kst_[7] = {0, 0, 0, 0, 0, 0, 0};        \
+    unsigned long long kst_t = __builtin_amdgcn_s_memtime()
+#define KST(i)                                                     \
+    do {                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        kst_[i] += t_ - kst_t;                                     \
+        kst_t = t_;                                                \
+    } while (0)
+#define KST_FLUSH_OUT()                                                             \
+    do {                                                                            \
+        if ((threadIdx.x & 63) == 0) {                                              \
+            for (int i_ = 0; i_ < 7; ++i_) atomicAdd(&knn_stamp_acc[i_], kst_[i_]); \
+            atomicAdd(&knn_stamp_acc[7], 1ull);                                     \
+        }                                                                           \
+    } while (0)
+extern "C" int ccg_debug_knn_stamps(unsigned long long* out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(knn_stamp_acc), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(knn_stamp_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#else
+#define KST_DECL
+#define KST(i)
+#define KST_FLUSH_OUT()
+#endif
+
 // s_waitcnt vmcnt(N) for a compile-time N (the LDS-DMA is issued as inline
 // asm, so the compiler does not track it).
 template <int N>
@@ -422,6 +454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int Lc = c0 - cl, Rc = ch - 1 - c0, Mc = min(Lc, Rc);
     const int nck = ch - cl;
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
+    KST_DECL;
     float T = -INFINITY;  // rejection threshold (see below)
     int qc = 0;           // this lane's queued candidates
     bool tdirty = false;  // lists changed since T was last set to the union threshold
@@ -451,14 +484,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     for (int k = 0; k < nck; ++k) {
         const int b = k % KNN_NBUF;
         const int c = chunk_at(k);
+        KST(1);
         if constexpr (knn_nbuf(KSTEPS) == 3) {
             if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
             else knn_wait_vmcnt<0>();
         } else {
             knn_wait_vmcnt<0>();
         }
+        KST(5);
         __syncthreads();
+        KST(6);
         if (k + KNN_NBUF - 1 < nck) KNN_STAGE_GLDS((k + KNN_NBUF - 1) % KNN_NBUF, chunk_at(k + KNN_NBUF - 1));
+        KST(0);
 #pragma nounroll  // unrolling the tiles multiplies live registers
         for (int tau = 0; tau < KNN_CHUNK / 32; ++tau) {
             const int row = tau * 32 + col;
@@ -487,27 +524,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     if (r == q || r >= qhi) acc[reg] = -INFINITY;
                 }
             }
-            // per half-tile of 8 registers: flush first if its candidates could
-            // overflow a queue, then enqueue each register's candidates under
-            // its own exec mask (a register no lane beats costs one compare)
+            // a tile no lane's value beats costs one max-reduce and compare;
+            // otherwise, per half-tile of 8 registers: flush first if its
+            // candidates could overflow a queue, then enqueue branch-free
             static_assert(QC >= 8, "queue must hold a half tile");
-#if KNN_ENQ_BRANCHY
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                if (__any(qc > QC - 8)) KNN_FLUSH();
-#pragma unroll
-                for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
-                    const float v = acc[reg];
-                    if (v > T) {
-                        qbw[qc * 64 + lane] = make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
-                        ++qc;
-                    }
-                }
-            }
-#else
             float vmax = acc[0];
 #pragma unroll
             for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
+            KST(1);
             if (__any(vmax > T)) {
                 // branch-free: a write at slot qc is kept only if qc advances
 #pragma unroll
@@ -515,7 +539,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     int c8 = 0;
 #pragma unroll
                     for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) c8 += acc[reg] > T ? 1 : 0;
+                    KST(2);
                     if (__any(qc + c8 > QC)) KNN_FLUSH();
+                    KST(3);
 #pragma unroll
                     for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
                         const float v = acc[reg];
@@ -524,18 +550,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                         qc += v > T ? 1 : 0;
                     }
                 }
+                KST(2);
             }
-#endif
             // After a flush (here, with the tile's accumulators dead) both halves
             // move to the union threshold; between flushes T only rises.
             if (tdirty) {
                 T = union_kth<KP>(lv);
                 tdirty = false;
+                KST(4);
             }
         }
     }
+    KST(1);
     KNN_FLUSH();
+    KST(3);
     T = union_kth<KP>(lv);
+    KST(4);
+    KST_FLUSH_OUT();
 #undef KNN_FLUSH
 #undef KNN_STAGE_GLDS
 #undef chunk_at

@@ -48,6 +48,18 @@ def main():
     st = eng.knn_rows_t(rows, 20, idx, stats=True)
     out = {"lib": os.path.basename(_lib.LIB_PATH),
            "screen_ms": scr[0] / scr[1], "knn_total_ms": tot[0] / tot[1], "fallback": st[1]}
+    lib = _lib.load()
+    if hasattr(lib, "ccg_debug_knn_stamps"):  # a -DKNN_STAMPS=1 variant: per-wave cycle attribution
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        lib.ccg_debug_knn_stamps(buf)  # reset
+        eng.knn_rows_t(rows, 20, idx)
+        torch.cuda.synchronize()
+        lib.ccg_debug_knn_stamps(buf)
+        waves = max(1, buf[7])
+        names = ["dma_issue", "tile_mfma_max", "enqueue", "flush", "union", "vmcnt_wait", "barrier"]
+        out["stamps_cycles_per_wave"] = {k: buf[i] / waves for i, k in enumerate(names)}
+        out["stamps_waves"] = waves
     print(json.dumps(out))
 
 
