@@ -19,12 +19,13 @@
 //      sits in hosts(knn[h][r])) and split[x] (hosts of x below x).
 //   2. capacity: per node the number M_j of (partner, member) items with
 //      partner p > j; a scan gives every node a row of M_j slots.
-//   3. build, one wave per node: the items are gathered, ordered by partner
-//      and merged (sum for NUMBER, bytewise min for RANK) into the node's row
-//      of (partner, packed per-graph values), ascending partner -- the union
+//   3. build: the items of a node are gathered, sorted by partner and
+//      merged (sum for NUMBER, bytewise min for RANK) into the node's row of
+//      (partner, packed per-graph values), ascending partner -- the union
 //      graph (the largest k) in CSR form with per-graph counts.  Tiers by
-//      size: register/LDS bucket sort (<= 1024 items), a 2048-slot LDS hash
-//      table, a 16K-slot block table, an exact O(n) dense pass.
+//      size: a register bitonic sort, one wave per node (<= 2048 items) or
+//      one 4-wave block per hub node (<= 4096); a 16K-slot block hash table;
+//      an exact O(n) dense pass.
 //   4. per-graph edge lists (i < j sorted by (i, j)) are streamed from the
 //      rows when the caller wants them (ccg_snn_multi_dev).
 #include <algorithm>
@@ -35,11 +36,11 @@
 #define WAVE_LDS_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
 
 #define SNN_MAXK 4           // graphs per pass (|kNum| <= 4)
-#define SNN_WT 2048          // wave hash-table slots
 #define SNN_WAVES 4          // waves per block in the wave kernels
 #define SNN_BT 16384         // block table slots (overflow path)
 #define SNN_DENSE_BLOCKS 64  // concurrent dense-path nodes
 #define SNN_EMPTY (-1)
+#define SNN_BITONIC_MAX 4096  // items of the largest bitonic-tier node
 
 struct SnnSpec {
     int nk;
@@ -246,230 +247,6 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
     }
 }
 
-// ------------------------------------------------------- sort (ESC) tier --
-// Nodes with at most 64*R items: the items are gathered to registers (all
-// host loads of the node in flight at once), bucketed by partner into an LDS
-// stage (histogram, wave scan, scatter), ranked inside their bucket by
-// (partner, stage slot) and rewritten in order; one pass over the sorted
-// stage merges equal partners and writes the row.  R is chosen per node
-// (4, 8, 12 or 16 rounds of 64 items) so a node pays for its own size only.
-#ifndef SNN_SNB
-#define SNN_SNB 240   // buckets
-#endif
-#define SNN_SI 1024   // items staged per wave (largest sort-tier node)
-
-template <int SI>
-struct SnnSortLds {
-    unsigned long long stage[SI];
-    union {
-        struct {  // gather phase: member headers
-            long long h0[64];
-            long long hend[64];
-            int cur[64];
-            int pre[65];
-        } g;
-        struct {  // bucket phase
-            int hist[SNN_SNB];
-            int bst[SNN_SNB + 1];
-        } s;
-    } u;
-};
-
-template <int R, int SI>
-__device__ __forceinline__ void snn_sort_node(SnnSortLds<SI>& L, const SnnSpec& sp, int64_t n, int64_t j, int M,
-                                              int lane, const int2* __restrict__ hosts_s,
-                                              const SnnRows& rows, int64_t* __restrict__ cnt) {
-    unsigned long long* stage = L.stage;
-    // gather: every host load of the node is issued before any is used;
-    // item r is held as (p << 32 | member << 8 | host rank) until its
-    // contribution is known, then as (p << 32 | packed contribution)
-    unsigned long long e[R];
-    int mi = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int t = 64 * r + lane;
-        e[r] = ~0ull;
-        if (t < M) {
-            while (L.u.g.pre[mi + 1] <= t) ++mi;
-            const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
-            int p = L.u.g.cur[mi], rp = 0;
-            if (q < L.u.g.hend[mi]) {
-                const int2 h = hosts_s[q];
-                p = h.x;
-                rp = h.y;
-            }
-            e[r] = ((unsigned long long)(unsigned)p << 32) | (unsigned)(mi << 8) | (unsigned)rp;
-        }
-    }
-    WAVE_LDS_SYNC();
-    int* hist = L.u.s.hist;
-    int* bst = L.u.s.bst;
-    for (int b = lane; b < SNN_SNB; b += 64) hist[b] = 0;
-    WAVE_LDS_SYNC();
-    const float inv = (float)SNN_SNB / (float)(n - j);
-    int bk[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        bk[r] = -1;
-        if (e[r] != ~0ull) {
-            const unsigned lo = (unsigned)e[r];
-            const unsigned c = snn_contrib(sp, (int)(lo >> 8), (int)(lo & 0xFFu));
-            const int p = (int)(e[r] >> 32);
-            if (c != sp.init) {
-                e[r] = ((unsigned long long)(unsigned)p << 32) | c;
-                bk[r] = min(SNN_SNB - 1, (int)((float)(p - (int)j - 1) * inv));
-                atomicAdd(&hist[bk[r]], 1);
-            } else {
-                e[r] = ~0ull;
-            }
-        }
-    }
-    WAVE_LDS_SYNC();
-    // bucket starts: lane owns buckets BPL*lane .. BPL*lane+BPL-1
-    constexpr int BPL = (SNN_SNB + 63) / 64;
-    int hv[BPL], hs = 0;
-#pragma unroll
-    for (int i = 0; i < BPL; ++i) {
-        const int b = BPL * lane + i;
-        hv[i] = b < SNN_SNB ? hist[b] : 0;
-        hs += hv[i];
-    }
-    int sc = hs;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(sc, o);
-        if (lane >= o) sc += y;
-    }
-    const int V = __shfl(sc, 63);
-    int run = sc - hs;
-    WAVE_LDS_SYNC();
-#pragma unroll
-    for (int i = 0; i < BPL; ++i) {
-        const int b = BPL * lane + i;
-        if (b < SNN_SNB) {
-            bst[b] = run;
-            hist[b] = run;  // scatter cursor
-        }
-        run += hv[i];
-    }
-    if (lane == 0) bst[SNN_SNB] = V;
-    WAVE_LDS_SYNC();
-    int pos[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        pos[r] = 0;
-        if (bk[r] >= 0) {
-            pos[r] = atomicAdd(&hist[bk[r]], 1);
-            stage[pos[r]] = e[r];
-        }
-    }
-    WAVE_LDS_SYNC();
-    // rank inside the bucket by (p, slot)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (bk[r] >= 0) {
-            const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
-            const unsigned key = (unsigned)(e[r] >> 32);
-            int rank = 0;
-            for (int q = b0; q < b1; ++q) {
-                const unsigned kq = (unsigned)(stage[q] >> 32);
-                rank += (kq < key || (kq == key && q < pos[r])) ? 1 : 0;
-            }
-            pos[r] = b0 + rank;
-        }
-    }
-    WAVE_LDS_SYNC();
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (bk[r] >= 0) stage[pos[r]] = e[r];
-    WAVE_LDS_SYNC();
-    // unique partners: the first of each run of equal keys merges the run
-    const bool write = rows.roff[n] <= rows.cap;
-    const int64_t ro = rows.roff[j];
-    int u = 0;
-    int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
-    for (int q0 = 0; q0 < V; q0 += 64) {
-        const int q = q0 + lane;
-        unsigned key = 0, agg = 0;
-        bool first = false;
-        if (q < V) {
-            const unsigned long long x = stage[q];
-            key = (unsigned)(x >> 32);
-            first = q == 0 || (unsigned)(stage[q - 1] >> 32) != key;
-            if (first) {
-                agg = (unsigned)x;
-                for (int q2 = q + 1; q2 < V; ++q2) {
-                    const unsigned long long y = stage[q2];
-                    if ((unsigned)(y >> 32) != key) break;
-                    agg = snn_combine(sp.type, agg, (unsigned)y);
-                }
-            }
-        }
-        const unsigned long long m = __ballot(first);
-        if (first) {
-            if (write) {
-                const int64_t o = ro + u + __popcll(m & lanemask_lt());
-                rows.nbr[o] = (int32_t)key;
-                rows.wpk[o] = agg;
-            }
-#pragma unroll
-            for (int t = 0; t < SNN_MAXK; ++t)
-                if (t < sp.nk && graph_has(sp, agg, t)) ++c4[t];
-        }
-        u += __popcll(m);
-    }
-    snn_row_counts(sp, c4, n, j, lane, cnt);
-    if (lane == 0) rows.rlen[j] = u;
-}
-
-// Three size classes, each its own kernel over its own node list (built by a
-// scan, so in ascending node order): CLS 0 sorts the nodes with <= 320 items
-// (R = 3 or 5), CLS 1 those with 321..640 (R = 8 or 10), CLS 2 641..1024
-// (R = 12 or 16).  The LDS stage is sized to the class, so small nodes --
-// the majority -- run at more waves per SIMD to hide the gather latency.  One
-// node per wave: no node loop whose invariants the compiler would hoist into
-// the item registers.
-template <int CLS>
-__global__ __launch_bounds__(64 * SNN_WAVES, CLS == 0 ? 8 : (CLS == 1 ? 6 : 4)) void snn_sort_build_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
-    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ list, const int64_t* __restrict__ count) {
-    constexpr int SI = CLS == 0 ? 320 : (CLS == 1 ? 640 : 1024);
-    __shared__ SnnSortLds<SI> lds_all[SNN_WAVES];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    SnnSortLds<SI>& L = lds_all[wv];
-    const int kmax = sp.kk[sp.nk - 1];
-    const int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv;
-    if (f >= *count) return;
-    const int64_t j = list[f];
-    const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
-    int incl = m.len;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    const int M = __shfl(incl, 63);
-    if (lane <= kmax) {
-        L.u.g.pre[lane] = incl - m.len;
-        L.u.g.h0[lane] = m.h0;
-        L.u.g.hend[lane] = m.hend;
-        L.u.g.cur[lane] = m.cur;
-    }
-    if (lane == 0) L.u.g.pre[kmax + 1] = M;
-    WAVE_LDS_SYNC();
-    if (CLS == 0) {
-        if (M <= 192) snn_sort_node<3>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else snn_sort_node<5>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-    } else if (CLS == 1) {
-        if (M <= 512) snn_sort_node<8>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else snn_sort_node<10>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-    } else {
-        if (M <= 768) snn_sort_node<12>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-        else snn_sort_node<16>(L, sp, n, j, M, lane, hosts_s, rows, cnt);
-    }
-}
-
 // Size class of every node from its capacity (items): packed one-hot counts
 // (class c in bits 21c..21c+20) for one scan that ranks every class at once.
 // Classes 0..2 in 21-bit fields (n < 2^21); class 3's rank is the node index
@@ -479,7 +256,7 @@ __global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, in
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const int64_t M = roff[j + 1] - roff[j];
-    const int c = M <= 320 ? 0 : (M <= 640 ? 1 : (M <= SNN_SI ? 2 : 3));
+    const int c = M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3));
     cls[j] = c < 3 ? 1LL << (SNN_CLS_BITS * c) : 0;
 }
 
@@ -504,248 +281,409 @@ __global__ void snn_class_scatter_kernel(const int64_t* __restrict__ cls_scan, i
     lists[c * n + r[c]] = (int)j;
 }
 
-// ---------------------------------------------------------- hash tier --
-// Nodes with more items: one wave per node builds an LDS hash table of
-// 64-bit slots (partner p << 32 | packed per-graph values): a new partner
-// costs one CAS, a repeat one add.  The table is compacted, sorted by p and
-// written to the row.  Nodes beyond its capacity go to the block tier.
-#define SNN_EMPTY64 (~0ull)
+// ------------------------------------------------------- bitonic tier --
+// Nodes with at most 64*E items (E = 4, 8, 16, 32): one wave per node.
+// Every item (partner p > j, member rank rj, host rank rp) becomes one key
+// that orders by p and carries all its merge needs:
+//   NUMBER: p << 6 | m, m = max(rj, rp)                      (32-bit)
+//   RANK:   p << 32 | (rj + rp) << 8 | m                     (64-bit)
+// Items are gathered element-major (item t = 64 e + lane, so host reads are
+// coalesced), transposed through LDS to lane-major (lane l holds items
+// E l .. E l + E - 1), bitonic-sorted in registers (in-lane stages are
+// min/max pairs; cross-lane stages one shuffle per element), and every run
+// of equal p is combined by a segmented scan (in lane, then across lanes by
+// DPP); the last item of each run writes the row entry.  No LDS round trip
+// sits inside a loop, so the tier is bound by VALU issue, not by latency.
 
-__device__ __forceinline__ bool table_insert64(unsigned long long* tab, int p, unsigned c, const SnnSpec& sp,
-                                               int bits, int T) {
-    unsigned s = snn_hash(p, bits);
-    const unsigned long long want = ((unsigned long long)(unsigned)p << 32) | c;
-    for (int probe = 0; probe < T; ++probe) {
-        unsigned long long cur = __hip_atomic_load(&tab[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == SNN_EMPTY64) {
-            const unsigned long long old = atomicCAS(&tab[s], SNN_EMPTY64, want);
-            if (old == SNN_EMPTY64) return true;
-            cur = old;
-        }
-        if ((unsigned)(cur >> 32) == (unsigned)p) {
-            if (sp.type == CCG_SNN_NUMBER) {
-                atomicAdd(&tab[s], (unsigned long long)c);  // per-byte counts never carry
-            } else {
-                while (true) {
-                    const unsigned nv = bytewise_min((unsigned)cur, c);
-                    if (nv == (unsigned)cur) break;
-                    const unsigned long long nw = (cur & 0xFFFFFFFF00000000ull) | nv;
-                    const unsigned long long old = atomicCAS(&tab[s], cur, nw);
-                    if (old == cur) break;
-                    cur = old;
-                }
-            }
-            return true;
-        }
-        s = (s + 1) & (T - 1);
-    }
-    return false;
+// Inclusive wave scans over lanes 0..lane (DPP row shifts, then the row
+// broadcasts of lanes 15 and 31).
+#define SNN_DPP_SHR(n) (0x110 | (n))
+#define SNN_DPP_BCAST15 0x142
+#define SNN_DPP_BCAST31 0x143
+__device__ __forceinline__ int snn_scan_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_SHR(1), 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_SHR(2), 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_SHR(4), 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_SHR(8), 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_BCAST15, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, SNN_DPP_BCAST31, 0xC, 0xF, false));
+    return v;
+}
+__device__ __forceinline__ int snn_scan_add(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_SHR(1), 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_SHR(2), 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_SHR(4), 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_SHR(8), 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_BCAST15, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, SNN_DPP_BCAST31, 0xC, 0xF, false);
+    return v;
 }
 
-template <int WT>
-constexpr int snn_log2() {
-    int b = 0;
-    while ((1 << b) < WT) ++b;
-    return b;
-}
-
-// Sort a node's u compacted entries (tab[0..u), distinct partners p in (j, n))
-// by p and store them to the row.  Each lane holds entries c = r*64 + lane
-// in registers; a 128-bucket split on p (monotone in p) gives every entry its
-// bucket's start by a histogram + wave scan, the entries are scattered into
-// bucket order in tab, and each entry's final place is its bucket start plus
-// the number of smaller partners in its (small) bucket.
-#define SNN_NB 128
-template <int RMAX>
-__device__ __forceinline__ void snn_bucket_store(unsigned long long* tab, int u, int lane, int64_t j, int64_t n,
-                                                 int* hist, int* bst, int32_t* __restrict__ nbr,
-                                                 uint32_t* __restrict__ wpk, bool write) {
-    unsigned long long e[RMAX];
-    int bk[RMAX];
-    const float inv = (float)SNN_NB / (float)(n - j - 1);
-    for (int b = lane; b < SNN_NB; b += 64) hist[b] = 0;
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r) {
-        const int c = r * 64 + lane;
-        e[r] = c < u ? tab[c] : SNN_EMPTY64;
-        const int p = (int)(e[r] >> 32);
-        bk[r] = min(SNN_NB - 1, (int)((float)(p - (int)j - 1) * inv));
+template <typename K>
+struct SnnKeyT;
+template <>
+struct SnnKeyT<uint32_t> {
+    static constexpr int PS = 6;  // p << 6 | m
+    __device__ static uint32_t make(int p, int rj, int rp) { return ((uint32_t)p << 6) | (uint32_t)max(rj, rp); }
+    __device__ static int m(uint32_t k) { return (int)(k & 63u); }
+    __device__ static int rs(uint32_t) { return 0; }
+    __device__ static uint32_t shx(uint32_t v, int msk) { return (uint32_t)__shfl_xor((int)v, msk, 64); }
+};
+template <>
+struct SnnKeyT<unsigned long long> {
+    static constexpr int PS = 32;  // p << 32 | (rj + rp) << 8 | m
+    __device__ static unsigned long long make(int p, int rj, int rp) {
+        return ((unsigned long long)(unsigned)p << 32) | ((unsigned)(rj + rp) << 8) | (unsigned)max(rj, rp);
     }
-    WAVE_LDS_SYNC();
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r)
-        if (r * 64 + lane < u) atomicAdd(&hist[bk[r]], 1);
-    WAVE_LDS_SYNC();
-    const int h0 = hist[2 * lane], h1 = hist[2 * lane + 1];
-    int incl = h0 + h1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
+    __device__ static int m(unsigned long long k) { return (int)(k & 0xFFu); }
+    __device__ static int rs(unsigned long long k) { return (int)((k >> 8) & 0xFFu); }
+    __device__ static unsigned long long shx(unsigned long long v, int msk) {
+        const int lo = __shfl_xor((int)(unsigned)v, msk, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), msk, 64);
+        return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
     }
-    const int excl = incl - h0 - h1;
-    bst[2 * lane] = excl;
-    bst[2 * lane + 1] = excl + h0;
-    hist[2 * lane] = excl;  // hist becomes the scatter cursor
-    hist[2 * lane + 1] = excl + h0;
-    if (lane == 0) bst[SNN_NB] = u;
-    WAVE_LDS_SYNC();
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r)
-        if (r * 64 + lane < u) tab[atomicAdd(&hist[bk[r]], 1)] = e[r];
-    WAVE_LDS_SYNC();
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r) {
-        if (r * 64 + lane < u) {
-            const int b0 = bst[bk[r]], b1 = bst[bk[r] + 1];
-            const unsigned p = (unsigned)(e[r] >> 32);
-            int rank = 0;
-            for (int i = b0; i < b1; ++i) rank += (unsigned)(tab[i] >> 32) < p;
-            if (write) {
-                nbr[b0 + rank] = (int32_t)p;
-                wpk[b0 + rank] = (uint32_t)e[r];
-            }
-        }
-    }
-}
-
-template <int WT>
-struct SnnWaveLds {
-    unsigned long long tab[WT];
-    union {
-        struct {  // gather phase: member headers
-            long long h0[64];
-            long long hend[64];
-            int cur[64];
-            int pre[65];
-        } g;
-        struct {  // sort phase: bucket histogram / starts
-            int hist[SNN_NB];
-            int bst[SNN_NB + 1];
-        } s;
-    } u;
 };
 
-template <int WT>
-__global__ __launch_bounds__(64 * SNN_WAVES, 2) void snn_wave_build_kernel(
-    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
-    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
-    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ in_list, const int64_t* __restrict__ in_count,
-    int* __restrict__ ov_list, int* __restrict__ ov_count) {
-    __shared__ SnnWaveLds<WT> lds_all[SNN_WAVES];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    SnnWaveLds<WT>& L = lds_all[wv];
-    unsigned long long* tab = L.tab;
-    const int kmax = sp.kk[sp.nk - 1];
-    constexpr int CAP = WT * 3 / 4;
-    const bool write = rows.roff[n] <= rows.cap;
-    const int64_t nn = *in_count;
-    for (int64_t f = (int64_t)blockIdx.x * SNN_WAVES + wv; f < nn; f += (int64_t)gridDim.x * SNN_WAVES) {
-        const int64_t j = in_list[f];
-        for (int s = lane; s < WT; s += 64) tab[s] = SNN_EMPTY64;
-        // Flat gather over the partners p > j; host entries are fetched one
-        // round ahead so their latency hides behind the current LDS inserts.
-        const SnnMember mem = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
-        int incl = mem.len;
+// Packed per-graph contribution of one item from its key (snn_contrib's
+// value: byte t live iff m <= kk[t]).
+template <typename K>
+__device__ __forceinline__ unsigned snn_key_contrib(const SnnSpec& sp, K key) {
+    const int m = SnnKeyT<K>::m(key);
+    unsigned live = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
+    for (int t = 0; t < SNN_MAXK; ++t) live |= (t < sp.nk && m <= sp.kk[t]) ? (0xFFu << (8 * t)) : 0u;
+    if (sp.type == CCG_SNN_NUMBER) return live & 0x01010101u;
+    return (((unsigned)SnnKeyT<K>::rs(key) * 0x01010101u) & live) | ~live;
+}
+
+template <typename K>
+__device__ __forceinline__ void snn_ce(K& a, K& b) {  // (a, b) <- (min, max)
+    const K lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// Bitonic sort (all compare-exchanges ascending: each merge starts with the
+// mirror stage i ^ (k - 1), then i ^ j for j = k/4 .. 1) of the 64*E keys in
+// lane-major order, element i = E*lane + e.  snn_bitonic_xor runs the xor
+// stages j = J .. 1 of one merge (J < 64*E).
+template <int E, typename K, int J>
+__device__ __forceinline__ void snn_bitonic_xor(K (&x)[E], int lane) {
+#pragma unroll
+    for (int j = J; j >= 1; j >>= 1) {
+        if (j < E) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((e & j) == 0) snn_ce(x[e], x[e ^ j]);
+        } else {
+            const bool lower = (lane & (j / E)) == 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const K o = SnnKeyT<K>::shx(x[e], j / E);
+                const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+                x[e] = lower ? lo : hi;
+            }
         }
-        const int M = __shfl(incl, 63);
-        if (lane <= kmax) {
-            L.u.g.pre[lane] = incl - mem.len;
-            L.u.g.h0[lane] = mem.h0;
-            L.u.g.hend[lane] = mem.hend;
-            L.u.g.cur[lane] = mem.cur;
+    }
+}
+
+template <int E, typename K, int k>
+__device__ __forceinline__ void snn_bitonic_merge(K (&x)[E], int lane) {
+    if constexpr (k <= E) {  // mirror stage inside the lane
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if ((e & (k / 2)) == 0) snn_ce(x[e], x[e ^ (k - 1)]);
+    } else {  // mirror stage across lanes: lane ^ (k/E - 1), element E-1-e
+        const bool lower = (lane & (k / (2 * E))) == 0;
+        K o[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[e] = SnnKeyT<K>::shx(x[E - 1 - e], k / E - 1);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const K lo = x[e] < o[e] ? x[e] : o[e], hi = x[e] < o[e] ? o[e] : x[e];
+            x[e] = lower ? lo : hi;
         }
-        if (lane == 0) L.u.g.pre[kmax + 1] = M;
-        WAVE_LDS_SYNC();
-        int mi = 0;
-        auto fetch = [&](int t, int& p, int& rp, int& ii) {
-            p = -1;
-            rp = 0;
-            ii = 0;
-            if (t < M) {
-                while (L.u.g.pre[mi + 1] <= t) ++mi;
-                ii = mi;
-                const long long q = L.u.g.h0[mi] + (t - L.u.g.pre[mi]);
-                if (q < L.u.g.hend[mi]) {
-                    const int2 hr = hosts_s[q];
-                    p = hr.x;
-                    rp = hr.y;
-                } else {
-                    p = L.u.g.cur[mi];
+    }
+    if constexpr (k >= 4) snn_bitonic_xor<E, K, k / 4>(x, lane);
+    if constexpr (k < 64 * E) snn_bitonic_merge<E, K, 2 * k>(x, lane);
+}
+
+template <int E, typename K>
+__device__ __forceinline__ void snn_bitonic(K (&x)[E], int lane) {
+    snn_bitonic_merge<E, K, 2>(x, lane);
+}
+
+// LDS of one node: the member table (lane i <= kmax holds member i; packed
+// for one 16-byte read per item: first host position, end, the member, first
+// item), the item -> member marks / transpose stage, and the W waves'
+// summaries.
+template <int E, int W, typename K>
+struct SnnBitonicLds {
+    int4 mem[64];
+    union {
+        int mark[64 * E * W];  // item t -> member whose run starts at t (-1 elsewhere)
+        K buf[64 * E * W];     // element-major -> lane-major transpose; cross-wave stages
+    } u;
+    int wfirst[W], wlast[W], wwhole[W], wcnt[W];
+    unsigned wout[W];
+    long long wc4[W][SNN_MAXK];
+};
+
+// One node, W waves (W = 1: one wave; W = 4: a 256-thread block for the
+// hubs); wave w holds sorted elements 64*E*w .. 64*E*(w+1) - 1.
+template <int E, int W, typename K>
+__device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, const SnnSpec& sp, int64_t n, int64_t j,
+                                                 const SnnMember& m, int wv, int lane,
+                                                 const int2* __restrict__ hosts_s, const SnnRows& rows,
+                                                 int64_t* __restrict__ cnt) {
+    constexpr int PS = SnnKeyT<K>::PS;
+    constexpr int S = 64 * E;  // elements per wave
+    const int kmax = sp.kk[sp.nk - 1];
+    const int incl = snn_scan_add(m.len);
+    const int M = __builtin_amdgcn_readlane(incl, 63);
+    const int pre = incl - m.len;
+    const int base = S * wv;  // this wave's first item / element
+#define SNN_SYNC()                            \
+    do {                                      \
+        if constexpr (W == 1) WAVE_LDS_SYNC(); \
+        else __syncthreads();                 \
+    } while (0)
+    // gather (element-major within the wave's slice)
+#pragma unroll
+    for (int e = 0; e < E; ++e) L.u.mark[base + 64 * e + lane] = -1;
+    if (wv == 0 && lane <= kmax) L.mem[lane] = make_int4((int)m.h0, (int)m.hend, m.cur, pre);
+    SNN_SYNC();
+    if (wv == 0 && lane <= kmax && m.len > 0) L.u.mark[pre] = lane;
+    SNN_SYNC();
+    int mi[E];
+    // the member of the slice's first item when its run starts in an earlier slice
+    const unsigned long long started = __ballot(lane <= kmax && m.len > 0 && pre < base);
+    int carry = started ? 63 - __clzll(started) : INT_MIN;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int v = snn_scan_max(max(L.u.mark[base + 64 * e + lane], carry));
+        carry = __builtin_amdgcn_readlane(v, 63);
+        mi[e] = v;
+    }
+    int2 hv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = base + 64 * e + lane;
+        hv[e] = make_int2(0, 0);
+        if (t < M) {
+            const int4 md = L.mem[mi[e]];
+            const int q = md.x + (t - md.w);
+            hv[e] = q < md.y ? hosts_s[q] : make_int2(md.z, 0);
+        }
+    }
+    K x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
+    SNN_SYNC();  // every mark is read
+#pragma unroll
+    for (int e = 0; e < E; ++e) L.u.buf[base + 64 * e + lane] = x[e];
+    SNN_SYNC();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = L.u.buf[base + E * lane + e];
+    snn_bitonic<E, K>(x, lane);
+    if constexpr (W > 1) {
+        // merges across waves through LDS: mirror stage, then the cross-wave
+        // xor stages, then the in-wave xor stages
+#pragma unroll
+        for (int k = 2 * S; k <= W * S; k <<= 1) {
+            SNN_SYNC();
+#pragma unroll
+            for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
+            SNN_SYNC();
+            {
+                const int pw = wv ^ (k / S - 1);
+                const bool lower = (wv & (k / (2 * S))) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const K o = L.u.buf[S * pw + E * (63 - lane) + (E - 1 - e)];
+                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+                    x[e] = lower ? lo : hi;
                 }
             }
-        };
-        int p, rp, ii;
-        fetch(lane, p, rp, ii);
-        bool full = false;
-        for (int t0 = 0; t0 < M; t0 += 64) {
-            int np, nrp, nii;
-            fetch(t0 + 64 + lane, np, nrp, nii);
-            bool ok = true;
-            if (p >= 0) {
-                const unsigned c = snn_contrib(sp, ii, rp);
-                if (c != sp.init) ok = table_insert64(tab, p, c, sp, snn_log2<WT>(), WT);
-            }
-            full = __any(!ok);
-            if (full) break;
-            p = np;
-            rp = nrp;
-            ii = nii;
-        }
-        WAVE_LDS_SYNC();
-        // Compact: every lane reads its WT/64 slots (slot r*64 + lane) to
-        // registers first, so the in-place writes cannot overtake a pending read.
-        int u = 0;
-        if (!full) {
-            unsigned long long e[WT / 64];
 #pragma unroll
-            for (int r = 0; r < WT / 64; ++r) e[r] = tab[r * 64 + lane];
-            WAVE_LDS_SYNC();
+            for (int jj = k / 4; jj >= S; jj >>= 1) {
+                SNN_SYNC();
 #pragma unroll
-            for (int r = 0; r < WT / 64; ++r) {
-                const bool occ = e[r] != SNN_EMPTY64;
-                const unsigned long long m = __ballot(occ);
-                if (occ) tab[u + __popcll(m & lanemask_lt())] = e[r];
-                u += __popcll(m);
+                for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
+                SNN_SYNC();
+                const int pw = wv ^ (jj / S);
+                const bool lower = (wv & (jj / S)) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const K o = L.u.buf[S * pw + E * lane + e];
+                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+                    x[e] = lower ? lo : hi;
+                }
             }
-            WAVE_LDS_SYNC();
+            snn_bitonic_xor<E, K, S / 2>(x, lane);
         }
-        if (full || u > CAP) {
-            if (lane == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
-            continue;
+    }
+    // runs of equal p: forward segmented combine inside the lane
+    int p[E];
+    unsigned agg[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        p[e] = (int)(x[e] >> PS);
+        const unsigned c = snn_key_contrib<K>(sp, x[e]);
+        agg[e] = (e > 0 && p[e] == p[e - 1]) ? snn_combine(sp.type, agg[e - 1], c) : c;
+    }
+    // across lanes: the lane's last run continues into the next lane when
+    // that lane starts with the same p; segmented inclusive scan of the lane
+    // tails (a lane that is one run continuing from the left is not a head)
+    const int first_p = p[0], last_p = p[E - 1];
+    const int prev_last = __shfl_up(last_p, 1, 64);
+    const bool cont = lane > 0 && prev_last == first_p;
+    unsigned out = agg[E - 1];
+    int head = !(cont && first_p == last_p);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = (unsigned)__shfl_up((int)out, o, 64);
+        const int fy = __shfl_up(head, o, 64);
+        if (lane >= o && !head) {
+            out = snn_combine(sp.type, y, out);
+            head = fy;
         }
-        const int64_t ro = rows.roff[j];
-        const int R = (u + 63) >> 6;
-        int* hist = L.u.s.hist;
-        int* bst = L.u.s.bst;
-        if (u == 0) {
-        } else if (R <= 4) snn_bucket_store<4>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
-        else if (R <= 8) snn_bucket_store<8>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
-        else if (R <= 12) snn_bucket_store<12>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
-        else snn_bucket_store<CAP / 64>(tab, u, lane, j, n, hist, bst, rows.nbr + ro, rows.wpk + ro, write);
-        WAVE_LDS_SYNC();
-        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
-        for (int c = lane; c < u; c += 64) {
-            const unsigned v = (unsigned)tab[c];
+    }
+    const unsigned from_left = (unsigned)__shfl_up((int)out, 1, 64);
+    const int next_first = __shfl_down(first_p, 1, 64);
+    const int wfirst = __builtin_amdgcn_readfirstlane(first_p);
+    int wnext = INT_MAX;  // the first p of the next wave
+    bool wcarry = false;
+    unsigned wc = 0;
+    if constexpr (W > 1) {
+        if (lane == 63) {
+            L.wlast[wv] = last_p;
+            L.wout[wv] = out;
+        }
+        if (lane == 0) L.wfirst[wv] = first_p;
+        SNN_SYNC();
+        if (lane == 0) L.wwhole[wv] = L.wfirst[wv] == L.wlast[wv];
+        SNN_SYNC();
+        if (wv + 1 < W) wnext = L.wfirst[wv + 1];
+        // the wave's first run continues runs ending the waves to its left
+        for (int v = wv - 1; v >= 0; --v) {
+            if (L.wlast[v] != wfirst) break;
+            wc = wcarry ? snn_combine(sp.type, L.wout[v], wc) : L.wout[v];
+            wcarry = true;
+            if (!L.wwhole[v]) break;
+        }
+    }
+    int u_lane = 0;
+    bool last[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (cont && p[e] == first_p) agg[e] = snn_combine(sp.type, from_left, agg[e]);
+        if (wcarry && p[e] == wfirst) agg[e] = snn_combine(sp.type, wc, agg[e]);
+        const int pn = e + 1 < E ? p[e + 1] : (lane < 63 ? next_first : wnext);
+        last[e] = (unsigned)p[e] < (unsigned)n && p[e] != pn;  // padding keys decode to p >= n or -1
+        u_lane += last[e] ? 1 : 0;
+    }
+    const int u_incl = snn_scan_add(u_lane);
+    int u = __builtin_amdgcn_readlane(u_incl, 63);
+    int64_t ro = rows.roff[j] + (u_incl - u_lane);
+    if constexpr (W > 1) {
+        if (lane == 0) L.wcnt[wv] = u;
+        SNN_SYNC();
+        int before = 0, tot = 0;
+        for (int v = 0; v < W; ++v) {
+            before += v < wv ? L.wcnt[v] : 0;
+            tot += L.wcnt[v];
+        }
+        ro += before;
+        u = tot;
+    }
+    const bool write = rows.roff[n] <= rows.cap;
+    int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+    int w = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (last[e]) {
+            if (write) {
+                rows.nbr[ro + w] = p[e];
+                rows.wpk[ro + w] = agg[e];
+            }
+            ++w;
 #pragma unroll
             for (int t = 0; t < SNN_MAXK; ++t)
-                if (t < sp.nk && graph_has(sp, v, t)) ++c4[t];
+                if (t < sp.nk && graph_has(sp, agg[e], t)) ++c4[t];
         }
+    }
+    if constexpr (W == 1) {
         snn_row_counts(sp, c4, n, j, lane, cnt);
-        if (lane == 0) rows.rlen[j] = u;
-        WAVE_LDS_SYNC();
+    } else {
+#pragma unroll
+        for (int t = 0; t < SNN_MAXK; ++t) {
+            int64_t v = c4[t];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) L.wc4[wv][t] = v;
+        }
+        SNN_SYNC();
+        if (wv == 0 && lane < sp.nk) {
+            int64_t v = 0;
+            for (int q = 0; q < W; ++q) v += L.wc4[q][lane];
+            cnt[(int64_t)lane * (n + 1) + j] = v;
+        }
+    }
+    if (wv == 0 && lane == 0) rows.rlen[j] = u;
+#undef SNN_SYNC
+}
+
+// Size classes (items M of a node): 0: M <= 512 (E = 4 or 8 per node),
+// 1: <= 1024 (E = 16), 2: <= 2048 (E = 32), 3: <= 4096 (the hubs: 4 waves x
+// E = 16 per node), larger: the block tier.  Classes 0..2 run one node per
+// wave (4 waves per block, 2 for class 2: its LDS stage is 8-16 KB per wave);
+// class 3 runs one node per 256-thread block over a fixed grid.
+__host__ __device__ constexpr int snn_bitonic_wpb(int cls) { return cls == 2 ? 2 : 4; }
+template <int CLS, typename K>
+__global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_kernel(
+    const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
+    const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
+    int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ list, const int64_t* __restrict__ count,
+    int* __restrict__ ov_list, int* __restrict__ ov_count) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kmax = sp.kk[sp.nk - 1];
+    if constexpr (CLS == 3) {
+        __shared__ SnnBitonicLds<16, 4, K> lds3;
+        const int64_t nl = *count;
+        for (int64_t f = blockIdx.x; f < nl; f += gridDim.x) {
+            const int64_t j = list[f];
+            if (rows.roff[j + 1] - rows.roff[j] > SNN_BITONIC_MAX) {
+                if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
+                continue;
+            }
+            const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+            snn_bitonic_node<16, 4, K>(lds3, sp, n, j, m, wv, lane, hosts_s, rows, cnt);
+            __syncthreads();
+        }
+    } else {
+        constexpr int EM = CLS == 0 ? 8 : (CLS == 1 ? 16 : 32);
+        constexpr int WPB = snn_bitonic_wpb(CLS);
+        __shared__ SnnBitonicLds<EM, 1, K> lds_all[WPB];
+        const int64_t f = (int64_t)blockIdx.x * WPB + wv;
+        if (f >= *count) return;
+        const int64_t j = list[f];
+        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        if constexpr (CLS == 0) {
+            if (__builtin_amdgcn_readlane(snn_scan_add(m.len), 63) <= 256) {
+                snn_bitonic_node<4, 1, K>(*reinterpret_cast<SnnBitonicLds<4, 1, K>*>(&lds_all[wv]), sp, n, j, m, 0,
+                                          lane, hosts_s, rows, cnt);
+                return;
+            }
+        }
+        snn_bitonic_node<EM, 1, K>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
     }
 }
 
 // --------------------------------------------------------- block tier --
-// Same algorithm with one 256-thread block and a 16K-slot table per node,
-// for the overflow list of the hash tier; the table is compacted and
-// bitonic-sorted by partner in LDS.  Nodes that overflow here too are
-// appended to ov2 for the dense tier.
+// Nodes beyond the bitonic tier (more than SNN_BITONIC_MAX items): one
+// 256-thread block and a 16K-slot LDS hash table per node; the table is
+// compacted and bitonic-sorted by partner in LDS.  Nodes that overflow here
+// too are appended to ov2 for the dense tier.
 __device__ __forceinline__ bool table_insert_blk(int* keys, unsigned* vals, int* count, int p, unsigned c,
                                                  const SnnSpec& sp, int bits) {
     unsigned s = snn_hash(p, bits);
@@ -1075,7 +1013,6 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     int32_t* vals = pairs + (nkk + 16);
     int32_t* skey = vals + (nkk + 16);
     int32_t* sval = skey + (nkk + 16);
-    int* ov_list = ov + 3 * n;
     int* ov2_list = ov + 4 * n;
     int* ov_count = ov + 5 * n;  // [1] block tier, [2] dense tier
     if (!roff) roff = hoff + (n + 1);
@@ -1107,15 +1044,23 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     rc = ccg_scan_i64(ctx, cls, cls, n, st);
     if (rc) return rc;
     snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
-    const unsigned nsb = (unsigned)ccg_cdiv(n, SNN_WAVES);
-    snn_sort_build_kernel<0><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
-                                                             lists, ccount);
-    snn_sort_build_kernel<1><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
-                                                             lists + n, ccount + 1);
-    snn_sort_build_kernel<2><<<nsb, 64 * SNN_WAVES, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows,
-                                                             lists + 2 * n, ccount + 2);
-    snn_wave_build_kernel<SNN_WT><<<(unsigned)std::min<int64_t>(nsb, 1024), 64 * SNN_WAVES, 0, st>>>(
-        knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + 3 * n, ccount + 3, ov_list, ov_count + 1);
+    int* ov_list = ov + 3 * n;
+#define SNN_BITONIC(CLS_, K_, GRID_)                                                                           \
+    snn_bitonic_build_kernel<CLS_, K_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                       \
+        knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
+        ov_count + 1)
+#define SNN_BITONIC_ALL(K_)                                                       \
+    do {                                                                          \
+        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)));             \
+        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)));             \
+        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)));             \
+        SNN_BITONIC(3, K_, 1024u);                                                 \
+    } while (0)
+    if (sp.type == CCG_SNN_NUMBER) SNN_BITONIC_ALL(uint32_t);
+    else SNN_BITONIC_ALL(unsigned long long);
+#undef SNN_BITONIC_ALL
+#undef SNN_BITONIC
+    // nodes with more than SNN_BITONIC_MAX items: the block tier, then dense
     snn_block_kernel<<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list, ov_count + 1,
                                           ov2_list, ov_count + 2);
     snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,

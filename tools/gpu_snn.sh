@@ -1,17 +1,14 @@
 #!/bin/bash
-# SNN micro-benchmark variants + kernel trace + one PMC pass.
+# SNN iteration on the GPU: the SNN parity tests, the cfg3 micro-benchmark
+# (tools/snn_micro.py), then its kernel trace.  Stops at the first crash-like exit.
 mkdir -p gpurun_out/snn
 export TMPDIR=/tmp
-: > gpurun_out/snn/micro.log
-for v in 0 1 2 3; do
-  CCG_SNN_EXP=$v timeout -k 10 300 python tools/snn_micro.py >> gpurun_out/snn/micro.log 2>>gpurun_out/snn/micro.err || exit $?
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+    -k "${PYTEST_K:-snn}" > gpurun_out/snn/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/snn/pytest.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/snn_micro.py > gpurun_out/snn/micro.log 2> gpurun_out/snn/micro.err || exit $?
+[ -n "$NO_PROF" ] && exit 0
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/snn/prof -o run -- \
-    python3 $GRAFT_REPO_ROOT/tools/snn_micro.py > $GRAFT_REPO_ROOT/gpurun_out/snn/prof.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS \
-    --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/snn/pmc/A -o run -- \
-    python3 $GRAFT_REPO_ROOT/tools/snn_micro.py > $GRAFT_REPO_ROOT/gpurun_out/snn/pmcA.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY \
-    --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/snn/pmc/B -o run -- \
-    python3 $GRAFT_REPO_ROOT/tools/snn_micro.py > $GRAFT_REPO_ROOT/gpurun_out/snn/pmcB.log 2>&1 || exit $?
+    python3 $GRAFT_REPO_ROOT/tools/snn_micro.py > $GRAFT_REPO_ROOT/gpurun_out/snn/prof.log 2>&1
