@@ -319,6 +319,29 @@ __device__ __forceinline__ int snn_scan_add(int v) {
     return v;
 }
 
+// Value of lane (lane ^ MSK) for the masks the bitonic network uses, without
+// an LDS address round trip where the hardware has a direct path: DPP
+// quad_perm / row (half-)mirror for 1, 2, 3, 7, 15; ds_swizzle (bit mode,
+// within 32 lanes) for 4, 8, 16, 31; v_permlane32_swap for 32 (and 63 = 32
+// then 31).
+template <int MSK>
+__device__ __forceinline__ unsigned snn_xlane(unsigned v) {
+    if constexpr (MSK == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (MSK == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (MSK == 3) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);
+    else if constexpr (MSK == 7) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    else if constexpr (MSK == 15) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    else if constexpr (MSK == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    } else if constexpr (MSK == 63) {
+        return snn_xlane<31>(snn_xlane<32>(v));
+    } else {
+        static_assert(MSK == 4 || MSK == 8 || MSK == 16 || MSK == 31, "unsupported lane mask");
+        return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (MSK << 10));
+    }
+}
+
 template <typename K>
 struct SnnKeyT;
 template <>
@@ -327,7 +350,8 @@ struct SnnKeyT<uint32_t> {
     __device__ static uint32_t make(int p, int rj, int rp) { return ((uint32_t)p << 6) | (uint32_t)max(rj, rp); }
     __device__ static int m(uint32_t k) { return (int)(k & 63u); }
     __device__ static int rs(uint32_t) { return 0; }
-    __device__ static uint32_t shx(uint32_t v, int msk) { return (uint32_t)__shfl_xor((int)v, msk, 64); }
+    template <int MSK>
+    __device__ static uint32_t shx(uint32_t v) { return snn_xlane<MSK>(v); }
 };
 template <>
 struct SnnKeyT<unsigned long long> {
@@ -337,9 +361,10 @@ struct SnnKeyT<unsigned long long> {
     }
     __device__ static int m(unsigned long long k) { return (int)(k & 0xFFu); }
     __device__ static int rs(unsigned long long k) { return (int)((k >> 8) & 0xFFu); }
-    __device__ static unsigned long long shx(unsigned long long v, int msk) {
-        const int lo = __shfl_xor((int)(unsigned)v, msk, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), msk, 64);
-        return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+    template <int MSK>
+    __device__ static unsigned long long shx(unsigned long long v) {
+        const unsigned lo = snn_xlane<MSK>((unsigned)v), hi = snn_xlane<MSK>((unsigned)(v >> 32));
+        return ((unsigned long long)hi << 32) | lo;
     }
 };
 
@@ -368,22 +393,20 @@ __device__ __forceinline__ void snn_ce(K& a, K& b) {  // (a, b) <- (min, max)
 // stages j = J .. 1 of one merge (J < 64*E).
 template <int E, typename K, int J>
 __device__ __forceinline__ void snn_bitonic_xor(K (&x)[E], int lane) {
+    if constexpr (J < E) {
 #pragma unroll
-    for (int j = J; j >= 1; j >>= 1) {
-        if (j < E) {
+        for (int e = 0; e < E; ++e)
+            if ((e & J) == 0) snn_ce(x[e], x[e ^ J]);
+    } else {
+        const bool lower = (lane & (J / E)) == 0;
 #pragma unroll
-            for (int e = 0; e < E; ++e)
-                if ((e & j) == 0) snn_ce(x[e], x[e ^ j]);
-        } else {
-            const bool lower = (lane & (j / E)) == 0;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const K o = SnnKeyT<K>::shx(x[e], j / E);
-                const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
-                x[e] = lower ? lo : hi;
-            }
+        for (int e = 0; e < E; ++e) {
+            const K o = SnnKeyT<K>::template shx<J / E>(x[e]);
+            const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+            x[e] = lower ? lo : hi;
         }
     }
+    if constexpr (J > 1) snn_bitonic_xor<E, K, J / 2>(x, lane);
 }
 
 template <int E, typename K, int k>
@@ -396,7 +419,7 @@ __device__ __forceinline__ void snn_bitonic_merge(K (&x)[E], int lane) {
         const bool lower = (lane & (k / (2 * E))) == 0;
         K o[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) o[e] = SnnKeyT<K>::shx(x[E - 1 - e], k / E - 1);
+        for (int e = 0; e < E; ++e) o[e] = SnnKeyT<K>::template shx<k / E - 1>(x[E - 1 - e]);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const K lo = x[e] < o[e] ? x[e] : o[e], hi = x[e] < o[e] ? o[e] : x[e];
