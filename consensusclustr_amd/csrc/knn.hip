@@ -323,9 +323,11 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
 // ccg_debug_knn_stamps reads the sums.  The stamps' own waits inflate the
 // tile share.
 #ifdef KNN_STAMPS
-__device__ unsigned long long knn_stamp_acc[8];
+// kst_[7..10] count events: tiles with a candidate (7), flushes (8), flush
+// insertion rounds (9), tiles (10); knn_stamp_acc[11] counts waves.
+__device__ unsigned long long knn_stamp_acc[12];
 #define KST_DECL                                                \
-    unsigned long long kst_[7] = {0, 0, 0, 0, 0, 0, 0};        \
+    unsigned long long kst_[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     unsigned long long kst_t = __builtin_amdgcn_s_memtime()
 #define KST(i)                                                     \
     do {                                                           \
@@ -336,18 +338,21 @@ __device__ unsigned long long knn_stamp_acc[8];
 #define KST_FLUSH_OUT()                                                             \
     do {                                                                            \
         if ((threadIdx.x & 63) == 0) {                                              \
-            for (int i_ = 0; i_ < 7; ++i_) atomicAdd(&knn_stamp_acc[i_], kst_[i_]); \
-            atomicAdd(&knn_stamp_acc[7], 1ull);                                     \
+            for (int i_ = 0; i_ < 11; ++i_) atomicAdd(&knn_stamp_acc[i_], kst_[i_]); \
+            atomicAdd(&knn_stamp_acc[11], 1ull);                                    \
         }                                                                           \
     } while (0)
-extern "C" int ccg_debug_knn_stamps(unsigned long long* out8) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(knn_stamp_acc), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define KSC(i) (kst_[i] += 1)
+extern "C" int ccg_debug_knn_stamps(unsigned long long* out12) {
+    if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(knn_stamp_acc), 12 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(knn_stamp_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #else
 #define KST_DECL
 #define KST(i)
+#define KSC(i)
 #define KST_FLUSH_OUT()
 #endif
 
@@ -460,7 +465,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     bool tdirty = false;  // lists changed since T was last set to the union threshold
 #define KNN_FLUSH()                                                                   \
     do {                                                                              \
+        KSC(8);                                                                       \
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
+            KSC(9);                                                                   \
             if (i_ < qc) {                                                            \
                 const uint2 e_ = qbw[i_ * 64 + lane];                                 \
                 const float v_ = __uint_as_float(e_.x);                               \
@@ -532,7 +539,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
             for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
             KST(1);
+            KSC(10);
             if (__any(vmax > T)) {
+                KSC(7);
                 // branch-free: a write at slot qc is kept only if qc advances
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {

@@ -13,13 +13,18 @@
 // reproducible regardless of scheduling; the scale is chosen on the device
 // from max|x| so no partial sum can overflow.  Quantisation error is below
 // 2^-36 relative for the sizes we support, far inside the 1e-5 tolerance.
-// Grid: (row tiles of 256) x (groups of SIL_LG labelings); x rows are held in
+// The widths' squared distances are |x|^2 + |mu|^2 + v - 2 x.mu with x.mu on
+// the fp64 matrix core (a fixed-order MFMA chain, so also reproducible).
+// Grid: (row tiles) x (groups of SIL_LG labelings); x rows are held in
 // registers and reused across the group.
 #include <math.h>
 
 #include "ccg_internal.h"
 
 #define SIL_T 256
+#ifndef SIL_EXP
+#define SIL_EXP 0  // tools only: 1 = no width epilogue, 2 = no MFMA (timing variants)
+#endif
 #ifndef SIL_LG
 #define SIL_LG 10
 #endif
@@ -56,7 +61,21 @@ __device__ __forceinline__ void load_row(const double* __restrict__ x, int64_t r
 
 // K1: fixed-point cluster sums and counts, staged in LDS when (cmax + 1) x d
 // accumulators fit (SIL_LDS_CAP), else added straight to the global sums.
+// A block covers SIL_CT tiles of SIL_T rows, so each labeling's LDS sums are
+// flushed to the global sums once per SIL_CT tiles (the flush atomics from
+// every block meet on the same words).  With SIL_CT == 1 the rows stay in
+// registers, already quantised, across the block's labelings.
 #define SIL_LDS_CAP 65536
+#ifndef SIL_CT
+#define SIL_CT 1
+#endif
+template <int DMAX>
+__device__ __forceinline__ void quant_row(const double* __restrict__ x, int64_t r, bool in, int d, double sc,
+                                          long long (&q)[DMAX]) {
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) q[k] = (in && k < d) ? __double2ll_rn(x[r * d + k] * sc) : 0ll;
+}
+
 template <int DMAX, bool LDS>
 __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__ x, int64_t m,
                                                       int d, const int32_t* __restrict__ labels,
@@ -67,12 +86,11 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* acc = (unsigned long long*)smem;          // [cmax+1][d]
     unsigned* cnt = (unsigned*)(acc + (int64_t)(cmax + 1) * d);   // [cmax+1]
-    const int64_t r = (int64_t)blockIdx.x * SIL_T + threadIdx.x;
-    const bool in = r < m;
-    double xr[DMAX];
-    load_row<DMAX>(x, in ? r : 0, d, xr);
+    const int64_t rb = (int64_t)blockIdx.x * (SIL_T * SIL_CT) + threadIdx.x;
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
     const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
+    long long q[DMAX];
+    if (SIL_CT == 1) quant_row<DMAX>(x, rb, rb < m, d, sc, q);
     const int nacc = (cmax + 1) * d;
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
@@ -83,18 +101,21 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
             for (int t = threadIdx.x; t <= cmax; t += SIL_T) cnt[t] = 0u;
             __syncthreads();
         }
-        if (in) {
-            const int lab = labels[(int64_t)l * m + r];
-            if (lab >= 1 && lab <= cmax) {
+        for (int ct = 0; ct < SIL_CT; ++ct) {
+            const int64_t r = rb + ct * SIL_T;
+            if (SIL_CT > 1) quant_row<DMAX>(x, r, r < m, d, sc, q);
+            if (r < m) {
+                const int lab = labels[(int64_t)l * m + r];
+                if (lab >= 1 && lab <= cmax) {
 #pragma unroll
-                for (int k = 0; k < DMAX; ++k)
-                    if (k < d) {
-                        const unsigned long long q = (unsigned long long)__double2ll_rn(xr[k] * sc);
-                        if (LDS) atomicAdd(&acc[lab * d + k], q);
-                        else atomicAdd(&gs[(int64_t)lab * d + k], q);
-                    }
-                if (LDS) atomicAdd(&cnt[lab], 1u);
-                else atomicAdd(&gc[lab], 1ull);
+                    for (int k = 0; k < DMAX; ++k)
+                        if (k < d) {
+                            if (LDS) atomicAdd(&acc[lab * d + k], (unsigned long long)q[k]);
+                            else atomicAdd(&gs[(int64_t)lab * d + k], (unsigned long long)q[k]);
+                        }
+                    if (LDS) atomicAdd(&cnt[lab], 1u);
+                    else atomicAdd(&gc[lab], 1ull);
+                }
             }
         }
         if (LDS) {
@@ -127,9 +148,19 @@ __device__ __forceinline__ int sil_block_excl_scan(int v, int* sh, int* total) {
     return woff + x - v;
 }
 
+// Dimension order of a centroid row in muc: position p holds dimension
+// (p % KS) * 4 + p / KS (KS = DMAX / 4), so the KS values a lane feeds to the
+// K steps of v_mfma_f64_16x16x4f64 (dims 4s + (lane >> 4)) are contiguous.
+template <int DMAX>
+__host__ __device__ __forceinline__ int sil_mfma_pos(int k) {
+    constexpr int KS = DMAX / 4;
+    return (k & 3) * KS + (k >> 2);
+}
+
 // K2: per labeling, the present codes (ascending = sort(unique(clusters)))
-// and the centroids mu[l][c][0..DMAX) (zero padded) plus |mu_c|^2, from the
-// fixed-point sums.  One block per labeling.
+// and the centroids mu[l][c][0..DMAX) (zero padded; muc: present clusters
+// only, in MFMA dimension order) plus |mu_c|^2, from the fixed-point sums.
+// One block per labeling.
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
                                                 const unsigned* __restrict__ maxabs_bits,
@@ -165,7 +196,7 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
         const double v = (n && k < d) ? ((double)(long long)gs[(int64_t)c * d + k] * inv_sc) / (double)n : 0.0;
         ml[t] = v;
         const int pc = pl[c];
-        if (pc >= 0) mcl[(int64_t)pc * DMAX + k] = v;
+        if (pc >= 0) mcl[(int64_t)pc * DMAX + sil_mfma_pos<DMAX>(k)] = v;
     }
     __syncthreads();
     for (int c = threadIdx.x; c <= cmax; c += SIL_T) {
@@ -245,17 +276,27 @@ __global__ void sil_vfin(int64_t m, int d, int L, int cmax, const unsigned* __re
     auxc[(l * cmax + p) * 2 + 1] = ((double)gvar[t] * inv_vsc) / (double)gcnt[t];
 }
 
-// K5: widths and their fixed-point sum over non-NaN rows.  Each thread
-// owns two rows (r and r + SIL_T of a 2*SIL_T-row tile) so that every
-// centroid value read from LDS (a broadcast ds_read_b128 = 2 dims) feeds 4
-// FMAs.  Squared distances to the other clusters use |x|^2 + |mu|^2 - 2 x.mu
-// (one FMA per dimension), clamped at 0 (|error| ~ 1e-16 |x|^2, far inside
-// the 1e-5 tolerance); the own-cluster distance, the one that can be ~0, is
-// taken in the difference form.  D is monotone in s + v_c, so the minimum is
-// taken on the squares and one sqrt applied at the end.
+// K5: widths and their fixed-point sum over non-NaN rows.
+//   D^2(i, c) = |x_i|^2 + (|mu_c|^2 + v_c) - 2 x_i.mu_c
+// with x.mu on the fp64 matrix core: v_mfma_f64_16x16x4f64 with A = 16
+// centroids x 4 dims (LDS) and B = 4 dims x 16 rows (registers, loaded once
+// per block), so accumulator i of lane (g, j) = g + 4i-th centroid of the
+// tile against row j of the lane's row tile.  The epilogue is branch-free and
+// per value costs one fma, one compare, three selects and one min: each lane
+// keeps, per row, min over the other clusters of (|mu|^2 + v - 2 x.mu) and the
+// own cluster's value; |x|^2 is added once per row, then clamped at 0 (the
+// identity's cancellation noise is ~1e-16 |x|^2, far inside the 1e-5
+// tolerance).  D is monotone in the square: one sqrt per row.  The four lane
+// groups are merged at the end.  Rows per block: 4 waves x RT tiles x 16.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
 template <int DMAX>
-__device__ __forceinline__ void sil_row_width(const double (&xr)[DMAX], double selfsq, double oth2, bool in,
-                                              int np, double wsc, double* out_w, long long& wq, unsigned& wn) {
+constexpr int sil_rt() {
+    return DMAX <= 32 ? 4 : 2;  // row tiles per wave (B fragments: RT x DMAX/4 doubles per lane)
+}
+
+__device__ __forceinline__ void sil_row_width(double selfsq, double oth2, bool in, int np, double wsc,
+                                              double* out_w, long long& wq, unsigned& wn) {
     if (!in) return;
     const double selfd = sqrt(selfsq), othd = sqrt(oth2);
     double w;
@@ -273,10 +314,18 @@ __device__ __forceinline__ void sil_row_width(const double (&xr)[DMAX], double s
     }
 }
 
-// centroids per LDS stage of sil_width: [CH][DMAX] f64 + [CH][2] f64 + [CH] int within 64 KB
+// LDS stage of sil_width: ch centroids ([ch][DMAX + 2] f64: the 16-byte row
+// pad spreads the 16 lanes of a fragment read over distinct banks), [ch] f64
+// |mu|^2 + v and [ch] codes; ch = min(sil_chunk, cmax rounded up to 16) keeps
+// the stage within 64 KB and, for the usual cmax <= 64, small enough for
+// several blocks per CU.
 template <int DMAX>
 constexpr int sil_chunk() {
-    return DMAX <= 16 ? 256 : (DMAX <= 32 ? 224 : 112);
+    return DMAX <= 16 ? 256 : (DMAX <= 32 ? 208 : 112);
+}
+template <int DMAX>
+constexpr int sil_sp() {
+    return DMAX + 2;
 }
 
 template <int DMAX>
@@ -284,124 +333,210 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
                                                    const int32_t* __restrict__ labels, int L, int cmax,
                                                    const int* __restrict__ npres,
                                                    const int* __restrict__ codes,
-                                                   const int* __restrict__ pos,
                                                    const double* __restrict__ muc,
                                                    const double* __restrict__ auxc,
                                                    unsigned long long* __restrict__ wsum,
                                                    unsigned long long* __restrict__ wcnt,
-                                                   double* __restrict__ out_width) {
+                                                   double* __restrict__ out_width, int CH) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int CH = sil_chunk<DMAX>();          // centroids staged per pass
-    double* smu = (double*)smem;                  // [CH][DMAX]
-    double* sau = smu + (int64_t)CH * DMAX;       // [CH][2]
-    int* scode = (int*)(sau + 2 * (int64_t)CH);   // [CH]
-    const int64_t ra = (int64_t)blockIdx.x * (2 * SIL_T) + threadIdx.x, rb = ra + SIL_T;
-    const bool ina = ra < m, inb = rb < m;
-    double xa[DMAX], xb[DMAX];
-    load_row<DMAX>(x, ina ? ra : 0, d, xa);
-    load_row<DMAX>(x, inb ? rb : 0, d, xb);
-    double xxa = 0.0, xxb = 0.0;
+    // CH: centroids staged per pass (a multiple of 16)
+    constexpr int KS = DMAX / 4;  // K steps of 4 dims
+    constexpr int RT = sil_rt<DMAX>();
+    constexpr int SP = sil_sp<DMAX>();
+    double* smu = (double*)smem;              // [CH][SP], MFMA dimension order
+    double* smv = smu + (int64_t)CH * SP;     // [CH] |mu|^2 + v (+inf: padding)
+    int* scode = (int*)(smv + CH);            // [CH]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int64_t r0 = (int64_t)blockIdx.x * (4 * RT * 16) + wave * (RT * 16);
+    double xb[RT][KS];
+    double xx[RT];
+    bool in[RT];
 #pragma unroll
-    for (int k = 0; k < DMAX; ++k) {
-        xxa = fma(xa[k], xa[k], xxa);
-        xxb = fma(xb[k], xb[k], xxb);
+    for (int t = 0; t < RT; ++t) {
+        const int64_t r = r0 + t * 16 + j;
+        in[t] = r < m;
+        double p = 0.0;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + g;
+            xb[t][s] = (in[t] && k < d) ? x[r * d + k] : 0.0;
+            p = fma(xb[t][s], xb[t][s], p);
+        }
+        p += __shfl_xor(p, 16, 64);
+        p += __shfl_xor(p, 32, 64);
+        xx[t] = p;
     }
     const double wsc = ldexp(1.0, scale_exp((double)m));
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
         const int np = npres[l];
-        const int laba = ina ? labels[(int64_t)l * m + ra] : 0;
-        const int labb = inb ? labels[(int64_t)l * m + rb] : 0;
+        int lab[RT];
+        double oth[RT], self[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            lab[t] = in[t] ? labels[(int64_t)l * m + r0 + t * 16 + j] : 0;
+            oth[t] = INFINITY;
+            self[t] = INFINITY;
+        }
         const double* ml = muc + (int64_t)l * cmax * DMAX;
         const double* al = auxc + (int64_t)l * cmax * 2;
-        double otha = INFINITY, othb = INFINITY;
         for (int p0 = 0; p0 < np; p0 += CH) {
             const int nc = min(CH, np - p0);
-            for (int t = threadIdx.x; t < nc * DMAX; t += SIL_T) smu[t] = ml[(int64_t)p0 * DMAX + t];
-            for (int t = threadIdx.x; t < 2 * nc; t += SIL_T) sau[t] = al[2 * (int64_t)p0 + t];
-            for (int t = threadIdx.x; t < nc; t += SIL_T) scode[t] = codes[(int64_t)l * cmax + p0 + t];
+            const int nct = (nc + 15) & ~15;  // whole 16-centroid tiles; padding: zero centroid, +inf offset
+            for (int t = threadIdx.x; t < nct * DMAX; t += SIL_T) {
+                const int c = t / DMAX, p = t - c * DMAX;
+                smu[c * SP + p] = t < nc * DMAX ? ml[(int64_t)p0 * DMAX + t] : 0.0;
+            }
+            for (int t = threadIdx.x; t < nct; t += SIL_T) {
+                smv[t] = t < nc ? al[2 * (int64_t)(p0 + t)] + al[2 * (int64_t)(p0 + t) + 1] : INFINITY;
+                scode[t] = t < nc ? codes[(int64_t)l * cmax + p0 + t] : -1;
+            }
             __syncthreads();
-            for (int pi = 0; pi < nc; ++pi) {
-                const double2* mc = reinterpret_cast<const double2*>(smu + pi * DMAX);
-                double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+            for (int c0 = 0; c0 < nct; c0 += 16) {
+                double a[KS];
+                const double* ap = smu + (c0 + j) * SP + g * KS;
 #pragma unroll
-                for (int k2 = 0; k2 < DMAX / 2; ++k2) {
-                    const double2 mv = mc[k2];
-                    a0 = fma(xa[2 * k2], mv.x, a0);
-                    a1 = fma(xa[2 * k2 + 1], mv.y, a1);
-                    b0 = fma(xb[2 * k2], mv.x, b0);
-                    b1 = fma(xb[2 * k2 + 1], mv.y, b1);
+                for (int s = 0; s < KS; s += 2) {
+                    const double2 v = *reinterpret_cast<const double2*>(ap + s);
+                    a[s] = v.x;
+                    a[s + 1] = v.y;
                 }
-                const double mm = sau[2 * pi], vc = sau[2 * pi + 1];
-                const int c = scode[pi];
-                const double sa = fmax(fma(-2.0, a0 + a1, xxa + mm), 0.0) + vc;
-                const double sb = fmax(fma(-2.0, b0 + b1, xxb + mm), 0.0) + vc;
-                if (c != laba && sa < otha) otha = sa;
-                if (c != labb && sb < othb) othb = sb;
+                double mv[4];
+                int code[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    mv[i] = smv[c0 + g + 4 * i];
+                    code[i] = scode[c0 + g + 4 * i];
+                }
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#if SIL_EXP == 2
+                    acc[0] = a[0] * xb[t][0];
+                    acc[1] = a[1] * xb[t][1];
+                    acc[2] = a[2] * xb[t][2];
+                    acc[3] = a[3] * xb[t][3];
+#else
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], xb[t][s], acc, 0, 0, 0);
+#endif
+#if SIL_EXP == 1
+                    oth[t] = fmin(oth[t], (acc[0] + acc[1]) + (acc[2] + acc[3]));
+                    continue;
+#endif
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double tv = fma(-2.0, acc[i], mv[i]);
+                        const bool own = code[i] == lab[t];
+                        self[t] = own ? tv : self[t];
+                        // the own cluster leaves the minimum by a high word of +DBL_MAX
+                        const double cand = __hiloint2double(own ? 0x7fefffff : __double2hiint(tv), __double2loint(tv));
+                        oth[t] = __builtin_fmin(oth[t], cand);
+                    }
+                }
             }
             __syncthreads();  // before the next chunk (or labeling) overwrites the stage
         }
-        // own cluster in the difference form: exact 0 for a singleton, as in R
-        double selfa = INFINITY, selfb = INFINITY;
-        if (ina && laba >= 1 && laba <= cmax) {
-            const int p = pos[(int64_t)l * (cmax + 1) + laba];
-            const double* mcp = ml + (int64_t)p * DMAX;
-            double s = 0.0;
+        // merge the four lane groups (each saw every fourth centroid of a
+        // tile); lane group g then finishes row tile t = g, so every lane
+        // takes one row's square roots and division
+        double ow = 0.0, sw = 0.0;
+        bool iw = false;
 #pragma unroll
-            for (int k = 0; k < DMAX; ++k) {
-                const double t = xa[k] - mcp[k];
-                s = fma(t, t, s);
-            }
-            selfa = s + al[2 * (int64_t)p + 1];
-        }
-        if (inb && labb >= 1 && labb <= cmax) {
-            const int p = pos[(int64_t)l * (cmax + 1) + labb];
-            const double* mcp = ml + (int64_t)p * DMAX;
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < DMAX; ++k) {
-                const double t = xb[k] - mcp[k];
-                s = fma(t, t, s);
-            }
-            selfb = s + al[2 * (int64_t)p + 1];
+        for (int t = 0; t < RT; ++t) {
+            double o = oth[t], sf = self[t];
+            o = fmin(o, __shfl_xor(o, 16, 64));
+            o = fmin(o, __shfl_xor(o, 32, 64));
+            sf = fmin(sf, __shfl_xor(sf, 16, 64));
+            sf = fmin(sf, __shfl_xor(sf, 32, 64));
+            ow = t == g ? fmax(xx[t] + o, 0.0) : ow;
+            sw = t == g ? fmax(xx[t] + sf, 0.0) : sw;
+            iw = t == g ? in[t] : iw;
         }
         long long wq = 0;
         unsigned wn = 0;
-        sil_row_width<DMAX>(xa, selfa, otha, ina, np, wsc, out_width ? out_width + (int64_t)l * m + ra : nullptr,
-                            wq, wn);
-        sil_row_width<DMAX>(xb, selfb, othb, inb, np, wsc, out_width ? out_width + (int64_t)l * m + rb : nullptr,
-                            wq, wn);
-        // integer wave reduction (order-independent), one atomic per wave
+        sil_row_width(sw, ow, iw, np, wsc, out_width ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn);
+        // integer reductions (order-independent): wave, then block; one
+        // partial per (labeling, block) -- same-line global atomics from every
+        // wave serialised at the L2
         for (int o = 32; o > 0; o >>= 1) {
             wq += __shfl_xor(wq, o, 64);
             wn += __shfl_xor(wn, o, 64);
         }
-        if ((threadIdx.x & 63) == 0) {
-            if (wq) atomicAdd(&wsum[l], (unsigned long long)wq);
-            if (wn) atomicAdd(&wcnt[l], (unsigned long long)wn);
+        __shared__ long long red_q[4];
+        __shared__ unsigned red_n[4];
+        if (lane == 0) {
+            red_q[wave] = wq;
+            red_n[wave] = wn;
         }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            wsum[(int64_t)l * gridDim.x + blockIdx.x] = (unsigned long long)(red_q[0] + red_q[1] + red_q[2] + red_q[3]);
+            wcnt[(int64_t)l * gridDim.x + blockIdx.x] = (unsigned long long)(red_n[0] + red_n[1] + red_n[2] + red_n[3]);
+        }
+        __syncthreads();  // red_q / red_n are rewritten by the next labeling
     }
 }
 
-__global__ void sil_final(int64_t m, int L, int cmax, const unsigned long long* __restrict__ gcnt,
-                          const unsigned long long* __restrict__ wsum,
-                          const unsigned long long* __restrict__ wcnt, double* __restrict__ out_mean,
-                          int32_t* __restrict__ out_nclust, int32_t* __restrict__ out_minsize) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= L) return;
+// One block per labeling: the cluster count and smallest size from the
+// counts, and the mean width from the per-block fixed-point partials.
+__global__ __launch_bounds__(256) void sil_final(int64_t m, int L, int cmax, int nbw,
+                                                 const unsigned long long* __restrict__ gcnt,
+                                                 const unsigned long long* __restrict__ wsum,
+                                                 const unsigned long long* __restrict__ wcnt,
+                                                 double* __restrict__ out_mean, int32_t* __restrict__ out_nclust,
+                                                 int32_t* __restrict__ out_minsize) {
+    __shared__ unsigned long long rq[4], rn[4];
+    __shared__ int rc[4];
+    __shared__ long long rmin[4];
+    const int l = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
     int np = 0;
-    long long mn = -1;
-    for (int c = 1; c <= cmax; ++c)
+    long long mn = LLONG_MAX;
+    for (int c = 1 + threadIdx.x; c <= cmax; c += 256)
         if (gc[c]) {
             ++np;
-            if (mn < 0 || (long long)gc[c] < mn) mn = (long long)gc[c];
+            mn = min(mn, (long long)gc[c]);
         }
-    const double inv_wsc = ldexp(1.0, -scale_exp((double)m));
-    const unsigned long long n = wcnt[l];
-    if (out_mean) out_mean[l] = n ? ((double)(long long)wsum[l] * inv_wsc) / (double)n : NAN;
-    if (out_nclust) out_nclust[l] = np;
-    if (out_minsize) out_minsize[l] = (int32_t)(mn < 0 ? 0 : mn);
+    unsigned long long q = 0, n = 0;
+    for (int b = threadIdx.x; b < nbw; b += 256) {
+        q += wsum[(int64_t)l * nbw + b];
+        n += wcnt[(int64_t)l * nbw + b];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        q += __shfl_xor(q, o, 64);
+        n += __shfl_xor(n, o, 64);
+        np += __shfl_xor(np, o, 64);
+        mn = min(mn, __shfl_xor(mn, o, 64));
+    }
+    if (lane == 0) {
+        rq[wv] = q;
+        rn[wv] = n;
+        rc[wv] = np;
+        rmin[wv] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        q = rq[0] + rq[1] + rq[2] + rq[3];
+        n = rn[0] + rn[1] + rn[2] + rn[3];
+        np = rc[0] + rc[1] + rc[2] + rc[3];
+        mn = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
+        const double inv_wsc = ldexp(1.0, -scale_exp((double)m));
+        if (out_mean) out_mean[l] = n ? ((double)(long long)q * inv_wsc) / (double)n : NAN;
+        if (out_nclust) out_nclust[l] = np;
+        if (out_minsize) out_minsize[l] = (int32_t)(mn == LLONG_MAX ? 0 : mn);
+    }
+}
+
+// rows per sil_width block and the number of such blocks (partials per labeling)
+template <int DMAX>
+constexpr int sil_width_rows() {
+    return 4 * sil_rt<DMAX>() * 16;
+}
+static int sil_width_blocks(int64_t m, int d) {
+    const int rb = d <= 16 ? sil_width_rows<16>() : (d <= 32 ? sil_width_rows<32>() : sil_width_rows<64>());
+    return (int)ccg_cdiv(m, rb);
 }
 
 template <int DMAX>
@@ -413,10 +548,11 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
     dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
     const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
     const size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
+    dim3 grid1((unsigned)ccg_cdiv(m, SIL_T * SIL_CT), (unsigned)ccg_cdiv(L, SIL_LG));
     if (lds1 <= SIL_LDS_CAP)
-        sil_centroid<DMAX, true><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+        sil_centroid<DMAX, true><<<grid1, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
     else
-        sil_centroid<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+        sil_centroid<DMAX, false><<<grid1, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
     sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gcnt, npres, codes, pos, mu, muc, auxc);
     if (lds2 <= SIL_LDS_CAP)
         sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
@@ -424,11 +560,11 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
         sil_var<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
     sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
                                                                                 gvar, pos, auxc);
-    dim3 grid2((unsigned)ccg_cdiv(m, 2 * SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
-    constexpr int CH = sil_chunk<DMAX>();
-    const size_t lds5 = (size_t)CH * DMAX * 8 + (size_t)CH * 16 + (size_t)CH * 4;
-    sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, pos, muc, auxc, wsum,
-                                            wcnt, out_width);
+    dim3 grid2((unsigned)ccg_cdiv(m, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
+    const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), ((int64_t)cmax + 15) / 16 * 16);
+    const size_t lds5 = (size_t)CH * sil_sp<DMAX>() * 8 + (size_t)CH * 8 + (size_t)CH * 4;
+    sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
+                                            out_width, CH);
 }
 
 extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
@@ -441,15 +577,16 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_dev: cmax=%d must be in [1, 2^24]", cmax);
     hipStream_t st = ccg_pick_stream(ctx, stream);
     const int64_t nacc = (int64_t)(cmax + 1) * d;
-    const int64_t words = (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L + 8;
+    const int nbw = sil_width_blocks(m, d);
+    const int64_t words = (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L * nbw + 8;
     unsigned long long* buf = (unsigned long long*)ccg_ws(ctx, WS_SIL_A, sizeof(unsigned long long) * words);
     if (!buf) return CCG_ENOMEM;
     unsigned long long* gsum = buf;
     unsigned long long* gcnt = gsum + (int64_t)L * nacc;
     unsigned long long* gvar = gcnt + (int64_t)L * (cmax + 1);
     unsigned long long* wsum = gvar + (int64_t)L * (cmax + 1);
-    unsigned long long* wcnt = wsum + L;
-    unsigned* maxabs = (unsigned*)(wcnt + L);
+    unsigned long long* wcnt = wsum + (int64_t)L * nbw;
+    unsigned* maxabs = (unsigned*)(wcnt + (int64_t)L * nbw);
     const int dmax = d <= 16 ? 16 : (d <= 32 ? 32 : 64);
     const size_t mu_words = (size_t)L * (cmax + 1) * dmax + (size_t)L * cmax * dmax + 2 * (size_t)L * cmax;
     const size_t tab_ints = (size_t)L * cmax + (size_t)L * (cmax + 1) + L + 8;
@@ -472,7 +609,7 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     else
         sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
                         out_width, st);
-    sil_final<<<(unsigned)ccg_cdiv(L, 64), 64, 0, st>>>(m, L, cmax, gcnt, wsum, wcnt, out_mean,
+    sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean,
                                                        out_nclust, out_minsize);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());

@@ -51,13 +51,14 @@ def main():
     lib = _lib.load()
     if hasattr(lib, "ccg_debug_knn_stamps"):  # a -DKNN_STAMPS=1 variant: per-wave cycle attribution
         import ctypes
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 12)()
         lib.ccg_debug_knn_stamps(buf)  # reset
         eng.knn_rows_t(rows, 20, idx)
         torch.cuda.synchronize()
         lib.ccg_debug_knn_stamps(buf)
-        waves = max(1, buf[7])
-        names = ["dma_issue", "tile_mfma_max", "enqueue", "flush", "union", "vmcnt_wait", "barrier"]
+        waves = max(1, buf[11])
+        names = ["dma_issue", "tile_mfma_max", "enqueue", "flush", "union", "vmcnt_wait", "barrier",
+                 "n_tiles_with_candidates", "n_flushes", "n_flush_rounds", "n_tiles"]
         out["stamps_cycles_per_wave"] = {k: buf[i] / waves for i, k in enumerate(names)}
         out["stamps_waves"] = waves
     print(json.dumps(out))
