@@ -25,6 +25,7 @@ enum ccg_ws_slot {
     WS_SNN_H,        // SNN node size classes (scan)
     WS_SIL_A,        // silhouette accumulators
     WS_SIL_B,        // silhouette centroids
+    WS_SIL_Q,        // silhouette fixed-point rows (x and x^2)
     WS_COC_A,        // co-cluster column tables
     WS_COC_B,        // co-cluster fused-path slot tables
     WS_COC_C,        // co-cluster partial counts between column chunks / consensus row slab

@@ -59,23 +59,11 @@ __device__ __forceinline__ void load_row(const double* __restrict__ x, int64_t r
     for (int k = 0; k < DMAX; ++k) xr[k] = (k < d) ? x[r * d + k] : 0.0;
 }
 
-// K1: fixed-point cluster sums and counts, staged in LDS when (cmax + 1) x d
-// accumulators fit (SIL_LDS_CAP), else added straight to the global sums.
-// A block covers SIL_CT tiles of SIL_T rows, so each labeling's LDS sums are
-// flushed to the global sums once per SIL_CT tiles (the flush atomics from
-// every block meet on the same words).  With SIL_CT == 1 the rows stay in
-// registers, already quantised, across the block's labelings.
+// K1 (fallback for large cmax, whose sorted-segment LDS would not fit):
+// fixed-point cluster sums and counts, one atomic per (row, dimension),
+// staged in LDS when (cmax + 1) x d accumulators fit (SIL_LDS_CAP), else added
+// straight to the global sums.  v_c then comes from sil_var.
 #define SIL_LDS_CAP 65536
-#ifndef SIL_CT
-#define SIL_CT 1
-#endif
-template <int DMAX>
-__device__ __forceinline__ void quant_row(const double* __restrict__ x, int64_t r, bool in, int d, double sc,
-                                          long long (&q)[DMAX]) {
-#pragma unroll
-    for (int k = 0; k < DMAX; ++k) q[k] = (in && k < d) ? __double2ll_rn(x[r * d + k] * sc) : 0ll;
-}
-
 template <int DMAX, bool LDS>
 __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__ x, int64_t m,
                                                       int d, const int32_t* __restrict__ labels,
@@ -86,11 +74,13 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* acc = (unsigned long long*)smem;          // [cmax+1][d]
     unsigned* cnt = (unsigned*)(acc + (int64_t)(cmax + 1) * d);   // [cmax+1]
-    const int64_t rb = (int64_t)blockIdx.x * (SIL_T * SIL_CT) + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * SIL_T + threadIdx.x;
+    const bool in = r < m;
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
     const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
-    long long q[DMAX];
-    if (SIL_CT == 1) quant_row<DMAX>(x, rb, rb < m, d, sc, q);
+    long long q[DMAX];  // the row, quantised once for all of the block's labelings
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) q[k] = (in && k < d) ? __double2ll_rn(x[r * d + k] * sc) : 0ll;
     const int nacc = (cmax + 1) * d;
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
@@ -101,21 +91,17 @@ __global__ __launch_bounds__(SIL_T) void sil_centroid(const double* __restrict__
             for (int t = threadIdx.x; t <= cmax; t += SIL_T) cnt[t] = 0u;
             __syncthreads();
         }
-        for (int ct = 0; ct < SIL_CT; ++ct) {
-            const int64_t r = rb + ct * SIL_T;
-            if (SIL_CT > 1) quant_row<DMAX>(x, r, r < m, d, sc, q);
-            if (r < m) {
-                const int lab = labels[(int64_t)l * m + r];
-                if (lab >= 1 && lab <= cmax) {
+        if (in) {
+            const int lab = labels[(int64_t)l * m + r];
+            if (lab >= 1 && lab <= cmax) {
 #pragma unroll
-                    for (int k = 0; k < DMAX; ++k)
-                        if (k < d) {
-                            if (LDS) atomicAdd(&acc[lab * d + k], (unsigned long long)q[k]);
-                            else atomicAdd(&gs[(int64_t)lab * d + k], (unsigned long long)q[k]);
-                        }
-                    if (LDS) atomicAdd(&cnt[lab], 1u);
-                    else atomicAdd(&gc[lab], 1ull);
-                }
+                for (int k = 0; k < DMAX; ++k)
+                    if (k < d) {
+                        if (LDS) atomicAdd(&acc[lab * d + k], (unsigned long long)q[k]);
+                        else atomicAdd(&gs[(int64_t)lab * d + k], (unsigned long long)q[k]);
+                    }
+                if (LDS) atomicAdd(&cnt[lab], 1u);
+                else atomicAdd(&gc[lab], 1ull);
             }
         }
         if (LDS) {
@@ -148,6 +134,137 @@ __device__ __forceinline__ int sil_block_excl_scan(int v, int* sh, int* total) {
     return woff + x - v;
 }
 
+// K1': fixed-point rows, once per call: q1 = round(x * sc), q2 = round(x^2 *
+// sc2), [m][DMAX] int64 (zero past d).
+template <int DMAX>
+__global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const unsigned* __restrict__ maxabs_bits,
+                          long long* __restrict__ q1, long long* __restrict__ q2) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * DMAX) return;
+    const int64_t r = t / DMAX;
+    const int k = (int)(t - r * DMAX);
+    const double maxabs = (double)__uint_as_float(*maxabs_bits);
+    const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
+    const double sc2 = ldexp(1.0, scale_exp(maxabs * maxabs * (double)m));
+    const double v = k < d ? x[r * d + k] : 0.0;
+    q1[t] = __double2ll_rn(v * sc);
+    q2[t] = __double2ll_rn(v * v * sc2);
+}
+
+// K1 (sorted segments): cluster sums S1 = sum x, S2 = sum x^2 and counts of
+// a SIL_SORT_ROWS-row tile for one labeling (grid y), without a per-row
+// atomic.  The tile's rows are counting-sorted by label in LDS; each wave
+// then walks a quarter of the sorted rows with lanes along the dimensions
+// (64 / DMAX rows per step) and keeps running sums in registers while the
+// label repeats, so a lane issues one LDS atomic per label segment instead of
+// one per row.  Large tiles keep the flush of the LDS sums to the global sums
+// (atomics from every block on the same words) rare.  Integer sums: any
+// order gives the same bits.  LDS: acc1, acc2 [cmax+1][DMAX] int64,
+// counts/offsets [cmax+1], sorted rows and labels [SIL_SORT_ROWS].
+#ifndef SIL_SORT_ROWS
+#define SIL_SORT_ROWS 1024
+#endif
+template <int DMAX>
+__host__ __device__ constexpr size_t sil_sorted_lds(int cmax) {
+    return (size_t)(cmax + 1) * DMAX * 16 + (size_t)(cmax + 1) * 8 + 2 * SIL_SORT_ROWS * 4;
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const int32_t* __restrict__ labels,
+                                                         int cmax, const long long* __restrict__ q1,
+                                                         const long long* __restrict__ q2,
+                                                         unsigned long long* __restrict__ gsum,
+                                                         unsigned long long* __restrict__ gsum2,
+                                                         unsigned long long* __restrict__ gcnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RPT = SIL_SORT_ROWS / SIL_T;  // rows per thread in the sort
+    constexpr int RPW = 64 / DMAX;              // rows per wave step
+    constexpr int STEPS = SIL_SORT_ROWS / 4 / RPW;
+    unsigned long long* acc1 = (unsigned long long*)smem;                 // [cmax+1][DMAX]
+    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * DMAX;         // [cmax+1][DMAX]
+    int* hcnt = (int*)(acc2 + (int64_t)(cmax + 1) * DMAX);                // [cmax+1]
+    int* hoff = hcnt + (cmax + 1);                                        // [cmax+1]
+    int* srow = hoff + (cmax + 1);                                        // [SIL_SORT_ROWS]
+    int* slab = srow + SIL_SORT_ROWS;                                     // [SIL_SORT_ROWS]
+    __shared__ int sh[SIL_T / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k = lane % DMAX, sub = lane / DMAX;
+    const int64_t rb = (int64_t)blockIdx.x * SIL_SORT_ROWS;
+    const int l = blockIdx.y;
+    const int nacc = (cmax + 1) * DMAX;
+    for (int t = tid; t < 2 * nacc; t += SIL_T) acc1[t] = 0ull;
+    for (int t = tid; t <= cmax; t += SIL_T) hcnt[t] = 0;
+    __syncthreads();
+    // label 0 collects rows past m and codes outside [1, cmax]
+    int lab[RPT], rank[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int64_t r = rb + i * SIL_T + tid;
+        int lb = 0;
+        if (r < m) {
+            lb = labels[(int64_t)l * m + r];
+            if (lb < 1 || lb > cmax) lb = 0;
+        }
+        lab[i] = lb;
+        rank[i] = atomicAdd(&hcnt[lb], 1);
+    }
+    __syncthreads();
+    int carry = 0;
+    for (int c0 = 0; c0 <= cmax; c0 += SIL_T) {
+        const int c = c0 + tid;
+        const int v = c <= cmax ? hcnt[c] : 0;
+        int tot;
+        const int ex = carry + sil_block_excl_scan(v, sh, &tot);
+        if (c <= cmax) hoff[c] = ex;
+        carry += tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        srow[hoff[lab[i]] + rank[i]] = i * SIL_T + tid;
+        slab[hoff[lab[i]] + rank[i]] = lab[i];
+    }
+    __syncthreads();
+    long long a1 = 0, a2 = 0;
+    int cur = 0;
+    const int p0 = wave * (SIL_SORT_ROWS / 4) + sub;
+#pragma unroll 8
+    for (int st = 0; st < STEPS; ++st) {
+        const int pos = p0 + st * RPW;
+        const int lb = slab[pos];
+        const int64_t r = rb + srow[pos];
+        const long long v1 = lb ? q1[r * DMAX + k] : 0ll;
+        const long long v2 = lb ? q2[r * DMAX + k] : 0ll;
+        if (lb != cur) {
+            if (cur && k < d) {
+                atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
+                atomicAdd(&acc2[cur * DMAX + k], (unsigned long long)a2);
+            }
+            cur = lb;
+            a1 = 0;
+            a2 = 0;
+        }
+        a1 += v1;
+        a2 += v2;
+    }
+    if (cur && k < d) {
+        atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
+        atomicAdd(&acc2[cur * DMAX + k], (unsigned long long)a2);
+    }
+    __syncthreads();
+    unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
+    unsigned long long* gs2 = gsum2 + (int64_t)l * (cmax + 1) * d;
+    for (int t = tid; t < nacc; t += SIL_T) {
+        const int c = t / DMAX, kk = t - c * DMAX;
+        if (kk < d && c >= 1) {
+            if (acc1[t]) atomicAdd(&gs[(int64_t)c * d + kk], acc1[t]);
+            if (acc2[t]) atomicAdd(&gs2[(int64_t)c * d + kk], acc2[t]);
+        }
+    }
+    for (int c = 1 + tid; c <= cmax; c += SIL_T)
+        if (hcnt[c]) atomicAdd(&gcnt[(int64_t)l * (cmax + 1) + c], (unsigned long long)hcnt[c]);
+}
+
 // Dimension order of a centroid row in muc: position p holds dimension
 // (p % KS) * 4 + p / KS (KS = DMAX / 4), so the KS values a lane feeds to the
 // K steps of v_mfma_f64_16x16x4f64 (dims 4s + (lane >> 4)) are contiguous.
@@ -160,11 +277,13 @@ __host__ __device__ __forceinline__ int sil_mfma_pos(int k) {
 // K2: per labeling, the present codes (ascending = sort(unique(clusters)))
 // and the centroids mu[l][c][0..DMAX) (zero padded; muc: present clusters
 // only, in MFMA dimension order) plus |mu_c|^2, from the fixed-point sums.
-// One block per labeling.
+// With the sums of squares (gsum2, the sorted-segment path) also
+// v_c = mean |x - mu_c|^2 = sum_k (S2 / n - mu_k^2).  One block per labeling.
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
                                                 const unsigned* __restrict__ maxabs_bits,
                                                 const unsigned long long* __restrict__ gsum,
+                                                const unsigned long long* __restrict__ gsum2,
                                                 const unsigned long long* __restrict__ gcnt,
                                                 int* __restrict__ npres, int* __restrict__ codes,
                                                 int* __restrict__ pos, double* __restrict__ mu,
@@ -205,6 +324,17 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
         double s = 0.0;
         for (int k = 0; k < d; ++k) s = fma(ml[(int64_t)c * DMAX + k], ml[(int64_t)c * DMAX + k], s);
         auxc[((int64_t)l * cmax + pc) * 2] = s;
+        if (gsum2) {
+            const double inv_sc2 = ldexp(1.0, -scale_exp(maxabs * maxabs * (double)m));
+            const unsigned long long* g2 = gsum2 + ((int64_t)l * (cmax + 1) + c) * d;
+            const double n = (double)gc[c];
+            double v = 0.0;
+            for (int k = 0; k < d; ++k) {
+                const double mk = ml[(int64_t)c * DMAX + k];
+                v += ((double)(long long)g2[k] * inv_sc2) / n - mk * mk;
+            }
+            auxc[((int64_t)l * cmax + pc) * 2 + 1] = fmax(v, 0.0);  // clamp the cancellation noise of equal points
+        }
     }
 }
 
@@ -541,25 +671,33 @@ static int sil_width_blocks(int64_t m, int d) {
 
 template <int DMAX>
 static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels, int L, int cmax,
-                       unsigned* maxabs, unsigned long long* gsum, unsigned long long* gcnt,
+                       unsigned* maxabs, unsigned long long* gsum, unsigned long long* gsum2, unsigned long long* gcnt,
                        unsigned long long* gvar, unsigned long long* wsum, unsigned long long* wcnt,
-                       int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc,
+                       int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc, long long* q,
                        double* out_width, hipStream_t st) {
-    dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
-    const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
-    const size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
-    dim3 grid1((unsigned)ccg_cdiv(m, SIL_T * SIL_CT), (unsigned)ccg_cdiv(L, SIL_LG));
-    if (lds1 <= SIL_LDS_CAP)
-        sil_centroid<DMAX, true><<<grid1, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
-    else
-        sil_centroid<DMAX, false><<<grid1, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
-    sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gcnt, npres, codes, pos, mu, muc, auxc);
-    if (lds2 <= SIL_LDS_CAP)
-        sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
-    else
-        sil_var<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
-    sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
-                                                                                gvar, pos, auxc);
+    if (q) {
+        // sorted segments: S1, S2 and counts in one pass, v_c in sil_mu
+        sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q, q + m * DMAX);
+        dim3 grid((unsigned)ccg_cdiv(m, SIL_SORT_ROWS), (unsigned)L);
+        sil_sums_sorted<DMAX><<<grid, SIL_T, sil_sorted_lds<DMAX>(cmax), st>>>(m, d, labels, cmax, q, q + m * DMAX,
+                                                                            gsum, gsum2, gcnt);
+        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
+    } else {
+        dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
+        const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
+        const size_t lds2 = (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 8;
+        if (lds1 <= SIL_LDS_CAP)
+            sil_centroid<DMAX, true><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+        else
+            sil_centroid<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
+        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, nullptr, gcnt, npres, codes, pos, mu, muc, auxc);
+        if (lds2 <= SIL_LDS_CAP)
+            sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
+        else
+            sil_var<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
+        sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
+                                                                                    gvar, pos, auxc);
+    }
     dim3 grid2((unsigned)ccg_cdiv(m, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
     const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), ((int64_t)cmax + 15) / 16 * 16);
     const size_t lds5 = (size_t)CH * sil_sp<DMAX>() * 8 + (size_t)CH * 8 + (size_t)CH * 4;
@@ -578,11 +716,12 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     hipStream_t st = ccg_pick_stream(ctx, stream);
     const int64_t nacc = (int64_t)(cmax + 1) * d;
     const int nbw = sil_width_blocks(m, d);
-    const int64_t words = (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L * nbw + 8;
+    const int64_t words = 2 * (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L * nbw + 8;
     unsigned long long* buf = (unsigned long long*)ccg_ws(ctx, WS_SIL_A, sizeof(unsigned long long) * words);
     if (!buf) return CCG_ENOMEM;
     unsigned long long* gsum = buf;
-    unsigned long long* gcnt = gsum + (int64_t)L * nacc;
+    unsigned long long* gsum2 = gsum + (int64_t)L * nacc;
+    unsigned long long* gcnt = gsum2 + (int64_t)L * nacc;
     unsigned long long* gvar = gcnt + (int64_t)L * (cmax + 1);
     unsigned long long* wsum = gvar + (int64_t)L * (cmax + 1);
     unsigned long long* wcnt = wsum + (int64_t)L * nbw;
@@ -597,17 +736,24 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     int* npres = (int*)(auxc + 2 * (size_t)L * cmax);
     int* codes = npres + L;
     int* pos = codes + (size_t)L * cmax;
+    const size_t lds_sorted = dmax == 16 ? sil_sorted_lds<16>(cmax)
+                                         : (dmax == 32 ? sil_sorted_lds<32>(cmax) : sil_sorted_lds<64>(cmax));
+    long long* q = nullptr;  // fixed-point rows of the sorted-segment path (cmax small enough for its LDS)
+    if (lds_sorted <= SIL_LDS_CAP) {
+        q = (long long*)ccg_ws(ctx, WS_SIL_Q, 2 * sizeof(long long) * (size_t)m * dmax);
+        if (!q) return CCG_ENOMEM;
+    }
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
     sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
     if (d <= 16)
-        sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+        sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         out_width, st);
     else if (d <= 32)
-        sil_launch<32>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+        sil_launch<32>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         out_width, st);
     else
-        sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc,
+        sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         out_width, st);
     sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean,
                                                        out_nclust, out_minsize);

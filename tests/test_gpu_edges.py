@@ -245,11 +245,13 @@ def test_consensus_knn_fused_nan_raises(engine):
 
 
 # ---------------------------------------------------------- silhouette --
-@pytest.mark.parametrize("m,d,C", [(6000, 30, 1000), (4000, 50, 200), (3000, 12, 2900), (5000, 64, 300)])
+@pytest.mark.parametrize("m,d,C", [(6000, 30, 1000), (4000, 50, 200), (3000, 12, 2900), (5000, 64, 300),
+                                   (3000, 64, 40), (3000, 9, 100), (2000, 32, 90)])
 def test_silhouette_many_clusters_vs_oracle(engine, m, d, C):
     """More than 256 clusters (high-resolution clusterings are scored too,
     R/consensusClust.R:663-664): global accumulation and chunked centroid
-    staging instead of the LDS fast path."""
+    staging instead of the LDS fast path.  The last three cases keep the
+    sorted-segment sums (LDS) at each padded width, up to its cmax limit."""
     rng = np.random.default_rng(m + C)
     X = _mixture(rng, m, d, C=16)
     labs = np.stack([rng.integers(1, C + 1, m), rng.integers(1, 9, m)]).astype(np.int32)
