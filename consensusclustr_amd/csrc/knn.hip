@@ -31,7 +31,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define KNN_KP 20          // candidates kept per half-lane for kmax <= 20
 #define KNN_KP_BIG 32      // ... for 20 < kmax <= 32 (2*KP <= 64 lanes in certify)
+#ifndef KNN_TMARGIN
 #define KNN_TMARGIN 8      // screen threshold: rank KP + KNN_TMARGIN of the two half-lists' union
+#endif
 #define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
 #define KNN_FB_K 32        // fallback list length (>= kmax)
 #ifndef KNN_FB_S
@@ -129,7 +131,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 __host__ __device__ constexpr int knn_chunk(int ksteps) { return ksteps == 4 ? 64 : 128; }
 __host__ __device__ constexpr int knn_nbuf(int ksteps) { return ksteps == 4 ? 3 : 2; }
 static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4); }  // d dims + the norm dim
+#ifndef KNN_QCAP
 #define KNN_QCAP 8          // per-lane insertion queue slots (flush before a half tile that could overflow)
+#endif
 #define KNN_NORM_SHIFT 15   // the query's norm-dimension value 2^15 (exact in fp16)
 #define KNN_PAD_NORM (-65504.0f)  // padding rows: below every real value (|v| < 1.6e9 < 2^31)
 
