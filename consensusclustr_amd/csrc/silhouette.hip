@@ -23,10 +23,10 @@
 
 #define SIL_T 256
 #ifndef SIL_EXP
-#define SIL_EXP 0  // tools only: 1 = no width epilogue, 2 = no MFMA (timing variants)
+#define SIL_EXP 0  // tools only: 1 = no width epilogue, 2 = no MFMA, 3 = no row widths (timing variants)
 #endif
 #ifndef SIL_LG
-#define SIL_LG 10
+#define SIL_LG 5
 #endif
 
 __device__ __forceinline__ int scale_exp(double bound) {
@@ -586,7 +586,12 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         }
         long long wq = 0;
         unsigned wn = 0;
+#if SIL_EXP == 3
+        wq = (long long)ow + (long long)sw;
+        wn = iw;
+#else
         sil_row_width(sw, ow, iw, np, wsc, out_width ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn);
+#endif
         // integer reductions (order-independent): wave, then block; one
         // partial per (labeling, block) -- same-line global atomics from every
         // wave serialised at the L2
