@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=3,
                     help="bootstraps in flight per GPU (one engine context + HIP stream each)")
+    ap.add_argument("--pipeline", default="",
+                    help="NK,NS: stage-split schedule instead of --streams: NK kNN streams feed NS "
+                         "SNN+silhouette streams through a ring of bootstrap buffers")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
@@ -245,6 +248,10 @@ def main():
     else:
         grp = DeviceGroup.open([local])
     S = max(1, args.streams)
+    NK = NS = 0
+    if args.pipeline:
+        NK, NS = (max(1, int(v)) for v in args.pipeline.split(","))
+        S = NK + NS
     engs = [grp.engines[0]] + [Engine(local) for _ in range(S - 1)]  # own workspaces per in-flight bootstrap
     eng = engs[0]
     N, d, B = args.cells, args.pcs, args.boots_per_gpu
@@ -263,8 +270,9 @@ def main():
         labels[j] = synth_labels(torch, pop[boots[j].long()], L, dev, 1000 + bids[j])
     cmax = int(labels.max().item())
 
-    rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(S)]
-    knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(S)]
+    RING = NK + NS + 1 if NK else S  # bootstrap buffers (gathered rows, kNN) in flight
+    rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(RING)]
+    knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(RING)]
     rows, knn = rows_s[0], knn_s[0]
     rcap = 700 * n  # SNN row entries (items per node ~ 560 at cfg3); grown once after the warmup if short
 
@@ -291,7 +299,39 @@ def main():
     co = torch.empty(P, dtype=torch.int16, device=dev)      # uint16 counts (viewed as int16)
     both = torch.empty(P, dtype=torch.int16, device=dev)
 
+    ev_k = [torch.cuda.Event() for _ in range(B)]
+    ev_s = [torch.cuda.Event() for _ in range(B)]
+
+    def step_pipeline():
+        # stage split: kNN streams (MFMA-bound screen) run ahead of the
+        # SNN + silhouette streams (issue/LDS-bound) by up to RING bootstraps,
+        # so the two kinds of work always share the GPU
+        cur = torch.cuda.current_stream()
+        for st_ in streams:
+            st_.wait_stream(cur)
+        for j in range(B):
+            slot, ks, ss = j % RING, j % NK, NK + j % NS
+            with torch.cuda.stream(streams[ks]):
+                if j >= RING:
+                    streams[ks].wait_event(ev_s[j - RING])  # the slot's previous bootstrap is consumed
+                engs[ks].gather_rows_t(pcs_cm, N, d, boots[j], rows_s[slot])
+                engs[ks].knn_rows_t(rows_s[slot], 20, knn_s[slot])
+                ev_k[j].record(streams[ks])
+            with torch.cuda.stream(streams[ss]):
+                streams[ss].wait_event(ev_k[j])
+                engs[ss].snn_rows_t(knn_s[slot], K_NUM, "number", *snn_out[ss - NK], nedges[j])
+                engs[ss].silhouette_t(rows_s[slot], labels[j], cmax, means[j], nclust[j], minsize[j])
+                ev_s[j].record(streams[ss])
+        for st_ in streams:
+            cur.wait_stream(st_)
+        eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
+                             minsize=minsize, out_choice=choice)
+        grp.allgather_columns_t([A_local], [B] * G, [A_full])
+        grp.cocluster_sharded_t([A_full], co=[co], both=[both])
+
     def step():
+        if NK:
+            return step_pipeline()
         # S bootstraps in flight: bootstrap j runs on stream j % S with its own
         # engine context (workspaces), so one bootstrap's latency-bound SNN
         # build overlaps another's MFMA-bound kNN screen
