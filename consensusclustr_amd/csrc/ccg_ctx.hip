@@ -97,6 +97,10 @@ int ccg_take_device_error(ccg_ctx* ctx) {
         ccg_set_error("cluster position outside [0, K)");
         return CCG_EINVAL;
     }
+    if (bits & CCG_DERR_KNN_UNIQUE) {
+        ccg_set_error("ccg_knn_boot_dev: n_unique is not the number of distinct cells in idx");
+        return CCG_EINVAL;
+    }
     ccg_set_error("SNN: neighbour index out of range or equal to the row itself");
     return CCG_EINVAL;
 }

@@ -26,6 +26,8 @@ enum ccg_ws_slot {
     WS_SIL_A,        // silhouette accumulators
     WS_SIL_B,        // silhouette centroids
     WS_SIL_Q,        // silhouette fixed-point rows (x and x^2)
+    WS_KB_A,         // distinct-cell kNN: sorted (cell, row) pairs, heads, tables
+    WS_KB_B,         // distinct-cell kNN: distinct rows and their kNN
     WS_COC_A,        // co-cluster column tables
     WS_COC_B,        // co-cluster fused-path slot tables
     WS_COC_C,        // co-cluster partial counts between column chunks / consensus row slab
@@ -58,6 +60,7 @@ struct ccg_timer_rec {
 #define CCG_DERR_LABEL_RANGE 1  // map-back: a label exceeds the assignment matrix's label width
 #define CCG_DERR_SNN_INDEX 2    // SNN: neighbour index out of range or self
 #define CCG_DERR_CLUSTER_INDEX 4  // block sums / contingency: cluster position outside [0, K)
+#define CCG_DERR_KNN_UNIQUE 8     // ccg_knn_boot_dev: n_unique differs from the distinct cells of idx
 
 struct ccg_ctx {
     int device;

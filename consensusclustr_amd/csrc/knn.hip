@@ -934,6 +934,32 @@ struct KnnSegs {
     const int4* blk;         // device, per query block: chunk range [x, y), query limit z
 };
 
+// Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
+static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
+                               const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
+                               int nseg, hipStream_t st) {
+    const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
+    double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
+    int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
+    if (!fb_d || !fb_i) return CCG_ENOMEM;
+#define CCG_FALLBACK(DM_, FK_)                                                                            \
+    knn_fallback_kernel<DM_, FK_><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots, \
+                                                        fb_d, fb_i, seg_off, nseg)
+    if (kmax <= KNN_KP) {  // per-thread lists of kmax <= 20 entries
+        if (d <= 16) CCG_FALLBACK(16, KNN_KP);
+        else if (d <= 32) CCG_FALLBACK(32, KNN_KP);
+        else CCG_FALLBACK(64, KNN_KP);
+    } else {
+        if (d <= 16) CCG_FALLBACK(16, KNN_FB_K);
+        else if (d <= 32) CCG_FALLBACK(32, KNN_FB_K);
+        else CCG_FALLBACK(64, KNN_FB_K);
+    }
+#undef CCG_FALLBACK
+    knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
+                                                   out_dist, seg_off, nseg);
+    return CCG_OK;
+}
+
 static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, int32_t* out_idx,
                    double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg) {
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
@@ -1022,25 +1048,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         else CCG_CERTIFY(KNN_KP_BIG, 64);
     }
 #undef CCG_CERTIFY
-    const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
-    double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
-    int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
-    if (!fb_d || !fb_i) return CCG_ENOMEM;
-#define CCG_FALLBACK(DM_, FK_)                                                                            \
-    knn_fallback_kernel<DM_, FK_><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots, \
-                                                        fb_d, fb_i, seg_off, nseg)
-    if (kmax <= KNN_KP) {  // per-thread lists of kmax <= 20 entries
-        if (d <= 16) CCG_FALLBACK(16, KNN_KP);
-        else if (d <= 32) CCG_FALLBACK(32, KNN_KP);
-        else CCG_FALLBACK(64, KNN_KP);
-    } else {
-        if (d <= 16) CCG_FALLBACK(16, KNN_FB_K);
-        else if (d <= 32) CCG_FALLBACK(32, KNN_FB_K);
-        else CCG_FALLBACK(64, KNN_FB_K);
-    }
-#undef CCG_FALLBACK
-    knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
-                                                   out_dist, seg_off, nseg);
+    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, seg_off, nseg, st);
+    if (rc) return rc;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {
@@ -1110,6 +1119,221 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
     return rc;
 }
 
+// ---------------------------------------------------- distinct cells --
+// A bootstrap draws cells with replacement (R/consensusClust.R:394), so at
+// cfg3 only about 1 - e^-0.9 = 59% of its rows are distinct cells; the rest
+// are copies at distance 0.  Under the contract (d2 of the rows, ties by row
+// index) the neighbours of row i (cell c) are, in (d2, row) order, the other
+// copies of c and the copies of c's nearest distinct cells.  So the screen /
+// certify / fallback pipeline runs on the u distinct cells only (about 0.35 of
+// the n^2 work), and an expansion pass turns each cell's kq = min(kmax, u-1)
+// nearest distinct cells back into row lists: groups of equal d2 (exact fp64,
+// unfused, dimension order -- the oracle's arithmetic) are merged by row
+// index.  A row whose kmax-th entry falls in a group that reaches the last
+// computed distinct neighbour (a tie that may continue past the list) is
+// re-searched exactly over all rows by the fallback kernels.
+
+// keys = the cells (clamped into [0, N): an index outside sets the sticky
+// error), values = the rows
+__global__ void kb_iota_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N, int32_t* __restrict__ cells,
+                               int32_t* __restrict__ rid, int* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int c = idx[t];
+    if (c < 0 || c >= N) {
+        atomicOr(err, CCG_DERR_KNN_UNIQUE);
+        c = 0;
+    }
+    cells[t] = c;
+    rid[t] = (int32_t)t;
+}
+
+// (cell, row) pairs sorted by cell (stable: each cell's rows ascending)
+__global__ void kb_heads_kernel(const int32_t* __restrict__ scell, int64_t n, int64_t* __restrict__ head) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) head[t] = (t == 0 || scell[t] != scell[t - 1]) ? 1 : 0;
+}
+
+// hs: exclusive scan of the heads (hs[n] = the number of distinct cells).
+// Distinct cell uid owns the sorted positions [ustart[uid], ustart[uid + 1]);
+// row2u maps a row to its uid.  If the caller's u is wrong the sticky error is
+// set and uids are clamped into [0, u) (tables zeroed beforehand), so every
+// later access stays in bounds; the outputs are then undefined.
+__global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_t* __restrict__ srow, int64_t n,
+                                 const int64_t* __restrict__ hs, int u, int* __restrict__ ustart,
+                                 int* __restrict__ ucell, int* __restrict__ row2u, int* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    if (t == 0 && hs[n] != u) atomicOr(err, CCG_DERR_KNN_UNIQUE);
+    const bool head = t == 0 || scell[t] != scell[t - 1];
+    const int uid = min((int)hs[t] - (head ? 0 : 1), u - 1);
+    if (head) {
+        ustart[uid] = (int)t;
+        ucell[uid] = scell[t];
+    }
+    row2u[srow[t]] = uid;
+    if (t == 0) ustart[u] = (int)n;
+}
+
+template <int DMAX>
+__device__ __forceinline__ double kb_d2(const double (&xq)[DMAX], const double* __restrict__ y, int d) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k)
+        if (k < d) {
+            const double t = __dsub_rn(xq[k], y[k]);
+            s = __dadd_rn(s, __dmul_rn(t, t));
+        }
+    return s;
+}
+
+#define KB_GMAX 33  // cells of one merge group (the own cell + kq <= 32 neighbours)
+template <int DMAX>
+__global__ __launch_bounds__(256) void kb_expand_kernel(const double* __restrict__ urows, int d, int64_t n, int u,
+                                                        int kq, const int* __restrict__ uidx,
+                                                        const int* __restrict__ ustart, const int* __restrict__ srow,
+                                                        const int* __restrict__ row2u, int kmax,
+                                                        int32_t* __restrict__ out_idx, double* __restrict__ out_dist,
+                                                        int* __restrict__ fail_list, int* __restrict__ fail_count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int uc = row2u[i];
+    double xq[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? urows[(int64_t)uc * d + k] : 0.0;
+    const int* nbl = uidx + (int64_t)uc * kq;
+    int o = 0;     // rows written
+    int t = 0;     // next distinct neighbour
+    double dn = kq > 0 ? kb_d2<DMAX>(xq, urows + (int64_t)nbl[0] * d, d) : INFINITY;
+    double gd = 0.0;  // the group's d2 (group 0: the own cell, d2 = 0)
+    bool first = true, fail = false;
+    int lo[KB_GMAX], hi[KB_GMAX];
+    while (o < kmax) {
+        int g = 0;
+        if (first) {
+            lo[0] = ustart[uc];
+            hi[0] = ustart[uc + 1];
+            g = 1;
+        }
+        const int t0 = t;
+        while (t < kq && dn == gd) {
+            const int v = nbl[t];
+            lo[g] = ustart[v];
+            hi[g] = ustart[v + 1];
+            ++g;
+            ++t;
+            dn = t < kq ? kb_d2<DMAX>(xq, urows + (int64_t)nbl[t] * d, d) : INFINITY;
+        }
+        if (t == kq && t > t0 && kq < u - 1) {  // the group may continue past the computed list
+            fail = true;
+            break;
+        }
+        // merge the group's row lists (each ascending) by row index, skipping row i
+        while (o < kmax) {
+            int best = 0x7fffffff, bg = -1;
+            for (int q = 0; q < g; ++q)
+                if (lo[q] < hi[q]) {
+                    const int r = srow[lo[q]];
+                    if (r < best) {
+                        best = r;
+                        bg = q;
+                    }
+                }
+            if (bg < 0) break;
+            ++lo[bg];
+            if (best == (int)i) continue;
+            out_idx[i * kmax + o] = best;
+            if (out_dist) out_dist[i * kmax + o] = sqrt(gd);
+            ++o;
+        }
+        if (o >= kmax) break;
+        if (t >= kq) {  // every distinct cell is listed (kq = u - 1) yet fewer than kmax rows: n - 1 < kmax
+            fail = true;
+            break;
+        }
+        gd = dn;
+        first = false;
+    }
+    if (fail) fail_list[atomicAdd(fail_count, 1)] = (int)i;
+}
+
+extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n,
+                                int n_unique, const double* rows, int kmax, int32_t* out_idx, double* out_dist,
+                                ccg_knn_stats* stats, void* stream) {
+    CCG_REQUIRE(ctx && pcs && idx && rows && out_idx, "ccg_knn_boot_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boot_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(N >= 1 && N < (1LL << 31) && n >= 2 && n < (1LL << 30), "ccg_knn_boot_dev: bad sizes");
+    CCG_REQUIRE(n_unique >= 1 && n_unique <= n && n_unique <= N, "ccg_knn_boot_dev: n_unique=%d out of range",
+                n_unique);
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
+                "ccg_knn_boot_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int u = n_unique;
+    const int kq = std::min(kmax, u - 1);
+    // workspaces (the full-size fail list first, so the distinct-cell run never grows it)
+    int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
+    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + 2 * (size_t)u + 1));
+    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * d + sizeof(int32_t) * (size_t)u * kq + 64);
+    unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
+    if (!fail_list || !ta || !urows || !misc) return CCG_ENOMEM;
+    int64_t* head = (int64_t*)ta;                // [n + 1] heads, then their exclusive scan in place
+    int32_t* cells = (int32_t*)(head + n + 1);   // [n] sort keys (the cells), later row2u
+    int32_t* scell = cells + n;                  // [n] sorted keys
+    int32_t* rid = scell + n;                    // [n] sort values (the rows)
+    int32_t* srow = rid + n;                     // [n] rows sorted by cell
+    int32_t* ustart = srow + n;                  // [u + 1]
+    int32_t* ucell = ustart + u + 1;             // [u]
+    int32_t* row2u = cells;
+    int32_t* uidx = (int32_t*)(urows + (size_t)u * d);
+    int* fail_count = (int*)(misc + 1);
+    const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
+    // 1. rows grouped by cell (stable radix sort on the cell index bits)
+    int bits = 1;
+    while (bits < 31 && (1LL << bits) < N) ++bits;
+    const unsigned ng = (unsigned)ccg_cdiv(n, 256);
+    kb_iota_kernel<<<ng, 256, 0, st>>>(idx, n, N, cells, rid, ctx->d_err);
+    int rc = ccg_sort_pairs_i32(ctx, cells, scell, rid, srow, n, bits, st);
+    if (rc) return rc;
+    // 2. distinct cells: heads -> scan -> tables
+    CCG_HIP(hipMemsetAsync(ustart, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
+    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head);
+    rc = ccg_scan_i64(ctx, head, head, n, st);
+    if (rc) return rc;
+    kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, ucell, row2u, ctx->d_err);
+    // 3. the distinct cells' rows and their kq nearest distinct cells
+    gather_rows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(pcs, N, d, ucell, u, urows);
+    ccg_knn_stats us = {0, 0};
+    if (kq >= 1) {
+        rc = knn_run(ctx, urows, u, d, kq, uidx, nullptr, stats ? &us : nullptr, st, nullptr);
+        if (rc) return rc;
+    }
+    // 4. expansion to rows; ties cut by the list go to the exact search over all rows
+    CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
+    const unsigned eg = ng;
+    if (d <= 16)
+        kb_expand_kernel<16><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
+                                                 out_dist, fail_list, fail_count);
+    else if (d <= 32)
+        kb_expand_kernel<32><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
+                                                 out_dist, fail_list, fail_count);
+    else
+        kb_expand_kernel<64><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
+                                                 out_dist, fail_list, fail_count);
+    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st);
+    if (rc) return rc;
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    if (stats) {
+        int nf = 0;
+        CCG_HIP(hipMemcpyAsync(&nf, fail_count, sizeof(int), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        stats->queries = n;
+        stats->fallback = us.fallback + nf;
+        ctx->last_stats = *stats;
+    }
+    return CCG_OK;
+}
+
 extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                             const int32_t* boot_idx, int64_t n, int nb, int kmax,
                             int32_t* out_idx, double* out_dist, ccg_knn_stats* stats) {
@@ -1128,11 +1352,20 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
     CCG_HIP(hipMemcpyAsync(dpcs, pcs, sizeof(double) * N * d, hipMemcpyHostToDevice, st));
     CCG_HIP(hipMemcpyAsync(didx, boot_idx, sizeof(int32_t) * n * nb, hipMemcpyHostToDevice, st));
     ccg_knn_stats acc = {0, 0};
+    std::vector<unsigned char> seen(N);
     for (int b = 0; b < nb; ++b) {
+        // the bootstrap's distinct cells (R: length(unique(idx)))
+        std::fill(seen.begin(), seen.end(), 0);
+        int u = 0;
+        for (int64_t t = 0; t < n; ++t) {
+            const int32_t c = boot_idx[(int64_t)b * n + t];
+            u += seen[c] ? 0 : 1;
+            seen[c] = 1;
+        }
         int rc = ccg_gather_rows_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, rows, st);
         if (rc) return rc;
         ccg_knn_stats s;
-        rc = ccg_knn_rows_dev(ctx, rows, n, d, kmax, dout, ddist, &s, st);
+        rc = ccg_knn_boot_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, dout, ddist, &s, st);
         if (rc) return rc;
         acc.queries += s.queries;
         acc.fallback += s.fallback;

@@ -281,6 +281,21 @@ class Engine:
             return self.last_knn_stats
         return None
 
+    def knn_boot_t(self, pcs_cm, N, d, idx, n_unique, rows, kmax, out_idx, out_dist=None, stats=False):
+        """Device flavour of the bootstrap kNN over distinct cells
+        (ccg_knn_boot_dev): pcs_cm (d, N) float64 (column-major N x d), idx (n,)
+        int32 cells, n_unique = len(unique(idx)) (host int), rows (n, d) the
+        gathered rows, out_idx (n, kmax) int32."""
+        n = idx.numel()
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_boot_dev(self.ctx, _ptr(pcs_cm), N, d, _ptr(idx), n, int(n_unique), _ptr(rows),
+                                        kmax, _ptr(out_idx), _ptr(out_dist), ctypes.byref(st) if stats else None,
+                                        _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
     def knn_segments_t(self, rows, seg_off, kmax, out_idx, out_dist=None, stats=False):
         """Device flavour: rows (n, d) tensor of concatenated segments, seg_off a
         host int64 array of nseg+1 offsets; out_idx (n, kmax) segment-local."""

@@ -121,6 +121,26 @@ int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
                      int kmax, int32_t* out_idx, double* out_dist,
                      ccg_knn_stats* stats, void* stream);
 
+/* kNN of the bootstrap rows pcs[idx[i], ] among each other -- the contract
+ * of ccg_knn_rows_dev on the gathered matrix, bit for bit -- computed over
+ * the bootstrap's distinct cells (duplicated cells are copies at distance 0;
+ * about 59% of the rows are distinct at cfg3, so the search does ~0.35 of
+ * the n^2 work), then expanded back to rows in (d2, row index) order.
+ *   pcs      : N x d float64 COLUMN-major (device)
+ *   idx      : n int32 0-based cell indices (device; R's sample() - 1)
+ *   n_unique : the number of distinct values in idx (host; R:
+ *              length(unique(idx))).  A wrong value -- or an index outside
+ *              [0, N) -- sets the sticky device error (CCG_EINVAL at the next
+ *              ccg_synchronize / ccg_check_errors); outputs are then undefined.
+ *   rows     : the gathered n x d rows (ccg_gather_rows_dev; read by the exact
+ *              fallback for rows whose kmax-th entry is a tie the distinct-cell
+ *              list may cut)
+ * Requires 1 <= kmax <= min(32, n-1), 2 <= n < 2^30, d <= 63. */
+int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                     const int32_t* idx, int64_t n, int n_unique,
+                     const double* rows, int kmax, int32_t* out_idx,
+                     double* out_dist, ccg_knn_stats* stats, void* stream);
+
 /* Batched kNN over independent segments: the iterate=TRUE subclustering
  * (R/consensusClust.R:541-566, BASELINE config 5) runs one bootstrap loop per
  * subcluster; their (small) bootstrap matrices are searched in ONE set of

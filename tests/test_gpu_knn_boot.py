@@ -1,0 +1,106 @@
+"""Bootstrap kNN over distinct cells (ccg_knn_boot_dev) against the oracle's
+full-row scan of the gathered bootstrap (R/consensusClust.R:394, :656-658).
+
+The device path searches the bootstrap's distinct cells and expands their
+lists back to rows; these cases pin the expansion's tie rules: copies of a
+cell at distance 0 (more copies than kmax), distinct cells at equal distance
+(integer lattices, where the kmax-th entry is often a tie the distinct-cell
+list cuts and the exact fallback takes over), bootstraps with fewer distinct
+cells than kmax + 1, kmax = 32, and a wrong distinct-cell count.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from consensusclustr_amd import CcgError
+
+pytestmark = pytest.mark.gpu
+
+
+def _boot_knn(engine, pcs, idx, kmax, want_dist=True, n_unique=None):
+    N, d = pcs.shape
+    dev = torch.device("cuda", engine.device)
+    pcs_cm = torch.from_numpy(np.ascontiguousarray(np.asarray(pcs, np.float64).T)).to(dev)
+    ti = torch.from_numpy(np.ascontiguousarray(idx, np.int32)).to(dev)
+    n = idx.size
+    rows = torch.empty((n, d), dtype=torch.float64, device=dev)
+    engine.gather_rows_t(pcs_cm, N, d, ti, rows)
+    out = torch.empty((n, kmax), dtype=torch.int32, device=dev)
+    dist = torch.empty((n, kmax), dtype=torch.float64, device=dev) if want_dist else None
+    u = len(np.unique(idx)) if n_unique is None else n_unique
+    q, fb = engine.knn_boot_t(pcs_cm, N, d, ti, u, rows, kmax, out, dist, stats=True)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), (dist.cpu().numpy() if want_dist else None), fb
+
+
+def _check(engine, pcs, idx, kmax):
+    oi, od = O.knn(O.gather_rows(pcs, idx), kmax)
+    gi, gd, fb = _boot_knn(engine, pcs, idx, kmax)
+    assert np.array_equal(gi, oi)
+    # distances: sqrt of the same fp64 sums; the device sqrt may differ in the last ulp
+    np.testing.assert_allclose(gd, od, rtol=1e-12, atol=1e-12)
+    return fb
+
+
+@pytest.mark.parametrize("N,n,d,kmax", [(4000, 3600, 30, 20), (3000, 6000, 12, 32), (2500, 2250, 50, 15)])
+def test_knn_boot_dev_random_bootstraps(engine, N, n, d, kmax):
+    rng = np.random.default_rng(N + n)
+    centers = rng.normal(scale=3.0, size=(10, d))
+    pcs = centers[rng.integers(0, 10, N)] + rng.normal(size=(N, d))
+    idx = rng.integers(0, N, n).astype(np.int32)
+    _check(engine, pcs, idx, kmax)
+
+
+def test_knn_boot_dev_cell_copies_beyond_kmax(engine):
+    """One cell drawn 45 times (> kmax + 1): its rows' lists are its other
+    copies only, in row order; a second cell drawn 12 times sits among them."""
+    rng = np.random.default_rng(3)
+    N, d = 800, 8
+    pcs = rng.normal(size=(N, d))
+    idx = rng.integers(0, N, 1000).astype(np.int32)
+    idx[rng.choice(1000, 45, replace=False)] = 17
+    idx[rng.choice(np.flatnonzero(idx != 17), 12, replace=False)] = 99
+    _check(engine, pcs, idx, 20)
+
+
+@pytest.mark.parametrize("kmax", [20, 32])
+def test_knn_boot_dev_lattice_ties(engine, kmax):
+    """Integer lattice cells (many distinct cells at exactly equal distance)
+    with heavy duplication: equal-d2 groups are merged by row index, and a
+    group cut by the distinct-cell list goes to the exact search."""
+    g = np.arange(6, dtype=np.float64)
+    pcs = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)  # 216 cells
+    rng = np.random.default_rng(kmax)
+    idx = rng.integers(0, pcs.shape[0], 600).astype(np.int32)
+    fb = _check(engine, pcs, idx, kmax)
+    assert fb > 0  # the lattice's cut ties must have taken the exact path
+
+
+def test_knn_boot_dev_few_distinct_cells(engine):
+    """9 distinct cells, 60 rows, kmax 20: every distinct cell is listed
+    (kq = u - 1 < kmax) and the rows come from the copies."""
+    rng = np.random.default_rng(5)
+    pcs = rng.normal(size=(9, 4))
+    idx = np.concatenate([np.arange(9), rng.integers(0, 9, 51)]).astype(np.int32)
+    rng.shuffle(idx)
+    _check(engine, pcs, idx, 20)
+
+
+def test_knn_boot_dev_single_cell(engine):
+    """Every row is the same cell: each list is the other rows in order."""
+    pcs = np.ones((5, 3))
+    idx = np.full(30, 2, np.int32)
+    _check(engine, pcs, idx, 20)
+
+
+def test_knn_boot_dev_wrong_unique_count(engine):
+    rng = np.random.default_rng(7)
+    pcs = rng.normal(size=(500, 6))
+    idx = rng.integers(0, 500, 400).astype(np.int32)
+    u = len(np.unique(idx))
+    _boot_knn(engine, pcs, idx, 10, want_dist=False, n_unique=u - 3)
+    with pytest.raises(CcgError, match="n_unique"):
+        engine.check_errors()
+    # the context is usable again afterwards
+    _check(engine, pcs, idx, 10)

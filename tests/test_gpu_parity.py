@@ -83,15 +83,23 @@ def test_knn_tiny_and_degenerate(engine):
 
 
 def test_knn_heavy_duplication_forces_fallback(engine):
-    # 60 distinct cells, 900 draws: every cell has ~15 copies at distance 0,
-    # so the k-th and (k+1)-th neighbours tie and certification must fail
+    # 60 distinct cells, 900 draws: every cell has ~15 copies at distance 0.
+    # Searched as rows (ccg_knn_rows_dev) the k-th and (k+1)-th neighbours tie
+    # and certification must fail; the bootstrap path (ccg_knn_boot ->
+    # ccg_knn_boot_dev) searches the 60 distinct cells and expands the copies.
+    import torch
     rng = np.random.default_rng(11)
     pcs = rng.normal(size=(60, 8))
     boot = rng.integers(0, 60, 900).astype(np.int32)
+    rows = O.gather_rows(pcs, boot)
+    oi, _ = O.knn(rows, 20)
     idx, _ = engine.knn_boot(pcs, boot, kmax=20)
-    oi, _ = O.knn(O.gather_rows(pcs, boot), 20)
     assert np.array_equal(idx[0], oi)
-    assert engine.last_knn_stats[1] > 0
+    tr = torch.from_numpy(rows).cuda()
+    out = torch.empty((900, 20), dtype=torch.int32, device="cuda")
+    _, fb = engine.knn_rows_t(tr, 20, out, stats=True)
+    assert np.array_equal(out.cpu().numpy(), oi)
+    assert fb > 0
 
 
 def test_knn_segments_vs_oracle(engine):

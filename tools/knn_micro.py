@@ -1,6 +1,9 @@
 """Micro-benchmark of ccg_knn_rows_dev at BASELINE cfg3 shapes (n=90000, d=30).
 
-Times the screen kernel and the whole kNN with the library's hipEvent timers.
+Times the screen kernel and the whole kNN with the library's hipEvent timers:
+by default the bench's path (ccg_knn_boot_dev: the bootstrap's distinct
+cells, then the expansion to rows); KM_MODE=rows searches all n rows
+(ccg_knn_rows_dev).
 Data: one 90k-row bootstrap of bench.py's synthetic NB-count PCs (KM_DATA=gauss:
 a 12-component Gaussian mixture instead).
 Variants are separate builds of libccg (tools/build_variant.sh, --lib);
@@ -36,24 +39,36 @@ def main():
         rows = torch.empty((n, d), dtype=torch.float64, device="cuda")
         eng.gather_rows_t(pcs.t().contiguous(), N, d, boot, rows)
     idx = torch.empty((n, 20), dtype=torch.int32, device="cuda")
-    eng.knn_rows_t(rows, 20, idx)
+    boot_mode = os.environ.get("KM_MODE", "boot") == "boot" and os.environ.get("KM_DATA") != "gauss"
+    if boot_mode:  # the bench's path: the bootstrap's distinct cells (ccg_knn_boot_dev)
+        pcs_cm = pcs.t().contiguous()
+        u = int(torch.unique(boot).numel())
+
+        def run(stats=False):
+            return eng.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, idx, stats=stats)
+    else:
+        u = n
+
+        def run(stats=False):
+            return eng.knn_rows_t(rows, 20, idx, stats=stats)
+    run()
     torch.cuda.synchronize()
     eng.timing(True)
     eng.timing_read("knn_screen")
     eng.timing_read("knn_total")
     for _ in range(reps):
-        eng.knn_rows_t(rows, 20, idx)
+        run()
     scr = eng.timing_read("knn_screen")
     tot = eng.timing_read("knn_total")
-    st = eng.knn_rows_t(rows, 20, idx, stats=True)
-    out = {"lib": os.path.basename(_lib.LIB_PATH),
+    st = run(stats=True)
+    out = {"lib": os.path.basename(_lib.LIB_PATH), "mode": "boot" if boot_mode else "rows", "n": n, "u": u,
            "screen_ms": scr[0] / scr[1], "knn_total_ms": tot[0] / tot[1], "fallback": st[1]}
     lib = _lib.load()
     if hasattr(lib, "ccg_debug_knn_stamps"):  # a -DKNN_STAMPS=1 variant: per-wave cycle attribution
         import ctypes
         buf = (ctypes.c_ulonglong * 12)()
         lib.ccg_debug_knn_stamps(buf)  # reset
-        eng.knn_rows_t(rows, 20, idx)
+        run()
         torch.cuda.synchronize()
         lib.ccg_debug_knn_stamps(buf)
         waves = max(1, buf[11])
