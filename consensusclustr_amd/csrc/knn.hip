@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
     const double* __restrict__ inv_scale2, double err_ulps, const int* __restrict__ perm,
     int32_t* __restrict__ out_idx, double* __restrict__ out_dist, int* __restrict__ fail_list,
-    int* __restrict__ fail_count, int npos, const int64_t* __restrict__ seg_off, int nseg) {
+    int* __restrict__ fail_count, int npos, const int64_t* __restrict__ seg_off, int nseg, bool dist_sq) {
     const int lane = threadIdx.x & 63;
     const int qs = blockIdx.x * 4 + (threadIdx.x >> 6);  // screening position
     if (qs >= npos) return;
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     if (ok) {
         if (lane < kmax) {
             out_idx[(int64_t)q * kmax + lane] = id - base;
-            if (out_dist) out_dist[(int64_t)q * kmax + lane] = sqrt(key);
+            if (out_dist) out_dist[(int64_t)q * kmax + lane] = dist_sq ? key : sqrt(key);
         }
     } else if (lane == 0) {
         int p = atomicAdd(fail_count, 1);
@@ -875,7 +875,8 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
 __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
     int kmax, const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
     const double* __restrict__ lst_d, const int* __restrict__ lst_i,
-    int32_t* __restrict__ out_idx, double* __restrict__ out_dist, const int64_t* __restrict__ seg_off, int nseg) {
+    int32_t* __restrict__ out_idx, double* __restrict__ out_dist, const int64_t* __restrict__ seg_off, int nseg,
+    bool dist_sq) {
     const int lane = threadIdx.x;
     const int nfail = *fail_count;
     const int S = knn_fb_splits(nfail, slots);
@@ -905,7 +906,7 @@ __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
             }
             if (lane == 0) {
                 out_idx[(int64_t)q * kmax + r] = bi - base;
-                if (out_dist) out_dist[(int64_t)q * kmax + r] = sqrt(bk);
+                if (out_dist) out_dist[(int64_t)q * kmax + r] = dist_sq ? bk : sqrt(bk);
             }
             if (lane < S && mi == bi && mk == bk) ++pos;
         }
@@ -937,7 +938,7 @@ struct KnnSegs {
 // Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
 static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
                                const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
-                               int nseg, hipStream_t st) {
+                               int nseg, hipStream_t st, bool dist_sq = false) {
     const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
     double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
@@ -956,12 +957,13 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
     }
 #undef CCG_FALLBACK
     knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
-                                                   out_dist, seg_off, nseg);
+                                                   out_dist, seg_off, nseg, dist_sq);
     return CCG_OK;
 }
 
+// dist_sq: out_dist receives the squared distances (the certified fp64 sums)
 static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, int32_t* out_idx,
-                   double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg) {
+                   double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg, bool dist_sq = false) {
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
     const int64_t npos = sg ? sg->npos : n;  // screening positions
     int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * npos * 2 * KP);
@@ -1037,7 +1039,7 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
 #define CCG_CERTIFY(KP_, DM_)                                                                             \
     knn_certify_kernel<KP_, DM_><<<(unsigned)ccg_cdiv(npos, 4), 256, 0, st>>>(                              \
         rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist, \
-        fail_list, fail_count, (int)npos, seg_off, nseg)
+        fail_list, fail_count, (int)npos, seg_off, nseg, dist_sq)
     if (KP == KNN_KP) {
         if (d <= 16) CCG_CERTIFY(KNN_KP, 16);
         else if (d <= 32) CCG_CERTIFY(KNN_KP, 32);
@@ -1048,7 +1050,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         else CCG_CERTIFY(KNN_KP_BIG, 64);
     }
 #undef CCG_CERTIFY
-    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, seg_off, nseg, st);
+    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, seg_off, nseg, st,
+                             dist_sq);
     if (rc) return rc;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
@@ -1175,22 +1178,9 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
     if (t == 0) ustart[u] = (int)n;
 }
 
-template <int DMAX>
-__device__ __forceinline__ double kb_d2(const double (&xq)[DMAX], const double* __restrict__ y, int d) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < DMAX; ++k)
-        if (k < d) {
-            const double t = __dsub_rn(xq[k], y[k]);
-            s = __dadd_rn(s, __dmul_rn(t, t));
-        }
-    return s;
-}
-
 #define KB_GMAX 33  // cells of one merge group (the own cell + kq <= 32 neighbours)
-template <int DMAX>
-__global__ __launch_bounds__(256) void kb_expand_kernel(const double* __restrict__ urows, int d, int64_t n, int u,
-                                                        int kq, const int* __restrict__ uidx,
+__global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq, const int* __restrict__ uidx,
+                                                        const double* __restrict__ ud2,
                                                         const int* __restrict__ ustart, const int* __restrict__ srow,
                                                         const int* __restrict__ row2u, int kmax,
                                                         int32_t* __restrict__ out_idx, double* __restrict__ out_dist,
@@ -1198,13 +1188,13 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(const double* __restrict
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int uc = row2u[i];
-    double xq[DMAX];
-#pragma unroll
-    for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? urows[(int64_t)uc * d + k] : 0.0;
+    // the distinct cell's kq nearest distinct cells with their certified d2
+    // (fp64, unfused, dimension order: the oracle's sums; copies share them)
     const int* nbl = uidx + (int64_t)uc * kq;
+    const double* d2l = ud2 + (int64_t)uc * kq;
     int o = 0;     // rows written
     int t = 0;     // next distinct neighbour
-    double dn = kq > 0 ? kb_d2<DMAX>(xq, urows + (int64_t)nbl[0] * d, d) : INFINITY;
+    double dn = kq > 0 ? d2l[0] : INFINITY;
     double gd = 0.0;  // the group's d2 (group 0: the own cell, d2 = 0)
     bool first = true, fail = false;
     int lo[KB_GMAX], hi[KB_GMAX];
@@ -1222,7 +1212,7 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(const double* __restrict
             hi[g] = ustart[v + 1];
             ++g;
             ++t;
-            dn = t < kq ? kb_d2<DMAX>(xq, urows + (int64_t)nbl[t] * d, d) : INFINITY;
+            dn = t < kq ? d2l[t] : INFINITY;
         }
         if (t == kq && t > t0 && kq < u - 1) {  // the group may continue past the computed list
             fail = true;
@@ -1273,7 +1263,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     // workspaces (the full-size fail list first, so the distinct-cell run never grows it)
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
     char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + 2 * (size_t)u + 1));
-    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * d + sizeof(int32_t) * (size_t)u * kq + 64);
+    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * (d + kq) + sizeof(int32_t) * (size_t)u * kq + 64);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
     if (!fail_list || !ta || !urows || !misc) return CCG_ENOMEM;
     int64_t* head = (int64_t*)ta;                // [n + 1] heads, then their exclusive scan in place
@@ -1284,7 +1274,8 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int32_t* ustart = srow + n;                  // [u + 1]
     int32_t* ucell = ustart + u + 1;             // [u]
     int32_t* row2u = cells;
-    int32_t* uidx = (int32_t*)(urows + (size_t)u * d);
+    double* ud2 = urows + (size_t)u * d;                 // [u][kq] certified squared distances
+    int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
     int* fail_count = (int*)(misc + 1);
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     // 1. rows grouped by cell (stable radix sort on the cell index bits)
@@ -1304,21 +1295,13 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     gather_rows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(pcs, N, d, ucell, u, urows);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1) {
-        rc = knn_run(ctx, urows, u, d, kq, uidx, nullptr, stats ? &us : nullptr, st, nullptr);
+        rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true);
         if (rc) return rc;
     }
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
     CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
-    const unsigned eg = ng;
-    if (d <= 16)
-        kb_expand_kernel<16><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
-                                                 out_dist, fail_list, fail_count);
-    else if (d <= 32)
-        kb_expand_kernel<32><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
-                                                 out_dist, fail_list, fail_count);
-    else
-        kb_expand_kernel<64><<<eg, 256, 0, st>>>(urows, d, n, u, kq, uidx, ustart, srow, row2u, kmax, out_idx,
-                                                 out_dist, fail_list, fail_count);
+    kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
+                                         fail_count);
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st);
     if (rc) return rc;
     ccg_timer_stop(ctx, t_all, st);
