@@ -41,6 +41,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 #define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
 #define KNN_FB_UNITS 448   // target (failed row, range) blocks
+#define KNN_FB_GRID 448    // fallback grids (grid-stride loops; usually 0-30 rows fail, and a
+                           // 1024-block launch of exiting blocks alone cost ~30 us)
 
 // Error budget of the fp16 hi/lo screen (DESIGN.md "kNN certification bound"):
 // relative part in units of the fp32 ulp (2^-24) times (2|x| + sqrt(dK))^2 --
@@ -944,8 +946,9 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
     if (!fb_d || !fb_i) return CCG_ENOMEM;
 #define CCG_FALLBACK(DM_, FK_)                                                                            \
-    knn_fallback_kernel<DM_, FK_><<<1024, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count, fb_slots, \
-                                                        fb_d, fb_i, seg_off, nseg)
+    knn_fallback_kernel<DM_, FK_><<<KNN_FB_GRID, 256, 0, st>>>(rows, (int)n, d, kmax, fail_list, fail_count,      \
+                                                               fb_slots,                                          \
+                                                               fb_d, fb_i, seg_off, nseg)
     if (kmax <= KNN_KP) {  // per-thread lists of kmax <= 20 entries
         if (d <= 16) CCG_FALLBACK(16, KNN_KP);
         else if (d <= 32) CCG_FALLBACK(32, KNN_KP);
@@ -956,7 +959,7 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         else CCG_FALLBACK(64, KNN_FB_K);
     }
 #undef CCG_FALLBACK
-    knn_fallback_merge_kernel<<<1024, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
+    knn_fallback_merge_kernel<<<KNN_FB_GRID, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
                                                    out_dist, seg_off, nseg, dist_sq);
     return CCG_OK;
 }
@@ -1197,19 +1200,30 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
     double dn = kq > 0 ? d2l[0] : INFINITY;
     double gd = 0.0;  // the group's d2 (group 0: the own cell, d2 = 0)
     bool first = true, fail = false;
-    int lo[KB_GMAX], hi[KB_GMAX];
+    int lo[KB_GMAX], hi[KB_GMAX];  // ranges of a multi-cell group (exact ties between distinct cells: rare)
     while (o < kmax) {
-        int g = 0;
+        // the group: the own cell first (group 0), then the distinct neighbours at d2 == gd
+        int g = 0, lo0 = 0, hi0 = 0;
         if (first) {
-            lo[0] = ustart[uc];
-            hi[0] = ustart[uc + 1];
+            lo0 = ustart[uc];
+            hi0 = ustart[uc + 1];
             g = 1;
         }
         const int t0 = t;
         while (t < kq && dn == gd) {
             const int v = nbl[t];
-            lo[g] = ustart[v];
-            hi[g] = ustart[v + 1];
+            const int a = ustart[v], b = ustart[v + 1];
+            if (g == 0) {
+                lo0 = a;
+                hi0 = b;
+            } else {
+                if (g == 1) {
+                    lo[0] = lo0;
+                    hi[0] = hi0;
+                }
+                lo[g] = a;
+                hi[g] = b;
+            }
             ++g;
             ++t;
             dn = t < kq ? d2l[t] : INFINITY;
@@ -1218,23 +1232,34 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
             fail = true;
             break;
         }
-        // merge the group's row lists (each ascending) by row index, skipping row i
-        while (o < kmax) {
-            int best = 0x7fffffff, bg = -1;
-            for (int q = 0; q < g; ++q)
-                if (lo[q] < hi[q]) {
-                    const int r = srow[lo[q]];
-                    if (r < best) {
-                        best = r;
-                        bg = q;
+        const double dist = out_dist ? sqrt(gd) : 0.0;
+        if (g == 1) {  // one cell: its rows are already ascending
+            for (int q = lo0; q < hi0 && o < kmax; ++q) {
+                const int r = srow[q];
+                if (r == (int)i) continue;
+                out_idx[i * kmax + o] = r;
+                if (out_dist) out_dist[i * kmax + o] = dist;
+                ++o;
+            }
+        } else {
+            // merge the group's row lists (each ascending) by row index, skipping row i
+            while (o < kmax) {
+                int best = 0x7fffffff, bg = -1;
+                for (int q = 0; q < g; ++q)
+                    if (lo[q] < hi[q]) {
+                        const int r = srow[lo[q]];
+                        if (r < best) {
+                            best = r;
+                            bg = q;
+                        }
                     }
-                }
-            if (bg < 0) break;
-            ++lo[bg];
-            if (best == (int)i) continue;
-            out_idx[i * kmax + o] = best;
-            if (out_dist) out_dist[i * kmax + o] = sqrt(gd);
-            ++o;
+                if (bg < 0) break;
+                ++lo[bg];
+                if (best == (int)i) continue;
+                out_idx[i * kmax + o] = best;
+                if (out_dist) out_dist[i * kmax + o] = dist;
+                ++o;
+            }
         }
         if (o >= kmax) break;
         if (t >= kq) {  // every distinct cell is listed (kq = u - 1) yet fewer than kmax rows: n - 1 < kmax
