@@ -133,6 +133,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 __host__ __device__ constexpr int knn_chunk(int ksteps) { return ksteps == 4 ? 64 : 128; }
 __host__ __device__ constexpr int knn_nbuf(int ksteps) { return ksteps == 4 ? 3 : 2; }
 static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 : 4); }  // d dims + the norm dim
+#ifndef KNN_NO_MORTON
+#define KNN_NO_MORTON 0     // tools only: screen in input order (no Morton bucketing)
+#endif
 #ifndef KNN_QCAP
 #define KNN_QCAP 8          // per-lane insertion queue slots (flush before a half tile that could overflow)
 #endif
@@ -160,7 +163,7 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
                                   uint4* __restrict__ img, double* __restrict__ inv_scale2) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in spatial order
     if (r >= npad) return;
-    const int64_t src = r < n ? perm[r] : -1;  // -1: padding position (segment padding or r >= n)
+    const int64_t src = r < n ? (perm ? perm[r] : r) : -1;  // -1: padding position (segment padding or r >= n)
     const bool valid = src >= 0;
     const int e = knn_scale_exp(maxabs_bits);
     if (r == 0) *inv_scale2 = ldexp(1.0, -2 * e);
@@ -195,10 +198,20 @@ __device__ __forceinline__ int swz_chunk(int row, int c) {
 }
 
 // ---------------------------------------------------- spatial ordering --
-// Bucket rows by a 15-bit Morton code of their first three coordinates (the
-// leading PCs) so that rows close in space sit in nearby chunks.  Any
-// permutation is correct; only screening speed depends on it.
+// Order rows by a Morton code of their leading KNN_MORTON_DIMS coordinates
+// (the leading PCs), KNN_MORTON_BITS bits each, so that rows close in space
+// sit in nearby chunks: the screen's thresholds tighten within the first
+// chunks it scans.  Any permutation is correct; only screening speed depends
+// on it.  Codes of <= 15 bits are bucketed by a counting sort; longer codes
+// are radix-sorted (key, row) pairs.
+#ifndef KNN_MORTON_DIMS
+#define KNN_MORTON_DIMS 3
+#endif
+#ifndef KNN_MORTON_BITS
 #define KNN_MORTON_BITS 5
+#endif
+#define KNN_MD KNN_MORTON_DIMS
+static_assert(KNN_MORTON_DIMS * KNN_MORTON_BITS <= 31 && KNN_MORTON_DIMS <= 24, "Morton code too long");
 __device__ __forceinline__ unsigned f2ord(float f) {
     const unsigned u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -207,65 +220,74 @@ __device__ __forceinline__ float ord2f(unsigned o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-// max|x| (fp32 bits, rounded up) and the ordered-float bounds of the first
-// three coordinates in one coalesced pass; block-level reduction so each
-// block issues 7 atomics (a per-wave atomic on one word serialises at ~13 ns
-// each).
+// max|x| (fp32 bits, rounded up) and the ordered-float bounds of the leading
+// KNN_MD coordinates in one coalesced pass; block-level reduction so each
+// block issues 1 + 2 KNN_MD atomics (a per-wave atomic on one word serialises
+// at ~13 ns each).  bnd: [0, KNN_MD) minima, [KNN_MD, 2 KNN_MD) maxima.
 __global__ __launch_bounds__(256) void knn_rowstats_kernel(const double* __restrict__ rows, int64_t n, int d,
                                                            unsigned* __restrict__ maxabs_bits,
                                                            unsigned* __restrict__ bnd) {
-    __shared__ unsigned red[4][7];
-    unsigned v7[7] = {0u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    constexpr int NV = 1 + 2 * KNN_MD;
+    __shared__ unsigned red[4][NV];
+    unsigned v[NV];
+    v[0] = 0u;
+#pragma unroll
+    for (int i = 0; i < KNN_MD; ++i) {
+        v[1 + i] = 0xffffffffu;
+        v[1 + KNN_MD + i] = 0u;
+    }
     const int64_t tot = n * d;
     const int64_t S = (int64_t)gridDim.x * blockDim.x;
     const int kstep = (int)(S % d);
     int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int k = (int)(t % d);
     for (; t < tot; t += S) {
-        const double v = rows[t];
-        float f = (float)fabs(v);
+        const double x = rows[t];
+        float f = (float)fabs(x);
         f = nextafterf(f, INFINITY);
-        v7[0] = max(v7[0], __float_as_uint(f));
-        if (k < 3) {
-            const unsigned o = f2ord((float)v);
-            v7[1 + k] = min(v7[1 + k], o);
-            v7[4 + k] = max(v7[4 + k], o);
-        }
+        v[0] = max(v[0], __float_as_uint(f));
+        const unsigned o = f2ord((float)x);
+#pragma unroll
+        for (int i = 0; i < KNN_MD; ++i)
+            if (k == i) {
+                v[1 + i] = min(v[1 + i], o);
+                v[1 + KNN_MD + i] = max(v[1 + KNN_MD + i], o);
+            }
         k += kstep;
         if (k >= d) k -= d;
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        unsigned a = v7[i];
+    for (int i = 0; i < NV; ++i) {
+        unsigned a = v[i];
         for (int o = 32; o > 0; o >>= 1) {
             const unsigned b = (unsigned)__shfl_xor((int)a, o, 64);
-            a = (i >= 1 && i <= 3) ? min(a, b) : max(a, b);
+            a = (i >= 1 && i <= KNN_MD) ? min(a, b) : max(a, b);
         }
         if (lane == 0) red[wv][i] = a;
     }
     __syncthreads();
-    if (threadIdx.x < 7) {
+    if (threadIdx.x < NV) {
         const int i = threadIdx.x;
         unsigned a = red[0][i];
-        for (int w = 1; w < 4; ++w) a = (i >= 1 && i <= 3) ? min(a, red[w][i]) : max(a, red[w][i]);
+        for (int w = 1; w < 4; ++w) a = (i >= 1 && i <= KNN_MD) ? min(a, red[w][i]) : max(a, red[w][i]);
         if (i == 0) atomicMax(maxabs_bits, a);
-        else if (i <= 3) { if (i - 1 < d) atomicMin(&bnd[i - 1], a); }
-        else if (i - 4 < d) atomicMax(&bnd[3 + (i - 4)], a);
+        else if (i <= KNN_MD) { if (i - 1 < d) atomicMin(&bnd[i - 1], a); }
+        else if (i - 1 - KNN_MD < d) atomicMax(&bnd[i - 1], a);
     }
 }
 
 __device__ __forceinline__ unsigned morton_key(const double* __restrict__ x, int d,
                                                const unsigned* __restrict__ bnd) {
-    const int nd = d < 3 ? d : 3;
+    const int nd = d < KNN_MD ? d : KNN_MD;
     unsigned code = 0;
     for (int k = 0; k < nd; ++k) {
-        const float lo = ord2f(bnd[k]), hi = ord2f(bnd[3 + k]);
+        const float lo = ord2f(bnd[k]), hi = ord2f(bnd[KNN_MD + k]);
         const float span = hi - lo;
         float t = span > 0.f ? ((float)x[k] - lo) / span : 0.f;
         t = fminf(fmaxf(t, 0.f), 0.999999f);
         const unsigned qv = (unsigned)(t * (float)(1u << KNN_MORTON_BITS));
-        for (int b = 0; b < KNN_MORTON_BITS; ++b) code |= ((qv >> b) & 1u) << (3 * b + k);
+        for (int b = 0; b < KNN_MORTON_BITS; ++b) code |= ((qv >> b) & 1u) << (KNN_MD * b + k);
     }
     return code;
 }
@@ -285,6 +307,16 @@ __global__ void knn_bucket_scatter_kernel(const double* __restrict__ rows, int64
     const unsigned key = morton_key(rows + r * d, d, bnd);
     const int64_t pos = (int64_t)atomicAdd((unsigned long long*)&cursor[key], 1ull);
     perm[pos] = (int)r;
+}
+
+// (Morton key, row) pairs for the radix-sorted order of long codes
+__global__ void knn_morton_keys_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                       const unsigned* __restrict__ bnd, int32_t* __restrict__ keys,
+                                       int32_t* __restrict__ ids) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    keys[r] = (int32_t)morton_key(rows + r * d, d, bnd);
+    ids[r] = (int32_t)r;
 }
 
 __device__ __forceinline__ int knn_chunk_at(int k, int c0, int Lc, int Rc, int Mc) {
@@ -989,16 +1021,18 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + 256);
         if (!img) return CCG_ENOMEM;
-        unsigned* bnd = misc + 8;
-        CCG_HIP(hipMemsetAsync(bnd, 0xff, 3 * sizeof(unsigned), st));
-        CCG_HIP(hipMemsetAsync(bnd + 3, 0, 3 * sizeof(unsigned), st));
+        unsigned* bnd = misc + 8;  // [2 KNN_MD]: minima then maxima of the leading coordinates
+        CCG_HIP(hipMemsetAsync(bnd, 0xff, KNN_MD * sizeof(unsigned), st));
+        CCG_HIP(hipMemsetAsync(bnd + KNN_MD, 0, KNN_MD * sizeof(unsigned), st));
         knn_rowstats_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 1024), 256), 256, 0, st>>>(rows, n, d,
                                                                                                     mbits, bnd);
         if (sg) {
             order_perm = sg->perm;  // segments keep their rows in input order
-        } else {
-            // spatial order: Morton buckets of the leading coordinates
-            const int64_t NB = 1LL << (3 * KNN_MORTON_BITS);
+        } else if (KNN_NO_MORTON) {
+            order_perm = nullptr;  // tools only: input order
+        } else if (KNN_MORTON_DIMS * KNN_MORTON_BITS <= 15) {
+            // spatial order: Morton buckets of the leading coordinates (counting sort)
+            const int64_t NB = 1LL << (KNN_MORTON_DIMS * KNN_MORTON_BITS);
             int64_t* hist =
                 (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
             if (!hist) return CCG_ENOMEM;
@@ -1010,6 +1044,17 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
             if (rc) return rc;
             CCG_HIP(hipMemcpyAsync(cursor, hist, sizeof(int64_t) * (NB + 1), hipMemcpyDeviceToDevice, st));
             knn_bucket_scatter_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, cursor, perm);
+            order_perm = perm;
+        } else {
+            // spatial order: radix-sorted Morton codes of the leading coordinates
+            int32_t* kk = (int32_t*)ccg_ws(ctx, WS_ORDER, sizeof(int32_t) * 4 * n + 64);
+            if (!kk) return CCG_ENOMEM;
+            int32_t* ids = kk + n;
+            int32_t* skeys = ids + n;
+            int32_t* perm = skeys + n;
+            knn_morton_keys_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, kk, ids);
+            rc = ccg_sort_pairs_i32(ctx, kk, skeys, ids, perm, n, KNN_MORTON_DIMS * KNN_MORTON_BITS, st);
+            if (rc) return rc;
             order_perm = perm;
         }
         const unsigned pg = (unsigned)ccg_cdiv(npad, 256);
