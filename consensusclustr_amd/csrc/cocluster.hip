@@ -323,21 +323,27 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             __syncthreads();
         }
     }
-    // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts)
+    // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts).
+    // Loops run row-major (mi, r outer) so each of a lane's 32 rows computes
+    // its packed-triangle offset once for its 4 column groups (the 64-bit
+    // offset arithmetic per element dominated the small-B epilogue).
     const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int r = 0; r < 16; ++r) {
+            const int64_t gi = rowA0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool row_ok = gi < r1;
+            // TRI: o = (row gi's start in the packed triangle) + (gj - gi - 1) - base
+            const int64_t rb = MODE == COF_TRI ? gi * N - gi * (gi + 1) / 2 - gi - 1 - base : (gi - r0) * N;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t gi = rowA0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            for (int ni = 0; ni < 4; ++ni) {
                 const int64_t gj = rowB0 + wc * 128 + ni * 32 + (lane & 31);
                 const int a = acc[mi][ni][r];
                 int cv = a & 16383, bv = a >> 14;
                 if (MODE == COF_TRI) {
-                    if (gi < r1 && gj < N && gj > gi) {
-                        const int64_t o = gi * N - gi * (gi + 1) / 2 + (gj - gi - 1) - base;
+                    if (row_ok && gj < N && gj > gi) {
+                        const int64_t o = rb + gj;
                         if (co_prev) {
                             cv += co_prev[o];
                             bv += both_prev[o];
@@ -350,8 +356,8 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
                         }
                     }
                 } else {
-                    if (gi < r1 && gj < N) {
-                        const int64_t o = (gi - r0) * N + gj;
+                    if (row_ok && gj < N) {
+                        const int64_t o = rb + gj;
                         if (cb_prev) {
                             const uint32_t pv = cb_prev[o];
                             cv += (int)(pv & 0xFFFFu);
@@ -361,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
                     }
                 }
             }
+        }
 }
 
 // Launch state shared by the triangle and full-row drivers.
