@@ -1323,17 +1323,19 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     CCG_REQUIRE(ctx && pcs && idx && rows && out_idx, "ccg_knn_boot_dev: NULL argument");
     CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boot_dev: d=%d must be in [1, 63]", d);
     CCG_REQUIRE(N >= 1 && N < (1LL << 31) && n >= 2 && n < (1LL << 30), "ccg_knn_boot_dev: bad sizes");
-    CCG_REQUIRE(n_unique >= 1 && n_unique <= n && n_unique <= N, "ccg_knn_boot_dev: n_unique=%d out of range",
-                n_unique);
+    CCG_REQUIRE(n_unique == -1 || (n_unique >= 1 && n_unique <= n && n_unique <= N),
+                "ccg_knn_boot_dev: n_unique=%d out of range", n_unique);
     CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
                 "ccg_knn_boot_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    const int u = n_unique;
-    const int kq = std::min(kmax, u - 1);
+    // n_unique = -1: counted on the device (one stream synchronisation); the
+    // workspaces are then sized for u <= min(n, N)
+    const int ucap = n_unique >= 0 ? n_unique : (int)std::min<int64_t>(n, N);
     // workspaces (the full-size fail list first, so the distinct-cell run never grows it)
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
-    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + 2 * (size_t)u + 1));
-    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * (d + kq) + sizeof(int32_t) * (size_t)u * kq + 64);
+    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + 2 * (size_t)ucap + 1));
+    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)ucap * (d + kmax) +
+                                                      sizeof(int32_t) * (size_t)ucap * kmax + 64);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
     if (!fail_list || !ta || !urows || !misc) return CCG_ENOMEM;
     int64_t* head = (int64_t*)ta;                // [n + 1] heads, then their exclusive scan in place
@@ -1341,11 +1343,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int32_t* scell = cells + n;                  // [n] sorted keys
     int32_t* rid = scell + n;                    // [n] sort values (the rows)
     int32_t* srow = rid + n;                     // [n] rows sorted by cell
-    int32_t* ustart = srow + n;                  // [u + 1]
-    int32_t* ucell = ustart + u + 1;             // [u]
     int32_t* row2u = cells;
-    double* ud2 = urows + (size_t)u * d;                 // [u][kq] certified squared distances
-    int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
     int* fail_count = (int*)(misc + 1);
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     // 1. rows grouped by cell (stable radix sort on the cell index bits)
@@ -1356,10 +1354,22 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int rc = ccg_sort_pairs_i32(ctx, cells, scell, rid, srow, n, bits, st);
     if (rc) return rc;
     // 2. distinct cells: heads -> scan -> tables
-    CCG_HIP(hipMemsetAsync(ustart, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
     kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head);
     rc = ccg_scan_i64(ctx, head, head, n, st);
     if (rc) return rc;
+    int u = n_unique;
+    if (u < 0) {
+        int64_t hu = 0;
+        CCG_HIP(hipMemcpyAsync(&hu, head + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        u = (int)hu;
+    }
+    const int kq = std::min(kmax, u - 1);
+    int32_t* ustart = srow + n;                  // [u + 1]
+    int32_t* ucell = ustart + u + 1;             // [u]
+    double* ud2 = urows + (size_t)u * d;         // [u][kq] certified squared distances
+    int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
+    CCG_HIP(hipMemsetAsync(ustart, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
     kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, ucell, row2u, ctx->d_err);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     gather_rows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(pcs, N, d, ucell, u, urows);

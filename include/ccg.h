@@ -129,7 +129,8 @@ int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
  *   pcs      : N x d float64 COLUMN-major (device)
  *   idx      : n int32 0-based cell indices (device; R's sample() - 1)
  *   n_unique : the number of distinct values in idx (host; R:
- *              length(unique(idx))).  A wrong value -- or an index outside
+ *              length(unique(idx))), or -1 to count them on the device (one
+ *              stream synchronisation).  A wrong value -- or an index outside
  *              [0, N) -- sets the sticky device error (CCG_EINVAL at the next
  *              ccg_synchronize / ccg_check_errors); outputs are then undefined.
  *   rows     : the gathered n x d rows (ccg_gather_rows_dev; read by the exact

@@ -94,6 +94,17 @@ def test_knn_boot_dev_single_cell(engine):
     _check(engine, pcs, idx, 20)
 
 
+def test_knn_boot_dev_counts_distinct_cells(engine):
+    """n_unique = -1: the device counts the distinct cells itself."""
+    rng = np.random.default_rng(13)
+    pcs = rng.normal(size=(700, 9))
+    idx = rng.integers(0, 700, 630).astype(np.int32)
+    oi, od = O.knn(O.gather_rows(pcs, idx), 20)
+    gi, gd, _ = _boot_knn(engine, pcs, idx, 20, n_unique=-1)
+    assert np.array_equal(gi, oi)
+    np.testing.assert_allclose(gd, od, rtol=1e-12, atol=1e-12)
+
+
 def test_knn_boot_dev_wrong_unique_count(engine):
     rng = np.random.default_rng(7)
     pcs = rng.normal(size=(500, 6))
