@@ -41,7 +41,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 #define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
 #define KNN_FB_UNITS 448   // target (failed row, range) blocks
-#define KNN_FB_GRID 448    // fallback grids (grid-stride loops; usually 0-30 rows fail, and a
+#define KNN_FB_GRID 128    // fallback grids (grid-stride loops; usually 0-30 rows fail, and a
                            // 1024-block launch of exiting blocks alone cost ~30 us)
 
 // Error budget of the fp16 hi/lo screen (DESIGN.md "kNN certification bound"):
@@ -307,6 +307,18 @@ __global__ void knn_bucket_scatter_kernel(const double* __restrict__ rows, int64
     const unsigned key = morton_key(rows + r * d, d, bnd);
     const int64_t pos = (int64_t)atomicAdd((unsigned long long*)&cursor[key], 1ull);
     perm[pos] = (int)r;
+}
+
+// One launch for knn_run's small initialisations: misc (max|x| bits, fail
+// count, 1/sigma^2), the coordinate bounds (minima all-ones, maxima zero) and
+// the Morton bucket histogram (hist may be null).
+__global__ void knn_init_kernel(unsigned* __restrict__ misc, unsigned* __restrict__ bnd,
+                                int64_t* __restrict__ hist, int64_t nhist) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 4) misc[t] = 0u;
+    if (t < 2 * KNN_MD) bnd[t] = t < KNN_MD ? 0xffffffffu : 0u;
+    if (hist)
+        for (int64_t i = t; i < nhist; i += (int64_t)gridDim.x * blockDim.x) hist[i] = 0;
 }
 
 // (Morton key, row) pairs for the radix-sorted order of long codes
@@ -1010,7 +1022,6 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     unsigned int* mbits = misc;
     int* fail_count = (int*)(misc + 1);
     double* inv_scale2 = (double*)(misc + 2);
-    CCG_HIP(hipMemsetAsync(misc, 0, 16, st));
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     int rc = CCG_OK;
     const double err_ulps = KNN_ERR_ULPS_F16;
@@ -1022,23 +1033,24 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + 256);
         if (!img) return CCG_ENOMEM;
         unsigned* bnd = misc + 8;  // [2 KNN_MD]: minima then maxima of the leading coordinates
-        CCG_HIP(hipMemsetAsync(bnd, 0xff, KNN_MD * sizeof(unsigned), st));
-        CCG_HIP(hipMemsetAsync(bnd + KNN_MD, 0, KNN_MD * sizeof(unsigned), st));
+        const bool buckets = !sg && !KNN_NO_MORTON && KNN_MORTON_DIMS * KNN_MORTON_BITS <= 15;
+        const int64_t NB = 1LL << (KNN_MORTON_DIMS * KNN_MORTON_BITS);
+        int64_t* hist = nullptr;
+        if (buckets) {
+            hist = (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
+            if (!hist) return CCG_ENOMEM;
+        }
+        knn_init_kernel<<<buckets ? 64 : 1, 256, 0, st>>>(misc, bnd, hist, NB + 1);
         knn_rowstats_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 1024), 256), 256, 0, st>>>(rows, n, d,
                                                                                                     mbits, bnd);
         if (sg) {
             order_perm = sg->perm;  // segments keep their rows in input order
         } else if (KNN_NO_MORTON) {
             order_perm = nullptr;  // tools only: input order
-        } else if (KNN_MORTON_DIMS * KNN_MORTON_BITS <= 15) {
+        } else if (buckets) {
             // spatial order: Morton buckets of the leading coordinates (counting sort)
-            const int64_t NB = 1LL << (KNN_MORTON_DIMS * KNN_MORTON_BITS);
-            int64_t* hist =
-                (int64_t*)ccg_ws(ctx, WS_ORDER, sizeof(int64_t) * (2 * (NB + 1)) + sizeof(int) * n + 64);
-            if (!hist) return CCG_ENOMEM;
             int64_t* cursor = hist + (NB + 1);
             int* perm = (int*)(cursor + (NB + 1));
-            CCG_HIP(hipMemsetAsync(hist, 0, sizeof(int64_t) * (NB + 1), st));
             knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
             rc = ccg_scan_i64(ctx, hist, hist, NB, st);
             if (rc) return rc;
