@@ -310,12 +310,12 @@ __global__ void knn_bucket_scatter_kernel(const double* __restrict__ rows, int64
 }
 
 // One launch for knn_run's small initialisations: misc (max|x| bits, fail
-// count, 1/sigma^2), the coordinate bounds (minima all-ones, maxima zero) and
+// count, 1/sigma^2, the distinct-cell expansion's fail count), the coordinate bounds (minima all-ones, maxima zero) and
 // the Morton bucket histogram (hist may be null).
 __global__ void knn_init_kernel(unsigned* __restrict__ misc, unsigned* __restrict__ bnd,
                                 int64_t* __restrict__ hist, int64_t nhist) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < 4) misc[t] = 0u;
+    if (t < 8) misc[t] = 0u;  // [4]: ccg_knn_boot_dev's expansion fail count
     if (t < 2 * KNN_MD) bnd[t] = t < KNN_MD ? 0xffffffffu : 0u;
     if (hist)
         for (int64_t i = t; i < nhist; i += (int64_t)gridDim.x * blockDim.x) hist[i] = 0;
@@ -1212,9 +1212,13 @@ __global__ void kb_iota_kernel(const int32_t* __restrict__ idx, int64_t n, int64
 }
 
 // (cell, row) pairs sorted by cell (stable: each cell's rows ascending)
-__global__ void kb_heads_kernel(const int32_t* __restrict__ scell, int64_t n, int64_t* __restrict__ head) {
+// (also zeroes the 2u + 1 table words when u is known: ztab / nz)
+__global__ void kb_heads_kernel(const int32_t* __restrict__ scell, int64_t n, int64_t* __restrict__ head,
+                                int32_t* __restrict__ ztab, int64_t nz) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) head[t] = (t == 0 || scell[t] != scell[t - 1]) ? 1 : 0;
+    if (ztab)
+        for (int64_t i = t; i < nz; i += (int64_t)gridDim.x * blockDim.x) ztab[i] = 0;
 }
 
 // hs: exclusive scan of the heads (hs[n] = the number of distinct cells).
@@ -1356,7 +1360,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int32_t* rid = scell + n;                    // [n] sort values (the rows)
     int32_t* srow = rid + n;                     // [n] rows sorted by cell
     int32_t* row2u = cells;
-    int* fail_count = (int*)(misc + 1);
+    int* fail_count = (int*)(misc + 4);  // zeroed by knn_run's init kernel (or below when u == 1)
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     // 1. rows grouped by cell (stable radix sort on the cell index bits)
     int bits = 1;
@@ -1365,8 +1369,10 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     kb_iota_kernel<<<ng, 256, 0, st>>>(idx, n, N, cells, rid, ctx->d_err);
     int rc = ccg_sort_pairs_i32(ctx, cells, scell, rid, srow, n, bits, st);
     if (rc) return rc;
-    // 2. distinct cells: heads -> scan -> tables
-    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head);
+    // 2. distinct cells: heads -> scan -> tables (zeroed first: see kb_tables_kernel)
+    int32_t* ustart0 = srow + n;
+    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head, n_unique >= 0 ? ustart0 : nullptr,
+                                        2 * (int64_t)n_unique + 1);
     rc = ccg_scan_i64(ctx, head, head, n, st);
     if (rc) return rc;
     int u = n_unique;
@@ -1375,13 +1381,13 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
         CCG_HIP(hipMemcpyAsync(&hu, head + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
         u = (int)hu;
+        CCG_HIP(hipMemsetAsync(ustart0, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
     }
     const int kq = std::min(kmax, u - 1);
-    int32_t* ustart = srow + n;                  // [u + 1]
+    int32_t* ustart = ustart0;                   // [u + 1]
     int32_t* ucell = ustart + u + 1;             // [u]
     double* ud2 = urows + (size_t)u * d;         // [u][kq] certified squared distances
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
-    CCG_HIP(hipMemsetAsync(ustart, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
     kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, ucell, row2u, ctx->d_err);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     gather_rows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(pcs, N, d, ucell, u, urows);
@@ -1391,7 +1397,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
         if (rc) return rc;
     }
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
-    CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
+    if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
     kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
                                          fail_count);
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st);
