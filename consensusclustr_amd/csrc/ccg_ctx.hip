@@ -285,6 +285,36 @@ __global__ __launch_bounds__(SCAN_T) void scan_tiles(const int64_t* in, int64_t*
     if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = bsum[nb];
 }
 
+// Second pass for up to SCAN_DIRECT_MAX tiles: each block adds up the raw
+// sums of the tiles before it itself (<= 1024 loads), so the single-block
+// pass over the tile sums -- a launch on the critical path -- is skipped.
+#define SCAN_DIRECT_MAX 1024
+__global__ __launch_bounds__(SCAN_T) void scan_tiles_direct(const int64_t* in, int64_t* out, int64_t n,
+                                                            const int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    constexpr int E = SCAN_TILE / SCAN_T;
+    int64_t pre = 0;
+    for (int64_t b = threadIdx.x; b < blockIdx.x; b += SCAN_T) pre += bsum[b];
+    int64_t prefix;
+    block_excl_scan(pre, sh, &prefix);
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * E;
+    int64_t v[E];
+    int64_t s = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        v[e] = (base + e < n) ? in[base + e] : 0;
+        s += v[e];
+    }
+    int64_t tot;
+    int64_t ex = block_excl_scan(s, sh, &tot) + prefix;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (base + e < n) out[base + e] = ex;
+        ex += v[e];
+    }
+    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = prefix + tot;
+}
+
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
     if (n <= 0) {
         CCG_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), st));
@@ -294,6 +324,11 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipSt
     int64_t* bsum = (int64_t*)ccg_ws(ctx, WS_SCAN, sizeof(int64_t) * (nb + 1));
     if (!bsum) return CCG_ENOMEM;
     scan_tile_sums<<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
+    if (nb <= SCAN_DIRECT_MAX) {
+        scan_tiles_direct<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
+        CCG_HIP(hipGetLastError());
+        return CCG_OK;
+    }
     scan_block_sums<<<1, SCAN_T, 0, st>>>(bsum, nb);
     scan_tiles<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
     CCG_HIP(hipGetLastError());
