@@ -252,8 +252,14 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
 // Classes 0..2 in 21-bit fields (n < 2^21); class 3's rank is the node index
 // minus the other three.
 #define SNN_CLS_BITS 21
-__global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, int64_t* __restrict__ cls) {
+// (also zeroes the per-graph counts cnt[nk][n+1] and the overflow counters,
+// which the build tiers fill: one launch instead of two memsets)
+__global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, int64_t* __restrict__ cls,
+                                 int64_t* __restrict__ cnt, int nk, int* __restrict__ ov_count) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < 64) ov_count[j] = 0;
+    if (j <= n)
+        for (int t = 0; t < nk; ++t) cnt[(int64_t)t * (n + 1) + j] = 0;
     if (j >= n) return;
     const int64_t M = roff[j + 1] - roff[j];
     const int c = M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3));
@@ -1055,15 +1061,15 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     if (rc) return rc;
     // 3. build: sort tier -> hash tier -> block tier -> dense tier
     SnnRows rows{roff, rlen, nbr, wpk, cap};
-    CCG_HIP(hipMemsetAsync(ov_count, 0, sizeof(int) * 64, st));
-    CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * sp.nk * (n + 1), st));
+
     // size classes -> node lists (scan of packed one-hot class counts)
     CCG_REQUIRE(n < (1LL << SNN_CLS_BITS), "SNN: n must be below 2^%d", SNN_CLS_BITS);
     int64_t* cls = (int64_t*)ccg_ws(ctx, WS_SNN_H, sizeof(int64_t) * (n + 1 + 8) + sizeof(int) * 4 * n);
     if (!cls) return CCG_ENOMEM;
     int64_t* ccount = cls + (n + 1);
     int* lists = (int*)(ccount + 8);
-    snn_class_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(roff, n, cls);
+    snn_class_kernel<<<(unsigned)ccg_cdiv(std::max<int64_t>(n + 1, 64), 256), 256, 0, st>>>(roff, n, cls, cnt, sp.nk,
+                                                                                           ov_count);
     rc = ccg_scan_i64(ctx, cls, cls, n, st);
     if (rc) return rc;
     snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
