@@ -1052,9 +1052,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
             int64_t* cursor = hist + (NB + 1);
             int* perm = (int*)(cursor + (NB + 1));
             knn_bucket_count_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, hist);
-            rc = ccg_scan_i64(ctx, hist, hist, NB, st);
+            rc = ccg_scan_i64(ctx, hist, cursor, NB, st);  // the bucket starts, advanced by the scatter
             if (rc) return rc;
-            CCG_HIP(hipMemcpyAsync(cursor, hist, sizeof(int64_t) * (NB + 1), hipMemcpyDeviceToDevice, st));
             knn_bucket_scatter_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, n, d, bnd, cursor, perm);
             order_perm = perm;
         } else {
