@@ -1241,6 +1241,18 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
     if (t == 0) ustart[u] = (int)n;
 }
 
+// the distinct cells' rows, copied from the gathered (row-major) bootstrap
+// rows of each cell's first copy: coalesced, unlike a gather from the
+// column-major PCs
+__global__ void kb_urows_kernel(const double* __restrict__ rows, int d, int u, const int* __restrict__ ustart,
+                                const int* __restrict__ srow, double* __restrict__ urows) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)u * d) return;
+    const int64_t uid = t / d;
+    const int k = (int)(t - uid * d);
+    urows[t] = rows[(int64_t)srow[ustart[uid]] * d + k];
+}
+
 #define KB_GMAX 33  // cells of one merge group (the own cell + kq <= 32 neighbours)
 __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq, const int* __restrict__ uidx,
                                                         const double* __restrict__ ud2,
@@ -1389,7 +1401,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
     kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, ucell, row2u, ctx->d_err);
     // 3. the distinct cells' rows and their kq nearest distinct cells
-    gather_rows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(pcs, N, d, ucell, u, urows);
+    kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1) {
         rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true);
