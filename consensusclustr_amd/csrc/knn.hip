@@ -1211,7 +1211,7 @@ __global__ void kb_iota_kernel(const int32_t* __restrict__ idx, int64_t n, int64
 }
 
 // (cell, row) pairs sorted by cell (stable: each cell's rows ascending)
-// (also zeroes the 2u + 1 table words when u is known: ztab / nz)
+// (also zeroes the u + 1 words of ustart when u is known: ztab / nz)
 __global__ void kb_heads_kernel(const int32_t* __restrict__ scell, int64_t n, int64_t* __restrict__ head,
                                 int32_t* __restrict__ ztab, int64_t nz) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1223,20 +1223,17 @@ __global__ void kb_heads_kernel(const int32_t* __restrict__ scell, int64_t n, in
 // hs: exclusive scan of the heads (hs[n] = the number of distinct cells).
 // Distinct cell uid owns the sorted positions [ustart[uid], ustart[uid + 1]);
 // row2u maps a row to its uid.  If the caller's u is wrong the sticky error is
-// set and uids are clamped into [0, u) (tables zeroed beforehand), so every
+// set and uids are clamped into [0, u) (ustart zeroed beforehand), so every
 // later access stays in bounds; the outputs are then undefined.
 __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_t* __restrict__ srow, int64_t n,
                                  const int64_t* __restrict__ hs, int u, int* __restrict__ ustart,
-                                 int* __restrict__ ucell, int* __restrict__ row2u, int* __restrict__ err) {
+                                 int* __restrict__ row2u, int* __restrict__ err) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     if (t == 0 && hs[n] != u) atomicOr(err, CCG_DERR_KNN_UNIQUE);
     const bool head = t == 0 || scell[t] != scell[t - 1];
     const int uid = min((int)hs[t] - (head ? 0 : 1), u - 1);
-    if (head) {
-        ustart[uid] = (int)t;
-        ucell[uid] = scell[t];
-    }
+    if (head) ustart[uid] = (int)t;
     row2u[srow[t]] = uid;
     if (t == 0) ustart[u] = (int)n;
 }
@@ -1360,7 +1357,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     const int ucap = n_unique >= 0 ? n_unique : (int)std::min<int64_t>(n, N);
     // workspaces (the full-size fail list first, so the distinct-cell run never grows it)
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
-    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + 2 * (size_t)ucap + 1));
+    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + (size_t)ucap + 1));
     double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)ucap * (d + kmax) +
                                                       sizeof(int32_t) * (size_t)ucap * kmax + 64);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
@@ -1382,8 +1379,7 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     if (rc) return rc;
     // 2. distinct cells: heads -> scan -> tables (zeroed first: see kb_tables_kernel)
     int32_t* ustart0 = srow + n;
-    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head, n_unique >= 0 ? ustart0 : nullptr,
-                                        2 * (int64_t)n_unique + 1);
+    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head, n_unique >= 0 ? ustart0 : nullptr, (int64_t)n_unique + 1);
     rc = ccg_scan_i64(ctx, head, head, n, st);
     if (rc) return rc;
     int u = n_unique;
@@ -1392,14 +1388,13 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
         CCG_HIP(hipMemcpyAsync(&hu, head + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
         u = (int)hu;
-        CCG_HIP(hipMemsetAsync(ustart0, 0, sizeof(int32_t) * (2 * (size_t)u + 1), st));
+        CCG_HIP(hipMemsetAsync(ustart0, 0, sizeof(int32_t) * ((size_t)u + 1), st));
     }
     const int kq = std::min(kmax, u - 1);
     int32_t* ustart = ustart0;                   // [u + 1]
-    int32_t* ucell = ustart + u + 1;             // [u]
     double* ud2 = urows + (size_t)u * d;         // [u][kq] certified squared distances
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
-    kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, ucell, row2u, ctx->d_err);
+    kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, row2u, ctx->d_err);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows);
     ccg_knn_stats us = {0, 0};

@@ -126,7 +126,8 @@ int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
  * the bootstrap's distinct cells (duplicated cells are copies at distance 0;
  * about 59% of the rows are distinct at cfg3, so the search does ~0.35 of
  * the n^2 work), then expanded back to rows in (d2, row index) order.
- *   pcs      : N x d float64 COLUMN-major (device)
+ *   pcs      : N x d float64 COLUMN-major (device; rows must be pcs[idx, ] --
+ *              the distinct cells' coordinates are copied from rows)
  *   idx      : n int32 0-based cell indices (device; R's sample() - 1)
  *   n_unique : the number of distinct values in idx (host; R:
  *              length(unique(idx))), or -1 to count them on the device (one
