@@ -206,8 +206,21 @@ def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
     }
 
 
+def visible_gpus():
+    """Devices this process could use.  torch.cuda.device_count() does not
+    initialise the GPU on this image, so the launcher may call it before it
+    starts the ranks."""
+    import torch
+    return torch.cuda.device_count()
+
+
 def main():
     args = parse()
+    if not args.launcher_check and "WORLD_SIZE" not in os.environ:
+        have = visible_gpus()
+        if have < args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} requested but {have} GPU(s) are visible\n")
+            sys.exit(2)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.launcher_check:

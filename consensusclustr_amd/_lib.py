@@ -88,6 +88,7 @@ SIGNATURES = {
     "ccg_row_slabs": (_i, [_i64, _i, _p]),
     "ccg_rect_slabs": (_i, [_i64, _i, _p]),
     "ccg_boot_shard": (_i, [_i64, _i, _i, _p, _p]),
+    "ccg_allgather_plan": (_i, [_i, _p, _p, _p, _p, _p]),
     "ccg_group_open": (_i, [_p, _i, _p]),
     "ccg_group_unique_id": (_i, [_p]),
     "ccg_group_open_rank": (_i, [_i, _i, _i, _p, _p]),

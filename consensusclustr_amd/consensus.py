@@ -418,8 +418,8 @@ def null_test_pvalue(silhouette, null_scores):
     x = np.asarray(null_scores, np.float64)
     mu = math.fsum(x) / x.size
     sd = math.sqrt(math.fsum((x - mu) ** 2) / x.size)
-    if sd == 0.0:
-        return 0.0 if silhouette > mu else 1.0
+    if sd == 0.0:  # pnorm(q, mu, 0) is a point mass at mu: 1 for q >= mu
+        return 0.0 if silhouette >= mu else 1.0
     return 1.0 - 0.5 * math.erfc(-((silhouette - mu) / sd) / math.sqrt(2.0))
 
 

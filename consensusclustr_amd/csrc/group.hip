@@ -116,6 +116,29 @@ extern "C" int ccg_boot_shard(int64_t nboots, int G, int rank, int64_t* b0, int6
     return CCG_OK;
 }
 
+// The collective plan of group_allgather_rows, host only (no device, no RCCL):
+// offsets = exclusive prefix of the counts; equal counts -> one ncclAllGather;
+// unequal -> one ncclBroadcast per rank with rows to send, in rank order.
+extern "C" int ccg_allgather_plan(int nranks, const int64_t* counts, int64_t* offsets, int* equal, int* roots,
+                                  int* nroots) {
+    CCG_REQUIRE(nranks >= 1 && counts && offsets && equal && nroots, "ccg_allgather_plan: bad arguments");
+    offsets[0] = 0;
+    int eq = 1, nr = 0;
+    for (int r = 0; r < nranks; ++r) {
+        CCG_REQUIRE(counts[r] >= 0, "ccg_allgather_plan: negative count for rank %d", r);
+        offsets[r + 1] = offsets[r] + counts[r];
+        eq = eq && counts[r] == counts[0];
+    }
+    for (int r = 0; r < nranks; ++r)
+        if (!eq && counts[r] > 0) {
+            if (roots) roots[nr] = r;
+            ++nr;
+        }
+    *equal = eq;
+    *nroots = eq ? 0 : nr;
+    return CCG_OK;
+}
+
 // ------------------------------------------------------------ lifecycle --
 extern "C" int ccg_group_unique_id(uint8_t* id) {
     CCG_REQUIRE(id, "ccg_group_unique_id: NULL id");
@@ -232,12 +255,11 @@ extern "C" int ccg_group_synchronize(ccg_group* g) {
 static int group_allgather_rows(ccg_group* g, const void* const* src, const int64_t* counts, size_t row_bytes,
                                 void* const* dst) {
     std::vector<int64_t> off(g->nranks + 1, 0);
-    bool equal = true;
-    for (int r = 0; r < g->nranks; ++r) {
-        CCG_REQUIRE(counts[r] >= 0, "allgather: negative count for rank %d", r);
-        off[r + 1] = off[r] + counts[r];
-        equal = equal && counts[r] == counts[0];
-    }
+    std::vector<int> roots(g->nranks);
+    int eq = 0, nroots = 0;
+    int rc = ccg_allgather_plan(g->nranks, counts, off.data(), &eq, roots.data(), &nroots);
+    if (rc) return rc;
+    const bool equal = eq != 0;
     for (int l = 0; l < g->nlocal; ++l)
         CCG_REQUIRE(dst[l] && (src[l] || counts[g->rank0 + l] == 0), "allgather: NULL buffer on local device %d", l);
     if (off[g->nranks] == 0) return CCG_OK;
@@ -254,8 +276,8 @@ static int group_allgather_rows(ccg_group* g, const void* const* src, const int6
             }
             continue;
         }
-        for (int root = 0; root < g->nranks; ++root) {
-            if (counts[root] == 0) continue;
+        for (int t = 0; t < nroots; ++t) {
+            const int root = roots[t];
             char* recv = d + (size_t)off[root] * row_bytes;
             const void* send = root == me ? src[l] : recv;
             ncclResult_t r = ncclBroadcast(send, recv, (size_t)counts[root] * row_bytes, ncclUint8, root, g->comm[l],

@@ -259,6 +259,8 @@ class Engine:
         g = np.arange(G, dtype=np.int32) if genes is None else np.ascontiguousarray(genes, dtype=np.int32)
         c = np.arange(N, dtype=np.int32) if cells is None else np.ascontiguousarray(cells, dtype=np.int32)
         sf = np.ascontiguousarray(sf, dtype=np.float64)
+        if sf.size != N:  # ccg_pca reads N size factors, indexed by the global cell
+            raise ValueError(f"sf has {sf.size} entries; counts has {N} cells (pass one size factor per column)")
         x = np.empty((npc, c.size), np.float64)  # column-major nc x npc
         sdev = np.empty(npc, np.float64)
         check(self.lib.ccg_pca(self.ctx, _ptr(C), G, N, _ptr(sf), _ptr(g), g.size, _ptr(c), c.size, npc, _ptr(x),

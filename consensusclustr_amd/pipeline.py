@@ -21,6 +21,22 @@ from .consensus import (K_NUM, RES_RANGE, consensus_cluster, default_engine, nul
                         subset_pcs)
 
 
+def live_genes(counts, sf, genes, cells, chunk=256):
+    """The genes of `genes` (None = all) whose log1p(counts / sf) varies
+    across `cells`.  The reference re-selects deviance features for every
+    subset (R/consensusClust.R:290-298, variableFeatures=NULL in the
+    recursive call :562-566), which never picks a gene that is constant over
+    the subset; prcomp_irlba would fail on one (:368-379)."""
+    g = np.arange(counts.shape[0]) if genes is None else np.asarray(genes)
+    c = np.asarray(cells)
+    s = np.asarray(sf, np.float64)[c]
+    keep = np.zeros(g.size, bool)
+    for a in range(0, g.size, chunk):
+        y = np.log1p(counts[g[a:a + chunk]][:, c] / s[None, :])
+        keep[a:a + chunk] = (y.max(1) > y.min(1))
+    return g[keep].astype(np.int32)
+
+
 def _silhouette_mean(eng, pca, labels):
     codes = np.unique(np.asarray(labels), return_inverse=True)[1].astype(np.int32) + 1
     return float(eng.silhouette(np.asarray(pca, np.float64), codes[None, :])[0][0])
@@ -33,18 +49,32 @@ def consensusClust(counts, sizeFactors, variableFeatures=None, pcNum="find", pcV
     """consensusClust (R/consensusClust.R:122-632) from counts.
 
     counts: genes x cells; sizeFactors: per cell; variableFeatures: gene
-    indices (None = all genes).  Returns dict(assignments = list of str
+    indices (None = every gene that varies over the cells; subclusters always
+    drop genes constant over their cells).  sizeFactors: one per column of
+    counts (subset_inputs must return a full-length array too).  Returns dict(assignments = list of str
     labels, nested "c_sub" under iterate=True as :576, pcNum, silhouette,
     pval)."""
-    eng = engine or default_engine()
     counts = np.asarray(counts, np.float64)
     all_cells = np.arange(counts.shape[1]) if cells is None else np.asarray(cells)
     N = all_cells.size
     sf = np.asarray(sizeFactors, np.float64)
-    genes = None if variableFeatures is None else np.asarray(variableFeatures, np.int32)
+    if sf.size != counts.shape[1]:
+        raise ValueError(f"sizeFactors has {sf.size} entries for {counts.shape[1]} cells (one per column of counts)")
+    # explicit top-level features are used as given (a constant one fails the
+    # PCA, as in the reference); the reference's own selection (None, and every
+    # subcluster) never picks a gene that is constant over the cells
+    if variableFeatures is None or depth > 1:
+        genes = live_genes(counts, sf, variableFeatures, all_cells)
+    else:
+        genes = np.asarray(variableFeatures, np.int32)
+    eng = engine or default_engine()
     if nboots <= 1:
         raise NotImplementedError("nboots <= 1 (the un-bootstrapped path, :498-511) is not mirrored")
-    # :337-382 -- PCs of these cells on the variable genes (a failed PCA -> one cluster)
+    # :337-382 -- PCs of these cells on the variable genes (a failed PCA -> one cluster;
+    # prcomp_irlba cannot return more components than genes or cells)
+    npc = 50 if (pcNum == "find" or int(pcNum) > 30) else int(pcNum)
+    if genes.size <= npc or N <= npc:
+        return {"assignments": ["1"] * N, "pcNum": None, "silhouette": None, "pval": None}
     try:
         pca, _sdev = subset_pcs(counts, sf, genes, all_cells.astype(np.int32), pcNum, pcVar, eng)
     except CcgError as e:
@@ -87,8 +117,10 @@ def consensusClust(counts, sizeFactors, variableFeatures=None, pcNum="find", pcV
             sub_sf, sub_genes = sf, genes
             if subset_inputs is not None:
                 sub_sf, sub_genes = subset_inputs(all_cells[idx])
+            # the reference's recursive call (:562-566) does not forward
+            # silhouetteThresh, alpha, minSize or seed: subclusters use the defaults
             sub = consensusClust(counts, sub_sf, sub_genes, "find", pcVar, nboots, bootSize, minStability,
-                                 clusterFun, resRange, kNum, silhouetteThresh, alpha, minSize, mode, seed, True,
+                                 clusterFun, resRange, kNum, 0.45, 0.05, 50, mode, 123, True,
                                  null_pcs, depth + 1, eng, subset_inputs, all_cells[idx])["assignments"]
             if len(set(sub)) > 1:  # :575-577
                 for t, i in enumerate(idx):

@@ -42,6 +42,21 @@ def boot_shard(nboots, G, rank):
     return b0.value, b1.value
 
 
+def allgather_plan(counts):
+    """The all-gather's collective plan (ccg_allgather_plan): (offsets,
+    equal, roots) -- one ncclAllGather when every rank sends the same number
+    of rows, else one ncclBroadcast per root in `roots` (rank order), root r
+    sending its block at offsets[r]."""
+    G = len(counts)
+    cnt = np.ascontiguousarray(counts, dtype=np.int64)
+    off = np.zeros(G + 1, np.int64)
+    roots = np.zeros(G, np.int32)
+    eq, nr = ctypes.c_int(), ctypes.c_int()
+    check(_lib.load().ccg_allgather_plan(G, cnt.ctypes.data_as(_vp), off.ctypes.data_as(_vp), ctypes.byref(eq),
+                                         roots.ctypes.data_as(_vp), ctypes.byref(nr)))
+    return [int(o) for o in off], bool(eq.value), [int(r) for r in roots[:nr.value]]
+
+
 def slab_offset(N, r0):
     """Packed-triangle offset of row r0 (rows hold j = i+1..N-1)."""
     return r0 * N - r0 * (r0 + 1) // 2

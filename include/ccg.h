@@ -374,6 +374,14 @@ int ccg_rect_slabs(int64_t N, int G, int64_t* cuts);
 /* Bootstrap block [*b0, *b1) of `rank` among G (sizes differ by <= 1). */
 int ccg_boot_shard(int64_t nboots, int G, int rank, int64_t* b0, int64_t* b1);
 
+/* Host-only plan of the all-gathers (ccg_allgather_columns and the row
+ * all-gather of ccg_consensus_knn_sharded_dev): offsets[0..nranks] = the
+ * exclusive prefix of counts (rank r's rows land at offsets[r]); *equal = 1
+ * when every count is equal (one ncclAllGather, *nroots = 0), else 0 with
+ * roots[0..*nroots) = the ranks with counts > 0 in rank order, each the root
+ * of one ncclBroadcast of its block (all in one RCCL group).  roots may be
+ * NULL (count only). */
+int ccg_allgather_plan(int nranks, const int64_t* counts, int64_t* offsets, int* equal, int* roots, int* nroots);
 /* One process, several devices (ncclCommInitAll over `devices`). */
 int ccg_group_open(const int* devices, int ndev, ccg_group** out);
 /* One process per device: rank 0 calls ccg_group_unique_id, the caller

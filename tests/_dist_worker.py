@@ -34,26 +34,38 @@ def main(rank, world, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from consensusclustr_amd.sharding import boot_shard, exchange_group_id, row_slabs, slab_pairs
+    from consensusclustr_amd.sharding import allgather_plan, boot_shard, exchange_group_id, row_slabs, slab_pairs
     import oracle as O
     # the RCCL id every rank passes to ccg_group_open_rank comes from rank 0
     gid = exchange_group_id(make_id=lambda: np.random.default_rng(99).integers(0, 256, 128, dtype=np.uint8))
     ids = [None] * world
     dist.all_gather_object(ids, gid)
     assert all(x == ids[0] for x in ids) and len(gid) == 128
-    N, nboots = 300, 10
+    N = 300
+    nboots = 10 if world != 2 else 12  # world 3: unequal blocks (broadcast plan); world 2: equal (all-gather)
     rng = np.random.default_rng(7)
     full = rng.integers(0, 6, (nboots, N)).astype(np.uint8)  # the assignment columns of all bootstraps
     spans = [boot_shard(nboots, world, r) for r in range(world)]
     b0, b1 = spans[rank]
     counts = [s[1] - s[0] for s in spans]
-    # rank-ordered all-gather of unequal blocks (pad to the largest, trim)
-    bmax = max(counts)
-    mine = np.zeros((bmax, N), np.uint8)
-    mine[:b1 - b0] = full[b0:b1]
-    parts = [torch.zeros((bmax, N), dtype=torch.uint8) for _ in range(world)]
-    dist.all_gather(parts, torch.from_numpy(mine))
-    A = np.concatenate([parts[r].numpy()[:counts[r]] for r in range(world)])
+    # the all-gather as libccg's group issues it over RCCL (ccg_allgather_plan):
+    # each rank writes its block in place into the full matrix, then one
+    # all-gather (equal counts) or one broadcast per root (unequal counts)
+    off, equal, roots = allgather_plan(counts)
+    assert off[rank] == b0 and off[rank + 1] == b1
+    A_t = torch.zeros((nboots, N), dtype=torch.uint8)
+    A_t[b0:b1] = torch.from_numpy(full[b0:b1])
+    if equal:
+        parts = list(A_t.split(counts[0]))
+        dist.all_gather(parts, A_t[b0:b1].clone())
+        A_t = torch.cat(parts)
+    else:
+        assert roots == [r for r in range(world) if counts[r] > 0]
+        for root in roots:
+            blk = A_t[off[root]:off[root + 1]].contiguous()
+            dist.broadcast(blk, src=root)
+            A_t[off[root]:off[root + 1]] = blk
+    A = A_t.numpy()
     assert np.array_equal(A, full), "all-gathered columns differ from the single-process matrix"
     cuts = row_slabs(N, world)
     r0, r1 = cuts[rank], cuts[rank + 1]

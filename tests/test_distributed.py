@@ -33,3 +33,15 @@ def test_bench_launcher_starts_the_requested_ranks():
     out = json.loads(line)
     assert out["n_gpus"] == 2
     assert sorted(x[0] for x in out["ranks_seen"]) == [0, 1]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N exits non-zero at once, with a message, when fewer
+    than N devices are visible (here: none)."""
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 2
+    assert "requested but" in r.stderr

@@ -213,3 +213,61 @@ def test_choose_pc_num_rule():
     assert choose_pc_num(sdev, 0.2) == 5
     assert choose_pc_num(sdev, 0.5) == 1 + int(np.flatnonzero(np.cumsum(sdev) / sdev.sum() > 0.5)[0])
     assert choose_pc_num(sdev, 0.5) == 18  # 33/65 = 0.508 at component 18
+
+
+def test_live_genes_drops_genes_constant_over_the_subset():
+    """Subclusters re-select features (R/consensusClust.R:290-298, :562-566):
+    genes constant over the subset's cells never reach the PCA."""
+    from consensusclustr_amd.pipeline import live_genes
+    rng = np.random.default_rng(0)
+    counts = rng.poisson(3.0, (6, 40)).astype(np.float64)
+    counts[1] = 0.0                 # all-zero gene
+    counts[4, :20] = 0.0            # zero only over the first 20 cells
+    sf = np.ones(40)
+    assert live_genes(counts, sf, None, np.arange(40)).tolist() == [0, 2, 3, 4, 5]
+    assert live_genes(counts, sf, None, np.arange(20)).tolist() == [0, 2, 3, 5]
+    assert live_genes(counts, sf, np.array([1, 4, 5]), np.arange(20)).tolist() == [5]
+
+
+def test_consensus_clust_rejects_subset_length_size_factors():
+    from consensusclustr_amd.pipeline import consensusClust
+    import pytest
+    with pytest.raises(ValueError, match="one per column"):
+        consensusClust(np.ones((5, 30)), np.ones(10), engine=object())
+
+
+def test_null_test_pvalue_sd_zero_is_point_mass():
+    """1 - pnorm(q, mu, 0): pnorm is 1 for q >= mu (R's point mass)."""
+    from consensusclustr_amd.consensus import null_test_pvalue
+    assert null_test_pvalue(0.3, [0.3, 0.3, 0.3]) == 0.0
+    assert null_test_pvalue(0.31, [0.3, 0.3]) == 0.0
+    assert null_test_pvalue(0.29, [0.3, 0.3]) == 1.0
+
+
+@pytest.mark.parametrize("G", [1, 3, 8])
+def test_allgather_plan_unequal_and_equal_counts(G):
+    """ccg_allgather_plan: the collective group_allgather_rows issues (one
+    ncclAllGather for equal blocks, one ncclBroadcast per non-empty root
+    otherwise), checked on CPU for every rank count the node can have."""
+    from consensusclustr_amd.sharding import allgather_plan
+    rng = np.random.default_rng(G)
+    for nboots in (0, G, 3 * G, 1000, 1000 + G - 1, G - 1 if G > 1 else 0):
+        counts = [boot_shard(nboots, G, r)[1] - boot_shard(nboots, G, r)[0] for r in range(G)]
+        off, equal, roots = allgather_plan(counts)
+        assert off == [0] + np.cumsum(counts).tolist()
+        assert equal == (len(set(counts)) == 1)
+        assert roots == ([] if equal else [r for r in range(G) if counts[r] > 0])
+    counts = rng.integers(0, 5, G).tolist()
+    counts[0] = 0
+    off, equal, roots = allgather_plan(counts)
+    assert off[-1] == sum(counts) and 0 not in roots
+    # simulate the broadcasts: every rank ends with every block at its offset
+    full = rng.integers(0, 9, (sum(counts), 4))
+    for me in range(G):
+        buf = np.zeros_like(full)
+        buf[off[me]:off[me + 1]] = full[off[me]:off[me + 1]]
+        for root in (roots if not equal else range(G)):
+            buf[off[root]:off[root + 1]] = full[off[root]:off[root + 1]]
+        assert np.array_equal(buf, full)
+    with pytest.raises(Exception):
+        allgather_plan([1, -1])
