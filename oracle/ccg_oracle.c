@@ -585,6 +585,91 @@ int orc_cocluster_rows(const void* A, int label_bits, int64_t N, int64_t B, cons
     return ORC_OK;
 }
 
+/* ---- consensus kNN of selected rows, straight from A ------------------ */
+/* dbscan::kNN(jaccardDist, k)$id (R/consensusClust.R:421-425) for the rows
+ * rows[0..nr) only, without the N x N distance: per row i the full co/both row
+ * (the customDist counts of :411-418), D_ij = 1 - (double)((float)co/(float)U)
+ * (fp32 quotient, :416), d[i,i] = Inf, stable order() (ties by ascending j),
+ * first k ids.  nan_row[t] = 1 if row i has a pair with U = 0 (dbscan stop()s
+ * on anyNA).  A: B x N column-major codes, uint8/uint16, 0 = NA. */
+int orc_consensus_knn_rows(const void* A, int label_bits, int64_t N, int64_t B, const int32_t* rows, int64_t nr,
+                           int k, int32_t* out_idx, int32_t* nan_row, int nthreads) {
+    if (N < 2 || B < 1 || k < 1 || k > N - 1 || (label_bits != 8 && label_bits != 16)) return ORC_EINVAL;
+    for (int64_t t = 0; t < nr; ++t)
+        if (rows[t] < 0 || rows[t] >= N) return ORC_EINVAL;
+    set_threads(nthreads);
+    const uint8_t* A8 = (const uint8_t*)A;
+    const uint16_t* A16 = (const uint16_t*)A;
+    int err = 0;
+#pragma omp parallel
+    {
+        uint32_t* cr = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)N);
+        uint32_t* br = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)N);
+        double* bd = (double*)malloc(sizeof(double) * (size_t)k);
+        int32_t* bi = (int32_t*)malloc(sizeof(int32_t) * (size_t)k);
+        if (!cr || !br || !bd || !bi) {
+#pragma omp atomic write
+            err = 1;
+        } else {
+#pragma omp for schedule(dynamic, 1)
+            for (int64_t t = 0; t < nr; ++t) {
+                const int64_t i = rows[t];
+                memset(cr, 0, sizeof(uint32_t) * (size_t)N);
+                memset(br, 0, sizeof(uint32_t) * (size_t)N);
+                for (int64_t b = 0; b < B; ++b) {
+                    if (label_bits == 8) {
+                        const uint8_t* col = A8 + b * N;
+                        const uint8_t a = col[i];
+                        if (!a) continue;
+                        for (int64_t j = 0; j < N; ++j) {
+                            cr[j] += col[j] == a;
+                            br[j] += col[j] != 0;
+                        }
+                    } else {
+                        const uint16_t* col = A16 + b * N;
+                        const uint16_t a = col[i];
+                        if (!a) continue;
+                        for (int64_t j = 0; j < N; ++j) {
+                            cr[j] += col[j] == a;
+                            br[j] += col[j] != 0;
+                        }
+                    }
+                }
+                int cnt = 0, nan = 0;
+                for (int64_t j = 0; j < N; ++j) {
+                    double s;
+                    if (j == i) {
+                        s = INFINITY;
+                    } else if (br[j] == 0) {
+                        nan = 1;
+                        continue;
+                    } else {
+                        float overlap = (float)cr[j], U = (float)br[j];
+                        volatile float q = overlap / U;
+                        s = 1.0 - (double)q;
+                    }
+                    if (cnt == k && !(s < bd[k - 1])) continue;
+                    int p = (cnt < k) ? cnt++ : k - 1;
+                    while (p > 0 && s < bd[p - 1]) {
+                        bd[p] = bd[p - 1];
+                        bi[p] = bi[p - 1];
+                        --p;
+                    }
+                    bd[p] = s;
+                    bi[p] = (int32_t)j;
+                }
+                for (int q = 0; q < k; ++q) out_idx[t * k + q] = q < cnt ? bi[q] : -1;
+                if (nan_row) nan_row[t] = nan;
+            }
+        }
+        free(cr);
+        free(br);
+        free(bd);
+        free(bi);
+    }
+    return err ? ORC_ENOMEM : ORC_OK;
+}
+
 /* ---- determineHierachy block means (R/consensusClust.R:699-721) -------- */
 /* dist packed as orc_cocluster.  f: N cluster positions 0..K-1 in
  * unique(assignments) order.  out (K x K, row-major): diagonal 0 (the matrix

@@ -17,7 +17,7 @@ __all__ = [
     "cocluster", "consensus_knn", "robust_choice", "consensus_choice",
     "py_knn", "py_snn", "py_cocluster", "packed_index", "RES_RANGE", "K_NUM",
     "robust_score", "consensus_score", "knn_queries", "cocluster_rows",
-    "block_means", "contingency", "pairwise_rand_ratio",
+    "block_means", "contingency", "pairwise_rand_ratio", "consensus_knn_rows",
 ]
 
 # consensusClust defaults, R/consensusClust.R:126-127
@@ -49,9 +49,11 @@ def lib():
         L.orc_cocluster_rows.argtypes = [p, i32, i64, i64, p, i64, p, p, i32]
         L.orc_block_means.argtypes = [p, i64, p, i32, p, i32]
         L.orc_contingency.argtypes = [p, i32, i64, i64, p, i32, i32, p]
+        L.orc_consensus_knn_rows.argtypes = [p, i32, i64, i64, p, i64, i32, p, p, i32]
         for f in (L.orc_gather_rows, L.orc_knn, L.orc_snn, L.orc_silhouette,
                   L.orc_mapback, L.orc_cocluster, L.orc_consensus_knn,
-                  L.orc_knn_queries, L.orc_cocluster_rows, L.orc_block_means, L.orc_contingency):
+                  L.orc_knn_queries, L.orc_cocluster_rows, L.orc_block_means, L.orc_contingency,
+                  L.orc_consensus_knn_rows):
             f.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -113,6 +115,23 @@ def cocluster_rows(A, rows, nthreads=0):
     _check(lib().orc_cocluster_rows(_ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(r), r.size, _ptr(co), _ptr(both),
                                     nthreads), "cocluster_rows")
     return co, both
+
+
+def consensus_knn_rows(A, rows, k, nthreads=0):
+    """dbscan::kNN(jaccardDist, k)$id rows (R/consensusClust.R:421-425) for
+    the selected rows only, from the assignment matrix (orc_consensus_knn_rows).
+
+    A: B x N uint8/uint16 codes (0 = NA).  Returns (idx (len(rows), k) int32
+    0-based, nan_row (len(rows),) bool: the row has a never co-sampled pair)."""
+    A = np.ascontiguousarray(A)
+    assert A.dtype in (np.uint8, np.uint16)
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    B, N = A.shape
+    out = np.empty((r.size, k), np.int32)
+    nan = np.empty(r.size, np.int32)
+    _check(lib().orc_consensus_knn_rows(_ptr(A), 8 * A.dtype.itemsize, N, B, _ptr(r), r.size, k, _ptr(out),
+                                        _ptr(nan), nthreads), "consensus_knn_rows")
+    return out, nan.astype(bool)
 
 
 def snn(knn_idx, k, type="number"):

@@ -175,3 +175,23 @@ def test_contingency_vs_numpy():
         for p in range(4):
             for a in range(7):
                 assert tab[b, p, a] == np.sum((f == p) & (A[b] == a))
+
+
+def test_consensus_knn_rows_matches_the_full_distance_path():
+    """orc_consensus_knn_rows (from A, rows only) equals orc_cocluster ->
+    orc_consensus_knn (the N x N dist) on the same rows, ties included."""
+    rng = np.random.default_rng(12)
+    for B, N, C in ((30, 257, 3), (400, 600, 9)):
+        A = rng.integers(1, C + 1, (B, N)).astype(np.uint8)
+        A[rng.random((B, N)) < 0.3] = 0
+        Ai = A.astype(np.int32)
+        Ai[Ai == 0] = -1
+        full = O.consensus_knn(O.cocluster(Ai)["dist"], N, 20)
+        rows = np.array([0, 1, N // 2, N - 1], np.int32)
+        got, nan = O.consensus_knn_rows(A, rows, 20)
+        assert not nan.any()
+        assert np.array_equal(got, full[rows])
+    A = np.zeros((3, 10), np.uint8)
+    A[:, :5] = 1
+    _, nan = O.consensus_knn_rows(A, np.array([0, 7], np.int32), 3)
+    assert nan.tolist() == [True, True]
