@@ -12,6 +12,19 @@
 # What moves to the GPU: findKNN, neighborsToSNNGraph, approxSilhouette,
 # parDist(customDist), dbscan::kNN(dist), determineHierachy's block means
 # and the counting of pairwiseRand.
+#
+# RNG streams.  In the reference each bootstrap's stream feeds, in order,
+# sample() (:394), then for every (k, res) findKNN and cluster_leiden
+# (:653-658).  Up to BiocNeighbors 1.x findKNN draws too (its KMKNN index
+# runs kmeans); from 1.99 (knncolle) it draws nothing.  The drop-in keeps the
+# sequence: pass 1 draws every bootstrap's sample() in its own stream and
+# notes the stream's state; the GPU searches the kNN of a batch of
+# bootstraps at once (split over the group's GPUs); pass 2 re-enters each
+# stream at that state, re-draws sample() (the same indices) and, per
+# (k, res), replays findKNN's draws (.ccg_replay_findknn_draws) before
+# cluster_leiden -- so Leiden reads the stream where a live reference run
+# would.  The replay follows stats::kmeans and BiocNeighbors 1.x buildKmknn
+# as published; neither is installed here, so it is unpinned (DESIGN.md).
 
 .ccg <- new.env(parent = emptyenv())
 
@@ -44,10 +57,38 @@ ccgEngine <- function(devices = getOption("ccg.devices", 0L)) {
   }
 }
 
+# neighborsToSNNGraph's graph: make_graph + weights + simplify(edge.attr.comb
+# = "first") as bluster builds it (the engine's edges are already unique,
+# i < j, so simplify only fixes igraph's internal edge order)
 .ccg_graph <- function(e, n) {
   g <- igraph::make_graph(rbind(e$from, e$to), n = n, directed = FALSE)
   igraph::E(g)$weight <- e$weight
-  g
+  igraph::simplify(g, edge.attr.comb = "first")
+}
+
+# TRUE when the installed BiocNeighbors draws random numbers inside findKNN
+# (versions before 1.99: the KMKNN index is built by kmeans on every call).
+.ccg_kmknn_draws <- function() {
+  if (is.null(.ccg$kmknn)) {
+    .ccg$kmknn <- requireNamespace("BiocNeighbors", quietly = TRUE) &&
+      utils::packageVersion("BiocNeighbors") < "1.99.0"
+  }
+  .ccg$kmknn
+}
+
+# The random draws of one findKNN(x, k) call under BiocNeighbors 1.x, without
+# the index: buildKmknn runs kmeans(x, ceiling(sqrt(nrow(x)))), whose only
+# random step picks the initial centres -- sample.int(m, k), and when those
+# rows repeat (bootstrap copies) sample.int(nrow(unique(x)), k) again.
+# nunique() returns nrow(unique(x)) (computed at most once per bootstrap).
+.ccg_replay_findknn_draws <- function(x, nunique) {
+  if (!.ccg_kmknn_draws()) return(invisible(NULL))
+  m <- nrow(x)
+  k <- ceiling(sqrt(m))
+  if (k >= m) return(invisible(NULL))
+  ctr <- x[sample.int(m, k), , drop = FALSE]
+  if (any(duplicated(ctr))) sample.int(nunique(), k)
+  invisible(NULL)
 }
 
 #' mean(approxSilhouette(x, l)[, 3], na.rm = TRUE) for every clustering in
@@ -59,18 +100,37 @@ ccgSilhouetteMeans <- function(x, labs, eng = ccgEngine()) {
 }
 
 #' Drop-in for getClustAssignments (R/consensusClust.R:650-692): one exact
-#' kNN at max(kNum) (the k = 10, 15 lists are its prefixes), the SNN graphs
-#' on the GPU, host clustering in the same (k, res) order, one batched
-#' silhouette over all candidate clusterings, the same scoring rules and
-#' rank(ties.method = "first") selection, first-copy map-back.
+#' kNN at max(kNum) (the k = 10, 15 lists are its prefixes) over the
+#' bootstrap's distinct cells, the SNN graphs on the GPU, host clustering in
+#' the same (k, res) order with findKNN's RNG draws replayed before each
+#' clustering, one batched silhouette over all candidate clusterings, the same
+#' scoring rules and rank(ties.method = "first") selection, first-copy
+#' map-back.  pca is the bootstrap matrix pca[sample(...), ] with its
+#' duplicated row names (:394); knn, when given, is its n x max(kNum)
+#' neighbour matrix already searched in a batch (ccgConsensusCore).
 getClustAssignments <- function(pca, clusterFun = "leiden", resRange, kNum, mode = "robust", cellOrder, seed,
-                                minSize = 0, ...) {
+                                minSize = 0, knn = NULL, ...) {
   eng <- ccgEngine()
-  knn <- .Call(C_ccg_r_knn_rows, eng, pca, as.integer(max(kNum)))
+  if (is.null(knn)) {
+    # rows -> distinct cells (copies share a row name), so the search runs
+    # over the distinct cells and expands back to rows
+    first <- !duplicated(rownames(pca))
+    cell <- match(rownames(pca), rownames(pca)[first])
+    knn <- .Call(C_ccg_r_knn_boot, eng, pca[first, , drop = FALSE], matrix(cell, ncol = 1L),
+                 as.integer(max(kNum)))[[1L]]
+  }
+  nu <- NULL
+  nunique <- function() {
+    if (is.null(nu)) nu <<- nrow(unique(pca))
+    nu
+  }
   labs <- list()
   for (k in kNum) {
     g <- .ccg_graph(.Call(C_ccg_r_snn, eng, knn, as.integer(k), 0L), nrow(pca))
-    for (res in resRange) labs[[length(labs) + 1L]] <- .ccg_cluster_graph(g, clusterFun, res)
+    for (res in resRange) {
+      .ccg_replay_findknn_draws(pca, nunique)  # the reference's findKNN for this (k, res), :656
+      labs[[length(labs) + 1L]] <- .ccg_cluster_graph(g, clusterFun, res)
+    }
   }
   mapback <- function(l) setNames(l, rownames(pca))[match(cellOrder, rownames(pca))]
   if (mode == "robust") {
@@ -129,7 +189,7 @@ ccgStabilityMatrix <- function(clustAssignments, finalAssignments, eng = ccgEngi
 #' over the engine: call it from consensusClust in place of those lines.
 #' Returns list(assignments, clustAssignments).
 ccgConsensusCore <- function(pca, nboots, bootSize, clusterFun, resRange, kNum, mode, seed, minStability,
-                             BPPARAM = BiocParallel::SerialParam(RNGseed = seed)) {
+                             BPPARAM = BiocParallel::SerialParam(RNGseed = seed), batch = 32L) {
   eng <- ccgEngine()
   if (!inherits(BPPARAM, "SerialParam")) {
     # HIP cannot run in forked workers; the same RNG streams come from a
@@ -137,12 +197,35 @@ ccgConsensusCore <- function(pca, nboots, bootSize, clusterFun, resRange, kNum, 
     BPPARAM <- BiocParallel::SerialParam(RNGseed = BiocParallel::bpRNGseed(BPPARAM))
   }
   cells <- rownames(pca)
-  clustAssignments <- BiocParallel::bplapply(seq_len(nboots), function(boot) {
-    tryCatch(getClustAssignments(pca[sample(cells, bootSize * nrow(pca), replace = TRUE), ],
-                                 resRange = resRange, kNum = kNum, clusterFun = clusterFun, cellOrder = cells,
-                                 mode = mode, seed = seed),
-             error = function(e) rep(1, length(cells)))
+  n <- bootSize * nrow(pca)
+  # pass 1 (:391-394): every bootstrap's sample() in its own stream, and the
+  # stream's state on entry (the global state is restored after bplapply)
+  draws <- BiocParallel::bplapply(seq_len(nboots), function(boot) {
+    st <- get(".Random.seed", envir = globalenv())
+    list(idx = match(sample(cells, n, replace = TRUE), cells), seed = st)
   }, BPPARAM = BPPARAM)
+  after <- get0(".Random.seed", envir = globalenv(), inherits = FALSE)
+  clustAssignments <- vector("list", nboots)
+  for (b0 in seq(1L, nboots, by = batch)) {
+    bs <- b0:min(nboots, b0 + batch - 1L)
+    # the batch's kNN in one engine call: the distinct-cell search per
+    # bootstrap, bootstraps split over the GPUs of a device group
+    boot <- vapply(draws[bs], function(d) d$idx, integer(length(draws[[1L]]$idx)))
+    knns <- tryCatch(.Call(C_ccg_r_knn_boot, eng, pca, matrix(boot, ncol = length(bs)), as.integer(max(kNum))),
+                     error = function(e) NULL)
+    # pass 2: re-enter each stream, re-draw sample() (the same indices: the
+    # stream then stands where the reference's getClustAssignments starts)
+    for (t in seq_along(bs)) {
+      b <- bs[t]
+      assign(".Random.seed", draws[[b]]$seed, envir = globalenv())
+      clustAssignments[[b]] <- tryCatch({
+        s <- sample(cells, n, replace = TRUE)
+        getClustAssignments(pca[s, ], resRange = resRange, kNum = kNum, clusterFun = clusterFun,
+                            cellOrder = cells, mode = mode, seed = seed, knn = if (is.null(knns)) NULL else knns[[t]])
+      }, error = function(e) rep(1, length(cells)))
+    }
+  }
+  if (is.null(after)) rm(".Random.seed", envir = globalenv()) else assign(".Random.seed", after, envir = globalenv())
   clustAssignments <- do.call(cbind, clustAssignments)
   rownames(clustAssignments) <- cells
   clustAssignments[is.na(clustAssignments)] <- -1

@@ -102,6 +102,7 @@ SIGNATURES = {
     "ccg_group_cocluster": (_i, [_p, _p, _i, _i64, _i64, _p, _p, _p]),
     "ccg_group_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
     "ccg_group_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
+    "ccg_sort_pairs_dev": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p]),
     "ccg_timing_enable": (_i, [_p, _i]),
     "ccg_timing_read": (_i, [_p, _i, _p, _p]),
 }

@@ -96,14 +96,16 @@ def mapback(boot_idx, labels_boot, N):
 # ------------------------------------------------------- bootstrap path --
 def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RANGE, kNum=K_NUM,
                         mode="robust", cellOrder=None, seed=123, minSize=0, engine=None,
-                        return_details=False):
+                        return_details=False, knn=None):
     """Mirror of getClustAssignments (R/consensusClust.R:650-692).
 
     pca: N x d PC matrix of all cells; the clustered matrix is pca[boot_idx]
     (the reference receives pca[sample(...), ] with duplicated row names,
     :394).  boot_idx=None clusters pca itself (the nboots == 1 path, :500).
     cellOrder: only the identity order of pca's rows is supported (the
-    reference always passes rownames(pca)).
+    reference always passes rownames(pca)).  knn: this bootstrap's n x kmax
+    neighbour rows when the caller already searched them in a batch
+    (consensus_cluster); None searches here.
     Returns length-N int32 labels (robust) or N x (|kNum|*|resRange|) (granular),
     -1 for cells not in the bootstrap.
     """
@@ -115,8 +117,11 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
     boot_idx = np.arange(N, dtype=np.int32) if boot_idx is None else np.asarray(boot_idx, np.int32)
     n = boot_idx.size
     kmax = max(kNum)
-    knn, _ = eng.knn_boot(pca, boot_idx, kmax=kmax, want_dist=False)
-    knn = knn[0]
+    if knn is None:
+        knn, _ = eng.knn_boot(pca, boot_idx, kmax=kmax, want_dist=False)
+        knn = knn[0]
+    elif knn.shape != (n, kmax):
+        raise ValueError(f"knn must be {n} x {kmax}, got {knn.shape}")
     fn = _cluster_fn(clusterFun)
     labels = []
     for k in kNum:  # :653-654, k outer, resolution inner
@@ -171,11 +176,31 @@ def assignment_matrix(columns):
     return A.astype(np.uint8 if A.max() <= 255 else np.uint16)
 
 
+def bootstrap_knn_batches(pca, boots, kmax, engine=None, group=None, batch=32):
+    """The kNN of every bootstrap, searched in batches of `batch` bootstraps
+    per call (ccg_knn_boot, or ccg_group_knn_boot splitting each batch over
+    the group's GPUs).  Yields (b0, knn[b0:b1]) with knn (b1-b0, n, kmax)."""
+    eng = engine or default_engine()
+    search = group.knn_boot if group is not None else eng.knn_boot
+    for b0 in range(0, boots.shape[0], batch):
+        b1 = min(boots.shape[0], b0 + batch)
+        try:
+            knn, _ = search(pca, boots[b0:b1], kmax=kmax, want_dist=False)
+        except Exception:  # one bootstrap at a time, so a failure hits only its own column (:397-399)
+            knn = None
+        yield b0, b1, knn
+
+
 def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRange=RES_RANGE, kNum=K_NUM,
                       mode="robust", seed=123, engine=None, boot_indices=None, return_matrix=None,
-                      merge=False, minStability=0.175):
+                      merge=False, minStability=0.175, group=None):
     """The bootstrap + consensus core of consensusClust (R/consensusClust.R:388-456).
 
+    The bootstrap loop runs as the R drop-in does (R/ccg.R ccgConsensusCore):
+    every bootstrap's indices are drawn first, the kNN of a batch of
+    bootstraps is one engine call (a DeviceGroup `group` splits each batch
+    over its GPUs), then per bootstrap the SNN graphs, host clustering and
+    one batched silhouette.
     Returns dict(assignments=<chosen consensus labels>, clustAssignments=<B x N
     uint8/uint16>, scores=<consensus scores>, choice=<index>, candidates,
     consensus_knn=<N x max(kNum)>) and, when return_matrix (default: N <=
@@ -191,12 +216,14 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
     boots = bootstrap_indices(N, nboots, bootSize, seed) if boot_indices is None else np.asarray(boot_indices)
     fn = _cluster_fn(clusterFun)
     columns = []
-    for b in range(boots.shape[0]):  # bplapply(1:nboots, ...), :391-400
-        try:
-            columns.append(getClustAssignments(pca, boots[b], clusterFun=fn, resRange=resRange, kNum=kNum,
-                                               mode=mode, seed=seed, engine=eng))
-        except Exception:  # tryCatch(..., error = rep(1, N)), :397-399
-            columns.append(np.ones(N, np.int32))
+    for b0, b1, knn in bootstrap_knn_batches(pca, boots, max(kNum), eng, group):  # bplapply(1:nboots), :391-400
+        for b in range(b0, b1):
+            try:
+                columns.append(getClustAssignments(pca, boots[b], clusterFun=fn, resRange=resRange, kNum=kNum,
+                                                   mode=mode, seed=seed, engine=eng,
+                                                   knn=None if knn is None else knn[b - b0]))
+            except Exception:  # tryCatch(..., error = rep(1, N)), :397-399
+                columns.append(np.ones(N, np.int32))
     A = assignment_matrix(columns)
     out = {"clustAssignments": A}
     if return_matrix is None:

@@ -585,12 +585,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             // otherwise, per half-tile of 8 registers: flush first if its
             // candidates could overflow a queue, then enqueue branch-free
             static_assert(QC >= 8, "queue must hold a half tile");
+#if defined(KNN_EXP_NOMAX)  // tools only: MFMA + staging alone (results wrong)
+            asm volatile("; exp keep acc" ::"v"(acc));
+            if (false) {
+#else
             float vmax = acc[0];
 #pragma unroll
             for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
             KST(1);
             KSC(10);
+#if defined(KNN_EXP_NOCAND)  // tools only: no candidate is ever queued (results wrong)
+            if (__any(vmax > T)) asm volatile("; exp cand" ::"v"(vmax));
+            if (false) {
+#else
             if (__any(vmax > T)) {
+#endif
+#endif
                 KSC(7);
                 // branch-free: a write at slot qc is kept only if qc advances
 #pragma unroll
@@ -1092,6 +1102,10 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         }
 #undef CCG_SCREEN16
         ccg_timer_stop(ctx, t_scr, st);
+#ifdef KNN_EXP_SCREEN_ONLY  // tools only: time the screen alone (outputs undefined)
+        ccg_timer_stop(ctx, t_all, st);
+        return CCG_OK;
+#endif
     }
     const int64_t* seg_off = sg ? sg->seg_off : nullptr;
     const int nseg = sg ? sg->nseg : 1;
@@ -1402,6 +1416,10 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
         rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true);
         if (rc) return rc;
     }
+#ifdef KNN_EXP_SCREEN_ONLY
+    ccg_timer_stop(ctx, t_all, st);
+    return CCG_OK;
+#endif
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
     if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
     kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,

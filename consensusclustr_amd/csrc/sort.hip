@@ -1,20 +1,175 @@
-// Device radix sort of (int32 key, int32 value) pairs for libccg (hipCUB).
-// Used by the SNN host-list build: a stable sort of the kNN entries by
-// neighbour keeps every host list in ascending host order.
-#include <hipcub/hipcub.hpp>
-
+// Stable LSD radix sort of (int32 key, int32 value) pairs, hand-written for
+// gfx950.  Used where the per-bootstrap path groups entries by a bounded key:
+// the distinct-cell kNN groups bootstrap rows by cell (keys < N, knn.hip) and
+// the SNN build lists every node's hosts (keys < n, snn.hip); both need the
+// equal keys in input order (rows / hosts ascending).
+//
+// One pass per digit of <= 8 bits (the key bits split evenly, so 17-bit keys
+// take three 6/6/5-bit passes), three launches per pass:
+//   rs_hist    : per tile of RS_TILE pairs, the digit histogram (LDS atomics),
+//                written digit-major: cnt[digit * ntiles + tile];
+//   rs_scan    : one block scans that matrix exclusively -> every (digit, tile)
+//                pair's first output position (digit-major = stable);
+//   rs_scatter : each tile ranks its pairs stably -- a wave takes a contiguous
+//                run of 64 * RS_IPT pairs, lanes along consecutive pairs, peers
+//                of equal digit found by one ballot per digit bit, running
+//                per-wave digit counts in LDS -- and writes them to their
+//                positions.
+// Keys outside [0, 2^key_bits) are the caller's contract (only the low
+// key_bits bits are looked at).
 #include "ccg_internal.h"
+
+#define RS_THREADS 256
+#define RS_WAVES (RS_THREADS / 64)
+#define RS_IPT 16                       // pairs per thread per tile
+#define RS_TILE (RS_THREADS * RS_IPT)   // 4096 pairs per tile
+#define RS_MAXBITS 8
+
+__global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift,
+                                                      int bits, int ntiles, int* __restrict__ cnt) {
+    __shared__ int h[1 << RS_MAXBITS];
+    const int nb = 1 << bits;
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) h[t] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int i = 0; i < RS_IPT; ++i) {
+        const int64_t e = base + (int64_t)i * RS_THREADS + threadIdx.x;
+        if (e < n) atomicAdd(&h[((unsigned)keys[e] >> shift) & (nb - 1)], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
+}
+
+// Exclusive scan of m ints in place by one block (m <= 2^8 * ntiles).
+__global__ __launch_bounds__(1024) void rs_scan(int* __restrict__ cnt, int m) {
+    __shared__ int part[1024];
+    const int per = (m + 1023) / 1024;
+    const int a = threadIdx.x * per, b = min(m, a + per);
+    int s = 0;
+    for (int i = a; i < b; ++i) s += cnt[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    // Hillis-Steele over the 1024 partial sums
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (int i = a; i < b; ++i) {
+        const int v = cnt[i];
+        cnt[i] = run;
+        run += v;
+    }
+}
+
+__device__ __forceinline__ unsigned long long rs_lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restrict__ kin,
+                                                         const int32_t* __restrict__ vin, int64_t n, int shift,
+                                                         int bits, int ntiles, const int* __restrict__ off,
+                                                         int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
+    __shared__ int wcnt[RS_WAVES][1 << RS_MAXBITS];  // per-wave running digit counts, then prefixes
+    __shared__ int goff[1 << RS_MAXBITS];
+    const int nb = 1 << bits;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int t = threadIdx.x; t < RS_WAVES * nb; t += RS_THREADS) wcnt[t / nb][t % nb] = 0;
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = off[(int64_t)t * ntiles + blockIdx.x];
+    __syncthreads();
+    // wave w's run: pairs [base, base + 64 * RS_IPT), item i at base + 64 i + lane
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE + (int64_t)w * 64 * RS_IPT;
+    int kk[RS_IPT], vv[RS_IPT], rk[RS_IPT];
+    const unsigned long long lt = rs_lanemask_lt();
+#pragma unroll
+    for (int i = 0; i < RS_IPT; ++i) {
+        const int64_t e = base + 64 * i + lane;
+        const bool ok = e < n;
+        kk[i] = ok ? kin[e] : 0;
+        vv[i] = ok ? vin[e] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < RS_IPT; ++i) {
+        const bool ok = base + 64 * i + lane < n;
+        const unsigned dg = ((unsigned)kk[i] >> shift) & (unsigned)(nb - 1);
+        unsigned long long peers = __ballot(ok);
+        for (int b = 0; b < bits; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const int before = ok ? wcnt[w][dg] : 0;  // every lane reads before the leader's update below
+        __builtin_amdgcn_wave_barrier();
+        rk[i] = before + __popcll(peers & lt);
+        if (ok && (peers & lt) == 0) wcnt[w][dg] = before + __popcll(peers);  // the lowest peer updates
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // per digit: exclusive prefix over the waves (tile order = wave order)
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) {
+        int s = 0;
+#pragma unroll
+        for (int ww = 0; ww < RS_WAVES; ++ww) {
+            const int c = wcnt[ww][t];
+            wcnt[ww][t] = s;
+            s += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RS_IPT; ++i) {
+        if (base + 64 * i + lane >= n) continue;
+        const unsigned dg = ((unsigned)kk[i] >> shift) & (unsigned)(nb - 1);
+        const int pos = goff[dg] + wcnt[w][dg] + rk[i];
+        kout[pos] = kk[i];
+        vout[pos] = vv[i];
+    }
+}
 
 int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
                        int32_t* vals_out, int64_t n, int key_bits, hipStream_t st) {
     CCG_REQUIRE(n >= 0 && n < (1LL << 31), "ccg_sort_pairs_i32: n out of range");
+    CCG_REQUIRE(key_bits >= 0 && key_bits <= 31, "ccg_sort_pairs_i32: key_bits out of range");
     if (n == 0) return CCG_OK;
-    size_t tmp = 0;
-    CCG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0,
-                                               key_bits, st));
-    void* ws = ccg_ws(ctx, WS_SORT, tmp + 256);
+    const int ntiles = (int)ccg_cdiv(n, RS_TILE);
+    if (key_bits == 0) {  // one digit value: the input order
+        CCG_HIP(hipMemcpyAsync(keys_out, keys_in, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+        CCG_HIP(hipMemcpyAsync(vals_out, vals_in, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+        return CCG_OK;
+    }
+    const int npass = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
+    const size_t cnt_ints = (size_t)(1 << RS_MAXBITS) * ntiles;
+    char* ws = (char*)ccg_ws(ctx, WS_SORT, sizeof(int) * cnt_ints + sizeof(int32_t) * 2 * (size_t)n + 256);
     if (!ws) return CCG_ENOMEM;
-    CCG_HIP(hipcub::DeviceRadixSort::SortPairs(ws, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, key_bits,
-                                               st));
+    int* cnt = (int*)ws;
+    int32_t* tk = (int32_t*)(ws + ccg_cdiv(sizeof(int) * cnt_ints, 256) * 256);
+    int32_t* tv = tk + n;
+    // pass p writes out when (npass - 1 - p) is even, so the last pass lands in out
+    const int32_t* ck = keys_in;
+    const int32_t* cv = vals_in;
+    int shift = 0;
+    for (int p = 0; p < npass; ++p) {
+        const int bits = (key_bits - shift + (npass - p) - 1) / (npass - p);  // the remaining bits split evenly
+        int32_t* ok = ((npass - 1 - p) % 2 == 0) ? keys_out : tk;
+        int32_t* ov = ((npass - 1 - p) % 2 == 0) ? vals_out : tv;
+        rs_hist<<<ntiles, RS_THREADS, 0, st>>>(ck, n, shift, bits, ntiles, cnt);
+        rs_scan<<<1, 1024, 0, st>>>(cnt, (1 << bits) * ntiles);
+        rs_scatter<<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov);
+        ck = ok;
+        cv = ov;
+        shift += bits;
+    }
+    CCG_HIP(hipGetLastError());
     return CCG_OK;
+}
+
+extern "C" int ccg_sort_pairs_dev(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
+                                  int32_t* vals_out, int64_t n, int key_bits, void* stream) {
+    CCG_REQUIRE(ctx && (n == 0 || (keys_in && keys_out && vals_in && vals_out)), "ccg_sort_pairs_dev: NULL argument");
+    CCG_REQUIRE(keys_in != keys_out && vals_in != vals_out, "ccg_sort_pairs_dev: in-place sorting is not supported");
+    return ccg_sort_pairs_i32(ctx, keys_in, keys_out, vals_in, vals_out, n, key_bits, ccg_pick_stream(ctx, stream));
 }

@@ -376,6 +376,12 @@ class Engine:
         check(self.lib.ccg_consensus_knn_dev(self.ctx, _ptr(co), _ptr(both), N, k, _ptr(out_idx),
                                              _ptr(d_flag), _stream()))
 
+    def sort_pairs_t(self, keys, vals, keys_out, vals_out, key_bits):
+        """Stable radix sort of int32 (key, value) tensors by the low key_bits
+        bits of the keys (ccg_sort_pairs_dev)."""
+        check(self.lib.ccg_sort_pairs_dev(self.ctx, _ptr(keys), _ptr(keys_out), _ptr(vals), _ptr(vals_out),
+                                          keys.numel(), key_bits, _stream()))
+
     def consensus_knn_assign_t(self, A, k, r0, r1, out_idx, d_flag):
         """Rows [r0, r1) of the consensus kNN from the (B, N) assignment tensor."""
         import torch

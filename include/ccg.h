@@ -427,6 +427,15 @@ int ccg_group_consensus_knn_assign(ccg_group* g, const void* A, int label_bits, 
 int ccg_group_knn_boot(ccg_group* g, const double* pcs, int64_t N, int d, const int32_t* boot_idx, int64_t n,
                        int nb, int kmax, int32_t* out_idx, double* out_dist, ccg_knn_stats* stats);
 
+/* --------------------------------------------------------- utilities -- */
+/* Stable radix sort of n (int32 key, int32 value) pairs by the low key_bits
+ * bits of the keys (device pointers; outputs must not alias the inputs): the
+ * grouping step of the distinct-cell kNN (rows by cell) and of the SNN host
+ * lists (kNN entries by neighbour), exported for testing and reuse.
+ * Requires 0 <= key_bits <= 31, n < 2^31. */
+int ccg_sort_pairs_dev(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
+                       int32_t* vals_out, int64_t n, int key_bits, void* stream);
+
 /* ------------------------------------------------------ kernel timing -- */
 /* Device time of selected kernels, measured with hipEvents recorded on the
  * stream each kernel is launched on (used by bench.py for the live roofline).

@@ -159,7 +159,11 @@ SEXP ccg_r_abi_version(void) { return Rf_ScalarInteger(ccg_abi_version()); }
 /* ctx|group.  pca: N x d double matrix; boot: n x nb integer matrix of
  * 1-based row indices (one column per bootstrap, R's sample(...) draws);
  * returns a list of nb n x kmax 1-based neighbour matrices (bootstrap-row
- * indices), attribute "fallback" = rows that took the exact path. */
+ * indices), attribute "fallback" = rows that took the exact path.  Each
+ * bootstrap is searched over its distinct cells and expanded back to rows
+ * (ccg_knn_boot); a group splits the bootstraps over its GPUs
+ * (ccg_group_knn_boot).  getClustAssignments alone passes its distinct rows
+ * as pca and the row -> cell map as boot. */
 SEXP ccg_r_knn_boot(SEXP e, SEXP pca, SEXP boot, SEXP kmax) {
     ccg_ctx* ctx;
     ccg_group* grp;
@@ -178,22 +182,6 @@ SEXP ccg_r_knn_boot(SEXP e, SEXP pca, SEXP boot, SEXP kmax) {
     Rf_setAttrib(out, Rf_install("fallback"), Rf_ScalarReal((double)st.fallback));
     UNPROTECT(1);
     return out;
-}
-
-/* kNN among the rows of one matrix (getClustAssignments receives the
- * bootstrap matrix pca[sample(...), ] itself, :394): identity gather. */
-SEXP ccg_r_knn_rows(SEXP e, SEXP x, SEXP kmax) {
-    ccg_ctx* ctx;
-    ccg_group* grp;
-    engine_of(e, &ctx, &grp);
-    const int64_t n = Rf_nrows(x);
-    const int d = Rf_ncols(x), k = Rf_asInteger(kmax);
-    int32_t* bi = (int32_t*)R_alloc((size_t)n, sizeof(int32_t));
-    for (int64_t i = 0; i < n; ++i) bi[i] = (int32_t)i;
-    int32_t* idx = (int32_t*)R_alloc((size_t)n * k, sizeof(int32_t));
-    ccg_knn_stats st;
-    CALL("ccg_knn_boot", ccg_knn_boot(ctx, REAL(x), n, d, bi, n, 1, k, idx, NULL, &st));
-    return knn_matrix(idx, n, k);
 }
 
 /* iterate=TRUE subclusters / null simulations: list of n_s x d_s matrices,
@@ -454,7 +442,6 @@ static const R_CallMethodDef call_methods[] = {
     {"ccg_r_close", (DL_FUNC)&ccg_r_close, 1},
     {"ccg_r_abi_version", (DL_FUNC)&ccg_r_abi_version, 0},
     {"ccg_r_knn_boot", (DL_FUNC)&ccg_r_knn_boot, 4},
-    {"ccg_r_knn_rows", (DL_FUNC)&ccg_r_knn_rows, 3},
     {"ccg_r_knn_segments", (DL_FUNC)&ccg_r_knn_segments, 3},
     {"ccg_r_snn", (DL_FUNC)&ccg_r_snn, 4},
     {"ccg_r_silhouette", (DL_FUNC)&ccg_r_silhouette, 3},

@@ -327,3 +327,23 @@ def test_snn_host_flavour_grows_row_reservation(engine):
         engine.snn_reserve(0)
     for x, y in zip(a, O.snn(idx[0], 20, "number")):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("n,bits", [(1, 5), (4095, 17), (4097, 3), (90000, 17), (1_800_000, 17), (70001, 30),
+                                    (5000, 0)])
+def test_sort_pairs_is_a_stable_radix_sort(engine, n, bits):
+    """ccg_sort_pairs_dev (the hand-written LSD radix sort behind the
+    distinct-cell grouping and the SNN host lists) equals numpy's stable
+    argsort on the low key_bits bits, duplicates kept in input order."""
+    import torch
+    rng = np.random.default_rng(n + bits)
+    hi = 1 << bits if bits else 1
+    keys = rng.integers(0, min(hi, max(2, n // 3)), n).astype(np.int32)  # many equal keys
+    vals = rng.permutation(n).astype(np.int32)
+    kt, vt = torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda()
+    ko, vo = torch.empty_like(kt), torch.empty_like(vt)
+    engine.sort_pairs_t(kt, vt, ko, vo, bits)
+    torch.cuda.synchronize()
+    o = np.argsort(keys & (hi - 1), kind="stable")
+    assert np.array_equal(ko.cpu().numpy(), keys[o])
+    assert np.array_equal(vo.cpu().numpy(), vals[o])

@@ -89,11 +89,22 @@ def test_getClustAssignments_matches_oracle_pipeline(engine, pca, mode):
             assert det["choice"] == choice
 
 
-def test_consensus_cluster_matches_oracle_pipeline(engine, pca):
+@pytest.mark.parametrize("via", ["ctx", "group"])
+def test_consensus_cluster_matches_oracle_pipeline(engine, pca, via):
+    """The R drop-in's loop (R/ccg.R ccgConsensusCore): every bootstrap drawn
+    first, batched kNN over bootstraps (through a device group: split over
+    its GPUs, ccg_group_knn_boot), then SNN + host clustering + one batched
+    silhouette per bootstrap."""
     from consensusclustr_amd.consensus import assignment_matrix, consensus_cluster
+    from consensusclustr_amd.sharding import DeviceGroup
     boots = _boots()
-    got = consensus_cluster(pca, clusterFun=components, resRange=RES, kNum=KNUM, engine=engine,
-                            boot_indices=boots, return_matrix=True)
+    grp = DeviceGroup.open([0]) if via == "group" else None
+    try:
+        got = consensus_cluster(pca, clusterFun=components, resRange=RES, kNum=KNUM, engine=engine,
+                                boot_indices=boots, return_matrix=True, group=grp)
+    finally:
+        if grp is not None:
+            grp.close()
     # oracle: the bootstrap columns, co-clustering, consensus kNN + SNN rank, scoring
     cols = [oracle_get_clust_assignments(pca, boots[b], "robust")[0] for b in range(NBOOTS)]
     A = assignment_matrix(cols)

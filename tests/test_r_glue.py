@@ -76,3 +76,23 @@ def test_r_code_covers_the_replaced_seams():
                "ccgClusterDistance", "ccgStabilityMatrix", "ccgSilhouetteMeans", "ccgNullStatistics",
                "ccgSubsetPCs"):
         assert re.search(rf"^{fn} <- function\(", code, re.M), fn
+
+
+def test_r_bootstrap_loop_is_batched_and_keeps_the_rng_sequence():
+    """ccgConsensusCore draws every bootstrap first (one bplapply pass, the
+    stream state kept), searches the kNN of a batch of bootstraps in one
+    ccg_r_knn_boot call (a group splits it over GPUs), then re-enters each
+    stream; getClustAssignments replays findKNN's draws before every
+    clustering and builds bluster's simplified graph (R/consensusClust.R:391-400,
+    :650-692)."""
+    code = open(RCODE).read()
+    core = code[code.index("ccgConsensusCore <- function("):code.index("ccgNullStatistics <- function(")]
+    assert core.count("bplapply(seq_len(nboots)") == 1
+    assert ".Random.seed" in core and "draws[[b]]$seed" in core
+    assert "C_ccg_r_knn_boot" in core and "knn = if (is.null(knns))" in core
+    gca = code[code.index("getClustAssignments <- function("):code.index("#' kNN(jaccardDist, k)$id")]
+    assert "C_ccg_r_knn_boot" in gca and "C_ccg_r_knn_rows" not in code
+    loop = gca[gca.index("for (res in resRange)"):]
+    assert loop.index(".ccg_replay_findknn_draws") < loop.index(".ccg_cluster_graph")
+    assert 'simplify(g, edge.attr.comb = "first")' in code
+    assert 'packageVersion("BiocNeighbors") < "1.99.0"' in code
