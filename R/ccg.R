@@ -316,8 +316,15 @@ ccgSubsetPCs <- function(counts, sizeFactors, genes, cells = seq_len(ncol(counts
   find <- identical(pcNum, "find") || pcNum > 30
   k <- if (find) 50L else as.integer(pcNum)
   if (is.logical(genes)) genes <- which(genes)
-  p <- .Call(C_ccg_r_pca, eng, as.matrix(counts) + 0, as.numeric(sizeFactors), as.integer(genes),
-             as.integer(cells), k)
+  p <- if (inherits(counts, "dgCMatrix")) {
+    # sparse counts stay sparse: the slots go to the GPU, which forms only the
+    # selected genes x cells (R/consensusClust.R:273-288)
+    .Call(C_ccg_r_pca_csc, eng, as.numeric(counts@x), counts@i, counts@p, nrow(counts),
+          as.numeric(sizeFactors), as.integer(genes), as.integer(cells), k)
+  } else {
+    .Call(C_ccg_r_pca, eng, as.matrix(counts) + 0, as.numeric(sizeFactors), as.integer(genes),
+          as.integer(cells), k)
+  }
   if (find) k <- max(which(cumsum(p$sdev[1:50]) / sum(p$sdev[1:50]) > pcVar)[1], 5)
   x <- p$x[, seq_len(k), drop = FALSE]
   rownames(x) <- colnames(counts)[cells]

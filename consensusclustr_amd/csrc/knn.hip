@@ -139,6 +139,9 @@ static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 
 #ifndef KNN_QCAP
 #define KNN_QCAP 8          // per-lane insertion queue slots (flush before a half tile that could overflow)
 #endif
+#ifndef KNN_PAIR
+#define KNN_PAIR 0          // two tiles per step (two MFMA chains in flight)
+#endif
 #define KNN_NORM_SHIFT 15   // the query's norm-dimension value 2^15 (exact in fp16)
 #define KNN_PAD_NORM (-65504.0f)  // padding rows: below every real value (|v| < 1.6e9 < 2^31)
 
@@ -418,8 +421,11 @@ __device__ __forceinline__ void knn_wait_vmcnt() {
     else static_assert(N == 0, "unsupported vmcnt");
 }
 
+#ifndef KNN_WPE
+#define KNN_WPE 3           // screen waves per SIMD the register budget is sized for
+#endif
 template <int KSTEPS, int KP, int QC = KNN_QCAP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void knn_screen16_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) void knn_screen16_kernel(
     const uint4* __restrict__ img, int n, int nchunks, int d, int* __restrict__ cand_idx,
     float* __restrict__ cand_thr, const int4* __restrict__ blk) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
@@ -553,19 +559,97 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         KST(6);
         if (k + KNN_NBUF - 1 < nck) KNN_STAGE_GLDS((k + KNN_NBUF - 1) % KNN_NBUF, chunk_at(k + KNN_NBUF - 1));
         KST(0);
-#pragma nounroll  // unrolling the tiles multiplies live registers
-        for (int tau = 0; tau < KNN_CHUNK / 32; ++tau) {
-            const int row = tau * 32 + col;
-            h8 ah[KSTEPS], al[KSTEPS];
+        // After the MFMA chain of a tile (accumulator ACC_, first ref RB_):
+        // self / padding masking, the tile maximum, and -- when some lane's
+        // value beats its threshold -- the branch-free enqueue (per half-tile
+        // of 8 registers: flush first if its candidates could overflow a
+        // queue).  After a flush both halves move to the union threshold;
+        // between flushes T only rises.
+#if defined(KNN_EXP_NOMAX)  // tools only: MFMA + staging alone (results wrong)
+#define KNN_TILE_TEST(ACC_) asm volatile("; exp keep acc" ::"v"(ACC_)); if (false)
+#elif defined(KNN_EXP_NOCAND)  // tools only: no candidate is ever queued (results wrong)
+#define KNN_TILE_TEST(ACC_)                                                                 \
+    float vmax = ACC_[0];                                                                   \
+    _Pragma("unroll") for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, ACC_[reg]);     \
+    if (__any(vmax > T)) asm volatile("; exp cand" ::"v"(vmax));                            \
+    if (false)
+#else
+#define KNN_TILE_TEST(ACC_)                                                                 \
+    float vmax = ACC_[0];                                                                   \
+    _Pragma("unroll") for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, ACC_[reg]);     \
+    KST(1);                                                                                 \
+    KSC(10);                                                                                \
+    if (__any(vmax > T))
+#endif
+#define KNN_TILE_POST(ACC_, RB_)                                                            \
+    do {                                                                                    \
+        const int rbase = (RB_);                                                            \
+        if (rbase == q0 || rbase + 32 > qhi) { /* diagonal tile (self) or padding refs */   \
+            _Pragma("unroll") for (int reg = 0; reg < 16; ++reg) {                          \
+                const int r = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;                   \
+                if (r == q || r >= qhi) ACC_[reg] = -INFINITY;                              \
+            }                                                                               \
+        }                                                                                   \
+        KNN_TILE_TEST(ACC_) {                                                               \
+            KSC(7);                                                                         \
+            _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                              \
+                int c8 = 0;                                                                 \
+                _Pragma("unroll") for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) c8 += ACC_[reg] > T ? 1 : 0; \
+                KST(2);                                                                     \
+                if (__any(qc + c8 > QC)) KNN_FLUSH();                                       \
+                KST(3);                                                                     \
+                _Pragma("unroll") for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {         \
+                    const float v = ACC_[reg];                                              \
+                    qbw[qc * 64 + lane] =                                                   \
+                        make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h); \
+                    qc += v > T ? 1 : 0;                                                    \
+                }                                                                           \
+            }                                                                               \
+            KST(2);                                                                         \
+        }                                                                                   \
+        if (tdirty) {                                                                       \
+            T = union_kth<KP>(lv);                                                          \
+            tdirty = false;                                                                 \
+            KST(4);                                                                         \
+        }                                                                                   \
+    } while (0)
+        static_assert(QC >= 8, "queue must hold a half tile");
+#define KNN_LOAD_A(AH_, AL_, ROW_)                                                                  \
+    _Pragma("unroll") for (int s = 0; s < KSTEPS; ++s) {                                            \
+        uint4 a_ = *reinterpret_cast<const uint4*>(                                                 \
+            lds(b) + (ROW_) * ROWB + swz_chunk<KSTEPS>((ROW_), h * 2 * KSTEPS + s) * 16);           \
+        uint4 b_ = *reinterpret_cast<const uint4*>(                                                 \
+            lds(b) + (ROW_) * ROWB + swz_chunk<KSTEPS>((ROW_), h * 2 * KSTEPS + KSTEPS + s) * 16);  \
+        AH_[s] = *reinterpret_cast<h8*>(&a_);                                                       \
+        AL_[s] = *reinterpret_cast<h8*>(&b_);                                                       \
+    }
+#if KNN_PAIR
+        // two tiles per step: two independent MFMA chains, the second tile's
+        // chain in flight while the first tile's values are tested
+#pragma nounroll
+        for (int tau = 0; tau < KNN_CHUNK / 32; tau += 2) {
+            h8 ah0[KSTEPS], al0[KSTEPS], ah1[KSTEPS], al1[KSTEPS];
+            KNN_LOAD_A(ah0, al0, tau * 32 + col);
+            KNN_LOAD_A(ah1, al1, tau * 32 + 32 + col);
+            f32x16 acc0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            f32x16 acc1 = acc0;
 #pragma unroll
             for (int s = 0; s < KSTEPS; ++s) {
-                uint4 a = *reinterpret_cast<const uint4*>(
-                    lds(b) + row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + s) * 16);
-                uint4 bb = *reinterpret_cast<const uint4*>(
-                    lds(b) + row * ROWB + swz_chunk<KSTEPS>(row, h * 2 * KSTEPS + KSTEPS + s) * 16);
-                ah[s] = *reinterpret_cast<h8*>(&a);
-                al[s] = *reinterpret_cast<h8*>(&bb);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0[s], qh[s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1[s], qh[s], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0[s], ql[s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1[s], ql[s], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0[s], qh[s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1[s], qh[s], acc1, 0, 0, 0);
             }
+            KNN_TILE_POST(acc0, c * KNN_CHUNK + tau * 32);
+            KNN_TILE_POST(acc1, c * KNN_CHUNK + tau * 32 + 32);
+        }
+#else
+#pragma nounroll  // unrolling the tiles multiplies live registers
+        for (int tau = 0; tau < KNN_CHUNK / 32; ++tau) {
+            h8 ah[KSTEPS], al[KSTEPS];
+            KNN_LOAD_A(ah, al, tau * 32 + col);
             f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KSTEPS; ++s) {
@@ -573,62 +657,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], ql[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], qh[s], acc, 0, 0, 0);
             }
-            const int rbase = c * KNN_CHUNK + tau * 32;
-            if (rbase == q0 || rbase + 32 > qhi) {  // diagonal tile (self) or padding refs (wave-uniform)
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const int r = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    if (r == q || r >= qhi) acc[reg] = -INFINITY;
-                }
-            }
-            // a tile no lane's value beats costs one max-reduce and compare;
-            // otherwise, per half-tile of 8 registers: flush first if its
-            // candidates could overflow a queue, then enqueue branch-free
-            static_assert(QC >= 8, "queue must hold a half tile");
-#if defined(KNN_EXP_NOMAX)  // tools only: MFMA + staging alone (results wrong)
-            asm volatile("; exp keep acc" ::"v"(acc));
-            if (false) {
-#else
-            float vmax = acc[0];
-#pragma unroll
-            for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, acc[reg]);
-            KST(1);
-            KSC(10);
-#if defined(KNN_EXP_NOCAND)  // tools only: no candidate is ever queued (results wrong)
-            if (__any(vmax > T)) asm volatile("; exp cand" ::"v"(vmax));
-            if (false) {
-#else
-            if (__any(vmax > T)) {
-#endif
-#endif
-                KSC(7);
-                // branch-free: a write at slot qc is kept only if qc advances
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    int c8 = 0;
-#pragma unroll
-                    for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) c8 += acc[reg] > T ? 1 : 0;
-                    KST(2);
-                    if (__any(qc + c8 > QC)) KNN_FLUSH();
-                    KST(3);
-#pragma unroll
-                    for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {
-                        const float v = acc[reg];
-                        qbw[qc * 64 + lane] =
-                            make_uint2(__float_as_uint(v), rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h);
-                        qc += v > T ? 1 : 0;
-                    }
-                }
-                KST(2);
-            }
-            // After a flush (here, with the tile's accumulators dead) both halves
-            // move to the union threshold; between flushes T only rises.
-            if (tdirty) {
-                T = union_kth<KP>(lv);
-                tdirty = false;
-                KST(4);
-            }
+            KNN_TILE_POST(acc, c * KNN_CHUNK + tau * 32);
         }
+#endif
+#undef KNN_LOAD_A
+#undef KNN_TILE_POST
+#undef KNN_TILE_TEST
     }
     KST(1);
     KNN_FLUSH();

@@ -25,69 +25,116 @@
 
 // ------------------------------------------------------------ DGEMM --
 // C[m][n] = alpha * sum_k A(m, k) B(k, n) (+ beta C), A(m, k) = A[m*sam + k*sak],
-// B(k, n) = B[k*sbk + n*sbn], C row-major with ldc.  64 x 64 tile per 256
-// threads (4 x 4 outputs each), K staged through LDS in steps of 16.
-#define PG_T 64
-#define PG_K 16
-__global__ __launch_bounds__(256) void pca_dgemm_kernel(int64_t M, int64_t N, int64_t K, const double* __restrict__ A,
-                                                        int64_t sam, int64_t sak, const double* __restrict__ B,
-                                                        int64_t sbk, int64_t sbn, double* __restrict__ C,
-                                                        int64_t ldc, double alpha, double beta) {
-    __shared__ double As[PG_K][PG_T + 1];
-    __shared__ double Bs[PG_K][PG_T + 1];
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int64_t m0 = (int64_t)blockIdx.y * PG_T, n0 = (int64_t)blockIdx.x * PG_T;
-    double acc[4][4] = {};
-    for (int64_t k0 = 0; k0 < K; k0 += PG_K) {
-        // 1024 elements of each tile, 4 per thread; the fastest index follows
-        // the operand's unit stride where it has one
-        for (int e = threadIdx.x; e < PG_K * PG_T; e += 256) {
-            int kk, mm;
-            if (sam == 1) { mm = e % PG_T; kk = e / PG_T; } else { kk = e % PG_K; mm = e / PG_K; }
-            const int64_t gm = m0 + mm, gk = k0 + kk;
-            As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.0;
-            int kb, nn;
-            if (sbn == 1) { nn = e % PG_T; kb = e / PG_T; } else { kb = e % PG_K; nn = e / PG_K; }
-            const int64_t gn = n0 + nn, gkb = k0 + kb;
-            Bs[kb][nn] = (gn < N && gkb < K) ? B[gkb * sbk + gn * sbn] : 0.0;
+// B(k, n) = B[k*sbk + n*sbn], C row-major with ldc, on the fp64 matrix core
+// (v_mfma_f64_16x16x4f64).  A 64 x 64 tile per 256 threads: each wave owns a
+// 32 x 32 quarter (2 x 2 MFMA tiles); K is staged through LDS 16 at a time,
+// the next stage's panels in registers while the current one is consumed.
+// Lane (g, j) = (lane >> 4, lane & 15) feeds A[m = j][k = g] and
+// B[k = g][n = j] of a 16 x 16 x 4 step, and holds D[m = g + 4 i][n = j] in
+// accumulator i.  sym: C is symmetric (A(m, k) = B(k, m)): only the tiles on
+// or above the diagonal are computed, pca_mirror_kernel copies the rest.
+#define PM_T 64
+#define PM_K 16
+#define PM_LD (PM_T + 2)  // LDS row pad: the 16 lanes of a fragment read hit distinct banks
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void pca_mfma_gemm_kernel(int64_t M, int64_t N, int64_t K,
+                                                            const double* __restrict__ A, int64_t sam, int64_t sak,
+                                                            const double* __restrict__ B, int64_t sbk, int64_t sbn,
+                                                            double* __restrict__ C, int64_t ldc, double alpha,
+                                                            double beta, int sym) {
+    __shared__ double As[PM_K][PM_LD];
+    __shared__ double Bs[PM_K][PM_LD];
+    const int64_t m0 = (int64_t)blockIdx.y * PM_T, n0 = (int64_t)blockIdx.x * PM_T;
+    if (sym && n0 + PM_T <= m0) return;  // strictly below the diagonal
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    // panel element e of a stage: (k, m) with the fastest index along the
+    // operand's unit stride where it has one (coalesced loads)
+    auto a_idx = [&](int e, int& kk, int& mm) {
+        if (sam == 1) { mm = e & (PM_T - 1); kk = e >> 6; } else { kk = e & (PM_K - 1); mm = e >> 4; }
+    };
+    auto b_idx = [&](int e, int& kk, int& nn) {
+        if (sbn == 1) { nn = e & (PM_T - 1); kk = e >> 6; } else { kk = e & (PM_K - 1); nn = e >> 4; }
+    };
+    double pa[4], pb[4];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = r * 256 + tid;
+            int kk, mm, kb, nn;
+            a_idx(e, kk, mm);
+            b_idx(e, kb, nn);
+            const int64_t gm = m0 + mm, gk = k0 + kk, gn = n0 + nn, gkb = k0 + kb;
+            pa[r] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.0;
+            pb[r] = (gn < N && gkb < K) ? B[gkb * sbk + gn * sbn] : 0.0;
+        }
+    };
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    load(0);
+    for (int64_t k0 = 0; k0 < K; k0 += PM_K) {
+        __syncthreads();  // the previous stage's reads are done
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = r * 256 + tid;
+            int kk, mm, kb, nn;
+            a_idx(e, kk, mm);
+            b_idx(e, kb, nn);
+            As[kk][mm] = pa[r];
+            Bs[kb][nn] = pb[r];
         }
         __syncthreads();
+        if (k0 + PM_K < K) load(k0 + PM_K);  // in flight during the MFMAs
 #pragma unroll
-        for (int kk = 0; kk < PG_K; ++kk) {
-            double a[4], b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+        for (int ks = 0; ks < PM_K / 4; ++ks) {
+            const int kk = ks * 4 + g;
+            const double a0 = As[kk][wm + j], a1 = As[kk][wm + 16 + j];
+            const double b0 = Bs[kk][wn + j], b1 = Bs[kk][wn + 16 + j];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
         }
-        __syncthreads();
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t gm = m0 + ty + 16 * i, gn = n0 + tx + 16 * j;
-            if (gm < M && gn < N) {
-                double* c = C + gm * ldc + gn;
-                *c = beta == 0.0 ? alpha * acc[i][j] : alpha * acc[i][j] + beta * *c;
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t gm = m0 + wm + mt * 16 + g + 4 * i, gn = n0 + wn + nt * 16 + j;
+                if (gm < M && gn < N && (!sym || gn >= gm)) {
+                    double* c = C + gm * ldc + gn;
+                    *c = beta == 0.0 ? alpha * acc[mt][nt][i] : alpha * acc[mt][nt][i] + beta * *c;
+                }
             }
-        }
+}
+
+// lower triangle of a symmetric n x n matrix from its upper triangle
+__global__ void pca_mirror_kernel(double* __restrict__ C, int64_t n, int64_t ldc) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n * n) return;
+    const int64_t r = t / n, c = t - r * n;
+    if (c < r) C[r * ldc + c] = C[c * ldc + r];
 }
 
 static int pca_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t sam, int64_t sak, const double* B,
-                    int64_t sbk, int64_t sbn, double* C, int64_t ldc, double alpha, double beta, hipStream_t st) {
-    const dim3 g((unsigned)ccg_cdiv(N, PG_T), (unsigned)ccg_cdiv(M, PG_T));
-    pca_dgemm_kernel<<<g, 256, 0, st>>>(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, alpha, beta);
+                    int64_t sbk, int64_t sbn, double* C, int64_t ldc, double alpha, double beta, hipStream_t st,
+                    bool sym = false) {
+    const dim3 g((unsigned)ccg_cdiv(N, PM_T), (unsigned)ccg_cdiv(M, PM_T));
+    pca_mfma_gemm_kernel<<<g, 256, 0, st>>>(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, alpha, beta, sym ? 1 : 0);
+    if (sym) pca_mirror_kernel<<<(unsigned)ccg_cdiv(M * M, 256), 256, 0, st>>>(C, M, ldc);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
 
 // ------------------------------------------------------ normalisation --
-// Z[i][g] = log1p(counts[genes[g] + cells[i] * G] / sf[cells[i]])
+// Z[i][g] = log1p(counts[genes[g] + cells[i] * G] / sf[cells[i]])  (dense G x N)
 __global__ __launch_bounds__(256) void pca_gather_kernel(const double* __restrict__ counts, int64_t G,
                                                          const double* __restrict__ sf,
                                                          const int32_t* __restrict__ genes, int ng,
@@ -100,40 +147,85 @@ __global__ __launch_bounds__(256) void pca_gather_kernel(const double* __restric
     Z[t] = log1p(counts[(int64_t)genes[g] + c * G] / sf[c]);
 }
 
-// One block per gene: mean, then the sample sd of the deviations, then
-// standardise in place.  sd == 0 flags the gene (prcomp_irlba cannot scale it).
-__global__ __launch_bounds__(256) void pca_standardize_kernel(double* __restrict__ Z, int64_t nc, int ng,
-                                                              int* __restrict__ zero_var) {
-    __shared__ double red[256];
-    const int g = blockIdx.x;
+// Sparse counts (dgCMatrix: column c's nonzeros are x[p[c] .. p[c+1]) at
+// gene rows ri[]): Z starts at log1p(0) = 0 and one wave per selected cell
+// scatters its nonzeros of selected genes (gpos[gene] = position or -1).
+__global__ __launch_bounds__(256) void pca_gather_csc_kernel(const double* __restrict__ xv,
+                                                             const int32_t* __restrict__ ri,
+                                                             const int64_t* __restrict__ cp,
+                                                             const double* __restrict__ sf,
+                                                             const int32_t* __restrict__ gpos,
+                                                             const int32_t* __restrict__ cells, int64_t nc, int ng,
+                                                             double* __restrict__ Z) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= nc) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t c = cells[i];
+    const double s = sf[c];
+    for (int64_t e = cp[c] + lane; e < cp[c + 1]; e += 64) {
+        const int pos = gpos[ri[e]];
+        if (pos >= 0) Z[i * ng + pos] = log1p(xv[e] / s);
+    }
+}
+
+__global__ void pca_fill_kernel(double* __restrict__ Z, int64_t n, double v) {
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) Z[t] = v;
+}
+
+// Per-gene column statistics with lanes along the genes (coalesced rows of
+// Z): block (gx, cy) sums genes [256 gx, +256) over the cells of slice cy;
+// pca_colstat_finish adds the slices in a fixed order (deterministic).
+// pass 0: partial sums of z; pass 1: partial sums of (z - mean)^2.
+#define PCA_SLICES 64
+__global__ __launch_bounds__(256) void pca_colstat_kernel(const double* __restrict__ Z, int64_t nc, int ng,
+                                                          const double* __restrict__ mean, int pass,
+                                                          double* __restrict__ part) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= ng) return;
+    const int64_t per = ccg_cdiv(nc, PCA_SLICES);
+    const int64_t i0 = (int64_t)blockIdx.y * per, i1 = min(nc, i0 + per);
+    const double mu = pass ? mean[g] : 0.0;
+    double s0 = 0.0, s1 = 0.0;  // two chains: more loads in flight
+    int64_t i = i0;
+    for (; i + 1 < i1; i += 2) {
+        const double a = Z[i * ng + g] - mu, b = Z[(i + 1) * ng + g] - mu;
+        s0 += pass ? a * a : a;
+        s1 += pass ? b * b : b;
+    }
+    if (i < i1) {
+        const double a = Z[i * ng + g] - mu;
+        s0 += pass ? a * a : a;
+    }
+    part[(int64_t)blockIdx.y * ng + g] = s0 + s1;
+}
+
+// pass 0: mean[g] = sum / nc; pass 1: inv_sd[g] = 1 / sample sd (flag 0 sd)
+__global__ void pca_colstat_finish(const double* __restrict__ part, int64_t nc, int ng, int pass,
+                                   double* __restrict__ mean, double* __restrict__ inv_sd,
+                                   int* __restrict__ zero_var) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= ng) return;
     double s = 0.0;
-    for (int64_t i = threadIdx.x; i < nc; i += 256) s += Z[i * ng + g];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
+    for (int y = 0; y < PCA_SLICES; ++y) s += part[(int64_t)y * ng + g];
+    if (pass == 0) {
+        mean[g] = s / (double)nc;
+    } else {
+        const double sd = sqrt(s / (double)(nc - 1));
+        if (!(sd > 0.0)) {
+            atomicOr(zero_var, 1);
+            inv_sd[g] = 0.0;
+        } else {
+            inv_sd[g] = 1.0 / sd;
+        }
     }
-    const double mu = red[0] / (double)nc;
-    __syncthreads();
-    double v = 0.0;
-    for (int64_t i = threadIdx.x; i < nc; i += 256) {
-        const double e = Z[i * ng + g] - mu;
-        v += e * e;
-    }
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    const double sd = sqrt(red[0] / (double)(nc - 1));
-    if (!(sd > 0.0)) {
-        if (threadIdx.x == 0) atomicOr(zero_var, 1);
-        return;
-    }
-    const double inv = 1.0 / sd;
-    for (int64_t i = threadIdx.x; i < nc; i += 256) Z[i * ng + g] = (Z[i * ng + g] - mu) * inv;
+}
+
+__global__ void pca_scale_kernel(double* __restrict__ Z, int64_t nc, int ng, const double* __restrict__ mean,
+                                 const double* __restrict__ inv_sd) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nc * ng) return;
+    const int g = (int)(t % ng);
+    Z[t] = (Z[t] - mean[g]) * inv_sd[g];
 }
 
 // deterministic start block: a hash of (row, column) in [-1, 1)
@@ -230,23 +322,48 @@ static void host_jacobi(std::vector<double> a, int p, std::vector<double>& w, st
 #define PCA_MAX_ITERS 3000
 #define PCA_RR_EVERY 8
 
-extern "C" int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
-                           const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
-                           double* sdev, void* stream) {
-    CCG_REQUIRE(ctx && counts && sf && genes && cells && x && sdev, "ccg_pca_dev: NULL argument");
-    CCG_REQUIRE(G >= 1 && N >= 1 && ng >= 2 && nc >= 3, "ccg_pca_dev: need >= 2 genes and >= 3 cells");
-    CCG_REQUIRE(npc >= 1 && npc < ng && npc < nc, "ccg_pca_dev: need 1 <= npc < min(genes, cells)");
-    hipStream_t st = ccg_pick_stream(ctx, stream);
-    const int p = std::min<int>(ng, npc + 16);  // block width (oversampled)
+// Workspace of one PCA: Z (cells x genes), C (genes x genes), V / W / T1 / T2
+// (genes x p), S / S2 (p x p), then the per-gene statistics and the flag.
+struct PcaWs {
+    double *Z, *C, *V, *W, *T1, *T2, *S, *S2, *mean, *inv_sd, *part;
+    int* flag;
+};
+static int pca_workspace(ccg_ctx* ctx, int64_t nc, int ng, int p, PcaWs* w) {
     const size_t nz = (size_t)nc * ng, ncv = (size_t)ng * ng, nv = (size_t)ng * p, np = (size_t)p * p;
-    double* ws = (double*)ccg_ws(ctx, WS_PCA, sizeof(double) * (nz + ncv + 4 * nv + 2 * np) + 64);
+    double* ws = (double*)ccg_ws(ctx, WS_PCA, sizeof(double) * (nz + ncv + 4 * nv + 2 * np +
+                                                                (size_t)(PCA_SLICES + 2) * ng) + 64);
     if (!ws) return CCG_ENOMEM;
-    // Z: cells x genes; C: genes x genes; V: basis; W = C V; T1, T2: scratch
-    double *Z = ws, *C = Z + nz, *V = C + ncv, *W = V + nv, *T1 = W + nv, *T2 = T1 + nv, *S = T2 + nv, *S2 = S + np;
-    int* flag = (int*)(S2 + np);
+    w->Z = ws;
+    w->C = w->Z + nz;
+    w->V = w->C + ncv;
+    w->W = w->V + nv;
+    w->T1 = w->W + nv;
+    w->T2 = w->T1 + nv;
+    w->S = w->T2 + nv;
+    w->S2 = w->S + np;
+    w->mean = w->S2 + np;
+    w->inv_sd = w->mean + ng;
+    w->part = w->inv_sd + ng;
+    w->flag = (int*)(w->part + (size_t)PCA_SLICES * ng);
+    return CCG_OK;
+}
+
+// Steps 2-5 on the gathered Z (cells x genes of y = log1p(c / sf)).
+static int pca_from_z(ccg_ctx* ctx, const PcaWs& ws, int64_t nc, int ng, int npc, double* x, double* sdev,
+                      hipStream_t st) {
+    const int p = std::min<int>(ng, npc + 16);  // block width (oversampled)
+    const size_t nv = (size_t)ng * p, np = (size_t)p * p;
+    double *Z = ws.Z, *C = ws.C, *V = ws.V, *W = ws.W, *T1 = ws.T1, *T2 = ws.T2, *S = ws.S, *S2 = ws.S2;
+    int* flag = ws.flag;
+    // per-gene mean and sample sd (two passes, deterministic slice order), standardise
     CCG_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
-    pca_gather_kernel<<<(unsigned)ccg_cdiv((int64_t)nz, 256), 256, 0, st>>>(counts, G, sf, genes, ng, cells, nc, Z);
-    pca_standardize_kernel<<<(unsigned)ng, 256, 0, st>>>(Z, nc, ng, flag);
+    const dim3 gs((unsigned)ccg_cdiv(ng, 256), PCA_SLICES);
+    const unsigned gf = (unsigned)ccg_cdiv(ng, 256);
+    pca_colstat_kernel<<<gs, 256, 0, st>>>(Z, nc, ng, ws.mean, 0, ws.part);
+    pca_colstat_finish<<<gf, 256, 0, st>>>(ws.part, nc, ng, 0, ws.mean, ws.inv_sd, flag);
+    pca_colstat_kernel<<<gs, 256, 0, st>>>(Z, nc, ng, ws.mean, 1, ws.part);
+    pca_colstat_finish<<<gf, 256, 0, st>>>(ws.part, nc, ng, 1, ws.mean, ws.inv_sd, flag);
+    pca_scale_kernel<<<(unsigned)ccg_cdiv(nc * (int64_t)ng, 256), 256, 0, st>>>(Z, nc, ng, ws.mean, ws.inv_sd);
     CCG_HIP(hipGetLastError());
     int zero_var = 0;
     CCG_HIP(hipMemcpyAsync(&zero_var, flag, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -255,8 +372,8 @@ extern "C" int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_
         ccg_set_error("ccg_pca: a selected gene has zero variance among the cells (prcomp_irlba cannot scale it)");
         return CCG_ENAN;
     }
-    // C = Z^T Z / (nc - 1): A(g, i) = Z[i ng + g], B(i, h) = Z[i ng + h]
-    int rc = pca_gemm(ng, ng, nc, Z, 1, ng, Z, ng, 1, C, ng, 1.0 / (double)(nc - 1), 0.0, st);
+    // C = Z^T Z / (nc - 1): A(g, i) = Z[i ng + g], B(i, h) = Z[i ng + h]; symmetric
+    int rc = pca_gemm(ng, ng, nc, Z, 1, ng, Z, ng, 1, C, ng, 1.0 / (double)(nc - 1), 0.0, st, true);
     if (rc) return rc;
     std::vector<double> hS(np), w, Q;
     // one CholeskyQR step: S = src^T src = L L^T, dst = src L^{-T}
@@ -353,6 +470,39 @@ extern "C" int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_
     }
 }
 
+extern "C" int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
+                           const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
+                           double* sdev, void* stream) {
+    CCG_REQUIRE(ctx && counts && sf && genes && cells && x && sdev, "ccg_pca_dev: NULL argument");
+    CCG_REQUIRE(G >= 1 && N >= 1 && ng >= 2 && nc >= 3, "ccg_pca_dev: need >= 2 genes and >= 3 cells");
+    CCG_REQUIRE(npc >= 1 && npc < ng && npc < nc, "ccg_pca_dev: need 1 <= npc < min(genes, cells)");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    PcaWs ws;
+    int rc = pca_workspace(ctx, nc, ng, std::min<int>(ng, npc + 16), &ws);
+    if (rc) return rc;
+    const int64_t nz = nc * (int64_t)ng;
+    pca_gather_kernel<<<(unsigned)ccg_cdiv(nz, 256), 256, 0, st>>>(counts, G, sf, genes, ng, cells, nc, ws.Z);
+    CCG_HIP(hipGetLastError());
+    return pca_from_z(ctx, ws, nc, ng, npc, x, sdev, st);
+}
+
+extern "C" int ccg_pca_csc_dev(ccg_ctx* ctx, const double* xv, const int32_t* ri, const int64_t* cp, int64_t G,
+                               int64_t N, const double* sf, const int32_t* gpos, int ng, const int32_t* cells,
+                               int64_t nc, int npc, double* x, double* sdev, void* stream) {
+    CCG_REQUIRE(ctx && cp && sf && gpos && cells && x && sdev, "ccg_pca_csc_dev: NULL argument");
+    CCG_REQUIRE(G >= 1 && N >= 1 && ng >= 2 && nc >= 3, "ccg_pca_csc_dev: need >= 2 genes and >= 3 cells");
+    CCG_REQUIRE(npc >= 1 && npc < ng && npc < nc, "ccg_pca_csc_dev: need 1 <= npc < min(genes, cells)");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    PcaWs ws;
+    int rc = pca_workspace(ctx, nc, ng, std::min<int>(ng, npc + 16), &ws);
+    if (rc) return rc;
+    const int64_t nz = nc * (int64_t)ng;
+    pca_fill_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(nz, 256), 4096), 256, 0, st>>>(ws.Z, nz, 0.0);
+    pca_gather_csc_kernel<<<(unsigned)ccg_cdiv(nc, 4), 256, 0, st>>>(xv, ri, cp, sf, gpos, cells, nc, ng, ws.Z);
+    CCG_HIP(hipGetLastError());
+    return pca_from_z(ctx, ws, nc, ng, npc, x, sdev, st);
+}
+
 extern "C" int ccg_pca(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
                        const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
                        double* sdev) {
@@ -376,6 +526,48 @@ extern "C" int ccg_pca(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N,
     int rc = ccg_pca_dev(ctx, dC, G, N, dsf, dg, ng, dcell, nc, npc, dx, sdev, st);
     if (rc) return rc;
     CCG_HIP(hipMemcpyAsync(x, dx, sizeof(double) * (size_t)(nc * npc), hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
+    return CCG_OK;
+}
+
+extern "C" int ccg_pca_csc(ccg_ctx* ctx, const double* xv, const int32_t* ri, const int64_t* cp, int64_t G,
+                           int64_t N, const double* sf, const int32_t* genes, int ng, const int32_t* cells, int64_t nc,
+                           int npc, double* x, double* sdev) {
+    CCG_REQUIRE(ctx && cp && sf && genes && cells && x && sdev, "ccg_pca_csc: NULL argument");
+    CCG_REQUIRE(G >= 1 && N >= 1 && ng >= 2 && nc >= 3, "ccg_pca_csc: need >= 2 genes and >= 3 cells");
+    const int64_t nnz = cp[N];
+    CCG_REQUIRE(cp[0] == 0 && nnz >= 0 && (nnz == 0 || (xv && ri)), "ccg_pca_csc: bad column pointers");
+    for (int64_t c = 0; c < N; ++c) CCG_REQUIRE(cp[c + 1] >= cp[c], "ccg_pca_csc: column pointers must not decrease");
+    for (int64_t e = 0; e < nnz; ++e) CCG_REQUIRE(ri[e] >= 0 && ri[e] < G, "ccg_pca_csc: row index out of range");
+    std::vector<int32_t> gpos(G, -1);
+    for (int g = 0; g < ng; ++g) {
+        CCG_REQUIRE(genes[g] >= 0 && genes[g] < G, "ccg_pca_csc: gene index out of range");
+        CCG_REQUIRE(gpos[genes[g]] < 0, "ccg_pca_csc: gene %d selected twice", genes[g]);
+        gpos[genes[g]] = g;
+    }
+    for (int64_t i = 0; i < nc; ++i) CCG_REQUIRE(cells[i] >= 0 && cells[i] < N, "ccg_pca_csc: cell index out of range");
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    double* dx = (double*)ccg_ws(ctx, WS_HOST_A, sizeof(double) * (size_t)std::max<int64_t>(nnz, 1));
+    int32_t* dri = (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1));
+    int64_t* dcp = (int64_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int64_t) * (N + 1) + sizeof(double) * N +
+                                                        sizeof(int32_t) * (G + nc) + 64);
+    double* dout = (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * (size_t)(nc * npc));
+    if (!dx || !dri || !dcp || !dout) return CCG_ENOMEM;
+    double* dsf = (double*)(dcp + N + 1);
+    int32_t* dgpos = (int32_t*)(dsf + N);
+    int32_t* dcell = dgpos + G;
+    if (nnz) {
+        CCG_HIP(hipMemcpyAsync(dx, xv, sizeof(double) * nnz, hipMemcpyHostToDevice, st));
+        CCG_HIP(hipMemcpyAsync(dri, ri, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, st));
+    }
+    CCG_HIP(hipMemcpyAsync(dcp, cp, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(dsf, sf, sizeof(double) * N, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(dgpos, gpos.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(dcell, cells, sizeof(int32_t) * nc, hipMemcpyHostToDevice, st));
+    int rc = ccg_pca_csc_dev(ctx, dx, dri, dcp, G, N, dsf, dgpos, ng, dcell, nc, npc, dout, sdev, st);
+    if (rc) return rc;
+    CCG_HIP(hipMemcpyAsync(x, dout, sizeof(double) * (size_t)(nc * npc), hipMemcpyDeviceToHost, st));
     CCG_HIP(hipStreamSynchronize(st));
     return CCG_OK;
 }

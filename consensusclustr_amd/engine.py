@@ -267,6 +267,25 @@ class Engine:
                                _ptr(sdev)))
         return x.T.copy(), sdev
 
+    def pca_csc(self, xv, ri, cp, G, sf, genes=None, cells=None, npc=50):
+        """ccg_pca on sparse counts in compressed-column form (R's dgCMatrix
+        slots x, i, p; scipy.sparse.csc_matrix data, indices, indptr): G genes
+        x N = len(cp) - 1 cells.  Returns (x: nc x npc, sdev)."""
+        xv = np.ascontiguousarray(xv, dtype=np.float64)
+        ri = np.ascontiguousarray(ri, dtype=np.int32)
+        cp = np.ascontiguousarray(cp, dtype=np.int64)
+        N = cp.size - 1
+        g = np.arange(G, dtype=np.int32) if genes is None else np.ascontiguousarray(genes, dtype=np.int32)
+        c = np.arange(N, dtype=np.int32) if cells is None else np.ascontiguousarray(cells, dtype=np.int32)
+        sf = np.ascontiguousarray(sf, dtype=np.float64)
+        if sf.size != N:
+            raise ValueError(f"sf has {sf.size} entries; the matrix has {N} cells")
+        x = np.empty((npc, c.size), np.float64)
+        sdev = np.empty(npc, np.float64)
+        check(self.lib.ccg_pca_csc(self.ctx, _ptr(xv), _ptr(ri), _ptr(cp), int(G), N, _ptr(sf), _ptr(g), g.size,
+                                   _ptr(c), c.size, npc, _ptr(x), _ptr(sdev)))
+        return x.T.copy(), sdev
+
     # ---------------------------------------------------------- device API
     def gather_rows_t(self, pcs_cm, N, d, idx, rows):
         """rows[i, :] = pcs[idx[i], :]; pcs_cm is a column-major (d, N) tensor."""

@@ -37,8 +37,8 @@
  *       block means (:463, :699-721).
  *   ccg_contingency                 : the counting of bluster::pairwiseRand
  *       (:470-474).
- *   ccg_pca                         : shifted_log_transform + prcomp_irlba
- *       (:287, :339, :369, :790).
+ *   ccg_pca / ccg_pca_csc           : shifted_log_transform + prcomp_irlba
+ *       (:287, :339, :369, :790), dense or dgCMatrix counts.
  *
  * Errors found by a kernel on the device (a label wider than the assignment
  * matrix, an invalid SNN neighbour index) are sticky in the context and are
@@ -348,6 +348,19 @@ int ccg_pca(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const doub
 int ccg_pca_dev(ccg_ctx* ctx, const double* counts, int64_t G, int64_t N, const double* sf,
                 const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc, double* x,
                 double* sdev, void* stream);
+/* The same from sparse counts as R's dgCMatrix holds them (compressed
+ * columns; R/consensusClust.R:273-288 normalises sparse matrices): column c's
+ * nonzeros are xv[cp[c] .. cp[c+1]) at gene rows ri[] (0-based, cp has N+1
+ * entries, cp[0] = 0).  genes must be distinct.  The dense G x N matrix is
+ * never formed; only the selected genes x cells are, on the device.  The
+ * device flavour takes gpos (G entries: the position of each gene in the
+ * selection, or -1) instead of genes. */
+int ccg_pca_csc(ccg_ctx* ctx, const double* xv, const int32_t* ri, const int64_t* cp, int64_t G, int64_t N,
+                const double* sf, const int32_t* genes, int ng, const int32_t* cells, int64_t nc, int npc,
+                double* x, double* sdev);
+int ccg_pca_csc_dev(ccg_ctx* ctx, const double* xv, const int32_t* ri, const int64_t* cp, int64_t G, int64_t N,
+                    const double* sf, const int32_t* gpos, int ng, const int32_t* cells, int64_t nc, int npc,
+                    double* x, double* sdev, void* stream);
 
 /* ------------------------------------------------------------ multi-GPU -- */
 /* A device group: one context (stream + workspaces) per device and one RCCL

@@ -435,6 +435,40 @@ SEXP ccg_r_pca(SEXP e, SEXP counts, SEXP sf, SEXP genes, SEXP cells, SEXP npc) {
     return res;
 }
 
+/* The same from a dgCMatrix's slots (x, i, p; 0-based row indices, p of
+ * length N + 1), so the genes x cells matrix is never densified in R
+ * (R/consensusClust.R:273-288 keeps counts sparse).  genes must be distinct. */
+SEXP ccg_r_pca_csc(SEXP e, SEXP xv, SEXP ri, SEXP cp, SEXP G, SEXP sf, SEXP genes, SEXP cells, SEXP npc) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    const int64_t N = XLENGTH(cp) - 1, nc = XLENGTH(cells), nG = (int64_t)Rf_asReal(G);
+    const int ng = Rf_length(genes), k = Rf_asInteger(npc);
+    if (N < 1 || XLENGTH(sf) != N) Rf_error("ccg_r_pca_csc: one size factor per column is required");
+    int64_t* p64 = (int64_t*)R_alloc((size_t)N + 1, sizeof(int64_t));
+    for (int64_t c = 0; c <= N; ++c) p64[c] = INTEGER(cp)[c];
+    int32_t* g0 = (int32_t*)R_alloc((size_t)ng, sizeof(int32_t));
+    int32_t* c0 = (int32_t*)R_alloc((size_t)nc, sizeof(int32_t));
+    for (int t = 0; t < ng; ++t) g0[t] = INTEGER(genes)[t] - 1;
+    for (int64_t t = 0; t < nc; ++t) c0[t] = INTEGER(cells)[t] - 1;
+    SEXP x = PROTECT(Rf_allocMatrix(REALSXP, (int)nc, k));
+    SEXP sd = PROTECT(Rf_allocVector(REALSXP, k));
+    int rc = ccg_pca_csc(ctx, REAL(xv), INTEGER(ri), p64, nG, N, REAL(sf), g0, ng, c0, nc, k, REAL(x), REAL(sd));
+    if (rc != CCG_OK) {
+        UNPROTECT(2);
+        fail("ccg_pca_csc", rc);
+    }
+    SEXP res = PROTECT(Rf_allocVector(VECSXP, 2));
+    SET_VECTOR_ELT(res, 0, x);
+    SET_VECTOR_ELT(res, 1, sd);
+    SEXP nm = PROTECT(Rf_allocVector(STRSXP, 2));
+    SET_STRING_ELT(nm, 0, Rf_mkChar("x"));
+    SET_STRING_ELT(nm, 1, Rf_mkChar("sdev"));
+    Rf_setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(4);
+    return res;
+}
+
 /* ------------------------------------------------------- registration -- */
 static const R_CallMethodDef call_methods[] = {
     {"ccg_r_open", (DL_FUNC)&ccg_r_open, 1},
@@ -450,6 +484,7 @@ static const R_CallMethodDef call_methods[] = {
     {"ccg_r_block_dist", (DL_FUNC)&ccg_r_block_dist, 4},
     {"ccg_r_stability", (DL_FUNC)&ccg_r_stability, 5},
     {"ccg_r_pca", (DL_FUNC)&ccg_r_pca, 6},
+    {"ccg_r_pca_csc", (DL_FUNC)&ccg_r_pca_csc, 9},
     {NULL, NULL, 0}};
 
 void R_init_consensusClustR(DllInfo* dll) {

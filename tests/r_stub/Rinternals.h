@@ -36,6 +36,7 @@ int Rf_length(SEXP);
 int Rf_nrows(SEXP);
 int Rf_ncols(SEXP);
 int Rf_asInteger(SEXP);
+double Rf_asReal(SEXP);
 int Rf_asLogical(SEXP);
 SEXP VECTOR_ELT(SEXP, R_xlen_t);
 SEXP SET_VECTOR_ELT(SEXP, R_xlen_t, SEXP);

