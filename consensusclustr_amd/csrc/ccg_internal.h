@@ -46,6 +46,9 @@ enum ccg_ws_slot {
     WS_SNN_ROWS,     // SNN per-node partner rows (padded CSR of the per-graph API)
     WS_HIER,         // cluster block sums: co/both row sub-slab
     WS_PCA,          // PCA: standardised cells x genes, covariance, subspace blocks
+    WS_COC_D,        // consensus kNN candidate path: the row-permuted assignment matrix
+    WS_COC_E,        // consensus kNN candidate path: per-row candidate lists
+    WS_COC_F,        // consensus kNN candidate path: thresholds, counters, flags
     WS_NSLOTS
 };
 

@@ -17,6 +17,8 @@
 // Outputs: the packed upper triangle by rows (== R's "dist" order) for a row
 // slab [r0, r1), or (consensus kNN) full rows [r0, r1) x [0, N) packed as
 // co | both << 16.
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -136,6 +138,68 @@ __device__ __forceinline__ int cof_entry(int lab, int sub16, int off) {
 // full rows [r0, r1) x [0, N) as one uint32 co | both << 16 per pair.
 #define COF_TRI 0
 #define COF_RECT 1
+#define COF_CAND 2  // packed-triangle tiles whose epilogue appends consensus-kNN candidates
+
+// Consensus-kNN candidate lists (COF_CAND): pair (i, j) of the triangle is
+// offered to row i if sim_ij >= tau_i and to row j if sim_ij >= tau_j, where
+// tau is a lower bound of each row's k-th largest similarity.  The test is
+// exact in fp64: (double)co >= tstar * (double)both with tstar = tau - ulp/2
+// (a superset of fp32 sim >= tau; 25 x 16 bits multiply exactly).  A row's
+// entries go to cand[row * cap + slot] as (original column id, co | both << 16).
+struct CofCand {
+    const double* tstar;
+    int* cnt;
+    uint2* cand;
+    int cap;
+    int64_t pmul, padd;  // the row permutation: original id of position p = (p * pmul + padd) mod N
+    int* flags;          // [0] a pair with both == 0, [1] a row overflowed cap
+};
+
+__device__ __forceinline__ int64_t cof_orig(int64_t p, int64_t N, const CofCand& cc) {
+    return (int64_t)(((unsigned __int128)p * (unsigned __int128)cc.pmul + (unsigned __int128)cc.padd) %
+                     (unsigned __int128)N);
+}
+
+// COF_CAND epilogue of one wave's 64 x 128 quarter (rows ia0.., columns
+// jb0..): lane (h, col) holds rows ia0 + 32 mi + (r & 3) + 8 (r >> 2) + 4 h
+// against column jb0 + 32 ni + col.  Passing pairs are rare (a row keeps a
+// few hundred of N columns): each costs one counter add on its row and one
+// 8-byte store; the common element two fp64 compares.  Kept register-light
+// (the 128 accumulators are live throughout): no wave-level aggregation.
+__device__ __forceinline__ void cof_cand_push(const CofCand& cc, int64_t row, int64_t other, int64_t N,
+                                              unsigned val) {
+    const int slot = atomicAdd(&cc.cnt[row], 1);
+    if (slot < cc.cap) cc.cand[row * cc.cap + slot] = make_uint2((unsigned)cof_orig(other, N, cc), val);
+    else cc.flags[1] = 1;
+}
+
+__device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64_t ia0, int64_t jb0, int64_t N,
+                                                  int64_t r1, const CofCand& cc) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    bool nan = false;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t gi = ia0 + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool row_ok = gi < r1;
+            const double ti = row_ok ? cc.tstar[gi] : INFINITY;
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int64_t gj = jb0 + 32 * ni + col;
+                const int a = acc[mi][ni][r];
+                const int cv = a & 16383, bv = a >> 14;
+                if (row_ok && gj < N && gj > gi) {
+                    nan |= bv == 0;
+                    const double dc = (double)cv, db = (double)bv;
+                    const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
+                    if (bv > 0 && dc >= ti * db) cof_cand_push(cc, gi, gj, N, val);
+                    if (bv > 0 && dc >= cc.tstar[gj] * db) cof_cand_push(cc, gj, gi, N, val);
+                }
+            }
+        }
+    if (__any(nan) && lane == 0) cc.flags[0] = 1;
+}
 
 // T: label type (uint8_t / uint16_t); VEC: N is a multiple of 4/sizeof(T),
 // so a dword load covers 4/sizeof(T) consecutive rows of a column.
@@ -145,7 +209,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     const int* __restrict__ desc, const int* __restrict__ stage_lo, const int* __restrict__ stage_nc,
     const int* __restrict__ ccol, const int* __restrict__ nslot_p, const uint16_t* co_prev,
     const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* __restrict__ dist,
-    const uint32_t* cb_prev, uint32_t* cb) {
+    const uint32_t* cb_prev, uint32_t* cb, int64_t NB, CofCand cc) {
     constexpr int RPD = 4 / (int)sizeof(T);             // rows per dword
     constexpr int ROWD = COF_ROWS / RPD;                // dwords per staged column
     constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
@@ -155,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     int64_t I, J;
-    if (MODE == COF_TRI) {
+    if (MODE != COF_RECT) {
         // tile t -> (I, J): row tiles of 128 from I0, col tiles of 256 from J = I/2
         // cum(Ir) = sum_{s<Ir} (TC - (I0+s)/2)
         auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };  // sum_{s<x} s/2
@@ -323,6 +387,10 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             __syncthreads();
         }
     }
+    if constexpr (MODE == COF_CAND) {
+        cof_cand_epilogue(acc, rowA0 + wr * 64, rowB0 + wc * 128, N, r1, cc);
+        return;
+    }
     // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts).
     // Loops run row-major (mi, r outer) so each of a lane's 32 rows computes
     // its packed-triangle offset once for its 4 column groups (the 64-bit
@@ -335,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             const int64_t gi = rowA0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             const bool row_ok = gi < r1;
             // TRI: o = (row gi's start in the packed triangle) + (gj - gi - 1) - base
-            const int64_t rb = MODE == COF_TRI ? gi * N - gi * (gi + 1) / 2 - gi - 1 - base : (gi - r0) * N;
+            const int64_t rb = MODE == COF_TRI ? gi * N - gi * (gi + 1) / 2 - gi - 1 - base : (gi - r0) * NB;
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int64_t gj = rowB0 + wc * 128 + ni * 32 + (lane & 31);
@@ -356,7 +424,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
                         }
                     }
                 } else {
-                    if (row_ok && gj < N) {
+                    if (row_ok && gj < NB) {
                         const int64_t o = rb + gj;
                         if (cb_prev) {
                             const uint32_t pv = cb_prev[o];
@@ -423,9 +491,9 @@ template <int MODE>
 static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t N, int64_t r0, int64_t r1, int64_t TC,
                        int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
                        const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
-                       uint32_t* cb, hipStream_t st) {
+                       uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{}) {
 #define COF_ARGS N, r0, r1, TC, I0, pl.desc, pl.slo, pl.snc, pl.ccol, pl.nslot, co_prev, both_prev, co, both, dist, \
-                 cb_prev, cb
+                 cb_prev, cb, (NB ? NB : N), cc
     if (label_bits == 8) {
         const uint8_t* Ac = (const uint8_t*)A + cb0 * N;
         if (N % 4 == 0) cof_tile_kernel<uint8_t, true, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
@@ -482,15 +550,16 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     return CCG_OK;
 }
 
-// Full rows [r0, r1) x [0, N) of (co, both), packed co | both << 16 into
-// cb[(i - r0) * N + j] (diagonal included).  Used by the consensus kNN on a
-// row slab so the N x N matrix never exists.
+// Rows [r0, r1) x columns [0, NB) of (co, both), packed co | both << 16 into
+// cb[(i - r0) * NB + j] (diagonal included; NB = N: full rows).  Used by the
+// consensus kNN on a row slab so the N x N matrix never exists.
 static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int64_t r0,
-                              int64_t r1, uint32_t* cb, hipStream_t st) {
+                              int64_t r1, uint32_t* cb, hipStream_t st, int64_t NB = 0) {
+    if (!NB) NB = N;
     CofPlan pl;
     int rc = cof_plan(ctx, A, label_bits, N, B, st, &pl);
     if (rc) return rc;
-    const int64_t TC = ccg_cdiv(N, COF_BN);
+    const int64_t TC = ccg_cdiv(NB, COF_BN);
     const int64_t I0 = r0 / COF_BM;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     const int64_t ntiles = TR * TC;
@@ -500,7 +569,7 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
         const int64_t cb0 = c * COF_CHUNK, Bc = std::min<int64_t>(COF_CHUNK, B - cb0);
         cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
         cof_launch<COF_RECT>(label_bits, A, cb0, N, r0, r1, TC, I0, ntiles, pl, nullptr, nullptr, nullptr, nullptr,
-                             nullptr, c ? cb : nullptr, cb, st);
+                             nullptr, c ? cb : nullptr, cb, st, NB);
     }
     CCG_HIP(hipGetLastError());
     return CCG_OK;
@@ -646,6 +715,192 @@ extern "C" int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co, const uin
     return CCG_OK;
 }
 
+// ---------------------------- fused consensus kNN, triangle + candidates --
+// For the whole matrix at once (rows [0, N), B <= COF_CHUNK): rows are
+// visited in a fixed pseudo-random order p -> orig(p) = (p pmul + padd) mod N
+// (the assignment columns permuted once), so the first CKC_SAMPLE positions
+// are a spread sample of cells.
+//   1. thresholds: per row, the k-th largest similarity over the sampled
+//      columns (full rows against them, CKC_SAMPLE-wide) -- a lower bound of
+//      the row's true k-th largest, so its k nearest all score at or above it;
+//   2. the packed triangle once (half the square's MFMA work), its epilogue
+//      offering each pair to both rows that it may enter (COF_CAND);
+//   3. per row, the exact fp32 similarities of its candidates, ordered (sim
+//      desc, original column asc) -- dbscan's stable order() -- top k.
+// A row with more than CKC_CAP candidates sends the call back to the
+// sub-slab path (full rows; bounded workspace).
+#define CKC_SAMPLE 4096
+#define CKC_CAP 2048
+#define CKC_MIN_N 32768
+
+template <typename T>
+__global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B, int64_t pmul, int64_t padd,
+                                   T* __restrict__ Ap) {
+    const int64_t tot = B * N;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = t / N, p = t - b * N;
+        const int64_t o = (int64_t)(((unsigned __int128)p * (unsigned __int128)pmul + (unsigned __int128)padd) %
+                                    (unsigned __int128)N);
+        Ap[t] = A[b * N + o];
+    }
+}
+
+// tstar[row] for rows [a, b): from cb[(row - a) * NS + q], the k-th largest
+// fp32 similarity over q != row with both > 0, minus half an ulp (as a
+// double, exact); -inf when fewer than k sampled columns are usable.
+__global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict__ cb, int64_t a, int64_t b,
+                                                      int64_t NS, int k, double* __restrict__ tstar) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = a + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= b) return;
+    const uint32_t* r = cb + (row - a) * NS;
+    float lv[CKNN_K];
+    int li[CKNN_K];
+#pragma unroll
+    for (int t = 0; t < CKNN_K; ++t) {
+        lv[t] = -INFINITY;
+        li[t] = 0x7fffffff;
+    }
+    for (int64_t q = lane; q < NS; q += 64) {
+        const uint32_t v = r[q];
+        const unsigned c = v & 0xFFFFu, u = v >> 16;
+        if (q == row || u == 0) continue;
+        const float s = (float)((double)c / (double)u);
+        if (!(s > lv[CKNN_K - 1])) continue;
+        cknn_insert(lv, li, s, (int)q);
+    }
+    // k rounds of wave arg-max: the k-th extracted value
+    float kth = -INFINITY;
+    for (int rr = 0; rr < k; ++rr) {
+        float bk = lv[0];
+        int bi = li[0];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ok = __shfl_xor(bk, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ok > bk || (ok == bk && oi < bi)) {
+                bk = ok;
+                bi = oi;
+            }
+        }
+        kth = bk;
+        if (li[0] == bi) {
+#pragma unroll
+            for (int t = 0; t < CKNN_K - 1; ++t) {
+                lv[t] = lv[t + 1];
+                li[t] = li[t + 1];
+            }
+            lv[CKNN_K - 1] = -INFINITY;
+            li[CKNN_K - 1] = 0x7fffffff;
+        }
+    }
+    if (lane == 0) {
+        double t;
+        if (!(kth > -INFINITY)) t = -INFINITY;
+        else if (kth <= 0.0f) t = -1.0;  // every co-sampled pair qualifies
+        else t = (double)kth - ldexp(1.0, ilogbf(kth) - 24);
+        tstar[row] = t;
+    }
+}
+
+// Per permuted row (one wave): the row's candidates, exact fp32 similarity,
+// top k by (sim desc, original column asc), written to the row's original
+// position.
+__global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict__ cand, const int* __restrict__ cnt,
+                                                         int cap, int64_t N, int64_t pmul, int64_t padd, int k,
+                                                         int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= N) return;
+    const int n = min(cnt[p], cap);
+    const uint2* c = cand + p * cap;
+    float lv[CKNN_K];
+    int li[CKNN_K];
+#pragma unroll
+    for (int t = 0; t < CKNN_K; ++t) {
+        lv[t] = -INFINITY;
+        li[t] = 0x7fffffff;
+    }
+    for (int e = lane; e < n; e += 64) {
+        const uint2 v = c[e];
+        const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
+        const float s = (float)((double)co / (double)u);
+        const int j = (int)v.x;
+        if (s < lv[CKNN_K - 1] || (s == lv[CKNN_K - 1] && j > li[CKNN_K - 1])) continue;
+        cknn_insert(lv, li, s, j);
+    }
+    const int64_t o = (int64_t)(((unsigned __int128)p * (unsigned __int128)pmul + (unsigned __int128)padd) %
+                                (unsigned __int128)N);
+    cknn_merge_out(lv, li, k, out + o * k);
+}
+
+static int64_t ckc_gcd(int64_t a, int64_t b) {
+    while (b) {
+        const int64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+// Returns CCG_OK with *done = false when a row overflowed its candidate list
+// (the caller then runs the sub-slab path); synchronises the stream once.
+static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int k, int32_t* out_idx,
+                   int32_t* d_nan_flag, hipStream_t st, bool* done) {
+    *done = false;
+    const size_t lb = label_bits / 8;
+    const int64_t NS = std::min<int64_t>(CKC_SAMPLE, (N / 8) / COF_BN * COF_BN);
+    int64_t pmul = (int64_t)(2654435761ull % (uint64_t)N);
+    if (pmul < 2) pmul = 2;
+    while (ckc_gcd(pmul, N) != 1) ++pmul;
+    const int64_t padd = N / 3;
+    void* Ap = ccg_ws(ctx, WS_COC_D, lb * (size_t)(B * N));
+    uint2* cand = (uint2*)ccg_ws(ctx, WS_COC_E, sizeof(uint2) * (size_t)N * CKC_CAP);
+    char* small = (char*)ccg_ws(ctx, WS_COC_F, sizeof(double) * N + sizeof(int) * (N + 64));
+    if (!Ap || !cand || !small) return CCG_ENOMEM;
+    double* tstar = (double*)small;
+    int* cnt = (int*)(tstar + N);
+    int* flags = cnt + N;  // [0] both == 0 somewhere, [1] overflow
+    const unsigned pg = (unsigned)std::min<int64_t>(ccg_cdiv(B * N, 256), 65536);
+    if (label_bits == 8) ckc_permute_kernel<uint8_t><<<pg, 256, 0, st>>>((const uint8_t*)A, N, B, pmul, padd, (uint8_t*)Ap);
+    else ckc_permute_kernel<uint16_t><<<pg, 256, 0, st>>>((const uint16_t*)A, N, B, pmul, padd, (uint16_t*)Ap);
+    // 1. thresholds, in row chunks of <= 2 GB of sampled similarities
+    int64_t R = ((2LL << 30) / (4 * NS)) / COF_BM * COF_BM;
+    R = std::max<int64_t>(R, COF_BM);
+    uint32_t* cb = (uint32_t*)ccg_ws(ctx, WS_COC_C, sizeof(uint32_t) * (size_t)std::min(R, N) * NS);
+    if (!cb) return CCG_ENOMEM;
+    for (int64_t a = 0; a < N; a += R) {
+        const int64_t b = std::min(N, a + R);
+        int rc = ccg_cocluster_rows_packed(ctx, Ap, label_bits, N, B, a, b, cb, st, NS);
+        if (rc) return rc;
+        ckc_tau_kernel<<<(unsigned)ccg_cdiv(b - a, 4), 256, 0, st>>>(cb, a, b, NS, k, tstar);
+    }
+    // 2. the triangle with the candidate epilogue
+    CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (N + 64), st));
+    CofPlan pl;
+    int rc = cof_plan(ctx, Ap, label_bits, N, B, st, &pl);
+    if (rc) return rc;
+    cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC, B, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
+    const int64_t TC = ccg_cdiv(N, COF_BN), TR = ccg_cdiv(N, COF_BM);
+    auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
+    const int64_t ntiles = TR * TC - fl(TR);
+    CCG_REQUIRE(ntiles < (1LL << 31), "consensus kNN: too many tiles");
+    CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, flags};
+    cof_launch<COF_CAND>(label_bits, Ap, 0, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, st, N, cc);
+    CCG_HIP(hipGetLastError());
+    int hf[2] = {0, 0};
+    CCG_HIP(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
+    if (hf[1]) return CCG_OK;  // overflow: not done
+    // 3. per-row selection
+    ckc_select_kernel<<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
+    CCG_HIP(hipMemcpyAsync(d_nan_flag, flags, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    CCG_HIP(hipGetLastError());
+    *done = true;
+    return CCG_OK;
+}
+
 // Rows per sub-slab of the fused consensus kNN: bounded by the packed-row
 // scratch (CKNN_SCRATCH bytes), a multiple of the co-cluster row tile.
 #define CKNN_SCRATCH (4LL << 30)
@@ -663,12 +918,23 @@ extern "C" int ccg_consensus_knn_assign_dev(ccg_ctx* ctx, const void* A, int lab
     if (r0 == r1) return CCG_OK;
     CCG_REQUIRE(r0 % CCG_COCLUSTER_ROW_ALIGN == 0, "ccg_consensus_knn_assign_dev: r0 must be a multiple of %d",
                 CCG_COCLUSTER_ROW_ALIGN);
+    const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
+    const char* path = getenv("CCG_CKNN_PATH");  // tools/tests: "slab" forces the sub-slab path
+    if (r0 == 0 && r1 == N && N >= CKC_MIN_N && B <= COF_CHUNK && !(path && !strcmp(path, "slab"))) {
+        bool done = false;
+        int rc = ckc_run(ctx, A, label_bits, N, B, k, out_idx, d_nan_flag, st, &done);
+        if (rc) return rc;
+        if (done) {
+            ccg_timer_stop(ctx, t_k, st);
+            return CCG_OK;
+        }
+        CCG_HIP(hipMemsetAsync(d_nan_flag, 0, sizeof(int32_t), st));
+    }
     int64_t R = (CKNN_SCRATCH / (4 * N)) / COF_BM * COF_BM;
     R = std::max<int64_t>(R, COF_BM);
     R = std::min<int64_t>(R, ccg_cdiv(r1 - r0, COF_BM) * COF_BM);
     uint32_t* cb = (uint32_t*)ccg_ws(ctx, WS_COC_C, sizeof(uint32_t) * R * N);
     if (!cb) return CCG_ENOMEM;
-    const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
     for (int64_t a = r0; a < r1; a += R) {
         const int64_t b = std::min(r1, a + R);
         int rc = ccg_cocluster_rows_packed(ctx, A, label_bits, N, B, a, b, cb, st);

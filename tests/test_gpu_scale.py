@@ -151,3 +151,43 @@ def test_knn_boot_cfg4_n225k_sampled_rows_vs_oracle(engine):
     oi, od = O.knn_queries(X, 20, q, nthreads=THREADS)
     assert np.array_equal(idx[0][q], oi)
     np.testing.assert_allclose(dist[0][q], od, rtol=RTOL, atol=1e-12)
+
+
+def test_consensus_knn_candidate_path_equals_subslab_path_with_fallback(engine, monkeypatch):
+    """The triangle + candidate-list path and the full-row sub-slab path give
+    identical neighbour matrices (N = 40 000 > the candidate path's minimum),
+    and a matrix whose similarities all tie (every row overflows its
+    candidate list) falls back to the sub-slab path and still matches the
+    oracle's stable order."""
+    import torch
+    N, B = 40000, 300
+    _, pop = _pcs(71, N, 2)
+    At = _robust_A(71, B, N, pop)
+    k = 20
+    outs = []
+    for path in ("", "slab"):
+        monkeypatch.setenv("CCG_CKNN_PATH", path)
+        out = torch.full((N, k), -1, dtype=torch.int32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        engine.consensus_knn_assign_t(At, k, 0, N, out, flag)
+        torch.cuda.synchronize()
+        assert flag.item() == 0
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    A = At.cpu().numpy()
+    rows = np.array([0, 1, 777, N - 1], np.int32)
+    ref, nan = O.consensus_knn_rows(A, rows, k, nthreads=THREADS)
+    assert np.array_equal(outs[0][rows], ref)
+    # all similarities tie: one label per column, 10% unsampled
+    monkeypatch.setenv("CCG_CKNN_PATH", "")
+    g = torch.Generator(device="cuda").manual_seed(72)
+    Ae = torch.ones((60, N), dtype=torch.uint8, device="cuda")
+    Ae[torch.rand((60, N), generator=g, device="cuda") < 0.1] = 0
+    out = torch.full((N, k), -1, dtype=torch.int32, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    engine.consensus_knn_assign_t(Ae, k, 0, N, out, flag)
+    torch.cuda.synchronize()
+    ref, nan = O.consensus_knn_rows(Ae.cpu().numpy(), rows, k, nthreads=THREADS)
+    assert flag.item() == int(nan.any())
+    if not nan.any():
+        assert np.array_equal(out.cpu().numpy()[rows], ref)

@@ -19,7 +19,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from consensusclustr_amd import _lib  # noqa: E402
 if len(sys.argv) > 2 and sys.argv[1] == "--lib":  # tools only: time a variant build of libccg
+    import ctypes
     _lib.LIB_PATH = os.path.abspath(sys.argv[2])
+    _raw = ctypes.CDLL(_lib.LIB_PATH)  # a variant may predate newer exports: bind what it has
+    _lib.SIGNATURES = {k: v for k, v in _lib.SIGNATURES.items() if hasattr(_raw, k)}
 import bench  # noqa: E402
 from consensusclustr_amd import Engine  # noqa: E402
 
