@@ -134,18 +134,21 @@ def synth_pcs(torch, N, d, G, seed, dev):
     return pcs, pop
 
 
-def synth_labels(torch, pop_boot, L, dev, seed):
+def synth_labels(torch, pop, boot, L, dev, seed):
     """60 clusterings of one bootstrap: C rising with resolution (2..40),
-    permuted true populations, 5% uniform flips; codes 1..C."""
+    permuted true populations, 5% uniform flips; codes 1..C.  Labels are
+    drawn per cell and gathered to the bootstrap rows: a cell's copies are
+    identical points with the same neighbours, which community detection puts
+    in one community."""
     g = torch.Generator(device=dev).manual_seed(seed)
-    n = pop_boot.numel()
+    N = pop.numel()
     li = torch.arange(L, device=dev)
     ki = (li // N_RES)[:, None]
     Cl = (2 + (38 * (li % N_RES)) // (N_RES - 1))[:, None]
-    lab = (pop_boot[None, :] * 7 + ki) % Cl + 1
-    flip = torch.rand(L, n, device=dev, generator=g) < 0.05
-    rnd = (torch.rand(L, n, device=dev, generator=g) * Cl).long() + 1
-    return torch.where(flip, rnd, lab).to(torch.int32)
+    lab = (pop[None, :] * 7 + ki) % Cl + 1
+    flip = torch.rand(L, N, device=dev, generator=g) < 0.05
+    rnd = (torch.rand(L, N, device=dev, generator=g) * Cl).long() + 1
+    return torch.where(flip, rnd, lab).to(torch.int32)[:, boot.long()].contiguous()
 
 
 def _cpu_boot_worker(a):
@@ -283,7 +286,7 @@ def main():
     uniq = [int(np.count_nonzero(np.bincount(b, minlength=N))) for b in boots_np]
     labels = torch.empty((B, L, n), dtype=torch.int32, device=dev)
     for j in range(B):
-        labels[j] = synth_labels(torch, pop[boots[j].long()], L, dev, 1000 + bids[j])
+        labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j])
     cmax = int(labels.max().item())
 
     RING = NK + NS + 1 if NK else S  # bootstrap buffers (gathered rows, kNN) in flight
@@ -336,7 +339,7 @@ def main():
             with torch.cuda.stream(streams[ss]):
                 streams[ss].wait_event(ev_k[j])
                 engs[ss].snn_rows_t(knn_s[slot], K_NUM, "number", *snn_out[ss - NK], nedges[j])
-                engs[ss].silhouette_t(rows_s[slot], labels[j], cmax, means[j], nclust[j], minsize[j])
+                engs[ss].silhouette_cells_t(rows_s[slot], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
                 ev_s[j].record(streams[ss])
         for st_ in streams:
             cur.wait_stream(st_)
@@ -364,7 +367,7 @@ def main():
                 e.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[si])
                 e.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[si], 20, knn_s[si])
                 e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
-                e.silhouette_t(rows_s[si], labels[j], cmax, means[j], nclust[j], minsize[j])
+                e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_t[0] += time.perf_counter() - th
         for st_ in streams:
             cur.wait_stream(st_)
@@ -428,7 +431,7 @@ def main():
             eng.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[0])
             eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[0], 20, knn_s[0])
             eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
-            eng.silhouette_t(rows_s[0], labels[j], cmax, means[j], nclust[j], minsize[j])
+            eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_idle.append(time.perf_counter() - th)
         torch.cuda.synchronize()
     host_idle_ms = 1000 * float(np.median(host_idle))

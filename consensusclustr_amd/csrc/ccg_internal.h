@@ -26,6 +26,7 @@ enum ccg_ws_slot {
     WS_SIL_A,        // silhouette accumulators
     WS_SIL_B,        // silhouette centroids
     WS_SIL_Q,        // silhouette fixed-point rows (x and x^2)
+    WS_SIL_C,        // silhouette distinct-cell tables (first rows, representatives, weights, exceptions)
     WS_KB_A,         // distinct-cell kNN: sorted (cell, row) pairs, heads, tables
     WS_KB_B,         // distinct-cell kNN: distinct rows and their kNN
     WS_COC_A,        // co-cluster column tables

@@ -426,7 +426,7 @@ constexpr int sil_rt() {
 }
 
 __device__ __forceinline__ void sil_row_width(double selfsq, double oth2, bool in, int np, double wsc,
-                                              double* out_w, long long& wq, unsigned& wn) {
+                                              double* out_w, long long& wq, unsigned& wn, int wt = 1) {
     if (!in) return;
     const double selfd = sqrt(selfsq), othd = sqrt(oth2);
     double w;
@@ -439,8 +439,8 @@ __device__ __forceinline__ void sil_row_width(double selfsq, double oth2, bool i
     }
     if (out_w) *out_w = w;
     if (!isnan(w)) {
-        wq += __double2ll_rn(w * wsc);
-        wn += 1;
+        wq += (long long)wt * __double2ll_rn(w * wsc);
+        wn += (unsigned)wt;
     }
 }
 
@@ -467,7 +467,9 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
                                                    const double* __restrict__ auxc,
                                                    unsigned long long* __restrict__ wsum,
                                                    unsigned long long* __restrict__ wcnt,
-                                                   double* __restrict__ out_width, int CH) {
+                                                   double* __restrict__ out_width, int CH,
+                                                   const int* __restrict__ rep, const int* __restrict__ mult,
+                                                   int64_t mw, int nbw, const int64_t* __restrict__ nrep) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // CH: centroids staged per pass (a multiple of 16)
     constexpr int KS = DMAX / 4;  // K steps of 4 dims
@@ -478,14 +480,21 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     int* scode = (int*)(smv + CH);            // [CH]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, j = lane & 15;
+    // tile position p = r0 + 16 t + j is row p, or (distinct-cell widths)
+    // the representative row rep[p] of a cell, weighted by mult[l][p]
     const int64_t r0 = (int64_t)blockIdx.x * (4 * RT * 16) + wave * (RT * 16);
+    const int64_t npos = rep ? *nrep : m;  // representatives: counted on the device
+    if ((int64_t)blockIdx.x * (4 * RT * 16) >= npos) return;  // the partials of idle blocks stay 0
     double xb[RT][KS];
     double xx[RT];
     bool in[RT];
+    int64_t rowof[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
-        const int64_t r = r0 + t * 16 + j;
-        in[t] = r < m;
+        const int64_t pp = r0 + t * 16 + j;
+        in[t] = pp < npos;
+        const int64_t r = in[t] ? (rep ? (int64_t)rep[pp] : pp) : 0;
+        rowof[t] = r;
         double p = 0.0;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -505,7 +514,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         double oth[RT], self[RT];
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            lab[t] = in[t] ? labels[(int64_t)l * m + r0 + t * 16 + j] : 0;
+            lab[t] = in[t] ? labels[(int64_t)l * m + rowof[t]] : 0;
             oth[t] = INFINITY;
             self[t] = INFINITY;
         }
@@ -573,6 +582,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         // takes one row's square roots and division
         double ow = 0.0, sw = 0.0;
         bool iw = false;
+        int64_t pw = 0;
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
             double o = oth[t], sf = self[t];
@@ -583,14 +593,17 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
             ow = t == g ? fmax(xx[t] + o, 0.0) : ow;
             sw = t == g ? fmax(xx[t] + sf, 0.0) : sw;
             iw = t == g ? in[t] : iw;
+            pw = t == g ? r0 + t * 16 + j : pw;
         }
+        const int wt = (rep && iw) ? mult[(int64_t)l * mw + pw] : 1;
         long long wq = 0;
         unsigned wn = 0;
 #if SIL_EXP == 3
         wq = (long long)ow + (long long)sw;
         wn = iw;
 #else
-        sil_row_width(sw, ow, iw, np, wsc, out_width ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn);
+        sil_row_width(sw, ow, iw, np, wsc,
+                      (out_width && !rep) ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn, wt);
 #endif
         // integer reductions (order-independent): wave, then block; one
         // partial per (labeling, block) -- same-line global atomics from every
@@ -607,8 +620,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            wsum[(int64_t)l * gridDim.x + blockIdx.x] = (unsigned long long)(red_q[0] + red_q[1] + red_q[2] + red_q[3]);
-            wcnt[(int64_t)l * gridDim.x + blockIdx.x] = (unsigned long long)(red_n[0] + red_n[1] + red_n[2] + red_n[3]);
+            wsum[(int64_t)l * nbw + blockIdx.x] = (unsigned long long)(red_q[0] + red_q[1] + red_q[2] + red_q[3]);
+            wcnt[(int64_t)l * nbw + blockIdx.x] = (unsigned long long)(red_n[0] + red_n[1] + red_n[2] + red_n[3]);
         }
         __syncthreads();  // red_q / red_n are rewritten by the next labeling
     }
@@ -674,12 +687,109 @@ static int sil_width_blocks(int64_t m, int d) {
     return (int)ccg_cdiv(m, rb);
 }
 
+// ---------------------------------------------- distinct-cell widths --
+// Bootstrap rows repeat cells (R/consensusClust.R:394): copies of a cell are
+// the same point, and with the same label they have the same width.  So the
+// widths run over one representative row per cell (its first row), weighted
+// by the number of the cell's rows that share the representative's label in
+// that labeling; rows whose label differs (rare) are exceptions, each
+// computed alone (sil_width_exc).  Cluster sums still run over every row.
+__global__ void sil_first_kernel(const int32_t* __restrict__ cell, int64_t m, int* __restrict__ first) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < m) atomicMin(&first[cell[r]], (int)r);
+}
+
+__global__ void sil_init_kernel(int* __restrict__ first, int64_t ncell, int* __restrict__ zero, int64_t nzero) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ncell || t < nzero;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        if (t < ncell) first[t] = 0x7fffffff;
+        if (t < nzero) zero[t] = 0;
+    }
+}
+
+__global__ void sil_isrep_kernel(const int32_t* __restrict__ cell, int64_t m, const int* __restrict__ first,
+                                 int64_t* __restrict__ flag) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < m) flag[r] = first[cell[r]] == (int)r ? 1 : 0;
+}
+
+// rep[pos] = the representative rows in row order (pos = exclusive scan)
+__global__ void sil_rep_kernel(const int32_t* __restrict__ cell, int64_t m, const int* __restrict__ first,
+                               const int64_t* __restrict__ scan, int* __restrict__ rep) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < m && first[cell[r]] == (int)r) rep[scan[r]] = (int)r;
+}
+
+// mult[l][pos of the cell's representative] += 1 for each row with the
+// representative's label; other rows -> exc (l << 32 | row)
+__global__ void sil_mult_kernel(const int32_t* __restrict__ cell, int64_t m, int L, const int32_t* __restrict__ labels,
+                                const int* __restrict__ first, const int64_t* __restrict__ scan, int64_t mw,
+                                int* __restrict__ mult, unsigned long long* __restrict__ exc,
+                                int* __restrict__ nexc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * L) return;
+    const int l = (int)(t / m);
+    const int64_t r = t - (int64_t)l * m;
+    const int rp = first[cell[r]];
+    if (labels[(int64_t)l * m + r] == labels[(int64_t)l * m + rp]) {
+        atomicAdd(&mult[(int64_t)l * mw + scan[rp]], 1);
+    } else {
+        const int e = atomicAdd(nexc, 1);
+        exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
+    }
+}
+
+// One thread per exception row: its width against labeling l's centroids
+// (fp64, the same D^2 = |x|^2 + (|mu|^2 + v) - 2 x.mu), added to the
+// labeling's first width partial (integer atomics: order-independent).
+template <int DMAX>
+__global__ void sil_width_exc(const double* __restrict__ x, int64_t m, int d, const int32_t* __restrict__ labels,
+                              int cmax, const int* __restrict__ npres, const int* __restrict__ codes,
+                              const double* __restrict__ muc, const double* __restrict__ auxc,
+                              const unsigned long long* __restrict__ exc, const int* __restrict__ nexc, int nbw,
+                              unsigned long long* __restrict__ wsum, unsigned long long* __restrict__ wcnt) {
+    const int ne = *nexc;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
+    const int l = (int)(exc[e] >> 32);
+    const int64_t r = (int64_t)(exc[e] & 0xffffffffull);
+    const int lab = labels[(int64_t)l * m + r];
+    double xr[DMAX];
+    double xx = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) {
+        xr[k] = k < d ? x[r * d + k] : 0.0;
+        xx = fma(xr[k], xr[k], xx);
+    }
+    const int np = npres[l];
+    double self = INFINITY, oth = INFINITY;
+    for (int p = 0; p < np; ++p) {
+        const double* mp = muc + ((int64_t)l * cmax + p) * DMAX;
+        double dot = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) dot = fma(xr[k], mp[sil_mfma_pos<DMAX>(k)], dot);
+        const double tv = fma(-2.0, dot, auxc[2 * ((int64_t)l * cmax + p)] + auxc[2 * ((int64_t)l * cmax + p) + 1]);
+        if (codes[(int64_t)l * cmax + p] == lab) self = tv;
+        else oth = fmin(oth, tv);
+    }
+    long long wq = 0;
+    unsigned wn = 0;
+    sil_row_width(fmax(xx + self, 0.0), fmax(xx + oth, 0.0), true, np, ldexp(1.0, scale_exp((double)m)), nullptr,
+                  wq, wn);
+    if (wn) {
+        atomicAdd(&wsum[(int64_t)l * nbw], (unsigned long long)wq);
+        atomicAdd(&wcnt[(int64_t)l * nbw], 1ull);
+    }
+    }
+}
+
 template <int DMAX>
 static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels, int L, int cmax,
                        unsigned* maxabs, unsigned long long* gsum, unsigned long long* gsum2, unsigned long long* gcnt,
                        unsigned long long* gvar, unsigned long long* wsum, unsigned long long* wcnt,
                        int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc, long long* q,
-                       double* out_width, hipStream_t st) {
+                       double* out_width, hipStream_t st, const int* rep = nullptr, const int* mult = nullptr,
+                       int64_t mw = 0, const unsigned long long* exc = nullptr, const int* nexc = nullptr,
+                       const int64_t* nrep = nullptr) {
     if (q) {
         // sorted segments: S1, S2 and counts in one pass, v_c in sil_mu
         sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q, q + m * DMAX);
@@ -703,11 +813,23 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
         sil_vfin<<<(unsigned)ccg_cdiv((int64_t)L * (cmax + 1), 256), 256, 0, st>>>(m, d, L, cmax, maxabs, gcnt,
                                                                                     gvar, pos, auxc);
     }
-    dim3 grid2((unsigned)ccg_cdiv(m, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
+    // the width partials are laid out for m rows (nbw blocks per labeling);
+    // the representative grid uses its first blocks
+    const int64_t nrows = rep ? mw : m;
+    dim3 grid2((unsigned)ccg_cdiv(nrows, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
     const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), ((int64_t)cmax + 15) / 16 * 16);
     const size_t lds5 = (size_t)CH * sil_sp<DMAX>() * 8 + (size_t)CH * 8 + (size_t)CH * 4;
-    sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
-                                            out_width, CH);
+    const int nbw = (int)ccg_cdiv(m, sil_width_rows<DMAX>());
+    if (rep) {
+        // partials of blocks past the representative grid stay 0 (zeroed with the buffer)
+        sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
+                                                nullptr, CH, rep, mult, mw, nbw, nrep);
+        sil_width_exc<DMAX><<<64, 256, 0, st>>>(
+            x, m, d, labels, cmax, npres, codes, muc, auxc, exc, nexc, nbw, wsum, wcnt);
+    } else {
+        sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
+                                                out_width, CH, nullptr, nullptr, 0, nbw, nullptr);
+    }
 }
 
 extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
@@ -762,6 +884,83 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
                         out_width, st);
     sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean,
                                                        out_nclust, out_minsize);
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels,
+                                        int L, int cmax, const int32_t* cell, int64_t ncell, double* out_mean,
+                                        int32_t* out_nclust, int32_t* out_minsize, void* stream) {
+    CCG_REQUIRE(ctx && x && labels && cell, "ccg_silhouette_cells_dev: NULL argument");
+    CCG_REQUIRE(m >= 1 && m < (1LL << 31) && d >= 1 && d <= 64 && L >= 1 && (int64_t)L * m < (1LL << 31),
+                "ccg_silhouette_cells_dev: bad sizes m=%lld d=%d L=%d", (long long)m, d, L);
+    CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_cells_dev: cmax=%d must be in [1, 2^24]", cmax);
+    CCG_REQUIRE(ncell >= 1 && ncell < (1LL << 31), "ccg_silhouette_cells_dev: bad ncell");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int64_t nacc = (int64_t)(cmax + 1) * d;
+    const int nbw = sil_width_blocks(m, d);
+    const int64_t words = 2 * (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L * nbw + 8;
+    unsigned long long* buf = (unsigned long long*)ccg_ws(ctx, WS_SIL_A, sizeof(unsigned long long) * words);
+    if (!buf) return CCG_ENOMEM;
+    unsigned long long* gsum = buf;
+    unsigned long long* gsum2 = gsum + (int64_t)L * nacc;
+    unsigned long long* gcnt = gsum2 + (int64_t)L * nacc;
+    unsigned long long* gvar = gcnt + (int64_t)L * (cmax + 1);
+    unsigned long long* wsum = gvar + (int64_t)L * (cmax + 1);
+    unsigned long long* wcnt = wsum + (int64_t)L * nbw;
+    unsigned* maxabs = (unsigned*)(wcnt + (int64_t)L * nbw);
+    const int dmax = d <= 16 ? 16 : (d <= 32 ? 32 : 64);
+    const size_t mu_words = (size_t)L * (cmax + 1) * dmax + (size_t)L * cmax * dmax + 2 * (size_t)L * cmax;
+    const size_t tab_ints = (size_t)L * cmax + (size_t)L * (cmax + 1) + L + 8;
+    double* mu = (double*)ccg_ws(ctx, WS_SIL_B, sizeof(double) * mu_words + sizeof(int) * tab_ints);
+    if (!mu) return CCG_ENOMEM;
+    double* muc = mu + (size_t)L * (cmax + 1) * dmax;
+    double* auxc = muc + (size_t)L * cmax * dmax;
+    int* npres = (int*)(auxc + 2 * (size_t)L * cmax);
+    int* codes = npres + L;
+    int* pos = codes + (size_t)L * cmax;
+    const size_t lds_sorted = dmax == 16 ? sil_sorted_lds<16>(cmax)
+                                         : (dmax == 32 ? sil_sorted_lds<32>(cmax) : sil_sorted_lds<64>(cmax));
+    long long* q = nullptr;
+    if (lds_sorted <= SIL_LDS_CAP) {
+        q = (long long*)ccg_ws(ctx, WS_SIL_Q, 2 * sizeof(long long) * (size_t)m * dmax);
+        if (!q) return CCG_ENOMEM;
+    }
+    // distinct-cell tables: first row per cell, representative list, weights, exceptions
+    char* tb = (char*)ccg_ws(ctx, WS_SIL_C, sizeof(int) * (size_t)ncell + sizeof(int64_t) * (size_t)(m + 1) +
+                                                sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
+                                                sizeof(unsigned long long) * (size_t)L * m + 256);
+    if (!tb) return CCG_ENOMEM;
+    int* first = (int*)tb;
+    int64_t* scan = (int64_t*)(tb + ccg_cdiv(sizeof(int) * ncell, 16) * 16);
+    int* rep = (int*)(scan + m + 1);
+    int* nexc = rep + m;                // [0] exception count, then the weights
+    int* mult = nexc + 4;               // [L][m] (first mw columns used)
+    unsigned long long* exc = (unsigned long long*)(mult + ccg_cdiv((int64_t)L * m, 2) * 2);
+    const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
+    CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
+    const unsigned gm = (unsigned)ccg_cdiv(m, 256);
+    sil_init_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(std::max(ncell, (int64_t)L * m + 4), 256), 4096), 256, 0,
+                      st>>>(first, ncell, nexc, (int64_t)L * m + 4);
+    sil_first_kernel<<<gm, 256, 0, st>>>(cell, m, first);
+    sil_isrep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan);
+    int rc = ccg_scan_i64(ctx, scan, scan, m, st);
+    if (rc) return rc;
+    sil_rep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan, rep);
+    // mw = the number of representatives (the distinct cells): device-side
+    // only, so the width grid covers m positions and the weights' stride is m
+    sil_mult_kernel<<<(unsigned)ccg_cdiv((int64_t)L * m, 256), 256, 0, st>>>(cell, m, L, labels, first, scan, m, mult,
+                                                                          exc, nexc);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
+#define SIL_CELLS(DM_)                                                                                              \
+    sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
+                    auxc, q, nullptr, st, rep, mult, m, exc, nexc, scan + m)
+    if (d <= 16) SIL_CELLS(16);
+    else if (d <= 32) SIL_CELLS(32);
+    else SIL_CELLS(64);
+#undef SIL_CELLS
+    sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean, out_nclust, out_minsize);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;

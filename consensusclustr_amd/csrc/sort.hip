@@ -4,8 +4,8 @@
 // the SNN build lists every node's hosts (keys < n, snn.hip); both need the
 // equal keys in input order (rows / hosts ascending).
 //
-// One pass per digit of <= 8 bits (the key bits split evenly, so 17-bit keys
-// take three 6/6/5-bit passes), three launches per pass:
+// One pass per digit of <= 9 bits (the key bits split evenly, so 17-bit keys
+// take two 9/8-bit passes), three launches per pass:
 //   rs_hist    : per tile of RS_TILE pairs, the digit histogram (LDS atomics),
 //                written digit-major: cnt[digit * ntiles + tile];
 //   rs_scan    : one block scans that matrix exclusively -> every (digit, tile)
@@ -23,7 +23,7 @@
 #define RS_WAVES (RS_THREADS / 64)
 #define RS_IPT 16                       // pairs per thread per tile
 #define RS_TILE (RS_THREADS * RS_IPT)   // 4096 pairs per tile
-#define RS_MAXBITS 8
+#define RS_MAXBITS 9
 
 __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift,
                                                       int bits, int ntiles, int* __restrict__ cnt) {
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict_
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
 }
 
-// Exclusive scan of m ints in place by one block (m <= 2^8 * ntiles).
+// Exclusive scan of m ints in place by one block (m <= 2^RS_MAXBITS * ntiles).
 __global__ __launch_bounds__(1024) void rs_scan(int* __restrict__ cnt, int m) {
     __shared__ int part[1024];
     const int per = (m + 1023) / 1024;

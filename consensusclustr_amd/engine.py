@@ -372,6 +372,15 @@ class Engine:
         check(self.lib.ccg_silhouette_dev(self.ctx, _ptr(x), m, d, _ptr(labels), L, cmax, _ptr(out_mean),
                                           _ptr(out_nclust), _ptr(out_minsize), _ptr(out_width), _stream()))
 
+    def silhouette_cells_t(self, x, labels, cmax, cell, ncell, out_mean, out_nclust, out_minsize):
+        """ccg_silhouette_cells_dev: bootstrap rows x (m, d) whose cells are
+        cell (m,) int32 in [0, ncell) (copies identical); widths once per
+        (cell, label), weighted."""
+        m, d = x.shape
+        L = labels.shape[0]
+        check(self.lib.ccg_silhouette_cells_dev(self.ctx, _ptr(x), m, d, _ptr(labels), L, cmax, _ptr(cell), ncell,
+                                                _ptr(out_mean), _ptr(out_nclust), _ptr(out_minsize), _stream()))
+
     def select_mapback_t(self, mode, labels, boot_idx, N, A, col0, means=None, nclust=None, minsize=None,
                          min_size=0, out_choice=None):
         """A: (B, N) uint8 or uint16 tensor (label width from its dtype)."""

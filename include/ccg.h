@@ -229,6 +229,18 @@ int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
                        double* out_mean, int32_t* out_nclust,
                        int32_t* out_minsize, double* out_width, void* stream);
 
+/* The same means for bootstrap rows that repeat cells: cell[r] (device, m
+ * entries in [0, ncell)) names row r's cell -- R's sample() indices -- and
+ * rows of one cell must be identical (bootstrap copies).  Widths are
+ * computed once per (cell, label) and weighted by the number of copies
+ * sharing it; cluster sums, counts and the mean are over every row, as in
+ * ccg_silhouette_dev (same fixed-point reductions, so deterministic).  No
+ * per-row widths. */
+int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
+                             const int32_t* labels, int L, int cmax,
+                             const int32_t* cell, int64_t ncell, double* out_mean,
+                             int32_t* out_nclust, int32_t* out_minsize, void* stream);
+
 /* ----------------------------------------------- selection + map-back -- */
 /* For nb bootstraps with L clusterings each (labels nb x L x n int32,
  * codes 1..2^label_bits - 1), map labels back to the N cells (first copy in

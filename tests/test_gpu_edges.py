@@ -347,3 +347,56 @@ def test_sort_pairs_is_a_stable_radix_sort(engine, n, bits):
     o = np.argsort(keys & (hi - 1), kind="stable")
     assert np.array_equal(ko.cpu().numpy(), keys[o])
     assert np.array_equal(vo.cpu().numpy(), vals[o])
+
+
+@pytest.mark.parametrize("labels_per", ["cell", "row"])
+def test_silhouette_cells_matches_row_path_and_oracle(engine, labels_per):
+    """ccg_silhouette_cells_dev: widths once per (cell, label), weighted by
+    the copies sharing it (R/consensusClust.R:664 on pca[sample(...), ]).
+    Labels per cell (as Leiden gives copies of a cell): bit-identical to the
+    per-row path.  Labels per row (copies may disagree: the exception path):
+    within 1e-12 of it, and within 1e-5 of the oracle."""
+    import torch
+    rng = np.random.default_rng(81)
+    N, d, L = 6000, 20, 9
+    centers = rng.normal(scale=3.0, size=(7, d))
+    pop = rng.integers(0, 7, N)
+    pcs = centers[pop] + rng.normal(size=(N, d))
+    boot = rng.integers(0, N, int(0.9 * N)).astype(np.int32)
+    X = pcs[boot]
+    n = boot.size
+    labs = np.empty((L, n), np.int32)
+    for l_ in range(L):
+        C = 2 + 4 * l_
+        if labels_per == "cell":
+            lc = (pop * 3 + l_) % C + 1
+            flip = rng.random(N) < 0.1
+            lc[flip] = rng.integers(1, C + 1, int(flip.sum()))
+            labs[l_] = lc[boot]
+        else:
+            labs[l_] = rng.integers(1, C + 1, n)
+    cmax = int(labs.max())
+    xt = torch.from_numpy(X).cuda()
+    lt = torch.from_numpy(labs).cuda()
+    ct = torch.from_numpy(boot).cuda()
+    outs = []
+    for cells in (False, True):
+        mean = torch.empty(L, dtype=torch.float64, device="cuda")
+        nc = torch.empty(L, dtype=torch.int32, device="cuda")
+        ms = torch.empty(L, dtype=torch.int32, device="cuda")
+        if cells:
+            engine.silhouette_cells_t(xt, lt, cmax, ct, N, mean, nc, ms)
+        else:
+            engine.silhouette_t(xt, lt, cmax, mean, nc, ms)
+        torch.cuda.synchronize()
+        outs.append((mean.cpu().numpy(), nc.cpu().numpy(), ms.cpu().numpy()))
+    (m0, c0, s0), (m1, c1, s1) = outs
+    assert np.array_equal(c0, c1) and np.array_equal(s0, s1)
+    if labels_per == "cell":
+        assert np.array_equal(m0, m1)
+    else:
+        np.testing.assert_allclose(m1, m0, rtol=1e-12)
+    for l_ in range(L):
+        _, m, C = O.silhouette(X, labs[l_])
+        np.testing.assert_allclose(m1[l_], m, rtol=1e-5)
+        assert c1[l_] == C
