@@ -86,7 +86,7 @@ SIGNATURES = {
     "ccg_pairwise_rand_ratio": (_i, [_i, _i, _p, _i, _p]),
     "ccg_pca": (_i, [_p, _p, _i64, _i64, _p, _p, _i, _p, _i64, _i, _p, _p]),
     "ccg_pca_dev": (_i, [_p, _p, _i64, _i64, _p, _p, _i, _p, _i64, _i, _p, _p, _p]),
-    "ccg_pca_csc": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i, _p, _i64, _i, _p, _p]),
+    "ccg_pca_csc": (_i, [_p, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, _i64, _i, _p, _p]),
     "ccg_pca_csc_dev": (_i, [_p, _p, _p, _p, _i64, _i64, _p, _p, _i, _p, _i64, _i, _p, _p, _p]),
     "ccg_row_slabs": (_i, [_i64, _i, _p]),
     "ccg_rect_slabs": (_i, [_i64, _i, _p]),

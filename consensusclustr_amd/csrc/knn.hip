@@ -545,8 +545,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
     KNN_STAGE_GLDS(0, chunk_at(0));
     if (KNN_NBUF == 3 && nck > 1) KNN_STAGE_GLDS(1, chunk_at(1));
     for (int k = 0; k < nck; ++k) {
+#ifdef KNN_EXP_NOSTAGE  // tools only: every chunk reads buffer 0 (staged once; results wrong)
+        const int b = 0;
+        const int c = chunk_at(k);
+        if (k == 0) {
+            knn_wait_vmcnt<0>();
+            __syncthreads();
+        }
+        if (false) {
+#else
         const int b = k % KNN_NBUF;
         const int c = chunk_at(k);
+        {
+#endif
         KST(1);
         if constexpr (knn_nbuf(KSTEPS) == 3) {
             if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
@@ -558,6 +569,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
         __syncthreads();
         KST(6);
         if (k + KNN_NBUF - 1 < nck) KNN_STAGE_GLDS((k + KNN_NBUF - 1) % KNN_NBUF, chunk_at(k + KNN_NBUF - 1));
+        }
         KST(0);
         // After the MFMA chain of a tile (accumulator ACC_, first ref RB_):
         // self / padding masking, the tile maximum, and -- when some lane's

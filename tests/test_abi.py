@@ -64,3 +64,31 @@ def test_consts_match_header():
 def test_library_links_rccl():
     out = subprocess.check_output(["readelf", "-d", _lib.LIB_PATH]).decode()
     assert "librccl.so" in out  # the device group's collectives are RCCL, inside the library
+
+
+def _header_prototypes():
+    """name -> list of parameter type strings, from include/ccg.h."""
+    import re
+    text = open(_lib.HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:int|const char\*|void\*)\s+(ccg_\w+)\s*\(([^)]*)\)\s*;", text, re.M | re.S):
+        args = " ".join(m.group(2).split())
+        out[m.group(1)] = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
+    return out
+
+
+def test_ctypes_signatures_match_header_prototypes():
+    """Every SIGNATURES entry has the header's parameter count, and each
+    integer parameter has the header's width (pointers are opaque)."""
+    protos = _header_prototypes()
+    for name, (_, args) in _lib.SIGNATURES.items():
+        params = protos[name]
+        assert len(args) == len(params), (name, len(args), len(params))
+        for a, p in zip(args, params):
+            if "*" in p:
+                assert a is ctypes.c_void_p, (name, p)
+            elif p.startswith(("int64_t", "const int64_t")):
+                assert a is ctypes.c_int64, (name, p)
+            elif p.startswith("int "):
+                assert a is ctypes.c_int, (name, p)
