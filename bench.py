@@ -284,6 +284,10 @@ def main():
     # distinct cells per bootstrap (R: length(unique(idx))), passed to the
     # distinct-cell kNN; host input like the indices themselves
     uniq = [int(np.count_nonzero(np.bincount(b, minlength=N))) for b in boots_np]
+    # per-cell k-th distances certified by earlier bootstraps of the same PCs:
+    # the screen's warm start (ccg_knn_boot_hint_dev; results do not depend on
+    # it), shared by the streams
+    hint = torch.zeros(N, dtype=torch.float32, device=dev)
     labels = torch.empty((B, L, n), dtype=torch.int32, device=dev)
     for j in range(B):
         labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j])
@@ -334,7 +338,7 @@ def main():
                 if j >= RING:
                     streams[ks].wait_event(ev_s[j - RING])  # the slot's previous bootstrap is consumed
                 engs[ks].gather_rows_t(pcs_cm, N, d, boots[j], rows_s[slot])
-                engs[ks].knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[slot], 20, knn_s[slot])
+                engs[ks].knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[slot], 20, knn_s[slot], hint)
                 ev_k[j].record(streams[ks])
             with torch.cuda.stream(streams[ss]):
                 streams[ss].wait_event(ev_k[j])
@@ -365,7 +369,7 @@ def main():
             e = engs[si]
             with torch.cuda.stream(streams[si]):
                 e.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[si])
-                e.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[si], 20, knn_s[si])
+                e.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[si], 20, knn_s[si], hint)
                 e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
                 e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_t[0] += time.perf_counter() - th
@@ -394,7 +398,8 @@ def main():
             raise RuntimeError(f"SNN row capacity too small: {rcap}")
     need = nedges.max(0).values.tolist()
     eng.gather_rows_t(pcs_cm, N, d, boots[0], rows)
-    fb = eng.knn_boot_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, stats=True)  # certification statistics
+    fb = eng.knn_boot_hint_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, hint, stats=True)  # certification statistics
+    fb_cold = eng.knn_boot_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, stats=True)
 
     # ---------------- timed region (library timers off: their event records
     # cost host time on every launch group)
@@ -429,7 +434,7 @@ def main():
         th = time.perf_counter()
         with torch.cuda.stream(streams[0]):
             eng.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[0])
-            eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[0], 20, knn_s[0])
+            eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[0], 20, knn_s[0], hint)
             eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
             eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_idle.append(time.perf_counter() - th)
@@ -440,11 +445,15 @@ def main():
     # they overlap other bootstraps' kernels
     eng.timing(True)
     eng.timing_read("knn_screen")
-    for j in range(min(B, 8)):
+    for j in range(min(B, 8)):  # as in the timed region: warm-started by earlier bootstraps
         eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
-        eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn)
+        eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn, hint)
     u_iso = float(np.mean(uniq[:min(B, 8)]))  # the screen searches the distinct cells
     iso_screen = eng.timing_read("knn_screen")
+    for j in range(min(B, 8)):  # cold: no hint (the first bootstrap of a run)
+        eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+        eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn)
+    iso_cold = eng.timing_read("knn_screen")
     eng.timing(False)
     if G > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -483,7 +492,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "dtype_detail": "kNN order exact in f64 (distinct cells: fp16 hi/lo x3 MFMA screen, f32 accumulate, "
-                        "f64 certify, exact f64 expansion to rows); "
+                        "f64 certify, exact f64 expansion to rows; screen warm-started by earlier bootstraps' "
+                        "certified distances); "
                         "silhouette f64 with fixed-point sums; co-cluster int8 MFMA, int32 counts",
         "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA; synthetic clusterings in place of host Leiden",
         "config": {
@@ -504,6 +514,8 @@ def main():
             "algorithmic_per_launch": f"2*u^2*d = {flops:.3e} flop (u={u_iso:.0f} distinct cells of the n={n} "
                                       f"bootstrap rows, d={d}), SURVEY 8(d) over the rows the screen searches",
             "avg_launch_ms": round(ms_screen, 4),
+            "avg_launch_ms_cold": round(iso_cold[0] / max(iso_cold[1], 1), 4),
+            "cold_note": "the same launches without the warm start (no certified distances from earlier bootstraps)",
             "avg_launch_ms_note": f"{iso_screen[1]} launches timed in isolation after the timed region; "
                                   f"in the timed region {S} bootstraps overlap (screen avg "
                                   f"{kt['knn_screen'][0] / max(kt['knn_screen'][1], 1):.3f} ms under overlap)",
@@ -529,6 +541,7 @@ def main():
         "host_launch_ms_per_boot_idle_gpu": round(host_idle_ms, 3),
         "cocluster_avg_ms": round(coc_ms, 3),
         "knn_fallback_rows_last_boot": int(fb[1]),
+        "knn_fallback_rows_last_boot_cold": int(fb_cold[1]),
         "snn_edges_max_per_boot": [int(e) for e in need],
     }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:

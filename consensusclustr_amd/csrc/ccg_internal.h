@@ -50,6 +50,7 @@ enum ccg_ws_slot {
     WS_COC_D,        // consensus kNN candidate path: the row-permuted assignment matrix
     WS_COC_E,        // consensus kNN candidate path: per-row candidate lists
     WS_COC_F,        // consensus kNN candidate path: thresholds, counters, flags
+    WS_HINT,         // kNN: per-cell threshold hints shared by the bootstraps of one host call
     WS_NSLOTS
 };
 

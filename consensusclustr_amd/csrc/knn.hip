@@ -143,6 +143,9 @@ static inline int knn_ksteps(int d) { return d + 1 <= 16 ? 1 : (d + 1 <= 32 ? 2 
 #define KNN_PAIR 0          // two tiles per step (two MFMA chains in flight)
 #endif
 #define KNN_NORM_SHIFT 15   // the query's norm-dimension value 2^15 (exact in fp16)
+#ifndef KNN_HINT_MARGIN
+#define KNN_HINT_MARGIN 0.15  // relative slack on a hinted squared distance (see ccg_knn_boot_hint_dev)
+#endif
 #define KNN_PAD_NORM (-65504.0f)  // padding rows: below every real value (|v| < 1.6e9 < 2^31)
 
 __device__ __forceinline__ int knn_scale_exp(const unsigned* maxabs_bits) {
@@ -163,7 +166,8 @@ __device__ __forceinline__ void knn_split16(double xs, _Float16& hi, _Float16& l
 template <int KSTEPS>
 __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, int64_t npad, int d,
                                   const unsigned* __restrict__ maxabs_bits, const int* __restrict__ perm,
-                                  uint4* __restrict__ img, double* __restrict__ inv_scale2) {
+                                  uint4* __restrict__ img, double* __restrict__ inv_scale2,
+                                  const float* __restrict__ row_hint, float* __restrict__ pos_t0) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // position in spatial order
     if (r >= npad) return;
     const int64_t src = r < n ? (perm ? perm[r] : r) : -1;  // -1: padding position (segment padding or r >= n)
@@ -175,6 +179,14 @@ __global__ void knn_prep16_kernel(const double* __restrict__ rows, int64_t n, in
     for (int k = 0; k < d; ++k) {
         const double x = valid ? rows[src * d + k] : 0.0;
         nr += x * x;
+    }
+    if (pos_t0) {
+        // the screen's initial rejection threshold from the row's hint (a
+        // squared distance its kq-th nearest distinct row is expected within):
+        // v = x.y - |y|^2/2 > t0  <=>  |x - y|^2 < hint (scaled by 2^2e)
+        const float hint = valid && row_hint ? row_hint[src] : 0.0f;
+        pos_t0[r] = hint > 0.0f ? (float)(0.5 * ldexp(nr - (double)hint * (1.0 + KNN_HINT_MARGIN), 2 * e))
+                                : -INFINITY;
     }
 #pragma unroll
     for (int k = 0; k < KSTEPS * 16; ++k) {
@@ -427,7 +439,7 @@ __device__ __forceinline__ void knn_wait_vmcnt() {
 template <int KSTEPS, int KP, int QC = KNN_QCAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) void knn_screen16_kernel(
     const uint4* __restrict__ img, int n, int nchunks, int d, int* __restrict__ cand_idx,
-    float* __restrict__ cand_thr, const int4* __restrict__ blk) {
+    float* __restrict__ cand_thr, const int4* __restrict__ blk, const float* __restrict__ pos_t0) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
     constexpr int ROWB = KSTEPS * 64;               // bytes per row
     constexpr int KNN_CHUNK = knn_chunk(KSTEPS);
@@ -516,7 +528,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
     const int nck = ch - cl;
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
     KST_DECL;
-    float T = -INFINITY;  // rejection threshold (see below)
+    // rejection threshold (see below); a hinted row starts at its hint's
+    // threshold, which every later T keeps as a floor (T0 is itself a valid
+    // rejection threshold for both halves, so certification stays exact)
+    const float T0 = pos_t0 ? pos_t0[qrow] : -INFINITY;
+    float T = T0;
     int qc = 0;           // this lane's queued candidates
     bool tdirty = false;  // lists changed since T was last set to the union threshold
 #define KNN_FLUSH()                                                                   \
@@ -620,7 +636,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
             KST(2);                                                                         \
         }                                                                                   \
         if (tdirty) {                                                                       \
-            T = union_kth<KP>(lv);                                                          \
+            T = fmaxf(T0, union_kth<KP>(lv));                                               \
             tdirty = false;                                                                 \
             KST(4);                                                                         \
         }                                                                                   \
@@ -679,7 +695,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
     KST(1);
     KNN_FLUSH();
     KST(3);
-    T = union_kth<KP>(lv);
+    T = fmaxf(T0, union_kth<KP>(lv));
     KST(4);
     KST_FLUSH_OUT();
 #undef KNN_FLUSH
@@ -1066,7 +1082,8 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
 
 // dist_sq: out_dist receives the squared distances (the certified fp64 sums)
 static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, int32_t* out_idx,
-                   double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg, bool dist_sq = false) {
+                   double* out_dist, ccg_knn_stats* stats, hipStream_t st, const KnnSegs* sg, bool dist_sq = false,
+                   const float* row_hint = nullptr) {
     const int KP = kmax <= KNN_KP ? KNN_KP : KNN_KP_BIG;
     const int64_t npos = sg ? sg->npos : n;  // screening positions
     int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * npos * 2 * KP);
@@ -1086,8 +1103,9 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const int KSTEPS = knn_ksteps(d);
         const int KNN_CHUNK = knn_chunk(KSTEPS);
         const int64_t npad = ccg_cdiv(npos, KNN_CHUNK) * KNN_CHUNK;
-        uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + 256);
+        uint4* img = (uint4*)ccg_ws(ctx, WS_REFS32, (size_t)npad * 64 * KSTEPS + sizeof(float) * npad + 256);
         if (!img) return CCG_ENOMEM;
+        float* pos_t0 = row_hint ? (float*)((char*)img + (size_t)npad * 64 * KSTEPS) : nullptr;
         unsigned* bnd = misc + 8;  // [2 KNN_MD]: minima then maxima of the leading coordinates
         const bool buckets = !sg && !KNN_NO_MORTON && KNN_MORTON_DIMS * KNN_MORTON_BITS <= 15;
         const int64_t NB = 1LL << (KNN_MORTON_DIMS * KNN_MORTON_BITS);
@@ -1126,17 +1144,20 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         }
         const unsigned pg = (unsigned)ccg_cdiv(npad, 256);
         if (KSTEPS == 1)
-            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
+            knn_prep16_kernel<1><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2,
+                                                      row_hint, pos_t0);
         else if (KSTEPS == 2)
-            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
+            knn_prep16_kernel<2><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2,
+                                                      row_hint, pos_t0);
         else
-            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2);
+            knn_prep16_kernel<4><<<pg, 256, 0, st>>>(rows, npos, npad, d, mbits, order_perm, img, inv_scale2,
+                                                      row_hint, pos_t0);
         const int nch = (int)(npad / KNN_CHUNK);
         const unsigned grid = (unsigned)ccg_cdiv(npos, KNN_QPB);
         const int4* blk = sg ? sg->blk : nullptr;
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
 #define CCG_SCREEN16(KS_, KP_) \
-    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk)
+    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk, pos_t0)
         if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
@@ -1302,12 +1323,28 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
 // rows of each cell's first copy: coalesced, unlike a gather from the
 // column-major PCs
 __global__ void kb_urows_kernel(const double* __restrict__ rows, int d, int u, const int* __restrict__ ustart,
-                                const int* __restrict__ srow, double* __restrict__ urows) {
+                                const int* __restrict__ srow, double* __restrict__ urows,
+                                const int32_t* __restrict__ idx, const float* __restrict__ cell_hint,
+                                float* __restrict__ urow_hint) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)u * d) return;
     const int64_t uid = t / d;
     const int k = (int)(t - uid * d);
-    urows[t] = rows[(int64_t)srow[ustart[uid]] * d + k];
+    const int r0 = srow[ustart[uid]];
+    urows[t] = rows[(int64_t)r0 * d + k];
+    if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
+}
+
+// The hint for the next bootstrap: each distinct cell's certified squared
+// distance to its kq-th nearest distinct cell (rows that went to the exact
+// fallback keep their previous hint).
+__global__ void kb_hint_kernel(int u, int kq, const int* __restrict__ ustart, const int* __restrict__ srow,
+                               const int32_t* __restrict__ idx, const double* __restrict__ ud2,
+                               float* __restrict__ cell_hint) {
+    const int64_t uid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (uid >= u || kq < 1) return;
+    const double v = ud2[uid * kq + kq - 1];
+    if (v > 0.0 && v < 3.0e38) cell_hint[idx[srow[ustart[uid]]]] = (float)v;
 }
 
 #define KB_GMAX 33  // cells of one merge group (the own cell + kq <= 32 neighbours)
@@ -1404,6 +1441,13 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
 extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n,
                                 int n_unique, const double* rows, int kmax, int32_t* out_idx, double* out_dist,
                                 ccg_knn_stats* stats, void* stream) {
+    return ccg_knn_boot_hint_dev(ctx, pcs, N, d, idx, n, n_unique, rows, kmax, out_idx, out_dist, nullptr, stats,
+                                 stream);
+}
+
+extern "C" int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx,
+                                     int64_t n, int n_unique, const double* rows, int kmax, int32_t* out_idx,
+                                     double* out_dist, float* cell_hint, ccg_knn_stats* stats, void* stream) {
     CCG_REQUIRE(ctx && pcs && idx && rows && out_idx, "ccg_knn_boot_dev: NULL argument");
     CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boot_dev: d=%d must be in [1, 63]", d);
     CCG_REQUIRE(N >= 1 && N < (1LL << 31) && n >= 2 && n < (1LL << 30), "ccg_knn_boot_dev: bad sizes");
@@ -1419,7 +1463,8 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
     char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + (size_t)ucap + 1));
     double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)ucap * (d + kmax) +
-                                                      sizeof(int32_t) * (size_t)ucap * kmax + 64);
+                                                      sizeof(int32_t) * (size_t)ucap * kmax +
+                                                      sizeof(float) * (size_t)ucap + 64);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
     if (!fail_list || !ta || !urows || !misc) return CCG_ENOMEM;
     int64_t* head = (int64_t*)ta;                // [n + 1] heads, then their exclusive scan in place
@@ -1456,11 +1501,15 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
     kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, row2u, ctx->d_err);
     // 3. the distinct cells' rows and their kq nearest distinct cells
-    kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows);
+    float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
+    kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
+                                                                            cell_hint, urow_hint);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1) {
-        rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true);
+        rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true, urow_hint);
         if (rc) return rc;
+        if (cell_hint)
+            kb_hint_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, kq, ustart, srow, idx, ud2, cell_hint);
     }
 #ifdef KNN_EXP_SCREEN_ONLY
     ccg_timer_stop(ctx, t_all, st);
@@ -1503,6 +1552,11 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
     CCG_HIP(hipMemcpyAsync(dpcs, pcs, sizeof(double) * N * d, hipMemcpyHostToDevice, st));
     CCG_HIP(hipMemcpyAsync(didx, boot_idx, sizeof(int32_t) * n * nb, hipMemcpyHostToDevice, st));
     ccg_knn_stats acc = {0, 0};
+    // the bootstraps of one call share a hint array (each bootstrap's certified
+    // k-th distances warm-start the next one's screen; results are exact either way)
+    float* hint = (float*)ccg_ws(ctx, WS_HINT, sizeof(float) * N);
+    if (!hint) return CCG_ENOMEM;
+    CCG_HIP(hipMemsetAsync(hint, 0, sizeof(float) * N, st));
     std::vector<unsigned char> seen(N);
     for (int b = 0; b < nb; ++b) {
         // the bootstrap's distinct cells (R: length(unique(idx)))
@@ -1516,7 +1570,8 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
         int rc = ccg_gather_rows_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, rows, st);
         if (rc) return rc;
         ccg_knn_stats s;
-        rc = ccg_knn_boot_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, dout, ddist, &s, st);
+        rc = ccg_knn_boot_hint_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, dout, ddist, hint, &s,
+                                   st);
         if (rc) return rc;
         acc.queries += s.queries;
         acc.fallback += s.fallback;

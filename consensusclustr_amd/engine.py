@@ -317,6 +317,21 @@ class Engine:
             return self.last_knn_stats
         return None
 
+    def knn_boot_hint_t(self, pcs_cm, N, d, idx, n_unique, rows, kmax, out_idx, cell_hint, out_dist=None,
+                        stats=False):
+        """knn_boot_t with a warm start (ccg_knn_boot_hint_dev): cell_hint an
+        (N,) float32 tensor of per-cell k-th squared distances (0 = none),
+        read and updated in place.  Results do not depend on it."""
+        n = idx.numel()
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_boot_hint_dev(self.ctx, _ptr(pcs_cm), N, d, _ptr(idx), n, int(n_unique), _ptr(rows),
+                                             kmax, _ptr(out_idx), _ptr(out_dist), _ptr(cell_hint),
+                                             ctypes.byref(st) if stats else None, _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
     def knn_segments_t(self, rows, seg_off, kmax, out_idx, out_dist=None, stats=False):
         """Device flavour: rows (n, d) tensor of concatenated segments, seg_off a
         host int64 array of nseg+1 offsets; out_idx (n, kmax) segment-local."""

@@ -143,6 +143,21 @@ int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                      const double* rows, int kmax, int32_t* out_idx,
                      double* out_dist, ccg_knn_stats* stats, void* stream);
 
+/* ccg_knn_boot_dev with a warm start: cell_hint (device, N floats, in/out)
+ * holds per cell a squared distance -- 0 = none -- that the cell's kq-th
+ * nearest distinct cell is expected within (kq = min(kmax, n_unique - 1)).
+ * The screen starts each hinted query with that radius (plus 15%) as its
+ * rejection threshold instead of nothing, and on return every searched cell's
+ * entry holds its certified kq-th distance for the next bootstrap of the same
+ * PC matrix.  Results are bit-identical with any hint values: a hint that is
+ * too tight only sends the row to the exact fallback.  Concurrent calls may
+ * share one array (a raced entry is still a valid hint). */
+int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                          const int32_t* idx, int64_t n, int n_unique,
+                          const double* rows, int kmax, int32_t* out_idx,
+                          double* out_dist, float* cell_hint,
+                          ccg_knn_stats* stats, void* stream);
+
 /* Batched kNN over independent segments: the iterate=TRUE subclustering
  * (R/consensusClust.R:541-566, BASELINE config 5) runs one bootstrap loop per
  * subcluster; their (small) bootstrap matrices are searched in ONE set of

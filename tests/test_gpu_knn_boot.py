@@ -115,3 +115,39 @@ def test_knn_boot_dev_wrong_unique_count(engine):
         engine.check_errors()
     # the context is usable again afterwards
     _check(engine, pcs, idx, 10)
+
+
+def test_knn_boot_hint_warm_start_is_exact(engine):
+    """ccg_knn_boot_hint_dev: each bootstrap's certified k-th distances seed
+    the next bootstrap's screen; outputs equal the un-hinted search bit for
+    bit, with good hints (few fallbacks), absurdly tight hints (every row to
+    the exact fallback) and loose ones."""
+    import torch
+    rng = np.random.default_rng(91)
+    N, d = 30000, 20
+    centers = rng.normal(scale=3.0, size=(9, d))
+    pcs = centers[rng.integers(0, 9, N)] + rng.normal(size=(N, d))
+    pcs_cm = torch.from_numpy(np.ascontiguousarray(pcs.T)).cuda()
+    hint = torch.zeros(N, dtype=torch.float32, device="cuda")
+    n = int(0.9 * N)
+    rows = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    a = torch.empty((n, 20), dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    da = torch.empty((n, 20), dtype=torch.float64, device="cuda")
+    db = torch.empty_like(da)
+    fb = []
+    for t in range(5):
+        boot_np = rng.integers(0, N, n).astype(np.int32)
+        boot = torch.from_numpy(boot_np).cuda()
+        u = len(np.unique(boot_np))
+        engine.gather_rows_t(pcs_cm, N, d, boot, rows)
+        engine.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, a, out_dist=da)
+        if t == 3:
+            hint.fill_(1e-6)       # far too tight: every hinted row falls back
+        elif t == 4:
+            hint.fill_(1e6)        # far too loose: a plain screen
+        fb.append(engine.knn_boot_hint_t(pcs_cm, N, d, boot, u, rows, 20, b, hint, out_dist=db, stats=True)[1])
+        torch.cuda.synchronize()
+        assert torch.equal(a, b) and torch.equal(da, db), t
+        assert float(hint.min()) >= 0.0
+    assert max(fb[1:3]) < n // 100  # warm-started bootstraps certify almost every row
