@@ -332,7 +332,10 @@ def stability_matrix(final, A, is_char=False, engine=None):
     (ccg_contingency); the ratio is host arithmetic (ccg_pairwise_rand_ratio).
     Returns None where the reference's tryCatch returns NULL (per-bootstrap
     matrices of different sizes), else the K x K matrix in level order with
-    diag 1 and NA -> 1 (:485-487)."""
+    diag 1 and NA -> 1 (:485-487).  pairwiseRand(mode="ratio") fills only the
+    lower triangle, so the upper one averages to NA and becomes 1: the merge's
+    which(stab == min) then sees each pair once (parity unpinned: bluster is
+    not installed; restated from its documented output)."""
     import math
     from .engine import pairwise_rand_ratio
     eng = engine or default_engine()
@@ -345,7 +348,9 @@ def stability_matrix(final, A, is_char=False, engine=None):
     for b in range(tab.shape[0]):
         t = tab[b]
         present = np.flatnonzero(t[:, 1:].sum(1) > 0)  # ref levels in f[mask]
-        mats.append(pairwise_rand_ratio(t[present]))
+        r = pairwise_rand_ratio(t[present])
+        r[np.triu_indices_from(r, 1)] = np.nan  # bluster fills the lower triangle only (upper NA)
+        mats.append(r)
     if len({m.shape for m in mats}) != 1:
         return None  # simplify2array cannot stack -> apply() errors -> NULL
     arr = np.stack(mats)

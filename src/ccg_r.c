@@ -392,8 +392,9 @@ SEXP ccg_r_stability(SEXP e, SEXP A, SEXP f, SEXP K, SEXP adjusted) {
         }
         CALL("ccg_pairwise_rand_ratio", ccg_pairwise_rand_ratio(kb, C, sub, adj, r));
         SEXP m = PROTECT(Rf_allocMatrix(REALSXP, kb, kb));
+        /* bluster's pairwiseRand(mode = "ratio") fills the lower triangle only */
         for (int p = 0; p < kb; ++p)
-            for (int q = 0; q < kb; ++q) REAL(m)[p + (R_xlen_t)q * kb] = r[(size_t)p * kb + q];
+            for (int q = 0; q < kb; ++q) REAL(m)[p + (R_xlen_t)q * kb] = q > p ? NA_REAL : r[(size_t)p * kb + q];
         SET_VECTOR_ELT(out, b, m);
         UNPROTECT(1);
     }

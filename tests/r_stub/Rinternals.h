@@ -16,6 +16,8 @@ typedef unsigned int SEXPTYPE;
 typedef int Rboolean;
 extern int R_NaInt;
 #define NA_INTEGER R_NaInt
+extern double R_NaReal;
+#define NA_REAL R_NaReal
 extern SEXP R_NilValue;
 extern SEXP R_NamesSymbol;
 SEXP Rf_install(const char*);

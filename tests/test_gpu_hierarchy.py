@@ -120,7 +120,9 @@ def _literal_merge(final, A, D, N, kNum, minStability):
         alt = A[b][mask]
         tab = np.array([[sum(1 for r, a in zip(ref, alt) if r == p and a == c) for c in range(1, int(A.max()) + 1)]
                         for p in present])
-        mats.append(O.pairwise_rand_ratio(tab))
+        m = O.pairwise_rand_ratio(tab)
+        m[np.triu_indices_from(m, 1)] = np.nan  # pairwiseRand(mode="ratio"): lower triangle only
+        mats.append(m)
     if len({m.shape for m in mats}) != 1:
         return np.ones(len(f), np.int64), None
     arr = np.stack(mats)
