@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--pipeline", default="",
                     help="NK,NS: stage-split schedule instead of --streams: NK kNN streams feed NS "
                          "SNN+silhouette streams through a ring of bootstrap buffers")
+    ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
+                    help="table: one cell table per step (ccg_knn_table_dev) filtered per bootstrap; "
+                         "screen: a screen per bootstrap (warm-started)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
@@ -288,6 +291,19 @@ def main():
     # the screen's warm start (ccg_knn_boot_hint_dev; results do not depend on
     # it), shared by the streams
     hint = torch.zeros(N, dtype=torch.float32, device=dev)
+    # the cell table (ccg_knn_table_dev): every cell's KT nearest other cells,
+    # recomputed inside every timed step, then filtered per bootstrap
+    KT = 48
+    use_table = args.knn_path == "table"
+    tab_idx = torch.empty((N, KT), dtype=torch.int32, device=dev)
+    tab_d2 = torch.empty((N, KT), dtype=torch.float64, device=dev)
+
+    def boot_knn(e, j, rows_j, knn_j):
+        if use_table:
+            e.knn_boot_table_t(pcs_cm, N, d, boots[j], uniq[j], rows_j, 20, tab_idx, tab_d2, knn_j)
+        else:
+            e.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_j, 20, knn_j, hint)
+
     labels = torch.empty((B, L, n), dtype=torch.int32, device=dev)
     for j in range(B):
         labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j])
@@ -330,6 +346,8 @@ def main():
         # SNN + silhouette streams (issue/LDS-bound) by up to RING bootstraps,
         # so the two kinds of work always share the GPU
         cur = torch.cuda.current_stream()
+        if use_table:
+            eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
         for st_ in streams:
             st_.wait_stream(cur)
         for j in range(B):
@@ -338,7 +356,7 @@ def main():
                 if j >= RING:
                     streams[ks].wait_event(ev_s[j - RING])  # the slot's previous bootstrap is consumed
                 engs[ks].gather_rows_t(pcs_cm, N, d, boots[j], rows_s[slot])
-                engs[ks].knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[slot], 20, knn_s[slot], hint)
+                boot_knn(engs[ks], j, rows_s[slot], knn_s[slot])
                 ev_k[j].record(streams[ks])
             with torch.cuda.stream(streams[ss]):
                 streams[ss].wait_event(ev_k[j])
@@ -362,6 +380,8 @@ def main():
         # engine context (workspaces), so one bootstrap's latency-bound SNN
         # build overlaps another's MFMA-bound kNN screen
         cur = torch.cuda.current_stream()
+        if use_table:  # one table per step: every bootstrap of the step filters it
+            eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
         for st_ in streams:
             st_.wait_stream(cur)
         for j in range(B):
@@ -369,7 +389,7 @@ def main():
             e = engs[si]
             with torch.cuda.stream(streams[si]):
                 e.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[si])
-                e.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[si], 20, knn_s[si], hint)
+                boot_knn(e, j, rows_s[si], knn_s[si])
                 e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
                 e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_t[0] += time.perf_counter() - th
@@ -400,6 +420,8 @@ def main():
     eng.gather_rows_t(pcs_cm, N, d, boots[0], rows)
     fb = eng.knn_boot_hint_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, hint, stats=True)  # certification statistics
     fb_cold = eng.knn_boot_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, stats=True)
+    fb_tab_build = eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2, stats=True)
+    fb_tab = eng.knn_boot_table_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, tab_idx, tab_d2, knn, stats=True)
 
     # ---------------- timed region (library timers off: their event records
     # cost host time on every launch group)
@@ -434,22 +456,34 @@ def main():
         th = time.perf_counter()
         with torch.cuda.stream(streams[0]):
             eng.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[0])
-            eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows_s[0], 20, knn_s[0], hint)
+            boot_knn(eng, j, rows_s[0], knn_s[0])
             eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
             eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_idle.append(time.perf_counter() - th)
         torch.cuda.synchronize()
     host_idle_ms = 1000 * float(np.median(host_idle))
-    # roofline of the kNN screen: its launches measured in isolation (one
-    # bootstrap at a time, nothing else on the GPU), since in the timed region
-    # they overlap other bootstraps' kernels
+    # roofline of the kNN screens, measured in isolation (one launch at a
+    # time, nothing else on the GPU), since in the timed region they overlap
+    # other bootstraps' kernels: the per-step cell-table screen over all N
+    # cells, and (for comparison) the per-bootstrap screen over the u
+    # distinct cells, warm-started and cold
     eng.timing(True)
     eng.timing_read("knn_screen")
-    for j in range(min(B, 8)):  # as in the timed region: warm-started by earlier bootstraps
+    eng.timing_read("knn_total")
+    for _ in range(3):
+        eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
+    iso_table = eng.timing_read("knn_screen")
+    iso_table_total = eng.timing_read("knn_total")
+    for j in range(min(B, 8)):
+        eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+        eng.knn_boot_table_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, tab_idx, tab_d2, knn)
+    iso_boot_table = eng.timing_read("knn_total")
+    for j in range(min(B, 8)):  # as in the screen path: warm-started by earlier bootstraps
         eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
         eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn, hint)
     u_iso = float(np.mean(uniq[:min(B, 8)]))  # the screen searches the distinct cells
     iso_screen = eng.timing_read("knn_screen")
+    iso_screen_total = eng.timing_read("knn_total")
     for j in range(min(B, 8)):  # cold: no hint (the first bootstrap of a run)
         eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
         eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn)
@@ -461,14 +495,20 @@ def main():
         el = t.item()
 
     value = G * B * args.steps / el
-    ms_screen = iso_screen[0] / max(iso_screen[1], 1)
-    # SURVEY 8(d)'s kNN F = 2 n^2 d per bootstrap, over the u distinct cells
-    # the screen actually searches (the copies are expanded afterwards)
+    avg = lambda r: r[0] / max(r[1], 1)  # noqa: E731
+    ms_screen = avg(iso_screen)
+    ms_table = avg(iso_table)
+    # SURVEY 8(d)'s kNN F = 2 n^2 d: for the cell-table screen over the N
+    # cells, per bootstrap screen over the u distinct cells it searches
+    flops_table = 2.0 * N * N * d
     flops = 2.0 * u_iso * u_iso * d
     achieved = flops / (ms_screen * 1e-3) / 1e12
+    achieved_table = flops_table / (ms_table * 1e-3) / 1e12
     # the screen runs on the fp16 MFMA pipe: 3 products (hi.hi, hi.lo, lo.hi)
     # per 16-dim block, d padded to 16*ceil(d/16)
-    mfma_exec = 3 * 2.0 * u_iso * u_iso * (16 * ((d + 15) // 16))
+    kpad = 16 * ((d + 15) // 16)
+    mfma_exec = 3 * 2.0 * u_iso * u_iso * kpad
+    mfma_exec_table = 3 * 2.0 * N * N * kpad
     # co-cluster roofline: OPS = 2 * P * (sum_b C_b + B) over this rank's slab
     colC = int(A_full.max(dim=1).values.to(torch.int64).sum().item())  # sum_b C_b over all ranks' columns
     coc_ops = 2.0 * P * (colC + G * B)
@@ -477,6 +517,45 @@ def main():
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("knn_screen_bytes_per_launch")
     per_step = {w: round(v[0], 3) for w, v in kt.items()}  # the one timer step
+    roof_screen = {
+        "kernel": "knn_screen16_kernel<2,20,28> per bootstrap (fp16 hi/lo split, v_mfma_f32_32x32x16_f16)",
+        "bound": "mfma",
+        "achieved": round(achieved, 2),
+        "peak": PEAK_F16_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_F16_TFLOPS, 4),
+        "traffic": traffic,
+        "algorithmic_per_launch": f"2*u^2*d = {flops:.3e} flop (u={u_iso:.0f} distinct cells of the n={n} "
+                                  f"bootstrap rows, d={d}), SURVEY 8(d) over the rows the screen searches",
+        "avg_launch_ms": round(ms_screen, 4),
+        "avg_launch_ms_cold": round(avg(iso_cold), 4),
+        "cold_note": "the same launches without the warm start (no certified distances from earlier bootstraps)",
+        "knn_total_ms_per_boot": round(avg(iso_screen_total), 4),
+        "avg_launch_ms_note": f"{iso_screen[1]} launches timed in isolation after the timed region",
+        "mfma_flops_executed_per_launch": mfma_exec,
+        "mfma_pipe_frac": round(mfma_exec / (ms_screen * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
+    }
+    roof_table = {
+        "kernel": "knn_screen16_kernel<2,32,56> cell table over all N cells, once per step "
+                  "(fp16 hi/lo split, v_mfma_f32_32x32x16_f16)",
+        "bound": "mfma",
+        "achieved": round(achieved_table, 2),
+        "peak": PEAK_F16_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved_table / PEAK_F16_TFLOPS, 4),
+        "traffic": None,
+        "algorithmic_per_launch": f"2*N^2*d = {flops_table:.3e} flop (N={N} cells, d={d}, K={KT} neighbours "
+                                  "each), SURVEY 8(d)'s 2 n^2 d over the cells the table searches",
+        "avg_launch_ms": round(ms_table, 4),
+        "table_total_ms": round(avg(iso_table_total), 4),
+        "table_fallback_cells": int(fb_tab_build[1]),
+        "knn_total_ms_per_boot_from_table": round(avg(iso_boot_table), 4),
+        "boot_fallback_last_boot": int(fb_tab[1]),
+        "avg_launch_ms_note": f"{iso_table[1]} launches timed in isolation after the timed region; one per step "
+                              f"serves the step's {B} bootstraps",
+        "mfma_flops_executed_per_launch": mfma_exec_table,
+        "mfma_pipe_frac": round(mfma_exec_table / (ms_table * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
+    }
     coc_ms = kt["cocluster"][0] / max(kt["cocluster"][1], 1)
     out = {
         "metric": METRIC,
@@ -491,9 +570,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "dtype_detail": "kNN order exact in f64 (distinct cells: fp16 hi/lo x3 MFMA screen, f32 accumulate, "
-                        "f64 certify, exact f64 expansion to rows; screen warm-started by earlier bootstraps' "
-                        "certified distances); "
+        "dtype_detail": ("kNN order exact in f64 (cell table over all cells once per step: fp16 hi/lo x3 MFMA "
+                         "screen, f32 accumulate, f64 certify; per bootstrap the table's present entries, exact "
+                         "f64 search for cells short of kq, exact f64 expansion to rows); " if use_table else
+                         "kNN order exact in f64 (distinct cells: fp16 hi/lo x3 MFMA screen, f32 accumulate, "
+                         "f64 certify, exact f64 expansion to rows; screen warm-started by earlier bootstraps' "
+                         "certified distances); ") +
                         "silhouette f64 with fixed-point sums; co-cluster int8 MFMA, int32 counts",
         "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA; synthetic clusterings in place of host Leiden",
         "config": {
@@ -502,27 +584,10 @@ def main():
             "cells": N, "pcs": d, "bootstrap_rows": n, "distinct_cells_mean": round(float(np.mean(uniq)), 1),
             "boots_per_gpu": B, "clusterings_per_boot": L,
             "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}", "streams_per_gpu": S,
+            "knn_path": args.knn_path,
         },
-        "roofline": {
-            "kernel": "knn_screen16_kernel (fp16 hi/lo split, v_mfma_f32_32x32x16_f16)",
-            "bound": "mfma",
-            "achieved": round(achieved, 2),
-            "peak": PEAK_F16_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_F16_TFLOPS, 4),
-            "traffic": traffic,
-            "algorithmic_per_launch": f"2*u^2*d = {flops:.3e} flop (u={u_iso:.0f} distinct cells of the n={n} "
-                                      f"bootstrap rows, d={d}), SURVEY 8(d) over the rows the screen searches",
-            "avg_launch_ms": round(ms_screen, 4),
-            "avg_launch_ms_cold": round(iso_cold[0] / max(iso_cold[1], 1), 4),
-            "cold_note": "the same launches without the warm start (no certified distances from earlier bootstraps)",
-            "avg_launch_ms_note": f"{iso_screen[1]} launches timed in isolation after the timed region; "
-                                  f"in the timed region {S} bootstraps overlap (screen avg "
-                                  f"{kt['knn_screen'][0] / max(kt['knn_screen'][1], 1):.3f} ms under overlap)",
-            "mfma_flops_executed_per_launch": mfma_exec,
-            "mfma_pipe_frac": round(mfma_exec / (ms_screen * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
-            "fp32_equivalent_frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-        },
+        "roofline": (roof_table if use_table else roof_screen),
+        "roofline_screen_path" if use_table else "roofline_table_path": (roof_screen if use_table else roof_table),
         "roofline_cocluster": {
             "kernel": "cof_tile_kernel (one-hot int8, v_mfma_i32_32x32x32_i8)",
             "bound": "mfma",

@@ -51,6 +51,9 @@ enum ccg_ws_slot {
     WS_COC_E,        // consensus kNN candidate path: per-row candidate lists
     WS_COC_F,        // consensus kNN candidate path: thresholds, counters, flags
     WS_HINT,         // kNN: per-cell threshold hints shared by the bootstraps of one host call
+    WS_TAB_ROWS,     // kNN cell table: the PCs row-major (certify / fallback rows)
+    WS_TAB_MAP,      // kNN cell table: cell -> distinct-cell id of a bootstrap (-1: absent)
+    WS_TAB,          // kNN cell table of a host call (ccg_knn_boot): ids then squared distances
     WS_NSLOTS
 };
 

@@ -31,11 +31,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define KNN_KP 20          // candidates kept per half-lane for kmax <= 20
 #define KNN_KP_BIG 32      // ... for 20 < kmax <= 32 (2*KP <= 64 lanes in certify)
+#define KNN_TAB_K 48       // cell tables (ccg_knn_table_dev): up to 48 neighbours from KP = 32 lists
+#define KNN_TABLE_MIN_BOOTS 8  // ccg_knn_boot: a cell table for calls of at least this many bootstraps
 #ifndef KNN_TMARGIN
 #define KNN_TMARGIN 8      // screen threshold: rank KP + KNN_TMARGIN of the two half-lists' union
 #endif
 #define KNN_QPB 128        // queries per 256-thread block (4 waves x 32)
-#define KNN_FB_K 32        // fallback list length (>= kmax)
+#define KNN_FB_K 48        // fallback list length (>= kmax)
 #ifndef KNN_FB_S
 #define KNN_FB_S 64        // max reference ranges per failed row
 #endif
@@ -87,7 +89,8 @@ __device__ __forceinline__ void list_insert_par(float (&lv)[KP], int (&li)[KP], 
     li[0] = keep[0] ? li[0] : id;
 }
 
-// R-th largest (R = KP + KNN_TMARGIN) of the union of this half-lane's list
+// R-th largest (R = KP + KNN_TMARGIN; kmax + KNN_TMARGIN for the cell
+// tables' kmax > KP) of the union of this half-lane's list
 // and its partner's (lane ^ 32), both sorted descending: max over splits i
 // of min(mine[i-1], other[R-1-i]).  The partner's entries arrive by
 // v_permlane32_swap (no LDS).  Every ref either half has rejected or evicted
@@ -95,9 +98,9 @@ __device__ __forceinline__ void list_insert_par(float (&lv)[KP], int (&li)[KP], 
 // tighter than max(thr_h0, thr_h1) (about rank 2*KP of the union); the
 // margin of KNN_TMARGIN ranks above k keeps certification (excl - E > dK)
 // provable.
-template <int KP>
+template <int KP, int R>
 __device__ __forceinline__ float union_kth(const float (&lv)[KP]) {
-    constexpr int R = KP + KNN_TMARGIN;
+    static_assert(R >= KP && R <= 2 * KP, "union rank out of range");
     const bool lo = (threadIdx.x & 32) == 0;
     float t = -INFINITY;
 #pragma unroll
@@ -436,7 +439,7 @@ __device__ __forceinline__ void knn_wait_vmcnt() {
 #ifndef KNN_WPE
 #define KNN_WPE 3           // screen waves per SIMD the register budget is sized for
 #endif
-template <int KSTEPS, int KP, int QC = KNN_QCAP>
+template <int KSTEPS, int KP, int R, int QC = KNN_QCAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) void knn_screen16_kernel(
     const uint4* __restrict__ img, int n, int nchunks, int d, int* __restrict__ cand_idx,
     float* __restrict__ cand_thr, const int4* __restrict__ blk, const float* __restrict__ pos_t0) {
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
             KST(2);                                                                         \
         }                                                                                   \
         if (tdirty) {                                                                       \
-            T = fmaxf(T0, union_kth<KP>(lv));                                               \
+            T = fmaxf(T0, union_kth<KP, R>(lv));                                            \
             tdirty = false;                                                                 \
             KST(4);                                                                         \
         }                                                                                   \
@@ -695,7 +698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) 
     KST(1);
     KNN_FLUSH();
     KST(3);
-    T = fmaxf(T0, union_kth<KP>(lv));
+    T = fmaxf(T0, union_kth<KP, R>(lv));
     KST(4);
     KST_FLUSH_OUT();
 #undef KNN_FLUSH
@@ -1069,7 +1072,11 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         if (d <= 16) CCG_FALLBACK(16, KNN_KP);
         else if (d <= 32) CCG_FALLBACK(32, KNN_KP);
         else CCG_FALLBACK(64, KNN_KP);
-    } else {
+    } else if (kmax <= KNN_KP_BIG) {
+        if (d <= 16) CCG_FALLBACK(16, KNN_KP_BIG);
+        else if (d <= 32) CCG_FALLBACK(32, KNN_KP_BIG);
+        else CCG_FALLBACK(64, KNN_KP_BIG);
+    } else {  // cell tables (kmax <= KNN_TAB_K): long lists, a rare path
         if (d <= 16) CCG_FALLBACK(16, KNN_FB_K);
         else if (d <= 32) CCG_FALLBACK(32, KNN_FB_K);
         else CCG_FALLBACK(64, KNN_FB_K);
@@ -1156,16 +1163,21 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const unsigned grid = (unsigned)ccg_cdiv(npos, KNN_QPB);
         const int4* blk = sg ? sg->blk : nullptr;
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
-#define CCG_SCREEN16(KS_, KP_) \
-    knn_screen16_kernel<KS_, KP_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk, pos_t0)
+#define CCG_SCREEN16(KS_, KP_, R_)                                                                \
+    knn_screen16_kernel<KS_, KP_, R_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk, \
+                                                            pos_t0)
         if (KP == KNN_KP) {
-            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP);
-            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP);
-            else CCG_SCREEN16(4, KNN_KP);
-        } else {
-            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG);
-            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG);
-            else CCG_SCREEN16(4, KNN_KP_BIG);
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP, KNN_KP + KNN_TMARGIN);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP, KNN_KP + KNN_TMARGIN);
+            else CCG_SCREEN16(4, KNN_KP, KNN_KP + KNN_TMARGIN);
+        } else if (kmax <= KNN_KP_BIG) {
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
+            else CCG_SCREEN16(4, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
+        } else {  // cell tables: the union threshold KNN_TMARGIN ranks past kmax <= KNN_TAB_K
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
+            else CCG_SCREEN16(4, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
         }
 #undef CCG_SCREEN16
         ccg_timer_stop(ctx, t_scr, st);
@@ -1445,9 +1457,97 @@ extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int 
                                  stream);
 }
 
+// ------------------------------------------------------- cell tables --
+// Every bootstrap of one consensusClust call draws from the same N cells
+// (R/consensusClust.R:394), so a cell's nearest distinct cells in a bootstrap
+// are the first kq PRESENT entries of its list of nearest cells among all N,
+// in that list's (d2, cell) order -- the distinct-cell order, since distinct
+// ids follow the cell order.  ccg_knn_table_dev computes the K nearest other
+// cells of every cell once (screen / certify / fallback over the N cells,
+// certified squared distances); ccg_knn_boot_table_dev then replaces the
+// per-bootstrap screen by a filter of the table rows (one wave per distinct
+// cell: presence ballot, prefix count).  A cell with fewer than kq present
+// entries in its K (about 0.6% of the distinct cells at a 59% presence rate
+// and K = 48, kq = 20) is searched exactly among the bootstrap's distinct
+// cells; the expansion to rows is shared with the screen path.  Results are
+// bit-identical to the screen path.
+__global__ void kt_transpose_kernel(const double* __restrict__ pcs, int64_t N, int d, double* __restrict__ rows) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // column-major position
+    if (t >= N * d) return;
+    const int64_t k = t / N, i = t - k * N;
+    rows[i * d + k] = pcs[t];
+}
+
+__global__ void kt_cellmap_kernel(int u, const int* __restrict__ ustart, const int32_t* __restrict__ scell,
+                                  int* __restrict__ cell2u) {
+    const int uid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (uid < u) cell2u[scell[ustart[uid]]] = uid;
+}
+
+// one wave per distinct cell: the first kq present entries of its table row
+__global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, const int* __restrict__ ustart,
+                                                        const int32_t* __restrict__ scell,
+                                                        const int* __restrict__ cell2u,
+                                                        const int32_t* __restrict__ tab_idx,
+                                                        const double* __restrict__ tab_d2, int32_t* __restrict__ uidx,
+                                                        double* __restrict__ ud2, int* __restrict__ fail_list,
+                                                        int* __restrict__ fail_count) {
+    const int uid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (uid >= u) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t c = scell[ustart[uid]];
+    const int v = lane < K ? tab_idx[c * K + lane] : -1;
+    const int w = v >= 0 ? cell2u[v] : -1;
+    const unsigned long long m = __ballot(w >= 0);
+    const int rank = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+    if (w >= 0 && rank < kq) {
+        uidx[(int64_t)uid * kq + rank] = w;
+        ud2[(int64_t)uid * kq + rank] = tab_d2[c * K + lane];
+    }
+    if (lane == 0 && __popcll(m) < kq) fail_list[atomicAdd(fail_count, 1)] = uid;
+}
+
+extern "C" int ccg_knn_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, int K, int32_t* tab_idx,
+                                 double* tab_d2, ccg_knn_stats* stats, void* stream) {
+    CCG_REQUIRE(ctx && pcs && tab_idx && tab_d2, "ccg_knn_table_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_table_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(N >= 2 && N < (1LL << 30), "ccg_knn_table_dev: N=%lld out of range", (long long)N);
+    CCG_REQUIRE(K >= 1 && K <= KNN_TAB_K && K <= N - 1, "ccg_knn_table_dev: K=%d must be in [1, min(%d, N-1)]", K,
+                KNN_TAB_K);
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    double* rows = (double*)ccg_ws(ctx, WS_TAB_ROWS, sizeof(double) * (size_t)N * d);
+    if (!rows) return CCG_ENOMEM;
+    kt_transpose_kernel<<<(unsigned)ccg_cdiv(N * d, 256), 256, 0, st>>>(pcs, N, d, rows);
+    return knn_run(ctx, rows, N, d, K, tab_idx, tab_d2, stats, st, nullptr, true);
+}
+
+static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n,
+                         int n_unique, const double* rows, int kmax, int32_t* out_idx, double* out_dist,
+                         float* cell_hint, const int32_t* tab_idx, const double* tab_d2, int K,
+                         ccg_knn_stats* stats, hipStream_t st);
+
+extern "C" int ccg_knn_boot_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx,
+                                      int64_t n, int n_unique, const double* rows, int kmax, const int32_t* tab_idx,
+                                      const double* tab_d2, int K, int32_t* out_idx, double* out_dist,
+                                      ccg_knn_stats* stats, void* stream) {
+    CCG_REQUIRE(tab_idx && tab_d2, "ccg_knn_boot_table_dev: NULL table");
+    CCG_REQUIRE(K >= 1 && K <= KNN_TAB_K && K <= N - 1, "ccg_knn_boot_table_dev: K=%d must be in [1, min(%d, N-1)]",
+                K, KNN_TAB_K);
+    return knn_boot_impl(ctx, pcs, N, d, idx, n, n_unique, rows, kmax, out_idx, out_dist, nullptr, tab_idx, tab_d2, K,
+                         stats, ccg_pick_stream(ctx, stream));
+}
+
 extern "C" int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx,
                                      int64_t n, int n_unique, const double* rows, int kmax, int32_t* out_idx,
                                      double* out_dist, float* cell_hint, ccg_knn_stats* stats, void* stream) {
+    return knn_boot_impl(ctx, pcs, N, d, idx, n, n_unique, rows, kmax, out_idx, out_dist, cell_hint, nullptr, nullptr,
+                         0, stats, ccg_pick_stream(ctx, stream));
+}
+
+static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n,
+                         int n_unique, const double* rows, int kmax, int32_t* out_idx, double* out_dist,
+                         float* cell_hint, const int32_t* tab_idx, const double* tab_d2, int K,
+                         ccg_knn_stats* stats, hipStream_t st) {
     CCG_REQUIRE(ctx && pcs && idx && rows && out_idx, "ccg_knn_boot_dev: NULL argument");
     CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boot_dev: d=%d must be in [1, 63]", d);
     CCG_REQUIRE(N >= 1 && N < (1LL << 31) && n >= 2 && n < (1LL << 30), "ccg_knn_boot_dev: bad sizes");
@@ -1455,7 +1555,6 @@ extern "C" int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N,
                 "ccg_knn_boot_dev: n_unique=%d out of range", n_unique);
     CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
                 "ccg_knn_boot_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
-    hipStream_t st = ccg_pick_stream(ctx, stream);
     // n_unique = -1: counted on the device (one stream synchronisation); the
     // workspaces are then sized for u <= min(n, N)
     const int ucap = n_unique >= 0 ? n_unique : (int)std::min<int64_t>(n, N);
@@ -1505,7 +1604,25 @@ extern "C" int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N,
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
                                                                             cell_hint, urow_hint);
     ccg_knn_stats us = {0, 0};
-    if (kq >= 1) {
+    if (kq >= 1 && tab_idx) {
+        // the table's present entries; cells short of kq of them: exact search among the distinct cells
+        int* cell2u = (int*)ccg_ws(ctx, WS_TAB_MAP, sizeof(int) * (size_t)N);
+        if (!cell2u) return CCG_ENOMEM;
+        int* ufail = (int*)(misc + 5);
+        CCG_HIP(hipMemsetAsync(cell2u, 0xff, sizeof(int) * (size_t)N, st));
+        CCG_HIP(hipMemsetAsync(misc + 4, 0, 2 * sizeof(unsigned), st));
+        kt_cellmap_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, ustart, scell, cell2u);
+        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, ustart, scell, cell2u, tab_idx, tab_d2,
+                                                                   uidx, ud2, fail_list, ufail);
+        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true);
+        if (rc) return rc;
+        if (stats) {
+            int nf = 0;
+            CCG_HIP(hipMemcpyAsync(&nf, ufail, sizeof(int), hipMemcpyDeviceToHost, st));
+            CCG_HIP(hipStreamSynchronize(st));
+            us.fallback = nf;
+        }
+    } else if (kq >= 1) {
         rc = knn_run(ctx, urows, u, d, kq, uidx, ud2, stats ? &us : nullptr, st, nullptr, true, urow_hint);
         if (rc) return rc;
         if (cell_hint)
@@ -1516,7 +1633,7 @@ extern "C" int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N,
     return CCG_OK;
 #endif
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
-    if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));
+    if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));  // (the table path zeroed it above)
     kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
                                          fail_count);
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st);
@@ -1552,11 +1669,27 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
     CCG_HIP(hipMemcpyAsync(dpcs, pcs, sizeof(double) * N * d, hipMemcpyHostToDevice, st));
     CCG_HIP(hipMemcpyAsync(didx, boot_idx, sizeof(int32_t) * n * nb, hipMemcpyHostToDevice, st));
     ccg_knn_stats acc = {0, 0};
-    // the bootstraps of one call share a hint array (each bootstrap's certified
-    // k-th distances warm-start the next one's screen; results are exact either way)
-    float* hint = (float*)ccg_ws(ctx, WS_HINT, sizeof(float) * N);
-    if (!hint) return CCG_ENOMEM;
-    CCG_HIP(hipMemsetAsync(hint, 0, sizeof(float) * N, st));
+    // Many bootstraps: one cell table for the call (ccg_knn_table_dev), each
+    // bootstrap filters it.  Few: per-bootstrap screens sharing a hint array
+    // (each bootstrap's certified k-th distances warm-start the next one's
+    // screen).  Results are identical either way.
+    const int K = (int)std::min<int64_t>(KNN_TAB_K, N - 1);
+    const bool table = nb >= KNN_TABLE_MIN_BOOTS && N >= 2;
+    float* hint = nullptr;
+    int32_t* tab_idx = nullptr;
+    double* tab_d2 = nullptr;
+    if (table) {
+        char* tb = (char*)ccg_ws(ctx, WS_TAB, (sizeof(int32_t) + sizeof(double)) * (size_t)N * K + 256);
+        if (!tb) return CCG_ENOMEM;
+        tab_d2 = (double*)tb;
+        tab_idx = (int32_t*)(tab_d2 + (size_t)N * K);
+        int rc = ccg_knn_table_dev(ctx, dpcs, N, d, K, tab_idx, tab_d2, nullptr, st);
+        if (rc) return rc;
+    } else {
+        hint = (float*)ccg_ws(ctx, WS_HINT, sizeof(float) * N);
+        if (!hint) return CCG_ENOMEM;
+        CCG_HIP(hipMemsetAsync(hint, 0, sizeof(float) * N, st));
+    }
     std::vector<unsigned char> seen(N);
     for (int b = 0; b < nb; ++b) {
         // the bootstrap's distinct cells (R: length(unique(idx)))
@@ -1570,8 +1703,10 @@ extern "C" int ccg_knn_boot(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
         int rc = ccg_gather_rows_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, rows, st);
         if (rc) return rc;
         ccg_knn_stats s;
-        rc = ccg_knn_boot_hint_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, dout, ddist, hint, &s,
-                                   st);
+        rc = table ? ccg_knn_boot_table_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, tab_idx, tab_d2,
+                                            K, dout, ddist, &s, st)
+                   : ccg_knn_boot_hint_dev(ctx, dpcs, N, d, didx + (int64_t)b * n, n, u, rows, kmax, dout, ddist, hint,
+                                           &s, st);
         if (rc) return rc;
         acc.queries += s.queries;
         acc.fallback += s.fallback;

@@ -469,7 +469,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
                                                    unsigned long long* __restrict__ wcnt,
                                                    double* __restrict__ out_width, int CH,
                                                    const int* __restrict__ rep, const int* __restrict__ mult,
-                                                   int64_t mw, int nbw, const int64_t* __restrict__ nrep) {
+                                                   const int* __restrict__ cnt, int64_t mw, int nbw,
+                                                   const int64_t* __restrict__ nrep) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // CH: centroids staged per pass (a multiple of 16)
     constexpr int KS = DMAX / 4;  // K steps of 4 dims
@@ -481,7 +482,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, j = lane & 15;
     // tile position p = r0 + 16 t + j is row p, or (distinct-cell widths)
-    // the representative row rep[p] of a cell, weighted by mult[l][p]
+    // the representative row rep[p] of a cell, weighted by its cnt[p] rows
+    // less the mult[l][p] of them labelled apart in labeling l
     const int64_t r0 = (int64_t)blockIdx.x * (4 * RT * 16) + wave * (RT * 16);
     const int64_t npos = rep ? *nrep : m;  // representatives: counted on the device
     if ((int64_t)blockIdx.x * (4 * RT * 16) >= npos) return;  // the partials of idle blocks stay 0
@@ -595,7 +597,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
             iw = t == g ? in[t] : iw;
             pw = t == g ? r0 + t * 16 + j : pw;
         }
-        const int wt = (rep && iw) ? mult[(int64_t)l * mw + pw] : 1;
+        const int wt = (rep && iw) ? cnt[pw] - mult[(int64_t)l * mw + pw] : 1;
         long long wq = 0;
         unsigned wn = 0;
 #if SIL_EXP == 3
@@ -713,29 +715,39 @@ __global__ void sil_isrep_kernel(const int32_t* __restrict__ cell, int64_t m, co
     if (r < m) flag[r] = first[cell[r]] == (int)r ? 1 : 0;
 }
 
-// rep[pos] = the representative rows in row order (pos = exclusive scan)
+// rep[pos] = the representative rows in row order (pos = exclusive scan);
+// cnt[pos] = the cell's rows; the other rows listed in row order (r - scan[r]
+// of them come before r)
 __global__ void sil_rep_kernel(const int32_t* __restrict__ cell, int64_t m, const int* __restrict__ first,
-                               const int64_t* __restrict__ scan, int* __restrict__ rep) {
+                               const int64_t* __restrict__ scan, int* __restrict__ rep, int* __restrict__ cnt,
+                               int* __restrict__ nonrep) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < m && first[cell[r]] == (int)r) rep[scan[r]] = (int)r;
+    if (r >= m) return;
+    const int rp = first[cell[r]];
+    atomicAdd(&cnt[scan[rp]], 1);
+    if (rp == (int)r) rep[scan[r]] = (int)r;
+    else nonrep[r - scan[r]] = (int)r;
 }
 
-// mult[l][pos of the cell's representative] += 1 for each row with the
-// representative's label; other rows -> exc (l << 32 | row)
+// Per labeling (blockIdx.y strides), every non-representative row whose
+// label differs from its representative's: dis[l][pos] += 1 (the weight is
+// cnt - dis) and the row joins the exception list (l << 32 | row).
 __global__ void sil_mult_kernel(const int32_t* __restrict__ cell, int64_t m, int L, const int32_t* __restrict__ labels,
-                                const int* __restrict__ first, const int64_t* __restrict__ scan, int64_t mw,
-                                int* __restrict__ mult, unsigned long long* __restrict__ exc,
-                                int* __restrict__ nexc) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m * L) return;
-    const int l = (int)(t / m);
-    const int64_t r = t - (int64_t)l * m;
-    const int rp = first[cell[r]];
-    if (labels[(int64_t)l * m + r] == labels[(int64_t)l * m + rp]) {
-        atomicAdd(&mult[(int64_t)l * mw + scan[rp]], 1);
-    } else {
-        const int e = atomicAdd(nexc, 1);
-        exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
+                                const int* __restrict__ first, const int64_t* __restrict__ scan,
+                                const int* __restrict__ nonrep, int64_t mw, int* __restrict__ dis,
+                                unsigned long long* __restrict__ exc, int* __restrict__ nexc) {
+    const int64_t nn = m - scan[m];
+    for (int l = blockIdx.y; l < L; l += gridDim.y) {
+        const int32_t* lab = labels + (int64_t)l * m;
+        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nn; j += (int64_t)gridDim.x * blockDim.x) {
+            const int r = nonrep[j];
+            const int rp = first[cell[r]];
+            if (lab[r] != lab[rp]) {
+                atomicAdd(&dis[(int64_t)l * mw + scan[rp]], 1);
+                const int e = atomicAdd(nexc, 1);
+                exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
+            }
+        }
     }
 }
 
@@ -788,8 +800,8 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
                        unsigned long long* gvar, unsigned long long* wsum, unsigned long long* wcnt,
                        int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc, long long* q,
                        double* out_width, hipStream_t st, const int* rep = nullptr, const int* mult = nullptr,
-                       int64_t mw = 0, const unsigned long long* exc = nullptr, const int* nexc = nullptr,
-                       const int64_t* nrep = nullptr) {
+                       const int* cnt = nullptr, int64_t mw = 0, const unsigned long long* exc = nullptr,
+                       const int* nexc = nullptr, const int64_t* nrep = nullptr) {
     if (q) {
         // sorted segments: S1, S2 and counts in one pass, v_c in sil_mu
         sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q, q + m * DMAX);
@@ -823,12 +835,12 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
     if (rep) {
         // partials of blocks past the representative grid stay 0 (zeroed with the buffer)
         sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
-                                                nullptr, CH, rep, mult, mw, nbw, nrep);
+                                                nullptr, CH, rep, mult, cnt, mw, nbw, nrep);
         sil_width_exc<DMAX><<<64, 256, 0, st>>>(
             x, m, d, labels, cmax, npres, codes, muc, auxc, exc, nexc, nbw, wsum, wcnt);
     } else {
         sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
-                                                out_width, CH, nullptr, nullptr, 0, nbw, nullptr);
+                                                out_width, CH, nullptr, nullptr, nullptr, 0, nbw, nullptr);
     }
 }
 
@@ -927,35 +939,38 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
         q = (long long*)ccg_ws(ctx, WS_SIL_Q, 2 * sizeof(long long) * (size_t)m * dmax);
         if (!q) return CCG_ENOMEM;
     }
-    // distinct-cell tables: first row per cell, representative list, weights, exceptions
+    // distinct-cell tables: first row per cell, representative list, rows per
+    // cell, the other rows, per-labeling disagreements, exceptions
     char* tb = (char*)ccg_ws(ctx, WS_SIL_C, sizeof(int) * (size_t)ncell + sizeof(int64_t) * (size_t)(m + 1) +
-                                                sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
+                                                3 * sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
                                                 sizeof(unsigned long long) * (size_t)L * m + 256);
     if (!tb) return CCG_ENOMEM;
     int* first = (int*)tb;
     int64_t* scan = (int64_t*)(tb + ccg_cdiv(sizeof(int) * ncell, 16) * 16);
     int* rep = (int*)(scan + m + 1);
-    int* nexc = rep + m;                // [0] exception count, then the weights
-    int* mult = nexc + 4;               // [L][m] (first mw columns used)
+    int* nonrep = rep + m;
+    int* nexc = nonrep + m;             // [0] exception count; then cnt and the disagreements (zeroed together)
+    int* cnt = nexc + 4;                // [m] (first mw used)
+    int* mult = cnt + m;                // [L][m] (first mw columns used)
     unsigned long long* exc = (unsigned long long*)(mult + ccg_cdiv((int64_t)L * m, 2) * 2);
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
     const unsigned gm = (unsigned)ccg_cdiv(m, 256);
-    sil_init_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(std::max(ncell, (int64_t)L * m + 4), 256), 4096), 256, 0,
-                      st>>>(first, ncell, nexc, (int64_t)L * m + 4);
+    sil_init_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(std::max(ncell, (int64_t)(L + 1) * m + 4), 256), 4096), 256,
+                      0, st>>>(first, ncell, nexc, (int64_t)(L + 1) * m + 4);
     sil_first_kernel<<<gm, 256, 0, st>>>(cell, m, first);
     sil_isrep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan);
     int rc = ccg_scan_i64(ctx, scan, scan, m, st);
     if (rc) return rc;
-    sil_rep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan, rep);
+    sil_rep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan, rep, cnt, nonrep);
     // mw = the number of representatives (the distinct cells): device-side
     // only, so the width grid covers m positions and the weights' stride is m
-    sil_mult_kernel<<<(unsigned)ccg_cdiv((int64_t)L * m, 256), 256, 0, st>>>(cell, m, L, labels, first, scan, m, mult,
-                                                                          exc, nexc);
+    dim3 gx((unsigned)std::min<int64_t>(ccg_cdiv(m, 256), 32), (unsigned)std::min(L, 65535));
+    sil_mult_kernel<<<gx, 256, 0, st>>>(cell, m, L, labels, first, scan, nonrep, m, mult, exc, nexc);
     sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
 #define SIL_CELLS(DM_)                                                                                              \
     sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
-                    auxc, q, nullptr, st, rep, mult, m, exc, nexc, scan + m)
+                    auxc, q, nullptr, st, rep, mult, cnt, m, exc, nexc, scan + m)
     if (d <= 16) SIL_CELLS(16);
     else if (d <= 32) SIL_CELLS(32);
     else SIL_CELLS(64);

@@ -8,8 +8,11 @@
 // take two 9/8-bit passes), three launches per pass:
 //   rs_hist    : per tile of RS_TILE pairs, the digit histogram (LDS atomics),
 //                written digit-major: cnt[digit * ntiles + tile];
-//   rs_scan    : one block scans that matrix exclusively -> every (digit, tile)
-//                pair's first output position (digit-major = stable);
+//   scan       : the library's two-launch multi-block scan (ccg_scan_i64) of
+//                that matrix -> every (digit, tile) pair's first output
+//                position (digit-major = stable).  A single-block scan here
+//                waited for a free CU behind the co-scheduled streams' kernels
+//                (~150 us per launch in the bench against ~5 us alone);
 //   rs_scatter : each tile ranks its pairs stably -- a wave takes a contiguous
 //                run of 64 * RS_IPT pairs, lanes along consecutive pairs, peers
 //                of equal digit found by one ballot per digit bit, running
@@ -26,7 +29,7 @@
 #define RS_MAXBITS 9
 
 __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift,
-                                                      int bits, int ntiles, int* __restrict__ cnt) {
+                                                      int bits, int ntiles, int64_t* __restrict__ cnt) {
     __shared__ int h[1 << RS_MAXBITS];
     const int nb = 1 << bits;
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) h[t] = 0;
@@ -41,30 +44,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict_
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
 }
 
-// Exclusive scan of m ints in place by one block (m <= 2^RS_MAXBITS * ntiles).
-__global__ __launch_bounds__(1024) void rs_scan(int* __restrict__ cnt, int m) {
-    __shared__ int part[1024];
-    const int per = (m + 1023) / 1024;
-    const int a = threadIdx.x * per, b = min(m, a + per);
-    int s = 0;
-    for (int i = a; i < b; ++i) s += cnt[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    // Hillis-Steele over the 1024 partial sums
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = a; i < b; ++i) {
-        const int v = cnt[i];
-        cnt[i] = run;
-        run += v;
-    }
-}
-
 __device__ __forceinline__ unsigned long long rs_lanemask_lt() {
     const int lane = threadIdx.x & 63;
     return lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -72,14 +51,14 @@ __device__ __forceinline__ unsigned long long rs_lanemask_lt() {
 
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restrict__ kin,
                                                          const int32_t* __restrict__ vin, int64_t n, int shift,
-                                                         int bits, int ntiles, const int* __restrict__ off,
+                                                         int bits, int ntiles, const int64_t* __restrict__ off,
                                                          int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
     __shared__ int wcnt[RS_WAVES][1 << RS_MAXBITS];  // per-wave running digit counts, then prefixes
     __shared__ int goff[1 << RS_MAXBITS];
     const int nb = 1 << bits;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int t = threadIdx.x; t < RS_WAVES * nb; t += RS_THREADS) wcnt[t / nb][t % nb] = 0;
-    for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = off[(int64_t)t * ntiles + blockIdx.x];
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = (int)off[(int64_t)t * ntiles + blockIdx.x];
     __syncthreads();
     // wave w's run: pairs [base, base + 64 * RS_IPT), item i at base + 64 i + lane
     const int64_t base = (int64_t)blockIdx.x * RS_TILE + (int64_t)w * 64 * RS_IPT;
@@ -143,10 +122,10 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
     }
     const int npass = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
     const size_t cnt_ints = (size_t)(1 << RS_MAXBITS) * ntiles;
-    char* ws = (char*)ccg_ws(ctx, WS_SORT, sizeof(int) * cnt_ints + sizeof(int32_t) * 2 * (size_t)n + 256);
+    char* ws = (char*)ccg_ws(ctx, WS_SORT, sizeof(int64_t) * (cnt_ints + 1) + sizeof(int32_t) * 2 * (size_t)n + 256);
     if (!ws) return CCG_ENOMEM;
-    int* cnt = (int*)ws;
-    int32_t* tk = (int32_t*)(ws + ccg_cdiv(sizeof(int) * cnt_ints, 256) * 256);
+    int64_t* cnt = (int64_t*)ws;
+    int32_t* tk = (int32_t*)(ws + ccg_cdiv(sizeof(int64_t) * (cnt_ints + 1), 256) * 256);
     int32_t* tv = tk + n;
     // pass p writes out when (npass - 1 - p) is even, so the last pass lands in out
     const int32_t* ck = keys_in;
@@ -157,7 +136,8 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
         int32_t* ok = ((npass - 1 - p) % 2 == 0) ? keys_out : tk;
         int32_t* ov = ((npass - 1 - p) % 2 == 0) ? vals_out : tv;
         rs_hist<<<ntiles, RS_THREADS, 0, st>>>(ck, n, shift, bits, ntiles, cnt);
-        rs_scan<<<1, 1024, 0, st>>>(cnt, (1 << bits) * ntiles);
+        const int rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)(1 << bits) * ntiles, st);
+        if (rc) return rc;
         rs_scatter<<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov);
         ck = ok;
         cv = ov;

@@ -332,6 +332,31 @@ class Engine:
             return self.last_knn_stats
         return None
 
+    def knn_table_t(self, pcs_cm, N, d, K, tab_idx, tab_d2, stats=False):
+        """ccg_knn_table_dev: every cell's K nearest other cells among the N
+        (tab_idx (N, K) int32, tab_d2 (N, K) float64 squared distances)."""
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_table_dev(self.ctx, _ptr(pcs_cm), N, d, K, _ptr(tab_idx), _ptr(tab_d2),
+                                         ctypes.byref(st) if stats else None, _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
+    def knn_boot_table_t(self, pcs_cm, N, d, idx, n_unique, rows, kmax, tab_idx, tab_d2, out_idx, out_dist=None,
+                         stats=False):
+        """knn_boot_t from a cell table of the same PCs (ccg_knn_boot_table_dev)."""
+        n = idx.numel()
+        K = tab_idx.shape[1]
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_boot_table_dev(self.ctx, _ptr(pcs_cm), N, d, _ptr(idx), n, int(n_unique), _ptr(rows),
+                                              kmax, _ptr(tab_idx), _ptr(tab_d2), K, _ptr(out_idx), _ptr(out_dist),
+                                              ctypes.byref(st) if stats else None, _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
     def knn_segments_t(self, rows, seg_off, kmax, out_idx, out_dist=None, stats=False):
         """Device flavour: rows (n, d) tensor of concatenated segments, seg_off a
         host int64 array of nseg+1 offsets; out_idx (n, kmax) segment-local."""

@@ -158,6 +158,35 @@ int ccg_knn_boot_hint_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                           double* out_dist, float* cell_hint,
                           ccg_knn_stats* stats, void* stream);
 
+/* Cell table: the K nearest OTHER cells of every one of the N cells, in
+ * (fp64 squared distance, cell index) order -- the kNN contract over the N
+ * cells -- with the certified squared distances.  Computed once per PC
+ * matrix; every bootstrap of the same PCs then filters it
+ * (ccg_knn_boot_table_dev) instead of searching.  (R/consensusClust.R:394
+ * draws every bootstrap from the same cells; :656-658 searches each.)
+ *   pcs     : N x d float64 COLUMN-major (device)
+ *   tab_idx : N x K int32 (device), tab_d2: N x K float64 (device)
+ * Requires 1 <= K <= min(48, N-1), 2 <= N < 2^30, d <= 63. */
+int ccg_knn_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                      int K, int32_t* tab_idx, double* tab_d2,
+                      ccg_knn_stats* stats, void* stream);
+
+/* ccg_knn_boot_dev from a cell table of the same pcs (ccg_knn_table_dev):
+ * each distinct cell's kq = min(kmax, n_unique - 1) nearest distinct cells
+ * are the first kq entries of its table row that the bootstrap holds; a cell
+ * with fewer than kq such entries among its K is searched exactly among the
+ * bootstrap's distinct cells.  Bit-identical to ccg_knn_boot_dev.  With a
+ * presence rate p = n_unique / N, a cell needs the exact search when fewer
+ * than kq of its K table entries are present (Binomial(K, p) < kq: about
+ * 0.6% of the cells at p = 0.59, K = 48, kq = 20).  stats->fallback counts
+ * those cells plus the rows of cut ties. */
+int ccg_knn_boot_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
+                           const int32_t* idx, int64_t n, int n_unique,
+                           const double* rows, int kmax,
+                           const int32_t* tab_idx, const double* tab_d2, int K,
+                           int32_t* out_idx, double* out_dist,
+                           ccg_knn_stats* stats, void* stream);
+
 /* Batched kNN over independent segments: the iterate=TRUE subclustering
  * (R/consensusClust.R:541-566, BASELINE config 5) runs one bootstrap loop per
  * subcluster; their (small) bootstrap matrices are searched in ONE set of

@@ -6,7 +6,10 @@ lists back to rows; these cases pin the expansion's tie rules: copies of a
 cell at distance 0 (more copies than kmax), distinct cells at equal distance
 (integer lattices, where the kmax-th entry is often a tie the distinct-cell
 list cuts and the exact fallback takes over), bootstraps with fewer distinct
-cells than kmax + 1, kmax = 32, and a wrong distinct-cell count.
+cells than kmax + 1, kmax = 32, and a wrong distinct-cell count.  Every case
+runs through both the per-bootstrap screen and the cell-table path
+(ccg_knn_table_dev once over the N cells, then ccg_knn_boot_table_dev: the
+first kq present entries of each distinct cell's table row).
 """
 import numpy as np
 import pytest
@@ -18,7 +21,20 @@ from consensusclustr_amd import CcgError
 pytestmark = pytest.mark.gpu
 
 
-def _boot_knn(engine, pcs, idx, kmax, want_dist=True, n_unique=None):
+@pytest.fixture(params=["screen", "table"])
+def path(request):
+    return request.param
+
+
+def _table(engine, pcs_cm, N, d, K):
+    dev = pcs_cm.device
+    ti = torch.empty((N, K), dtype=torch.int32, device=dev)
+    td = torch.empty((N, K), dtype=torch.float64, device=dev)
+    engine.knn_table_t(pcs_cm, N, d, K, ti, td)
+    return ti, td
+
+
+def _boot_knn(engine, pcs, idx, kmax, want_dist=True, n_unique=None, path="screen", K=48):
     N, d = pcs.shape
     dev = torch.device("cuda", engine.device)
     pcs_cm = torch.from_numpy(np.ascontiguousarray(np.asarray(pcs, np.float64).T)).to(dev)
@@ -29,14 +45,18 @@ def _boot_knn(engine, pcs, idx, kmax, want_dist=True, n_unique=None):
     out = torch.empty((n, kmax), dtype=torch.int32, device=dev)
     dist = torch.empty((n, kmax), dtype=torch.float64, device=dev) if want_dist else None
     u = len(np.unique(idx)) if n_unique is None else n_unique
-    q, fb = engine.knn_boot_t(pcs_cm, N, d, ti, u, rows, kmax, out, dist, stats=True)
+    if path == "table":
+        tab = _table(engine, pcs_cm, N, d, min(K, N - 1))
+        q, fb = engine.knn_boot_table_t(pcs_cm, N, d, ti, u, rows, kmax, *tab, out, dist, stats=True)
+    else:
+        q, fb = engine.knn_boot_t(pcs_cm, N, d, ti, u, rows, kmax, out, dist, stats=True)
     torch.cuda.synchronize()
     return out.cpu().numpy(), (dist.cpu().numpy() if want_dist else None), fb
 
 
-def _check(engine, pcs, idx, kmax):
+def _check(engine, pcs, idx, kmax, path="screen", K=48):
     oi, od = O.knn(O.gather_rows(pcs, idx), kmax)
-    gi, gd, fb = _boot_knn(engine, pcs, idx, kmax)
+    gi, gd, fb = _boot_knn(engine, pcs, idx, kmax, path=path, K=K)
     assert np.array_equal(gi, oi)
     # distances: sqrt of the same fp64 sums; the device sqrt may differ in the last ulp
     np.testing.assert_allclose(gd, od, rtol=1e-12, atol=1e-12)
@@ -44,15 +64,15 @@ def _check(engine, pcs, idx, kmax):
 
 
 @pytest.mark.parametrize("N,n,d,kmax", [(4000, 3600, 30, 20), (3000, 6000, 12, 32), (2500, 2250, 50, 15)])
-def test_knn_boot_dev_random_bootstraps(engine, N, n, d, kmax):
+def test_knn_boot_dev_random_bootstraps(engine, path, N, n, d, kmax):
     rng = np.random.default_rng(N + n)
     centers = rng.normal(scale=3.0, size=(10, d))
     pcs = centers[rng.integers(0, 10, N)] + rng.normal(size=(N, d))
     idx = rng.integers(0, N, n).astype(np.int32)
-    _check(engine, pcs, idx, kmax)
+    _check(engine, pcs, idx, kmax, path)
 
 
-def test_knn_boot_dev_cell_copies_beyond_kmax(engine):
+def test_knn_boot_dev_cell_copies_beyond_kmax(engine, path):
     """One cell drawn 45 times (> kmax + 1): its rows' lists are its other
     copies only, in row order; a second cell drawn 12 times sits among them."""
     rng = np.random.default_rng(3)
@@ -61,11 +81,11 @@ def test_knn_boot_dev_cell_copies_beyond_kmax(engine):
     idx = rng.integers(0, N, 1000).astype(np.int32)
     idx[rng.choice(1000, 45, replace=False)] = 17
     idx[rng.choice(np.flatnonzero(idx != 17), 12, replace=False)] = 99
-    _check(engine, pcs, idx, 20)
+    _check(engine, pcs, idx, 20, path)
 
 
 @pytest.mark.parametrize("kmax", [20, 32])
-def test_knn_boot_dev_lattice_ties(engine, kmax):
+def test_knn_boot_dev_lattice_ties(engine, path, kmax):
     """Integer lattice cells (many distinct cells at exactly equal distance)
     with heavy duplication: equal-d2 groups are merged by row index, and a
     group cut by the distinct-cell list goes to the exact search."""
@@ -73,48 +93,48 @@ def test_knn_boot_dev_lattice_ties(engine, kmax):
     pcs = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)  # 216 cells
     rng = np.random.default_rng(kmax)
     idx = rng.integers(0, pcs.shape[0], 600).astype(np.int32)
-    fb = _check(engine, pcs, idx, kmax)
+    fb = _check(engine, pcs, idx, kmax, path)
     assert fb > 0  # the lattice's cut ties must have taken the exact path
 
 
-def test_knn_boot_dev_few_distinct_cells(engine):
+def test_knn_boot_dev_few_distinct_cells(engine, path):
     """9 distinct cells, 60 rows, kmax 20: every distinct cell is listed
     (kq = u - 1 < kmax) and the rows come from the copies."""
     rng = np.random.default_rng(5)
     pcs = rng.normal(size=(9, 4))
     idx = np.concatenate([np.arange(9), rng.integers(0, 9, 51)]).astype(np.int32)
     rng.shuffle(idx)
-    _check(engine, pcs, idx, 20)
+    _check(engine, pcs, idx, 20, path)
 
 
-def test_knn_boot_dev_single_cell(engine):
+def test_knn_boot_dev_single_cell(engine, path):
     """Every row is the same cell: each list is the other rows in order."""
     pcs = np.ones((5, 3))
     idx = np.full(30, 2, np.int32)
-    _check(engine, pcs, idx, 20)
+    _check(engine, pcs, idx, 20, path)
 
 
-def test_knn_boot_dev_counts_distinct_cells(engine):
+def test_knn_boot_dev_counts_distinct_cells(engine, path):
     """n_unique = -1: the device counts the distinct cells itself."""
     rng = np.random.default_rng(13)
     pcs = rng.normal(size=(700, 9))
     idx = rng.integers(0, 700, 630).astype(np.int32)
     oi, od = O.knn(O.gather_rows(pcs, idx), 20)
-    gi, gd, _ = _boot_knn(engine, pcs, idx, 20, n_unique=-1)
+    gi, gd, _ = _boot_knn(engine, pcs, idx, 20, n_unique=-1, path=path)
     assert np.array_equal(gi, oi)
     np.testing.assert_allclose(gd, od, rtol=1e-12, atol=1e-12)
 
 
-def test_knn_boot_dev_wrong_unique_count(engine):
+def test_knn_boot_dev_wrong_unique_count(engine, path):
     rng = np.random.default_rng(7)
     pcs = rng.normal(size=(500, 6))
     idx = rng.integers(0, 500, 400).astype(np.int32)
     u = len(np.unique(idx))
-    _boot_knn(engine, pcs, idx, 10, want_dist=False, n_unique=u - 3)
+    _boot_knn(engine, pcs, idx, 10, want_dist=False, n_unique=u - 3, path=path)
     with pytest.raises(CcgError, match="n_unique"):
         engine.check_errors()
     # the context is usable again afterwards
-    _check(engine, pcs, idx, 10)
+    _check(engine, pcs, idx, 10, path)
 
 
 def test_knn_boot_hint_warm_start_is_exact(engine):
@@ -151,3 +171,36 @@ def test_knn_boot_hint_warm_start_is_exact(engine):
         assert torch.equal(a, b) and torch.equal(da, db), t
         assert float(hint.min()) >= 0.0
     assert max(fb[1:3]) < n // 100  # warm-started bootstraps certify almost every row
+
+
+def test_knn_table_matches_oracle(engine):
+    """ccg_knn_table_dev: each cell's K = 48 nearest other cells among all N
+    (ids and certified squared distances) equal the oracle's exact kNN of the
+    N cells, clustered data with exact duplicate cells included."""
+    rng = np.random.default_rng(401)
+    N, d = 6000, 30
+    centers = rng.normal(scale=3.0, size=(12, d))
+    pcs = centers[rng.integers(0, 12, N)] + rng.normal(size=(N, d))
+    pcs[100:140] = pcs[7]  # 41 cells at one point
+    K = 48
+    oi, od = O.knn(pcs, K)
+    pcs_cm = torch.from_numpy(np.ascontiguousarray(pcs.T)).cuda()
+    ti, td = _table(engine, pcs_cm, N, d, K)
+    torch.cuda.synchronize()
+    assert np.array_equal(ti.cpu().numpy(), oi)
+    np.testing.assert_allclose(np.sqrt(td.cpu().numpy()), od, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("frac,K", [(0.9, 48), (0.2, 48), (0.9, 8), (2.0, 48)])
+def test_knn_boot_table_presence_rates(engine, frac, K):
+    """Table path at presence rates from ~18% (most cells short of kq present
+    table entries: the exact search among distinct cells) to ~86%, and a
+    table shorter than kq (K = 8 < 20: every cell searched exactly)."""
+    rng = np.random.default_rng(int(frac * 100) + K)
+    N, d = 5000, 16
+    centers = rng.normal(scale=3.0, size=(8, d))
+    pcs = centers[rng.integers(0, 8, N)] + rng.normal(size=(N, d))
+    idx = rng.integers(0, N, int(frac * N)).astype(np.int32)
+    fb = _check(engine, pcs, idx, 20, "table", K=K)
+    if K < 20:
+        assert fb >= len(np.unique(idx))

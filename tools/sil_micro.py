@@ -1,7 +1,8 @@
 """Micro-benchmark of the batched silhouette (ccg_silhouette_dev) at cfg3
 shapes: one 90k-row bootstrap of bench.py's synthetic PCs (d = 30) and 60
-synthetic clusterings (bench.synth_labels).  Reports ms per call (library
-hipEvent timer).  --lib selects a variant build (tools/build_variant.sh)."""
+synthetic clusterings (bench.synth_labels, drawn per cell).  Reports ms per
+call (library hipEvent timer) of the row path (ccg_silhouette_dev) and of the
+distinct-cell path (ccg_silhouette_cells_dev).  --lib selects a variant build (tools/build_variant.sh)."""
 import json
 import os
 import sys
@@ -27,7 +28,7 @@ def main():
     eng = Engine(0)
     rows = torch.empty((n, d), dtype=torch.float64, device=dev)
     eng.gather_rows_t(pcs.t().contiguous(), N, d, boot, rows)
-    labels = bench.synth_labels(torch, pop[boot.long()], L, dev, 1000)
+    labels = bench.synth_labels(torch, pop, boot, L, dev, 1000)
     cmax = int(labels.max().item())
     mean = torch.empty(L, dtype=torch.float64, device=dev)
     ncl = torch.empty(L, dtype=torch.int32, device=dev)
@@ -39,8 +40,16 @@ def main():
     for _ in range(reps):
         eng.silhouette_t(rows, labels, cmax, mean, ncl, mns)
     ms, cnt = eng.timing_read("silhouette")
-    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "sil_ms": ms / cnt, "cmax": cmax,
-                      "mean0": float(mean[0].item())}))
+    mean_rows = mean.clone()
+    eng.silhouette_cells_t(rows, labels, cmax, boot, N, mean, ncl, mns)
+    torch.cuda.synchronize()
+    eng.timing_read("silhouette")
+    for _ in range(reps):
+        eng.silhouette_cells_t(rows, labels, cmax, boot, N, mean, ncl, mns)
+    ms_c, cnt_c = eng.timing_read("silhouette")
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "sil_ms": ms / cnt, "sil_cells_ms": ms_c / cnt_c,
+                      "cmax": cmax, "mean0": float(mean_rows[0].item()),
+                      "max_abs_diff_cells": float((mean - mean_rows).abs().max().item())}))
 
 
 if __name__ == "__main__":
