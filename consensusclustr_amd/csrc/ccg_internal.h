@@ -54,6 +54,8 @@ enum ccg_ws_slot {
     WS_TAB_ROWS,     // kNN cell table: the PCs row-major (certify / fallback rows)
     WS_TAB_MAP,      // kNN cell table: cell -> distinct-cell id of a bootstrap (-1: absent)
     WS_TAB,          // kNN cell table of a host call (ccg_knn_boot): ids then squared distances
+    WS_FX_A,         // kNN exact search of failed rows: radii, candidate counts, overflow list
+    WS_FX_B,         // kNN exact search of failed rows: candidate (d2, row) buffers
     WS_NSLOTS
 };
 
@@ -78,6 +80,7 @@ struct ccg_ctx {
     void* ws[WS_NSLOTS];
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
+    void* fx_zeroed;  // kNN radius search: the WS_FX_A buffer whose counters were zeroed at allocation
     // kernel timing (ccg_timing_*)
     int timing;
     ccg_timer_rec* timers;   // pool, grows

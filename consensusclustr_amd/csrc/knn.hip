@@ -439,8 +439,8 @@ __device__ __forceinline__ void knn_wait_vmcnt() {
 #ifndef KNN_WPE
 #define KNN_WPE 3           // screen waves per SIMD the register budget is sized for
 #endif
-template <int KSTEPS, int KP, int R, int QC = KNN_QCAP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KNN_WPE))) void knn_screen16_kernel(
+template <int KSTEPS, int KP, int R, int WPE = KNN_WPE, int QC = KNN_QCAP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void knn_screen16_kernel(
     const uint4* __restrict__ img, int n, int nchunks, int d, int* __restrict__ cand_idx,
     float* __restrict__ cand_thr, const int4* __restrict__ blk, const float* __restrict__ pos_t0) {
     constexpr int C16 = KSTEPS * 4;                 // 16-B chunks per row
@@ -762,7 +762,8 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     const int* __restrict__ cand_idx, const float* __restrict__ cand_thr,
     const double* __restrict__ inv_scale2, double err_ulps, const int* __restrict__ perm,
     int32_t* __restrict__ out_idx, double* __restrict__ out_dist, int* __restrict__ fail_list,
-    int* __restrict__ fail_count, int npos, const int64_t* __restrict__ seg_off, int nseg, bool dist_sq) {
+    int* __restrict__ fail_count, int npos, const int64_t* __restrict__ seg_off, int nseg, bool dist_sq,
+    double* __restrict__ fail_tau) {
     const int lane = threadIdx.x & 63;
     const int qs = blockIdx.x * 4 + (threadIdx.x >> 6);  // screening position
     if (qs >= npos) return;
@@ -841,6 +842,8 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(
     } else if (lane == 0) {
         int p = atomicAdd(fail_count, 1);
         fail_list[p] = q;
+        // the radius search's bound: kmax candidates (a subset of the references) lie within dK
+        if (fail_tau) fail_tau[p] = idK < n ? dK : INFINITY;
     }
 }
 
@@ -1056,10 +1059,189 @@ struct KnnSegs {
     const int4* blk;         // device, per query block: chunk range [x, y), query limit z
 };
 
+// ------------------------------------------ exact search by a radius --
+// The exact search of the rows certification (or a cell table) could not
+// settle, when the caller knows for each such row a radius tau that at least
+// kmax references lie within (certify: the kmax-th exact candidate distance;
+// a candidate set is a subset of the references, so its kmax-th distance
+// bounds the true kmax-th from above):
+//   scan   : (64-row group, reference range) blocks, one failed row per lane,
+//            the range staged through LDS in 64-reference chunks that every
+//            lane reads by broadcast; the exact d2 (the contract's unfused
+//            dimension-order arithmetic) of each (row, reference) pair, and
+//            every reference within tau is appended to the row's candidate
+//            buffer (rare: tau is tight);
+//   select : one block per row bitonic-sorts its candidates by (d2, row) in
+//            LDS and writes the first kmax.
+// The failed rows' references are read once per 64 rows instead of once per
+// row.  Rows with tau = +inf, past KNN_FX_ROWS, or with more than KNN_FX_CAP
+// candidates (massive ties at the radius) go to the per-thread-list kernels
+// below.
+#define KNN_FX_CAP 1024
+#define KNN_FX_ROWS 16384
+#define KNN_FX_CHUNK 64
+#define KNN_FX_GRID 1024
+
+template <int DMAX>
+__device__ __forceinline__ double knn_exact_d2(const double (&xq)[DMAX], const double* y, int d) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k)
+        if (k < d) {
+            const double t = __dsub_rn(xq[k], y[k]);
+            s = __dadd_rn(s, __dmul_rn(t, t));
+        }
+    return s;
+}
+
+// In-LDS bitonic sort of m (a power of two) (key, id) pairs, ascending.
+__device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
+    for (int k = 2; k <= m; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < m; i += blockDim.x) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const bool up = (i & k) == 0;
+                    const double a = kd[i], b = kd[p];
+                    const int ia = ki[i], ib = ki[p];
+                    if (key_less(b, ib, a, ia) == up) {
+                        kd[i] = b;
+                        kd[p] = a;
+                        ki[i] = ib;
+                        ki[p] = ia;
+                    }
+                }
+            }
+        }
+    __syncthreads();
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, int n, int d,
+                                                          const int* __restrict__ fail_list,
+                                                          const int* __restrict__ fail_count,
+                                                          const double* __restrict__ fail_tau, int* __restrict__ cnt,
+                                                          double* __restrict__ bd, int* __restrict__ bi,
+                                                          int* __restrict__ ovf_count) {
+    __shared__ double sy[KNN_FX_CHUNK * DMAX];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
+    const int nf = min(*fail_count, KNN_FX_ROWS);
+    // reference ranges: about 2 units per block of the grid whatever the row count
+    const int ng = (nf + 63) / 64;
+    const int want = max(1, 2 * (int)gridDim.x / max(ng, 1));
+    const int range = (((n + want - 1) / want) + KNN_FX_CHUNK - 1) / KNN_FX_CHUNK * KNN_FX_CHUNK;
+    const int nr = (n + range - 1) / range;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t w = blockIdx.x; w < (int64_t)ng * nr; w += gridDim.x) {
+        const int g = (int)(w / nr), r = (int)(w - (int64_t)g * nr);
+        const int f = g * 64 + lane;
+        const double tf = f < nf ? fail_tau[f] : -1.0;
+        const bool valid = f < nf && tf < INFINITY;  // no radius: the per-thread-list kernels
+        const int q = valid ? fail_list[f] : -1;
+        const double t = valid ? tf : -1.0;
+        double xq[DMAX];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) xq[k] = (valid && k < d) ? rows[(int64_t)q * d + k] : 0.0;
+        const int j0 = r * range, j1 = min(n, j0 + range);
+        for (int c0 = j0; c0 < j1; c0 += KNN_FX_CHUNK) {
+            const int cn = min(KNN_FX_CHUNK, j1 - c0);
+            __syncthreads();
+            for (int e = threadIdx.x; e < cn * d; e += 256) {  // the chunk's rows are contiguous
+                const int jj = e / d, k = e - jj * d;
+                sy[jj * DMAX + k] = rows[(int64_t)c0 * d + e];
+            }
+            __syncthreads();
+            for (int jj = wv; jj < cn; jj += 4) {
+                const int j = c0 + jj;
+                const double v = knn_exact_d2<DMAX>(xq, sy + jj * DMAX, d);
+                if (v <= t && j != q) {
+                    const int slot = atomicAdd(&cnt[f], 1);
+                    if (slot < KNN_FX_CAP) {
+                        bd[(int64_t)f * KNN_FX_CAP + slot] = v;
+                        bi[(int64_t)f * KNN_FX_CAP + slot] = j;
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void knn_fx_select_kernel(int kmax, const int* __restrict__ fail_list,
+                                                            const int* __restrict__ fail_count,
+                                                            const double* __restrict__ fail_tau,
+                                                            int* __restrict__ cnt, const double* __restrict__ bd,
+                                                            const int* __restrict__ bi, int32_t* __restrict__ out_idx,
+                                                            double* __restrict__ out_dist, bool dist_sq,
+                                                            int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
+    __shared__ double kd[KNN_FX_CAP];
+    __shared__ int ki[KNN_FX_CAP];
+    const int nf = *fail_count;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        const int q = fail_list[f];
+        int c = KNN_FX_CAP + 1;
+        if (f < KNN_FX_ROWS) {
+            c = cnt[f];
+            if (!(fail_tau[f] < INFINITY)) c = KNN_FX_CAP + 1;
+        }
+        __syncthreads();
+        if (f < KNN_FX_ROWS && threadIdx.x == 0) cnt[f] = 0;  // zero for the next call
+        if (c > KNN_FX_CAP || c < kmax) {  // the per-thread-list kernels take it
+            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
+            continue;
+        }
+        int m = 1;
+        while (m < c) m <<= 1;
+        for (int s = threadIdx.x; s < m; s += blockDim.x) {
+            kd[s] = s < c ? bd[(int64_t)f * KNN_FX_CAP + s] : INFINITY;
+            ki[s] = s < c ? bi[(int64_t)f * KNN_FX_CAP + s] : 0x7fffffff;
+        }
+        knn_lds_bitonic(kd, ki, m);
+        for (int r = threadIdx.x; r < kmax; r += blockDim.x) {
+            out_idx[(int64_t)q * kmax + r] = ki[r];
+            if (out_dist) out_dist[(int64_t)q * kmax + r] = dist_sq ? kd[r] : sqrt(kd[r]);
+        }
+        __syncthreads();
+    }
+}
+
+// The failed-row list of n rows and the radii beside it (one workspace).
+static int* knn_fail_ws(ccg_ctx* ctx, int64_t n, double** tau) {
+    const size_t li = (size_t)ccg_cdiv(n, 2) * 2;
+    int* p = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * li + sizeof(double) * (size_t)n + 16);
+    if (p && tau) *tau = (double*)(p + li);
+    return p;
+}
+
 // Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
 static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
                                const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
-                               int nseg, hipStream_t st, bool dist_sq = false) {
+                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr) {
+    if (!seg_off && fail_tau) {
+        // the radius search; its leftovers (overflow) continue below
+        int* cnt = (int*)ccg_ws(ctx, WS_FX_A, sizeof(int) * (KNN_FX_ROWS + 64 + n));
+        char* buf = (char*)ccg_ws(ctx, WS_FX_B, (sizeof(double) + sizeof(int)) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
+        if (!cnt || !buf) return CCG_ENOMEM;
+        if (ctx->fx_zeroed != (void*)cnt) {  // fresh buffer: the select kernel keeps the counters zero afterwards
+            CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * KNN_FX_ROWS, st));
+            ctx->fx_zeroed = (void*)cnt;
+        }
+        int* ovf_count = cnt + KNN_FX_ROWS;
+        int* ovf_list = ovf_count + 64;
+        double* bd = (double*)buf;
+        int* bi = (int*)(bd + (size_t)KNN_FX_ROWS * KNN_FX_CAP);
+#define CCG_FX(DM_)                                                                                                \
+    knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, bd, bi, \
+                                                         ovf_count)
+        if (d <= 16) CCG_FX(16);
+        else if (d <= 32) CCG_FX(32);
+        else CCG_FX(64);
+#undef CCG_FX
+        knn_fx_select_kernel<<<256, 256, 0, st>>>(kmax, fail_list, fail_count, fail_tau, cnt, bd, bi, out_idx,
+                                                          out_dist, dist_sq, ovf_list, ovf_count);
+        fail_list = ovf_list;
+        fail_count = ovf_count;
+    }
     const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
     double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
@@ -1095,7 +1277,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     const int64_t npos = sg ? sg->npos : n;  // screening positions
     int* cand_idx = (int*)ccg_ws(ctx, WS_CAND_IDX, sizeof(int) * npos * 2 * KP);
     float* cand_thr = (float*)ccg_ws(ctx, WS_CAND_THR, sizeof(float) * npos * 2);
-    int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
+    double* fail_tau = nullptr;
+    int* fail_list = knn_fail_ws(ctx, n, &fail_tau);
     unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
     if (!cand_idx || !cand_thr || !fail_list || !misc) return CCG_ENOMEM;
     // misc: [0] max-norm / max|x| bits, [1] fail count, [2..3] double 1/sigma^2
@@ -1163,9 +1346,9 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         const unsigned grid = (unsigned)ccg_cdiv(npos, KNN_QPB);
         const int4* blk = sg ? sg->blk : nullptr;
         const int t_scr = ccg_timer_start(ctx, CCG_KT_KNN_SCREEN, st);
-#define CCG_SCREEN16(KS_, KP_, R_)                                                                \
-    knn_screen16_kernel<KS_, KP_, R_><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, blk, \
-                                                            pos_t0)
+#define CCG_SCREEN16(KS_, KP_, R_, ...)                                                                      \
+    knn_screen16_kernel<KS_, KP_, R_, ##__VA_ARGS__><<<grid, 256, 0, st>>>(img, (int)npos, nch, d, cand_idx, cand_thr, \
+                                                                           blk, pos_t0)
         if (KP == KNN_KP) {
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP, KNN_KP + KNN_TMARGIN);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP, KNN_KP + KNN_TMARGIN);
@@ -1174,10 +1357,11 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
             if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
             else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
             else CCG_SCREEN16(4, KNN_KP_BIG, KNN_KP_BIG + KNN_TMARGIN);
-        } else {  // cell tables: the union threshold KNN_TMARGIN ranks past kmax <= KNN_TAB_K
-            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
-            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
-            else CCG_SCREEN16(4, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN);
+        } else {  // cell tables: the union threshold KNN_TMARGIN ranks past kmax <= KNN_TAB_K (2 waves per
+                  // SIMD: the 32-entry lists do not fit the 3-wave register budget)
+            if (KSTEPS == 1) CCG_SCREEN16(1, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN, 2);
+            else if (KSTEPS == 2) CCG_SCREEN16(2, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN, 2);
+            else CCG_SCREEN16(4, KNN_KP_BIG, KNN_TAB_K + KNN_TMARGIN, 2);
         }
 #undef CCG_SCREEN16
         ccg_timer_stop(ctx, t_scr, st);
@@ -1191,7 +1375,7 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
 #define CCG_CERTIFY(KP_, DM_)                                                                             \
     knn_certify_kernel<KP_, DM_><<<(unsigned)ccg_cdiv(npos, 4), 256, 0, st>>>(                              \
         rows, (int)n, d, kmax, cand_idx, cand_thr, inv_scale2, err_ulps, order_perm, out_idx, out_dist, \
-        fail_list, fail_count, (int)npos, seg_off, nseg, dist_sq)
+        fail_list, fail_count, (int)npos, seg_off, nseg, dist_sq, fail_tau)
     if (KP == KNN_KP) {
         if (d <= 16) CCG_CERTIFY(KNN_KP, 16);
         else if (d <= 32) CCG_CERTIFY(KNN_KP, 32);
@@ -1203,7 +1387,7 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     }
 #undef CCG_CERTIFY
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, seg_off, nseg, st,
-                             dist_sq);
+                             dist_sq, fail_tau);
     if (rc) return rc;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
@@ -1507,6 +1691,75 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, co
     if (lane == 0 && __popcll(m) < kq) fail_list[atomicAdd(fail_count, 1)] = uid;
 }
 
+// Radius for a cell short of kq present table entries (one wave per cell):
+// the kq-th smallest exact d2 over distinct present cells near it -- its
+// present table entries, and for every table entry the first present cell of
+// that entry's own row outside the cell's row.  Any kq distinct present
+// cells bound the kq-th neighbour distance from above; +inf (the
+// per-thread-list search) when fewer than kq are found.
+#define KT_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
+__global__ __launch_bounds__(256) void kt_tau_kernel(int kq, int K, int d, const int* __restrict__ ustart,
+                                                     const int32_t* __restrict__ scell, const int* __restrict__ cell2u,
+                                                     const int32_t* __restrict__ tab_idx,
+                                                     const double* __restrict__ tab_d2, const double* __restrict__ urows,
+                                                     const int* __restrict__ fail_list,
+                                                     const int* __restrict__ fail_count, double* __restrict__ tau) {
+    __shared__ int srow_[4][64];
+    __shared__ int pick_[4][64];
+    __shared__ double val_[4][128];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int nf = *fail_count;
+    for (int f = blockIdx.x * 4 + wv; f < nf; f += gridDim.x * 4) {
+        const int uid = fail_list[f];
+        const int64_t c = scell[ustart[uid]];
+        const int v = lane < K ? tab_idx[c * K + lane] : -1;
+        srow_[wv][lane] = v;
+        const int u1 = v >= 0 ? cell2u[v] : -1;
+        const double val1 = u1 >= 0 ? tab_d2[c * K + lane] : INFINITY;
+        KT_SYNC();
+        int w = -1;
+        if (v >= 0) {
+            for (int s = 0; s < K && w < 0; ++s) {
+                const int x = tab_idx[(int64_t)v * K + s];
+                if (x < 0 || x == (int)c || cell2u[x] < 0) continue;
+                bool in_row = false;
+                for (int t = 0; t < K; ++t) in_row |= srow_[wv][t] == x;
+                if (!in_row) w = x;
+            }
+        }
+        pick_[wv][lane] = w;
+        KT_SYNC();
+        bool dup = false;
+        for (int t = 0; t < lane; ++t) dup |= w >= 0 && pick_[wv][t] == w;
+        double val2 = INFINITY;
+        if (w >= 0 && !dup) {
+            const double* xr = urows + (int64_t)uid * d;
+            const double* yr = urows + (int64_t)cell2u[w] * d;
+            double s2 = 0.0;
+            for (int k = 0; k < d; ++k) {
+                const double t = __dsub_rn(xr[k], yr[k]);
+                s2 = __dadd_rn(s2, __dmul_rn(t, t));
+            }
+            val2 = s2;
+        }
+        val_[wv][lane] = val1;
+        val_[wv][64 + lane] = val2;
+        KT_SYNC();
+        int c1 = 0, c2 = 0;
+        for (int t = 0; t < 128; ++t) {
+            const double b = val_[wv][t];
+            c1 += b <= val1 ? 1 : 0;
+            c2 += b <= val2 ? 1 : 0;
+        }
+        double best = INFINITY;
+        if (val1 < INFINITY && c1 >= kq) best = val1;
+        if (val2 < INFINITY && c2 >= kq) best = fmin(best, val2);
+        for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+        if (lane == 0) tau[f] = best;
+        KT_SYNC();
+    }
+}
+
 extern "C" int ccg_knn_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, int K, int32_t* tab_idx,
                                  double* tab_d2, ccg_knn_stats* stats, void* stream) {
     CCG_REQUIRE(ctx && pcs && tab_idx && tab_d2, "ccg_knn_table_dev: NULL argument");
@@ -1559,7 +1812,8 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     // workspaces are then sized for u <= min(n, N)
     const int ucap = n_unique >= 0 ? n_unique : (int)std::min<int64_t>(n, N);
     // workspaces (the full-size fail list first, so the distinct-cell run never grows it)
-    int* fail_list = (int*)ccg_ws(ctx, WS_FAIL_LIST, sizeof(int) * n);
+    double* ftau = nullptr;
+    int* fail_list = knn_fail_ws(ctx, n, &ftau);
     char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + (size_t)ucap + 1));
     double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)ucap * (d + kmax) +
                                                       sizeof(int32_t) * (size_t)ucap * kmax +
@@ -1614,7 +1868,9 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         kt_cellmap_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, ustart, scell, cell2u);
         kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, ustart, scell, cell2u, tab_idx, tab_d2,
                                                                    uidx, ud2, fail_list, ufail);
-        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true);
+        kt_tau_kernel<<<256, 256, 0, st>>>(kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, fail_list, ufail,
+                                           ftau);
+        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau);
         if (rc) return rc;
         if (stats) {
             int nf = 0;

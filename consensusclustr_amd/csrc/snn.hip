@@ -254,15 +254,18 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
 #define SNN_CLS_BITS 21
 // (also zeroes the per-graph counts cnt[nk][n+1] and the overflow counters,
 // which the build tiers fill: one launch instead of two memsets)
+// Copy nodes (src[j] >= 0, snn_src_kernel) join class 3, whose fixed-grid
+// kernel skips them: the copy pass writes their rows.
 __global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, int64_t* __restrict__ cls,
-                                 int64_t* __restrict__ cnt, int nk, int* __restrict__ ov_count) {
+                                 int64_t* __restrict__ cnt, int nk, int* __restrict__ ov_count,
+                                 const int* __restrict__ src) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < 64) ov_count[j] = 0;
     if (j <= n)
         for (int t = 0; t < nk; ++t) cnt[(int64_t)t * (n + 1) + j] = 0;
     if (j >= n) return;
     const int64_t M = roff[j + 1] - roff[j];
-    const int c = M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3));
+    const int c = (src && src[j] >= 0) ? 3 : (M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3)));
     cls[j] = c < 3 ? 1LL << (SNN_CLS_BITS * c) : 0;
 }
 
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
     int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ list, const int64_t* __restrict__ count,
-    int* __restrict__ ov_list, int* __restrict__ ov_count) {
+    int* __restrict__ ov_list, int* __restrict__ ov_count, const int* __restrict__ src) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kmax = sp.kk[sp.nk - 1];
     if constexpr (CLS == 3) {
@@ -681,6 +684,7 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
         const int64_t nl = *count;
         for (int64_t f = blockIdx.x; f < nl; f += gridDim.x) {
             const int64_t j = list[f];
+            if (src && src[j] >= 0) continue;  // a copy node (snn_copy_rows_kernel)
             if (rows.roff[j + 1] - rows.roff[j] > SNN_BITONIC_MAX) {
                 if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
                 continue;
@@ -705,6 +709,74 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
             }
         }
         snn_bitonic_node<EM, 1, K>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
+    }
+}
+
+// ------------------------------------------------------- copy nodes --
+// Bootstrap rows repeat cells (R/consensusClust.R:394): copies of a cell are
+// at distance 0, so their kNN lists hold each other first and then the same
+// rows, and their sets N+_k = {j} u knn_k(j) coincide for every k of kNum
+// (whenever the zero-distance group fits in the smallest k + 1).  For NUMBER
+// weights |N+_k(j) n N+_k(p)| depend on those sets only, so such a node j has
+// the same weight to every partner as the node r = min N+_kmin(j) < j, and
+// its row (partners p > j) is the part of r's row past j.  snn_src_kernel
+// finds r and checks the sets (any input: the test is exact set equality);
+// the build tiers skip these nodes and snn_copy_rows_kernel copies their
+// rows after them.
+__global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                      SnnSpec sp, int* __restrict__ src) {
+    const int lane = threadIdx.x & 63;
+    const int kmin = sp.kk[0], kmax = sp.kk[sp.nk - 1];
+    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+        int a = (int)j;
+        if (lane >= 1 && lane <= kmax) a = knn[j * kstride + lane - 1];
+        const bool bad = lane <= kmax && ((unsigned)a >= (unsigned)n || (lane >= 1 && a == (int)j));
+        int r = lane <= kmin ? a : 0x7fffffff;
+        for (int o = 32; o > 0; o >>= 1) r = min(r, __shfl_xor(r, o, 64));
+        bool ok = r < (int)j && !__any(bad);
+        if (ok) {
+            int b = r;
+            if (lane >= 1 && lane <= kmax) b = knn[(int64_t)r * kstride + lane - 1];
+            // N+_k(j) == N+_k(r) for every graph: every member of j's k-prefix is in r's
+            // (both hold k + 1 distinct rows)
+            for (int t = 0; t < sp.nk && ok; ++t) {
+                const int k = sp.kk[t];
+                bool found = lane > k;
+                for (int q = 0; q <= k; ++q) found |= a == __shfl(b, q, 64);
+                ok = __all(found);
+            }
+        }
+        if (lane == 0) src[j] = ok ? r : -1;
+    }
+}
+
+__global__ __launch_bounds__(256) void snn_copy_rows_kernel(int64_t n, SnnSpec sp, const int* __restrict__ src,
+                                                            int64_t* __restrict__ cnt, SnnRows rows) {
+    if (rows.roff[n] > rows.cap) return;  // rows not written (the caller sizes and retries)
+    const int lane = threadIdx.x & 63;
+    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+        const int r = src[j];
+        if (r < 0) continue;
+        const int64_t a = rows.roff[r];
+        const int len = rows.rlen[r];
+        // first entry of r's row with partner > j (partners ascending)
+        int lo = 0, hi = len;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (rows.nbr[a + mid] <= (int)j) lo = mid + 1;
+            else hi = mid;
+        }
+        const int64_t o = rows.roff[j];
+        int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
+        for (int i = lo + lane; i < len; i += 64) {
+            const unsigned w = rows.wpk[a + i];
+            rows.nbr[o + i - lo] = rows.nbr[a + i];
+            rows.wpk[o + i - lo] = w;
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t) c4[t] += (t < sp.nk && graph_has(sp, w, t)) ? 1 : 0;
+        }
+        snn_row_counts(sp, c4, n, j, lane, cnt);
+        if (lane == 0) rows.rlen[j] = len - lo;
     }
 }
 
@@ -1006,6 +1078,15 @@ __global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int 
 }
 
 // --------------------------------------------------------------- driver --
+// CCG_SNN_NO_COPY=1 builds every node (tools / A-B checks of the copy pass)
+static bool snn_no_copy() {
+    static const bool v = [] {
+        const char* e = getenv("CCG_SNN_NO_COPY");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 static int snn_spec(const int* ks, int nk, int type, int kstride, SnnSpec* sp) {
     CCG_REQUIRE(ks, "SNN: NULL ks");
     CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "SNN: 1 <= nk <= %d", SNN_MAXK);
@@ -1068,8 +1149,12 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     if (!cls) return CCG_ENOMEM;
     int64_t* ccount = cls + (n + 1);
     int* lists = (int*)(ccount + 8);
+    // copy nodes (NUMBER graphs only: RANK weights depend on the ranks)
+    int* src = sp.type == CCG_SNN_NUMBER && !snn_no_copy() ? ov : nullptr;
+    if (src)
+        snn_src_kernel<<<nblk, 256, 0, st>>>(knn, n, kstride, sp, src);
     snn_class_kernel<<<(unsigned)ccg_cdiv(std::max<int64_t>(n + 1, 64), 256), 256, 0, st>>>(roff, n, cls, cnt, sp.nk,
-                                                                                           ov_count);
+                                                                                           ov_count, src);
     rc = ccg_scan_i64(ctx, cls, cls, n, st);
     if (rc) return rc;
     snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
@@ -1077,7 +1162,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
 #define SNN_BITONIC(CLS_, K_, GRID_)                                                                           \
     snn_bitonic_build_kernel<CLS_, K_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                       \
         knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
-        ov_count + 1)
+        ov_count + 1, src)
 #define SNN_BITONIC_ALL(K_)                                                       \
     do {                                                                          \
         SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)));             \
@@ -1094,6 +1179,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
                                           ov2_list, ov_count + 2);
     snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,
                                                        dense, cnt, rows);
+    if (src) snn_copy_rows_kernel<<<nblk, 256, 0, st>>>(n, sp, src, cnt, rows);
     for (int t = 0; t < sp.nk; ++t) {
         rc = ccg_scan_i64(ctx, cnt + (int64_t)t * (n + 1), cnt + (int64_t)t * (n + 1), n, st);
         if (rc) return rc;

@@ -316,6 +316,42 @@ def test_snn_rows_match_per_graph_edges(engine, t):
     assert ne2[0].item() < 0 and -ne2[0].item() == off[-1].item()
 
 
+def test_snn_rows_copy_nodes_from_bootstrap_copies(engine):
+    """Bootstrap rows repeat cells, and the rows of a cell's copies are
+    copied from its first copy's row (identical N+ sets for every k).  Cases:
+    copies in twos and threes, a cell copied 14 times (more than the smallest
+    k + 1, so its copies' sets differ and they are built), and distinct cells
+    at one point (zero-distance groups mixing cells).  Every graph equals the
+    oracle's."""
+    import torch
+    rng = np.random.default_rng(35)
+    N = 5000
+    X = _mixture(rng, N, 10)
+    X[100:108] = X[7]  # 9 distinct cells at one point
+    boot = rng.integers(0, N, 4500).astype(np.int32)
+    boot[rng.choice(4500, 14, replace=False)] = 3  # one cell drawn 14 times
+    boot[rng.choice(4500, 5, replace=False)] = 104
+    idx, _ = engine.knn_boot(X, boot, kmax=20)
+    n = idx.shape[1]
+    knn_t = torch.from_numpy(idx[0]).cuda()
+    ks = (10, 15, 20)
+    off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    ln = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cap = n * 400
+    nbr = torch.empty(cap, dtype=torch.int32, device="cuda")
+    wpk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    ne = torch.zeros(3, dtype=torch.int64, device="cuda")
+    engine.snn_rows_t(knn_t, ks, "number", off, ln, nbr, wpk, ne)
+    torch.cuda.synchronize()
+    got = _rows_to_graphs(off.cpu().numpy(), ln.cpu().numpy(), nbr.cpu().numpy(),
+                          wpk.cpu().numpy().view(np.uint32), ks, "number")
+    for g, k in enumerate(ks):
+        ref = O.snn(idx[0], k, "number")
+        assert ne[g].item() == ref[0].size
+        for a, b in zip(got[g], ref):
+            assert np.array_equal(a, b)
+
+
 def test_snn_host_flavour_grows_row_reservation(engine):
     rng = np.random.default_rng(34)
     X = _mixture(rng, 3000, 8)

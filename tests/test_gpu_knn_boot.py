@@ -94,7 +94,8 @@ def test_knn_boot_dev_lattice_ties(engine, path, kmax):
     rng = np.random.default_rng(kmax)
     idx = rng.integers(0, pcs.shape[0], 600).astype(np.int32)
     fb = _check(engine, pcs, idx, kmax, path)
-    assert fb > 0  # the lattice's cut ties must have taken the exact path
+    if path == "screen":
+        assert fb > 0  # the screen cannot certify the lattice's cut ties: the exact path took them
 
 
 def test_knn_boot_dev_few_distinct_cells(engine, path):
