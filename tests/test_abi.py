@@ -72,7 +72,7 @@ def _header_prototypes():
     text = open(_lib.HEADER_PATH).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     out = {}
-    for m in re.finditer(r"^\s*(?:int|const char\*|void\*)\s+(ccg_\w+)\s*\(([^)]*)\)\s*;", text, re.M | re.S):
+    for m in re.finditer(r"^\s*(?:int|int64_t|const char\*|void\*)\s+(ccg_\w+)\s*\(([^)]*)\)\s*;", text, re.M | re.S):
         args = " ".join(m.group(2).split())
         out[m.group(1)] = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
     return out
