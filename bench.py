@@ -36,6 +36,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
 PEAK_F16_TFLOPS = 2500.0   # dense fp16/bf16 MFMA (the screen's v_mfma_f32_32x32x16_f16)
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA (2x bf16 dense 2.5 PF)
 PEAK_HBM_GBS = 8000.0
+PEAK_F64_TFLOPS = 78.6     # dense fp64 MFMA (MI355X spec; not in the guide)
 K_NUM = (10, 15, 20)
 N_RES = 20
 
@@ -60,7 +61,12 @@ def parse():
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
                     help="table: one cell table per step (ccg_knn_table_dev) filtered per bootstrap; "
                          "screen: a screen per bootstrap (warm-started)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="HIP hardware queues for this process (0: the runtime's default)")
+    ap.add_argument("--table-k", type=int, default=48,
+                    help="cell-table length K (<= 48): cells with fewer than 20 of their K nearest cells in a "
+                         "bootstrap take the exact search")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
     return ap.parse_args()
@@ -237,6 +243,8 @@ def main():
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.hw_queues > 0:  # hardware queues per process (read at HIP initialisation)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
     import torch
     import torch.distributed as dist
 
@@ -293,7 +301,7 @@ def main():
     hint = torch.zeros(N, dtype=torch.float32, device=dev)
     # the cell table (ccg_knn_table_dev): every cell's KT nearest other cells,
     # recomputed inside every timed step, then filtered per bootstrap
-    KT = 48
+    KT = args.table_k
     use_table = args.knn_path == "table"
     tab_idx = torch.empty((N, KT), dtype=torch.int32, device=dev)
     tab_d2 = torch.empty((N, KT), dtype=torch.float64, device=dev)
@@ -355,7 +363,7 @@ def main():
             with torch.cuda.stream(streams[ks]):
                 if j >= RING:
                     streams[ks].wait_event(ev_s[j - RING])  # the slot's previous bootstrap is consumed
-                engs[ks].gather_rows_t(pcs_cm, N, d, boots[j], rows_s[slot])
+                engs[ks].gather_rows_rm_t(pcs, N, d, boots[j], rows_s[slot])
                 boot_knn(engs[ks], j, rows_s[slot], knn_s[slot])
                 ev_k[j].record(streams[ks])
             with torch.cuda.stream(streams[ss]):
@@ -388,7 +396,7 @@ def main():
             si = j % S
             e = engs[si]
             with torch.cuda.stream(streams[si]):
-                e.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[si])
+                e.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[si])
                 boot_knn(e, j, rows_s[si], knn_s[si])
                 e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
                 e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
@@ -417,7 +425,7 @@ def main():
         if int(nedges.min().item()) < 0:
             raise RuntimeError(f"SNN row capacity too small: {rcap}")
     need = nedges.max(0).values.tolist()
-    eng.gather_rows_t(pcs_cm, N, d, boots[0], rows)
+    eng.gather_rows_rm_t(pcs, N, d, boots[0], rows)
     fb = eng.knn_boot_hint_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, hint, stats=True)  # certification statistics
     fb_cold = eng.knn_boot_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, stats=True)
     fb_tab_build = eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2, stats=True)
@@ -455,7 +463,7 @@ def main():
         torch.cuda.synchronize()
         th = time.perf_counter()
         with torch.cuda.stream(streams[0]):
-            eng.gather_rows_t(pcs_cm, N, d, boots[j], rows_s[0])
+            eng.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[0])
             boot_knn(eng, j, rows_s[0], knn_s[0])
             eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
             eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
@@ -475,19 +483,34 @@ def main():
     iso_table = eng.timing_read("knn_screen")
     iso_table_total = eng.timing_read("knn_total")
     for j in range(min(B, 8)):
-        eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+        eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         eng.knn_boot_table_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, tab_idx, tab_d2, knn)
     iso_boot_table = eng.timing_read("knn_total")
     for j in range(min(B, 8)):  # as in the screen path: warm-started by earlier bootstraps
-        eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+        eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn, hint)
     u_iso = float(np.mean(uniq[:min(B, 8)]))  # the screen searches the distinct cells
     iso_screen = eng.timing_read("knn_screen")
     iso_screen_total = eng.timing_read("knn_total")
     for j in range(min(B, 8)):  # cold: no hint (the first bootstrap of a run)
-        eng.gather_rows_t(pcs_cm, N, d, boots[j], rows)
+        eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         eng.knn_boot_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn)
     iso_cold = eng.timing_read("knn_screen")
+    # SNN and silhouette per bootstrap, in isolation (one stream, nothing else
+    # on the GPU): the per-bootstrap rooflines below
+    eng.timing_read("snn")
+    eng.timing_read("silhouette")
+    nis = min(B, 4)
+    for j in range(nis):
+        eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
+        boot_knn(eng, j, rows, knn)
+        eng.snn_rows_t(knn, K_NUM, "number", *snn_out[0], nedges[j])
+        eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+    iso_snn = eng.timing_read("snn")
+    iso_sil = eng.timing_read("silhouette")
+    torch.cuda.synchronize()
+    iso_edges = nedges[:nis].sum(0).tolist()  # per graph, over the nis bootstraps
+    iso_npres = int(nclust[:nis].sum().item())  # sum over the bootstraps' labelings of present clusters
     eng.timing(False)
     if G > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -557,6 +580,51 @@ def main():
         "mfma_pipe_frac": round(mfma_exec_table / (ms_table * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
     }
     coc_ms = kt["cocluster"][0] / max(kt["cocluster"][1], 1)
+    coc_traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            coc_traffic = json.load(f).get("cocluster_bytes_per_launch_B125")
+    roof_coc = {
+        "kernel": "cof_tile_kernel (one-hot int8 co/both GEMM, v_mfma_i32_32x32x32_i8), this rank's row slab",
+        "bound": "mfma",
+        "achieved": round(coc_ops / (coc_ms * 1e-3) / 1e12, 2),
+        "peak": PEAK_I8_TOPS,
+        "unit": "TOP/s",
+        "frac": round(coc_ops / (coc_ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
+        "traffic": coc_traffic,
+        "algorithmic_per_launch": f"2*P*(sum C_b + B) = {coc_ops:.3e} int8 ops (P={P} pairs in this slab, "
+                                  f"sum C_b={colC}, B={G * B}), SURVEY 8(d); one launch per step",
+        "avg_launch_ms": round(coc_ms, 4),
+        "avg_launch_ms_note": "library hipEvent timer on the launch stream, the timer step after the timed region",
+        "output_bytes_per_launch": 4 * P,
+    }
+    # SNN rows (bytes = sum_K (n K 4 + E_K 16) per bootstrap) and
+    # silhouette (fp64 MFMA widths: 2 d u sum_l C_l over the distinct cells),
+    # per bootstrap in isolation
+    snn_ms = iso_snn[0] / max(iso_snn[1], 1)
+    sil_ms = iso_sil[0] / max(iso_sil[1], 1)
+    snn_bytes = sum(n * k * 4 for k in K_NUM) + 16 * sum(iso_edges) / max(nis, 1)
+    sil_flop = 2.0 * d * u_iso * iso_npres / max(nis, 1)
+    roof_snn = {
+        "kernel": "SNN union-graph rows (ccg_snn_rows_dev: host lists, bitonic build tiers, copy rows)",
+        "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+        "achieved": round(snn_bytes / (snn_ms * 1e-3) / 1e9, 1),
+        "frac": round(snn_bytes / (snn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+        "traffic": None,
+        "algorithmic_per_launch": f"sum_K (n K 4 + E_K 16) = {snn_bytes:.3e} B per bootstrap (E_K the edges of "
+                                  f"graph K), SURVEY 8(d)",
+        "ms_per_boot": round(snn_ms, 4),
+    }
+    roof_sil = {
+        "kernel": "silhouette of the 60 clusterings (ccg_silhouette_cells_dev; widths on v_mfma_f64_16x16x4f64)",
+        "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_F64_TFLOPS,
+        "achieved": round(sil_flop / (sil_ms * 1e-3) / 1e12, 2),
+        "frac": round(sil_flop / (sil_ms * 1e-3) / 1e12 / PEAK_F64_TFLOPS, 4),
+        "traffic": None,
+        "algorithmic_per_launch": f"2 d u sum_l C_l = {sil_flop:.3e} flop per bootstrap (x.mu of the u distinct "
+                                  f"cells against every present centroid of the 60 labelings)",
+        "ms_per_boot": round(sil_ms, 4),
+    }
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -586,19 +654,13 @@ def main():
             "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}", "streams_per_gpu": S,
             "knn_path": args.knn_path,
         },
-        "roofline": (roof_table if use_table else roof_screen),
-        "roofline_screen_path" if use_table else "roofline_table_path": (roof_screen if use_table else roof_table),
-        "roofline_cocluster": {
-            "kernel": "cof_tile_kernel (one-hot int8, v_mfma_i32_32x32x32_i8)",
-            "bound": "mfma",
-            "achieved": round(coc_ops / (coc_ms * 1e-3) / 1e12, 2),
-            "peak": PEAK_I8_TOPS,
-            "unit": "TOP/s",
-            "frac": round(coc_ops / (coc_ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
-            "algorithmic_per_launch": f"2*P*(sum C_b + B) = {coc_ops:.3e} (P={P} pairs in this slab, "
-                                      f"sum C_b={colC}, B={G * B})",
-            "avg_launch_ms": round(coc_ms, 4),
-        },
+        "roofline": roof_coc,
+        "roofline_note": "the co-cluster GEMM is the largest single launch of a step; the per-bootstrap "
+                         "stages follow (kNN table screen once per step, SNN, silhouette)",
+        "roofline_knn_table" if use_table else "roofline_knn_screen": (roof_table if use_table else roof_screen),
+        "roofline_knn_screen_path" if use_table else "roofline_knn_table_path": (roof_screen if use_table else roof_table),
+        "roofline_snn": roof_snn,
+        "roofline_silhouette": roof_sil,
         "kernel_ms_per_step": per_step,
         "kernel_ms_per_step_note": "library hipEvent timers over one extra step after the timed region "
                                    "(bootstraps overlap, so kernel times sum to more than the step)",

@@ -59,6 +59,7 @@ SIGNATURES = {
     "ccg_ctx_device": (_i, [_p, _p]),
     "ccg_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
     "ccg_gather_rows_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p]),
+    "ccg_gather_rows_rm_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p]),
     "ccg_knn_rows_dev": (_i, [_p, _p, _i64, _i, _i, _p, _p, _p, _p]),
     "ccg_knn_boot_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _p, _i, _p, _p, _p, _p]),
     "ccg_knn_boot_hint_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _p, _i, _p, _p, _p, _p, _p]),

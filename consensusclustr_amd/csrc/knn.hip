@@ -43,6 +43,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 #define KNN_FB_SLOTS 65536 // min scratch lists (failed rows x ranges)
 #define KNN_FB_UNITS 448   // target (failed row, range) blocks
+#ifndef KNN_EXPAND_CELLS
+#define KNN_EXPAND_CELLS 1  // tools only: 0 = the per-row expansion for every row (A/B)
+#endif
+#ifndef KNN_EXPAND_RADIUS
+#define KNN_EXPAND_RADIUS 1  // tools only: 0 = cut ties by the per-thread-list search (A/B)
+#endif
 #define KNN_FB_GRID 128    // fallback grids (grid-stride loops; usually 0-30 rows fail, and a
                            // 1024-block launch of exiting blocks alone cost ~30 us)
 
@@ -1049,6 +1055,38 @@ extern "C" int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, i
     return CCG_OK;
 }
 
+// row-major source: one thread per 16-byte piece of an output row (d even) or per value
+__global__ void gather_rows_rm_kernel(const double* __restrict__ pcs, int64_t N, int d,
+                                      const int32_t* __restrict__ idx, int64_t n, double* __restrict__ rows) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((d & 1) == 0) {
+        const int h = d >> 1;
+        if (t >= n * h) return;
+        const int64_t i = t / h;
+        const int k = (int)(t - i * h);
+        const int c = idx[i];
+        reinterpret_cast<double2*>(rows)[t] =
+            (c >= 0 && c < N) ? reinterpret_cast<const double2*>(pcs)[(int64_t)c * h + k] : make_double2(0.0, 0.0);
+    } else {
+        if (t >= n * d) return;
+        const int64_t i = t / d;
+        const int k = (int)(t - i * d);
+        const int c = idx[i];
+        rows[t] = (c >= 0 && c < N) ? pcs[(int64_t)c * d + k] : 0.0;
+    }
+}
+
+extern "C" int ccg_gather_rows_rm_dev(ccg_ctx* ctx, const double* pcs_rm, int64_t N, int d, const int32_t* idx,
+                                      int64_t n, double* rows, void* stream) {
+    CCG_REQUIRE(ctx && pcs_rm && idx && rows, "ccg_gather_rows_rm_dev: NULL argument");
+    CCG_REQUIRE(N > 0 && n > 0 && d > 0, "ccg_gather_rows_rm_dev: bad sizes");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int64_t tot = (d & 1) == 0 ? n * (d / 2) : n * d;
+    gather_rows_rm_kernel<<<(unsigned)ccg_cdiv(tot, 256), 256, 0, st>>>(pcs_rm, N, d, idx, n, rows);
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
 // Batched-segment description (ccg_knn_segments_dev): screening positions
 // are the segments laid end to end, each padded to a multiple of KNN_QPB.
 struct KnnSegs {
@@ -1544,14 +1582,11 @@ __global__ void kb_hint_kernel(int u, int kq, const int* __restrict__ ustart, co
 }
 
 #define KB_GMAX 33  // cells of one merge group (the own cell + kq <= 32 neighbours)
-__global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq, const int* __restrict__ uidx,
-                                                        const double* __restrict__ ud2,
-                                                        const int* __restrict__ ustart, const int* __restrict__ srow,
-                                                        const int* __restrict__ row2u, int kmax,
-                                                        int32_t* __restrict__ out_idx, double* __restrict__ out_dist,
-                                                        int* __restrict__ fail_list, int* __restrict__ fail_count) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ void kb_expand_row(int64_t i, int u, int kq, const int* __restrict__ uidx, const double* __restrict__ ud2,
+                              const int* __restrict__ ustart, const int* __restrict__ srow,
+                              const int* __restrict__ row2u, int kmax, int32_t* __restrict__ out_idx,
+                              double* __restrict__ out_dist, int* __restrict__ fail_list, int* __restrict__ fail_count,
+                              double* __restrict__ fail_tau) {
     const int uc = row2u[i];
     // the distinct cell's kq nearest distinct cells with their certified d2
     // (fp64, unfused, dimension order: the oracle's sums; copies share them)
@@ -1562,6 +1597,7 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
     double dn = kq > 0 ? d2l[0] : INFINITY;
     double gd = 0.0;  // the group's d2 (group 0: the own cell, d2 = 0)
     bool first = true, fail = false;
+    double ftau = INFINITY;  // no radius (n - 1 < kmax): the per-thread-list search
     int lo[KB_GMAX], hi[KB_GMAX];  // ranges of a multi-cell group (exact ties between distinct cells: rare)
     while (o < kmax) {
         // the group: the own cell first (group 0), then the distinct neighbours at d2 == gd
@@ -1592,6 +1628,7 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
         }
         if (t == kq && t > t0 && kq < u - 1) {  // the group may continue past the computed list
             fail = true;
+            ftau = gd;  // the radius search's bound: the rows so far and the cut group lie within gd
             break;
         }
         const double dist = out_dist ? sqrt(gd) : 0.0;
@@ -1631,7 +1668,118 @@ __global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq
         gd = dn;
         first = false;
     }
-    if (fail) fail_list[atomicAdd(fail_count, 1)] = (int)i;
+    if (fail) {
+        const int p = atomicAdd(fail_count, 1);
+        fail_list[p] = (int)i;
+        if (fail_tau) fail_tau[p] = ftau;
+    }
+}
+
+__global__ __launch_bounds__(256) void kb_expand_kernel(int64_t n, int u, int kq, const int* __restrict__ uidx,
+                                                        const double* __restrict__ ud2,
+                                                        const int* __restrict__ ustart, const int* __restrict__ srow,
+                                                        const int* __restrict__ row2u, int kmax,
+                                                        int32_t* __restrict__ out_idx, double* __restrict__ out_dist,
+                                                        int* __restrict__ fail_list, int* __restrict__ fail_count,
+                                                        double* __restrict__ fail_tau) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        kb_expand_row(i, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list, fail_count,
+                      fail_tau);
+}
+
+// The rows of the cells kb_expand_cells_kernel left to the per-row merge.
+__global__ __launch_bounds__(256) void kb_expand_ties_kernel(int u, int kq, const int* __restrict__ uidx,
+                                                             const double* __restrict__ ud2,
+                                                             const int* __restrict__ ustart,
+                                                             const int* __restrict__ srow,
+                                                             const int* __restrict__ row2u, int kmax,
+                                                             int32_t* __restrict__ out_idx,
+                                                             double* __restrict__ out_dist, int* __restrict__ fail_list,
+                                                             int* __restrict__ fail_count, double* __restrict__ fail_tau,
+                                                             const int* __restrict__ tie_list,
+                                                             const int* __restrict__ tie_count) {
+    const int nt = *tie_count;
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nt; f += gridDim.x * blockDim.x) {
+        const int uc = tie_list[f];
+        for (int z = ustart[uc]; z < ustart[uc + 1]; ++z)
+            kb_expand_row(srow[z], u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
+                          fail_count, fail_tau);
+    }
+}
+
+// The same expansion, one wave per DISTINCT cell (copies of a cell share
+// everything but the row they exclude): lanes load the cell's kq neighbour
+// cells and their row ranges at once, a wave scan places each neighbour's
+// rows, and every copy writes its list.  Valid when no two listed cells tie in
+// d2 (nor a listed cell with the own cell at d2 = 0): every group is one cell
+// whose rows are already ascending.  A cell with such a tie takes the
+// per-row merge (kb_expand_kernel's loop) for its rows.  kq <= 64.
+__global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, int kq, const int* __restrict__ uidx,
+                                                              const double* __restrict__ ud2,
+                                                              const int* __restrict__ ustart,
+                                                              const int* __restrict__ srow, const int* __restrict__ row2u,
+                                                              int kmax, int32_t* __restrict__ out_idx,
+                                                              double* __restrict__ out_dist, int* __restrict__ fail_list,
+                                                              int* __restrict__ fail_count,
+                                                              double* __restrict__ fail_tau,
+                                                              int* __restrict__ tie_list, int* __restrict__ tie_count) {
+    const int lane = threadIdx.x & 63;
+    const int uc = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (uc >= u) return;
+    const int oa = ustart[uc], ob = ustart[uc + 1], oc = ob - oa;  // the own cell's rows (sorted positions)
+    const bool has = lane < kq;
+    const int v = has ? uidx[(int64_t)uc * kq + lane] : 0;
+    const double dd = has ? ud2[(int64_t)uc * kq + lane] : INFINITY;
+    const int a = has ? ustart[v] : 0, cn = has ? ustart[v + 1] - a : 0;
+    const double dprev = __shfl_up(dd, 1, 64);
+    const bool tie = has && (lane == 0 ? dd == 0.0 : dd == dprev);
+    if (__any(tie)) {  // equal-d2 groups of several cells: the per-row merge
+        if (lane == 0) tie_list[atomicAdd(tie_count, 1)] = uc;
+        return;
+    }
+    int incl = cn;  // exclusive prefix of the neighbours' row counts
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int pre = incl - cn;
+    const int own = oc - 1;                    // own rows in every copy's list
+    const int need = kmax - own;               // neighbour rows a list takes (<= 0: own rows only)
+    const int total = __shfl(incl, 63, 64);    // all listed neighbours' rows
+    // the last listed cell reached while the list is short: a tie may continue past it
+    const int plast = __shfl(pre, kq - 1, 64);
+    const bool cut = need > 0 && kq >= 1 && plast < need && kq < u - 1;
+    const bool shortl = need > 0 && total < need;  // (kq = u - 1 and fewer than kmax rows: n - 1 < kmax)
+    const double glast = __shfl(dd, kq - 1, 64);
+    for (int z = oa; z < ob; ++z) {
+        const int i = srow[z];  // a copy (wave-uniform)
+        if (cut || shortl) {
+            if (lane == 0) {
+                const int p = atomicAdd(fail_count, 1);
+                fail_list[p] = i;
+                if (fail_tau) fail_tau[p] = cut ? glast : INFINITY;
+            }
+            continue;
+        }
+        int32_t* oi = out_idx + (int64_t)i * kmax;
+        double* od = out_dist ? out_dist + (int64_t)i * kmax : nullptr;
+        // own copies except i, ascending
+        for (int q = lane; q < oc && q - (q > z - oa ? 1 : 0) < kmax; q += 64) {
+            if (oa + q == z) continue;
+            const int pos = q - (q > z - oa ? 1 : 0);
+            oi[pos] = srow[oa + q];
+            if (od) od[pos] = 0.0;
+        }
+        // neighbour cells' rows
+        if (has && pre < need) {
+            const double dist = od ? sqrt(dd) : 0.0;
+            for (int q = 0; q < cn && pre + q < need; ++q) {
+                oi[own + pre + q] = srow[a + q];
+                if (od) od[own + pre + q] = dist;
+            }
+        }
+    }
 }
 
 extern "C" int ccg_knn_boot_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n,
@@ -1864,7 +2012,7 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         if (!cell2u) return CCG_ENOMEM;
         int* ufail = (int*)(misc + 5);
         CCG_HIP(hipMemsetAsync(cell2u, 0xff, sizeof(int) * (size_t)N, st));
-        CCG_HIP(hipMemsetAsync(misc + 4, 0, 2 * sizeof(unsigned), st));
+        CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));  // fail counts, expansion tie count
         kt_cellmap_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, ustart, scell, cell2u);
         kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, ustart, scell, cell2u, tab_idx, tab_d2,
                                                                    uidx, ud2, fail_list, ufail);
@@ -1889,10 +2037,25 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     return CCG_OK;
 #endif
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
-    if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, sizeof(int), st));  // (the table path zeroed it above)
-    kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
-                                         fail_count);
-    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st);
+    if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, 3 * sizeof(int), st));  // (the table path zeroed it above)
+    // one wave per distinct cell; cells whose list holds an equal-d2 tie
+    // between cells take the per-row merge.  Cut ties: a radius search over
+    // all rows (fewer than kmax rows within the radius, or more than the
+    // candidate cap: the per-thread-list search)
+    if (KNN_EXPAND_CELLS) {
+        int* tie_count = (int*)(misc + 6);  // zeroed with the fail counts
+        int* tie_list = (int*)head;         // the heads' scan is consumed (kb_tables_kernel)
+        kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u,
+                                                                         kmax, out_idx, out_dist, fail_list, fail_count,
+                                                                         ftau, tie_list, tie_count);
+        kb_expand_ties_kernel<<<64, 256, 0, st>>>(u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
+                                                  fail_list, fail_count, ftau, tie_list, tie_count);
+    } else {
+        kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
+                                             fail_list, fail_count, ftau);
+    }
+    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st, false,
+                             KNN_EXPAND_RADIUS ? ftau : nullptr);
     if (rc) return rc;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());

@@ -18,6 +18,10 @@
 // Grid: (row tiles) x (groups of SIL_LG labelings); x rows are held in
 // registers and reused across the group.
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "ccg_internal.h"
 
@@ -39,13 +43,12 @@ __device__ __forceinline__ int scale_exp(double bound) {
 __global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, int64_t tot,
                                                   unsigned* __restrict__ bits) {
     __shared__ unsigned red[4];
-    unsigned local = 0;
+    double mx = 0.0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
-         t += (int64_t)gridDim.x * blockDim.x) {
-        float f = (float)fabs(x[t]);
-        f = nextafterf(f, INFINITY);
-        local = max(local, __float_as_uint(f));
-    }
+         t += (int64_t)gridDim.x * blockDim.x)
+        mx = fmax(mx, fabs(x[t]));
+    // a float at or above max|x| (rounded up)
+    unsigned local = __float_as_uint(nextafterf((float)mx, INFINITY));
     for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
     __syncthreads();
@@ -134,24 +137,32 @@ __device__ __forceinline__ int sil_block_excl_scan(int v, int* sh, int* total) {
     return woff + x - v;
 }
 
-// K1': fixed-point rows, once per call: q1 = round(x * sc), q2 = round(x^2 *
-// sc2), [m][DMAX] int64 (zero past d).
+// K1': fixed-point rows, once per call: q1 = round(x * sc) [m][DMAX] int64
+// (zero past d) and q2 = round(|x|^2 * sc2) [m] (v_c needs only the
+// cluster's total sum of squares: v_c = S2 / n - |mu_c|^2).
+__host__ __device__ inline double sil_s2_bound(double maxabs, int d, int64_t m) {
+    return maxabs * maxabs * (double)d * (double)m;
+}
 template <int DMAX>
 __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const unsigned* __restrict__ maxabs_bits,
                           long long* __restrict__ q1, long long* __restrict__ q2) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m * DMAX) return;
-    const int64_t r = t / DMAX;
+    const int64_t r = t / DMAX;  // m * DMAX is a multiple of DMAX: a row's threads are all in or all out
+    if (r >= m) return;
     const int k = (int)(t - r * DMAX);
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
     const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
-    const double sc2 = ldexp(1.0, scale_exp(maxabs * maxabs * (double)m));
     const double v = k < d ? x[r * d + k] : 0.0;
     q1[t] = __double2ll_rn(v * sc);
-    q2[t] = __double2ll_rn(v * v * sc2);
+    // |x|^2 of the row: its DMAX threads are DMAX-aligned lanes of one wave
+    // (fixed xor tree: deterministic)
+    double s2 = v * v;
+#pragma unroll
+    for (int o = DMAX / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    if (k == 0) q2[r] = __double2ll_rn(s2 * ldexp(1.0, scale_exp(sil_s2_bound(maxabs, d, m))));
 }
 
-// K1 (sorted segments): cluster sums S1 = sum x, S2 = sum x^2 and counts of
+// K1 (sorted segments): cluster sums S1 = sum x, S2 = sum |x|^2 and counts of
 // a SIL_SORT_ROWS-row tile for one labeling (grid y), without a per-row
 // atomic.  The tile's rows are counting-sorted by label in LDS; each wave
 // then walks a quarter of the sorted rows with lanes along the dimensions
@@ -159,15 +170,26 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
 // label repeats, so a lane issues one LDS atomic per label segment instead of
 // one per row.  Large tiles keep the flush of the LDS sums to the global sums
 // (atomics from every block on the same words) rare.  Integer sums: any
-// order gives the same bits.  LDS: acc1, acc2 [cmax+1][DMAX] int64,
-// counts/offsets [cmax+1], sorted rows and labels [SIL_SORT_ROWS].
+// order gives the same bits.  LDS: acc1 [cmax+1][DMAX] and acc2 [cmax+1]
+// int64, counts/offsets [cmax+1], sorted rows, labels and weights
+// [SIL_SORT_ROWS].
 #ifndef SIL_SORT_ROWS
 #define SIL_SORT_ROWS 1024
 #endif
+#ifndef SIL_SUMS_ROWS
+#define SIL_SUMS_ROWS 0  // tools only: 1 = cluster sums over every row, not the representatives (A/B)
+#endif
 template <int DMAX>
 __host__ __device__ constexpr size_t sil_sorted_lds(int cmax) {
-    return (size_t)(cmax + 1) * DMAX * 16 + (size_t)(cmax + 1) * 8 + 2 * SIL_SORT_ROWS * 4;
+    return (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 16 + 3 * SIL_SORT_ROWS * 4;
 }
+
+// Distinct-cell form (rep != nullptr): tile position p is the representative
+// row rep[p] of a cell, weighted by the cnt[p] rows of the cell less the
+// mult[l][p] of them labelled apart in labeling l (those rows are added by
+// sil_sums_exc); the integer sums are those of the rows.  (Grid order: tiles
+// fastest.  Dealing a tile's labelings to one XCD instead, so its rows are
+// read into one L2, measured slower: 335 against 223 us at cfg3.)
 
 template <int DMAX>
 __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const int32_t* __restrict__ labels,
@@ -175,37 +197,47 @@ __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const
                                                          const long long* __restrict__ q2,
                                                          unsigned long long* __restrict__ gsum,
                                                          unsigned long long* __restrict__ gsum2,
-                                                         unsigned long long* __restrict__ gcnt) {
+                                                         unsigned long long* __restrict__ gcnt,
+                                                         const int* __restrict__ rep, const int* __restrict__ mult,
+                                                         const int* __restrict__ cnt, int64_t mw,
+                                                         const int64_t* __restrict__ nrep) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int RPT = SIL_SORT_ROWS / SIL_T;  // rows per thread in the sort
     constexpr int RPW = 64 / DMAX;              // rows per wave step
     constexpr int STEPS = SIL_SORT_ROWS / 4 / RPW;
     unsigned long long* acc1 = (unsigned long long*)smem;                 // [cmax+1][DMAX]
-    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * DMAX;         // [cmax+1][DMAX]
-    int* hcnt = (int*)(acc2 + (int64_t)(cmax + 1) * DMAX);                // [cmax+1]
+    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * DMAX;         // [cmax+1]
+    int* hcnt = (int*)(acc2 + (cmax + 1));                                // [cmax+1]
     int* hoff = hcnt + (cmax + 1);                                        // [cmax+1]
     int* srow = hoff + (cmax + 1);                                        // [SIL_SORT_ROWS]
     int* slab = srow + SIL_SORT_ROWS;                                     // [SIL_SORT_ROWS]
+    int* swgt = slab + SIL_SORT_ROWS;                                     // [SIL_SORT_ROWS]
     __shared__ int sh[SIL_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k = lane % DMAX, sub = lane / DMAX;
-    const int64_t rb = (int64_t)blockIdx.x * SIL_SORT_ROWS;
     const int l = blockIdx.y;
+    const int64_t rb = (int64_t)blockIdx.x * SIL_SORT_ROWS;
+    const int64_t npos = rep ? *nrep : m;  // positions: rows, or the representatives (counted on the device)
+    if (rb >= npos) return;
     const int nacc = (cmax + 1) * DMAX;
-    for (int t = tid; t < 2 * nacc; t += SIL_T) acc1[t] = 0ull;
+    for (int t = tid; t < nacc + cmax + 1; t += SIL_T) acc1[t] = 0ull;
     for (int t = tid; t <= cmax; t += SIL_T) hcnt[t] = 0;
     __syncthreads();
     // label 0 collects rows past m and codes outside [1, cmax]
-    int lab[RPT], rank[RPT];
+    int lab[RPT], rank[RPT], wgt[RPT], row[RPT];
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-        const int64_t r = rb + i * SIL_T + tid;
-        int lb = 0;
-        if (r < m) {
+        const int64_t p = rb + i * SIL_T + tid;
+        int lb = 0, w = 0, r = 0;
+        if (p < npos) {
+            r = rep ? rep[p] : (int)p;
             lb = labels[(int64_t)l * m + r];
-            if (lb < 1 || lb > cmax) lb = 0;
+            w = rep ? cnt[p] - mult[(int64_t)l * mw + p] : 1;
+            if (lb < 1 || lb > cmax || w <= 0) lb = 0;
         }
         lab[i] = lb;
+        wgt[i] = w;
+        row[i] = r;
         rank[i] = atomicAdd(&hcnt[lb], 1);
     }
     __syncthreads();
@@ -219,10 +251,17 @@ __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const
         carry += tot;
     }
     __syncthreads();
+    // the sorted positions carry (position in the tile, weight); hcnt becomes
+    // the weighted row count of each label
+    __syncthreads();
+    for (int t = tid; t <= cmax; t += SIL_T) hcnt[t] = 0;
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-        srow[hoff[lab[i]] + rank[i]] = i * SIL_T + tid;
+        srow[hoff[lab[i]] + rank[i]] = row[i];  // the row itself: no dependent load in the walk
         slab[hoff[lab[i]] + rank[i]] = lab[i];
+        swgt[hoff[lab[i]] + rank[i]] = wgt[i];
+        if (lab[i]) atomicAdd(&hcnt[lab[i]], wgt[i]);
     }
     __syncthreads();
     long long a1 = 0, a2 = 0;
@@ -232,13 +271,14 @@ __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const
     for (int st = 0; st < STEPS; ++st) {
         const int pos = p0 + st * RPW;
         const int lb = slab[pos];
-        const int64_t r = rb + srow[pos];
-        const long long v1 = lb ? q1[r * DMAX + k] : 0ll;
-        const long long v2 = lb ? q2[r * DMAX + k] : 0ll;
+        const int64_t r = srow[pos];
+        const long long w = swgt[pos];
+        const long long v1 = lb ? w * q1[r * DMAX + k] : 0ll;
+        const long long v2 = (lb && k == 0) ? w * q2[r] : 0ll;
         if (lb != cur) {
             if (cur && k < d) {
                 atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
-                atomicAdd(&acc2[cur * DMAX + k], (unsigned long long)a2);
+                if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
             }
             cur = lb;
             a1 = 0;
@@ -249,20 +289,39 @@ __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const
     }
     if (cur && k < d) {
         atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
-        atomicAdd(&acc2[cur * DMAX + k], (unsigned long long)a2);
+        if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
     }
     __syncthreads();
     unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
-    unsigned long long* gs2 = gsum2 + (int64_t)l * (cmax + 1) * d;
     for (int t = tid; t < nacc; t += SIL_T) {
         const int c = t / DMAX, kk = t - c * DMAX;
-        if (kk < d && c >= 1) {
-            if (acc1[t]) atomicAdd(&gs[(int64_t)c * d + kk], acc1[t]);
-            if (acc2[t]) atomicAdd(&gs2[(int64_t)c * d + kk], acc2[t]);
-        }
+        if (kk < d && c >= 1 && acc1[t]) atomicAdd(&gs[(int64_t)c * d + kk], acc1[t]);
     }
-    for (int c = 1 + tid; c <= cmax; c += SIL_T)
+    for (int c = 1 + tid; c <= cmax; c += SIL_T) {
         if (hcnt[c]) atomicAdd(&gcnt[(int64_t)l * (cmax + 1) + c], (unsigned long long)hcnt[c]);
+        if (acc2[c]) atomicAdd(&gsum2[(int64_t)l * (cmax + 1) + c], acc2[c]);
+    }
+}
+
+// Rows labelled apart from their cell's representative (the exception list
+// of sil_mult_kernel, l << 32 | row): their fixed-point rows added alone.
+template <int DMAX>
+__global__ void sil_sums_exc(int64_t m, int d, const int32_t* __restrict__ labels, int cmax,
+                             const long long* __restrict__ q1, const long long* __restrict__ q2,
+                             const unsigned long long* __restrict__ exc, const int* __restrict__ nexc,
+                             unsigned long long* __restrict__ gsum, unsigned long long* __restrict__ gsum2,
+                             unsigned long long* __restrict__ gcnt) {
+    const int ne = *nexc;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
+        const int l = (int)(exc[e] >> 32);
+        const int64_t r = (int64_t)(exc[e] & 0xffffffffull);
+        const int lab = labels[(int64_t)l * m + r];
+        if (lab < 1 || lab > cmax) continue;
+        unsigned long long* gs = gsum + ((int64_t)l * (cmax + 1) + lab) * d;
+        for (int k = 0; k < d; ++k) atomicAdd(&gs[k], (unsigned long long)q1[r * DMAX + k]);
+        atomicAdd(&gsum2[(int64_t)l * (cmax + 1) + lab], (unsigned long long)q2[r]);
+        atomicAdd(&gcnt[(int64_t)l * (cmax + 1) + lab], 1ull);
+    }
 }
 
 // Dimension order of a centroid row in muc: position p holds dimension
@@ -324,15 +383,10 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
         double s = 0.0;
         for (int k = 0; k < d; ++k) s = fma(ml[(int64_t)c * DMAX + k], ml[(int64_t)c * DMAX + k], s);
         auxc[((int64_t)l * cmax + pc) * 2] = s;
-        if (gsum2) {
-            const double inv_sc2 = ldexp(1.0, -scale_exp(maxabs * maxabs * (double)m));
-            const unsigned long long* g2 = gsum2 + ((int64_t)l * (cmax + 1) + c) * d;
+        if (gsum2) {  // v_c = S2 / n - |mu_c|^2
+            const double inv_sc2 = ldexp(1.0, -scale_exp(sil_s2_bound(maxabs, d, m)));
             const double n = (double)gc[c];
-            double v = 0.0;
-            for (int k = 0; k < d; ++k) {
-                const double mk = ml[(int64_t)c * DMAX + k];
-                v += ((double)(long long)g2[k] * inv_sc2) / n - mk * mk;
-            }
+            const double v = ((double)(long long)gsum2[(int64_t)l * (cmax + 1) + c] * inv_sc2) / n - s;
             auxc[((int64_t)l * cmax + pc) * 2 + 1] = fmax(v, 0.0);  // clamp the cancellation noise of equal points
         }
     }
@@ -806,8 +860,11 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
         // sorted segments: S1, S2 and counts in one pass, v_c in sil_mu
         sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q, q + m * DMAX);
         dim3 grid((unsigned)ccg_cdiv(m, SIL_SORT_ROWS), (unsigned)L);
-        sil_sums_sorted<DMAX><<<grid, SIL_T, sil_sorted_lds<DMAX>(cmax), st>>>(m, d, labels, cmax, q, q + m * DMAX,
-                                                                            gsum, gsum2, gcnt);
+        const bool reps = rep && !SIL_SUMS_ROWS;
+        sil_sums_sorted<DMAX><<<grid, SIL_T, sil_sorted_lds<DMAX>(cmax), st>>>(
+            m, d, labels, cmax, q, q + m * DMAX, gsum, gsum2, gcnt, reps ? rep : nullptr, mult, cnt, mw, nrep);
+        if (reps)
+            sil_sums_exc<DMAX><<<64, 256, 0, st>>>(m, d, labels, cmax, q, q + m * DMAX, exc, nexc, gsum, gsum2, gcnt);
         sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
     } else {
         dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
@@ -884,7 +941,7 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     }
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 1024), 256, 0, st>>>(x, m * d, maxabs);
     if (d <= 16)
         sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         out_width, st);
@@ -967,7 +1024,7 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     // only, so the width grid covers m positions and the weights' stride is m
     dim3 gx((unsigned)std::min<int64_t>(ccg_cdiv(m, 256), 32), (unsigned)std::min(L, 65535));
     sil_mult_kernel<<<gx, 256, 0, st>>>(cell, m, L, labels, first, scan, nonrep, m, mult, exc, nexc);
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 256), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 1024), 256, 0, st>>>(x, m * d, maxabs);
 #define SIL_CELLS(DM_)                                                                                              \
     sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
                     auxc, q, nullptr, st, rep, mult, cnt, m, exc, nexc, scan + m)

@@ -1037,7 +1037,9 @@ __global__ __launch_bounds__(256) void snn_dense_kernel(const int32_t* __restric
 
 // ------------------------------------------------- per-graph edge lists --
 // Graph t's edges of node j are the row entries with byte t present, already
-// in ascending partner order; off_t = exclusive scan of the per-graph counts.
+// in ascending partner order; off = ONE exclusive scan of the graphs' counts
+// laid end to end (block t = [t (n+1), (t+1)(n+1)), slot n zero), so graph
+// t's offsets are off[t (n+1) + j] - off[t (n+1)].
 __global__ __launch_bounds__(256) void snn_emit_kernel(int64_t n, SnnSpec sp, const int64_t* __restrict__ off,
                                                        SnnRows rows, SnnOut out) {
     const int lane = threadIdx.x & 63;
@@ -1047,7 +1049,7 @@ __global__ __launch_bounds__(256) void snn_emit_kernel(int64_t n, SnnSpec sp, co
         const int64_t ro = rows.roff[j];
         for (int t = 0; t < sp.nk; ++t) {
             if (out.cap[t] <= 0) continue;
-            int64_t e = off[(int64_t)t * (n + 1) + j];
+            int64_t e = off[(int64_t)t * (n + 1) + j] - off[(int64_t)t * (n + 1)];
             for (int c0 = 0; c0 < u; c0 += 64) {
                 const int c = c0 + lane;
                 const unsigned v = c < u ? rows.wpk[ro + c] : sp.init;
@@ -1074,7 +1076,7 @@ __global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int 
     int64_t* ds[4] = {d0, d1, d2, d3};
     const bool fit = roff[n] <= rcap;
     for (int t = 0; t < nk; ++t)
-        if (ds[t]) *ds[t] = fit ? cnt[(int64_t)t * (n + 1) + n] : -roff[n];
+        if (ds[t]) *ds[t] = fit ? cnt[(int64_t)t * (n + 1) + n] - cnt[(int64_t)t * (n + 1)] : -roff[n];
 }
 
 // --------------------------------------------------------------- driver --
@@ -1102,7 +1104,8 @@ static int snn_spec(const int* ks, int nk, int type, int kstride, SnnSpec* sp) {
 }
 
 // Builds the node rows (union graph) and per-graph counts; on return
-// cnt[t][0..n] holds their exclusive scans (graph t's edge offsets and total).
+// cnt[t (n+1) + j] holds one exclusive scan of all graphs' counts (graph t's edge
+// offsets and total relative to cnt[t (n+1)]).
 // roff: n+1 row offsets (capacity-based), from the workspace when NULL.
 static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const SnnSpec& sp, hipStream_t st,
                      int32_t* nbr, uint32_t* wpk, int64_t cap, int64_t* roff, int32_t* rlen, int64_t** cnt_out,
@@ -1112,7 +1115,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     CCG_REQUIRE(nkk < (1LL << 31) - 1, "SNN: n*kmax too large");
     int64_t* hoff = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
     int2* hosts_s = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (nkk + 1));
-    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * sp.nk * (n + 1));
+    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * (sp.nk * (n + 1) + 1));
     int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (5 * n + 64));
     unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
     int32_t* pairs = (int32_t*)ccg_ws(ctx, WS_SNN_F, sizeof(int32_t) * 4 * (nkk + 16));
@@ -1180,10 +1183,8 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,
                                                        dense, cnt, rows);
     if (src) snn_copy_rows_kernel<<<nblk, 256, 0, st>>>(n, sp, src, cnt, rows);
-    for (int t = 0; t < sp.nk; ++t) {
-        rc = ccg_scan_i64(ctx, cnt + (int64_t)t * (n + 1), cnt + (int64_t)t * (n + 1), n, st);
-        if (rc) return rc;
-    }
+    rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)sp.nk * (n + 1), st);  // every graph's offsets in one scan
+    if (rc) return rc;
     *cnt_out = cnt;
     *roff_out = roff;
     CCG_HIP(hipGetLastError());

@@ -6,7 +6,7 @@
 //
 // One pass per digit of <= 9 bits (the key bits split evenly, so 17-bit keys
 // take two 9/8-bit passes), three launches per pass:
-//   rs_hist    : per tile of RS_TILE pairs, the digit histogram (LDS atomics),
+//   rs_hist    : per tile of 256 * IPT pairs, the digit histogram (LDS atomics),
 //                written digit-major: cnt[digit * ntiles + tile];
 //   scan       : the library's two-launch multi-block scan (ccg_scan_i64) of
 //                that matrix -> every (digit, tile) pair's first output
@@ -24,17 +24,23 @@
 
 #define RS_THREADS 256
 #define RS_WAVES (RS_THREADS / 64)
-#define RS_IPT 16                       // pairs per thread per tile
-#define RS_TILE (RS_THREADS * RS_IPT)   // 4096 pairs per tile
 #define RS_MAXBITS 9
+// pairs per thread per tile (IPT = 1..16, tiles of 256 * IPT pairs): chosen per
+// sort so that about 256 or more tiles fill the GPU (the bootstrap's 90k-row
+// grouping ran 22 tiles of 4096 pairs, each a long serial chain)
+#define RS_TILES_MIN 256
+#ifndef RS_ADAPT
+#define RS_ADAPT 1  // tools only: 0 = tiles of 4096 pairs always (A/B)
+#endif
 
+template <int RS_IPT>
 __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift,
                                                       int bits, int ntiles, int64_t* __restrict__ cnt) {
     __shared__ int h[1 << RS_MAXBITS];
     const int nb = 1 << bits;
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) h[t] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    const int64_t base = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT);
 #pragma unroll 4
     for (int i = 0; i < RS_IPT; ++i) {
         const int64_t e = base + (int64_t)i * RS_THREADS + threadIdx.x;
@@ -49,6 +55,7 @@ __device__ __forceinline__ unsigned long long rs_lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+template <int RS_IPT>
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restrict__ kin,
                                                          const int32_t* __restrict__ vin, int64_t n, int shift,
                                                          int bits, int ntiles, const int64_t* __restrict__ off,
@@ -61,7 +68,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = (int)off[(int64_t)t * ntiles + blockIdx.x];
     __syncthreads();
     // wave w's run: pairs [base, base + 64 * RS_IPT), item i at base + 64 i + lane
-    const int64_t base = (int64_t)blockIdx.x * RS_TILE + (int64_t)w * 64 * RS_IPT;
+    const int64_t base = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT) + (int64_t)w * 64 * RS_IPT;
     int kk[RS_IPT], vv[RS_IPT], rk[RS_IPT];
     const unsigned long long lt = rs_lanemask_lt();
 #pragma unroll
@@ -114,7 +121,9 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
     CCG_REQUIRE(n >= 0 && n < (1LL << 31), "ccg_sort_pairs_i32: n out of range");
     CCG_REQUIRE(key_bits >= 0 && key_bits <= 31, "ccg_sort_pairs_i32: key_bits out of range");
     if (n == 0) return CCG_OK;
-    const int ntiles = (int)ccg_cdiv(n, RS_TILE);
+    int ipt = 16;
+    while (RS_ADAPT && ipt > 1 && ccg_cdiv(n, (int64_t)RS_THREADS * ipt) < RS_TILES_MIN) ipt >>= 1;
+    const int ntiles = (int)ccg_cdiv(n, (int64_t)RS_THREADS * ipt);
     if (key_bits == 0) {  // one digit value: the input order
         CCG_HIP(hipMemcpyAsync(keys_out, keys_in, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
         CCG_HIP(hipMemcpyAsync(vals_out, vals_in, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
@@ -135,10 +144,19 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
         const int bits = (key_bits - shift + (npass - p) - 1) / (npass - p);  // the remaining bits split evenly
         int32_t* ok = ((npass - 1 - p) % 2 == 0) ? keys_out : tk;
         int32_t* ov = ((npass - 1 - p) % 2 == 0) ? vals_out : tv;
-        rs_hist<<<ntiles, RS_THREADS, 0, st>>>(ck, n, shift, bits, ntiles, cnt);
-        const int rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)(1 << bits) * ntiles, st);
-        if (rc) return rc;
-        rs_scatter<<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov);
+#define RS_PASS(IPT_)                                                                              \
+    do {                                                                                           \
+        rs_hist<IPT_><<<ntiles, RS_THREADS, 0, st>>>(ck, n, shift, bits, ntiles, cnt);             \
+        const int rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)(1 << bits) * ntiles, st);            \
+        if (rc) return rc;                                                                         \
+        rs_scatter<IPT_><<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov); \
+    } while (0)
+        if (ipt == 16) RS_PASS(16);
+        else if (ipt == 8) RS_PASS(8);
+        else if (ipt == 4) RS_PASS(4);
+        else if (ipt == 2) RS_PASS(2);
+        else RS_PASS(1);
+#undef RS_PASS
         ck = ok;
         cv = ov;
         shift += bits;

@@ -292,6 +292,11 @@ class Engine:
         check(self.lib.ccg_gather_rows_dev(self.ctx, _ptr(pcs_cm), N, d, _ptr(idx), idx.numel(),
                                            _ptr(rows), _stream()))
 
+    def gather_rows_rm_t(self, pcs_rm, N, d, idx, rows):
+        """rows[i, :] = pcs[idx[i], :] from a row-major (N, d) tensor (ccg_gather_rows_rm_dev)."""
+        check(self.lib.ccg_gather_rows_rm_dev(self.ctx, _ptr(pcs_rm), N, d, _ptr(idx), idx.numel(),
+                                              _ptr(rows), _stream()))
+
     def knn_rows_t(self, rows, kmax, out_idx, out_dist=None, stats=False):
         n, d = rows.shape
         st = _lib.ccg_knn_stats() if stats else None

@@ -115,6 +115,14 @@ int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                         const int32_t* idx, int64_t n, double* rows,
                         void* stream);
 
+/* The same from a ROW-major N x d copy of the PCs (pcs_rm[c*d + k]): each
+ * row is d contiguous doubles, so the gather reads whole rows instead of one
+ * 8-byte word per column-major line (a caller drawing many bootstraps of one
+ * PC matrix transposes it once). */
+int ccg_gather_rows_rm_dev(ccg_ctx* ctx, const double* pcs_rm, int64_t N, int d,
+                           const int32_t* idx, int64_t n, double* rows,
+                           void* stream);
+
 /* kNN among the rows of a row-major n x d float64 matrix (device).
  * stats may be NULL; when given, the call synchronises to fill it. */
 int ccg_knn_rows_dev(ccg_ctx* ctx, const double* rows, int64_t n, int d,
