@@ -20,7 +20,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <type_traits>
 #include <vector>
 
 #include "ccg_internal.h"
@@ -63,7 +62,7 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 #define COF_CHUNK 16383     // columns per accumulation chunk
 #define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
 #ifndef COF_EXP
-#define COF_EXP 0           // tools only: 1 = no epilogue stores, 2 = the direct (unstaged) epilogue
+#define COF_EXP 0           // tools only: 1 = no epilogue stores
 #endif
 
 __device__ __forceinline__ int block_excl_scan1024(int v, int* sh, int* total) {
@@ -397,124 +396,11 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     }
     // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts).
     const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
-#if COF_EXP == 0
-    if constexpr (MODE == COF_TRI) {
-        // Through LDS, 8 rows of the wave's 64 x 128 quarter at a time: staged
-        // as co | both << 16, then written back row by row, each row's 128
-        // counts as 64 aligned 4-byte stores per array (256 contiguous bytes
-        // per store instead of 2 x 64).  A packed-triangle row starts at an even
-        // or odd offset; an odd row pairs its columns shifted by one and writes
-        // its first and last count alone.
-        constexpr int LD = 136;  // staged row stride (words): the two half-waves' rows on disjoint banks
-        static_assert(4 * 8 * LD * 4 <= (int)sizeof(panel), "epilogue stage must fit the panels");
-        __syncthreads();  // every wave is done with the panels
-        uint32_t* stg = reinterpret_cast<uint32_t*>(&panel[0][0][0]) + wv * (8 * LD);
-        const int64_t gj0 = rowB0 + wc * 128;
-        uint32_t* co32 = reinterpret_cast<uint32_t*>(co);
-        uint32_t* both32 = reinterpret_cast<uint32_t*>(both);
-        const uint32_t* cp32 = reinterpret_cast<const uint32_t*>(co_prev);
-        const uint32_t* bp32 = reinterpret_cast<const uint32_t*>(both_prev);
-        // one round per 8 rows, instantiated per (mi, q) so every accumulator
-        // index is a compile-time constant (runtime indices put acc in scratch)
-        auto round = [&](auto MIc, auto Qc) {
-            constexpr int mi = decltype(MIc)::value, q = decltype(Qc)::value;
-            {
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-                    for (int ni = 0; ni < 4; ++ni) {
-                        const int a = acc[mi][ni][4 * q + rr];
-                        stg[(rr + 4 * h) * LD + ni * 32 + (lane & 31)] = (uint32_t)(a & 16383) | ((uint32_t)(a >> 14) << 16);
-                    }
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");
-                for (int rho = 0; rho < 8; ++rho) {
-                    const int64_t gi = rowA0 + wr * 64 + mi * 32 + 8 * q + rho;
-                    if (gi >= r1) break;  // wave-uniform; later rows are past r1 too
-                    const int64_t rb = gi * N - gi * (gi + 1) / 2 - gi - 1 - base;  // o = rb + gj
-                    const int sft = (int)((rb + gj0) & 1);
-                    const int c0 = 2 * lane - sft;  // this lane's columns c0, c0 + 1 (tile-relative)
-                    const int64_t o = rb + gj0 + c0;  // even
-                    const bool ok0 = c0 >= 0 && gj0 + c0 < N && gj0 + c0 > gi;
-                    const bool ok1 = gj0 + c0 + 1 < N && gj0 + c0 + 1 > gi;  // c0 + 1 <= 127 always
-                    const uint32_t v0 = c0 >= 0 ? stg[rho * LD + c0] : 0u;
-                    const uint32_t v1 = stg[rho * LD + c0 + 1];
-                    int cv0 = (int)(v0 & 0xFFFFu), bv0 = (int)(v0 >> 16);
-                    int cv1 = (int)(v1 & 0xFFFFu), bv1 = (int)(v1 >> 16);
-                    if (co_prev) {
-                        if (ok0 && ok1) {
-                            const uint32_t pc = cp32[o >> 1], pb = bp32[o >> 1];
-                            cv0 += (int)(pc & 0xFFFFu);
-                            cv1 += (int)(pc >> 16);
-                            bv0 += (int)(pb & 0xFFFFu);
-                            bv1 += (int)(pb >> 16);
-                        } else {
-                            if (ok0) {
-                                cv0 += co_prev[o];
-                                bv0 += both_prev[o];
-                            }
-                            if (ok1) {
-                                cv1 += co_prev[o + 1];
-                                bv1 += both_prev[o + 1];
-                            }
-                        }
-                    }
-                    if (ok0 && ok1) {
-                        if (co) co32[o >> 1] = (uint32_t)cv0 | ((uint32_t)cv1 << 16);
-                        if (both) both32[o >> 1] = (uint32_t)bv0 | ((uint32_t)bv1 << 16);
-                    } else {
-                        if (ok0 && co) co[o] = (uint16_t)cv0;
-                        if (ok0 && both) both[o] = (uint16_t)bv0;
-                        if (ok1 && co) co[o + 1] = (uint16_t)cv1;
-                        if (ok1 && both) both[o + 1] = (uint16_t)bv1;
-                    }
-                    if (dist) {
-                        const double d0 = 1.0 - (double)(float)((double)cv0 / (double)bv0);
-                        const double d1 = 1.0 - (double)(float)((double)cv1 / (double)bv1);
-                        if (ok0 && ok1) *reinterpret_cast<double2*>(dist + o) = make_double2(d0, d1);
-                        else {
-                            if (ok0) dist[o] = d0;
-                            if (ok1) dist[o + 1] = d1;
-                        }
-                    }
-                    if (sft && lane == 63) {  // column 127 (the pairs covered -1 .. 126)
-                        const int64_t gj = gj0 + 127, o1 = rb + gj;
-                        if (gj < N && gj > gi) {
-                            const uint32_t v = stg[rho * LD + 127];
-                            int cv = (int)(v & 0xFFFFu), bv = (int)(v >> 16);
-                            if (co_prev) {
-                                cv += co_prev[o1];
-                                bv += both_prev[o1];
-                            }
-                            if (co) co[o1] = (uint16_t)cv;
-                            if (both) both[o1] = (uint16_t)bv;
-                            if (dist) dist[o1] = 1.0 - (double)(float)((double)cv / (double)bv);
-                        }
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");  // the stage is rewritten by the next 8 rows
-            }
-        };
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        round(I0{}, I0{});
-        round(I0{}, I1{});
-        round(I0{}, I2{});
-        round(I0{}, I3{});
-        round(I1{}, I0{});
-        round(I1{}, I1{});
-        round(I1{}, I2{});
-        round(I1{}, I3{});
-        return;
-    }
-#endif
     // Loops run row-major (mi, r outer) so each of a lane's 32 rows computes
     // its packed-triangle offset once for its 4 column groups (the 64-bit
-    // offset arithmetic per element dominated the small-B epilogue).  (TRI:
-    // the COF_EXP timing variants only.)
+    // offset arithmetic per element dominated the small-B epilogue).  Staging
+    // 8-row groups through LDS for 256-byte row stores was measured slower
+    // (25.9 against 22.6 ms at N = 100k, B = 125; 95.5 against 92.3 at B = 1000).
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
