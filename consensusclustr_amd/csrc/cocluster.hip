@@ -57,7 +57,9 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 // compacted list of non-empty columns.
 #define COF_BM 128          // output rows per block (2 waves x 64)
 #define COF_BN 256          // output cols per block (2 waves x 128)
+#ifndef COF_SLOTS
 #define COF_SLOTS 32        // slots per stage (16 K-steps of v_mfma_i32_32x32x32_i8)
+#endif
 #define COF_ROWS (COF_BM + COF_BN)
 #define COF_CHUNK 16383     // columns per accumulation chunk
 #define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)

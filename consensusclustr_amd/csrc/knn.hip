@@ -1155,6 +1155,16 @@ __device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
     __syncthreads();
 }
 
+// Each (row, reference) pair is first tested by an fp32 dot product,
+// approx = |x|^2 + |y|^2 - 2 (float) x.y, against radius + margin, the margin
+// covering the fp32 rounding of x, y and the 30-term accumulation
+// (<= 2^-17 (|x|^2 + |y|^2) with room to spare, plus an absolute 2^-60); only
+// pairs within it take the exact fp64 sum.  So the candidates are exactly the
+// plain scan's.  (The exact form costs three fp64 operations per dimension;
+// the filter one packed fp32 FMA per two.)
+#ifndef KNN_FX_FILTER
+#define KNN_FX_FILTER 1  // tools only: 0 = exact fp64 for every pair (A/B)
+#endif
 template <int DMAX>
 __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, int n, int d,
                                                           const int* __restrict__ fail_list,
@@ -1162,7 +1172,10 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                                                           const double* __restrict__ fail_tau, int* __restrict__ cnt,
                                                           double* __restrict__ bd, int* __restrict__ bi,
                                                           int* __restrict__ ovf_count) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
     __shared__ double sy[KNN_FX_CHUNK * DMAX];
+    __shared__ f2 syf[KNN_FX_CHUNK * DMAX / 2];
+    __shared__ double sny[KNN_FX_CHUNK];
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
     const int nf = min(*fail_count, KNN_FX_ROWS);
     // reference ranges: about 2 units per block of the grid whatever the row count
@@ -1179,8 +1192,15 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
         const int q = valid ? fail_list[f] : -1;
         const double t = valid ? tf : -1.0;
         double xq[DMAX];
+        f2 xf[DMAX / 2];
+        double nx = 0.0;
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) xq[k] = (valid && k < d) ? rows[(int64_t)q * d + k] : 0.0;
+        for (int k = 0; k < DMAX; ++k) {
+            xq[k] = (valid && k < d) ? rows[(int64_t)q * d + k] : 0.0;
+            nx = fma(xq[k], xq[k], nx);
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < DMAX / 2; ++k2) xf[k2] = f2{(float)xq[2 * k2], (float)xq[2 * k2 + 1]};
         const int j0 = r * range, j1 = min(n, j0 + range);
         for (int c0 = j0; c0 < j1; c0 += KNN_FX_CHUNK) {
             const int cn = min(KNN_FX_CHUNK, j1 - c0);
@@ -1189,15 +1209,39 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                 const int jj = e / d, k = e - jj * d;
                 sy[jj * DMAX + k] = rows[(int64_t)c0 * d + e];
             }
+            if (d < DMAX)
+                for (int e = threadIdx.x; e < cn * DMAX; e += 256) {  // zero the padding dims
+                    const int jj = e / DMAX, k = e - jj * DMAX;
+                    if (k >= d) sy[e] = 0.0;
+                }
+            __syncthreads();
+            for (int jj = threadIdx.x; jj < cn; jj += 256) {
+                double ny = 0.0;
+                for (int k = 0; k < DMAX; ++k) ny = fma(sy[jj * DMAX + k], sy[jj * DMAX + k], ny);
+                sny[jj] = ny;
+            }
+            for (int e = threadIdx.x; e < cn * DMAX / 2; e += 256)
+                syf[e] = f2{(float)sy[2 * e], (float)sy[2 * e + 1]};
             __syncthreads();
             for (int jj = wv; jj < cn; jj += 4) {
                 const int j = c0 + jj;
-                const double v = knn_exact_d2<DMAX>(xq, sy + jj * DMAX, d);
-                if (v <= t && j != q) {
-                    const int slot = atomicAdd(&cnt[f], 1);
-                    if (slot < KNN_FX_CAP) {
-                        bd[(int64_t)f * KNN_FX_CAP + slot] = v;
-                        bi[(int64_t)f * KNN_FX_CAP + slot] = j;
+                bool maybe = true;
+                if (KNN_FX_FILTER) {
+                    f2 acc = {0.f, 0.f};
+#pragma unroll
+                    for (int k2 = 0; k2 < DMAX / 2; ++k2) acc = __builtin_elementwise_fma(xf[k2], syf[jj * DMAX / 2 + k2], acc);
+                    const double ny = sny[jj];
+                    const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
+                    maybe = approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60;
+                }
+                if (maybe) {
+                    const double v = knn_exact_d2<DMAX>(xq, sy + jj * DMAX, d);
+                    if (v <= t && j != q) {
+                        const int slot = atomicAdd(&cnt[f], 1);
+                        if (slot < KNN_FX_CAP) {
+                            bd[(int64_t)f * KNN_FX_CAP + slot] = v;
+                            bi[(int64_t)f * KNN_FX_CAP + slot] = j;
+                        }
                     }
                 }
             }
