@@ -128,7 +128,7 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n,
                  hipStream_t st);
 
 // Stable device radix sort of (key, value) int32 pairs on the low key_bits
-// bits of the keys (hipCUB; temporary storage in WS_SORT).
+// bits of the keys (sort.hip; temporary storage in WS_SORT).
 int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
                        int32_t* vals_out, int64_t n, int key_bits, hipStream_t st);
 

@@ -176,6 +176,9 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
 #ifndef SIL_SORT_ROWS
 #define SIL_SORT_ROWS 1024
 #endif
+#ifndef SIL_SUMS_UNROLL
+#define SIL_SUMS_UNROLL 8  // walk steps whose loads are in flight together per wave
+#endif
 #ifndef SIL_SUMS_ROWS
 #define SIL_SUMS_ROWS 0  // tools only: 1 = cluster sums over every row, not the representatives (A/B)
 #endif
@@ -267,25 +270,43 @@ __global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const
     long long a1 = 0, a2 = 0;
     int cur = 0;
     const int p0 = wave * (SIL_SORT_ROWS / 4) + sub;
-#pragma unroll 8
-    for (int st = 0; st < STEPS; ++st) {
-        const int pos = p0 + st * RPW;
-        const int lb = slab[pos];
-        const int64_t r = srow[pos];
-        const long long w = swgt[pos];
-        const long long v1 = lb ? w * q1[r * DMAX + k] : 0ll;
-        const long long v2 = (lb && k == 0) ? w * q2[r] : 0ll;
-        if (lb != cur) {
-            if (cur && k < d) {
-                atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
-                if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
-            }
-            cur = lb;
-            a1 = 0;
-            a2 = 0;
+    // batches of U steps: the batch's LDS reads, then its gathered global
+    // loads (all in flight together), then the segment logic and its LDS
+    // atomics (an atomic between them would keep the compiler from hoisting
+    // the next step's reads: the walk waited on one load at a time)
+    constexpr int U = SIL_SUMS_UNROLL;
+    static_assert(STEPS % U == 0, "walk batches");
+    for (int st0 = 0; st0 < STEPS; st0 += U) {
+        int lbv[U];
+        int64_t rv[U];
+        long long wv[U], v1[U], v2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int pos = p0 + (st0 + u) * RPW;
+            lbv[u] = slab[pos];
+            rv[u] = srow[pos];
+            wv[u] = swgt[pos];
         }
-        a1 += v1;
-        a2 += v2;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v1[u] = lbv[u] ? q1[rv[u] * DMAX + k] : 0ll;
+            v2[u] = (lbv[u] && k == 0) ? q2[rv[u]] : 0ll;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int lb = lbv[u];
+            if (lb != cur) {
+                if (cur && k < d) {
+                    atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
+                    if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
+                }
+                cur = lb;
+                a1 = 0;
+                a2 = 0;
+            }
+            a1 += wv[u] * v1[u];
+            a2 += wv[u] * v2[u];
+        }
     }
     if (cur && k < d) {
         atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
@@ -564,15 +585,30 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     }
     const double wsc = ldexp(1.0, scale_exp((double)m));
     const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
+    // the next labeling's labels and cluster count are loaded a labeling ahead
+    // (their latency hides behind the current labeling's MFMA work)
+    int labn[RT];
+    int npn = 0;
+    {
+        const int l = blockIdx.y * SIL_LG;
+#pragma unroll
+        for (int t = 0; t < RT; ++t) labn[t] = (l < l1 && in[t]) ? labels[(int64_t)l * m + rowof[t]] : 0;
+        npn = l < l1 ? npres[l] : 0;
+    }
     for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
-        const int np = npres[l];
+        const int np = npn;
         int lab[RT];
         double oth[RT], self[RT];
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            lab[t] = in[t] ? labels[(int64_t)l * m + rowof[t]] : 0;
+            lab[t] = labn[t];
             oth[t] = INFINITY;
             self[t] = INFINITY;
+        }
+        if (l + 1 < l1) {
+#pragma unroll
+            for (int t = 0; t < RT; ++t) labn[t] = in[t] ? labels[(int64_t)(l + 1) * m + rowof[t]] : 0;
+            npn = npres[l + 1];
         }
         const double* ml = muc + (int64_t)l * cmax * DMAX;
         const double* al = auxc + (int64_t)l * cmax * 2;
