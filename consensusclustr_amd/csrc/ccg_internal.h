@@ -50,6 +50,7 @@ enum ccg_ws_slot {
     WS_COC_D,        // consensus kNN candidate path: the row-permuted assignment matrix
     WS_COC_E,        // consensus kNN candidate path: per-row candidate lists
     WS_COC_F,        // consensus kNN candidate path: thresholds, counters, flags
+    WS_COC_G,        // co-cluster fragment-entry matrix of a column chunk (slots x rows bytes)
     WS_HINT,         // kNN: per-cell threshold hints shared by the bootstraps of one host call
     WS_TAB_ROWS,     // kNN cell table: the PCs row-major (certify / fallback rows)
     WS_TAB_MAP,      // kNN cell table: cell -> distinct-cell id of a bootstrap (-1: absent)

@@ -48,13 +48,16 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 // and K = 16 * sum_b S_b instead of sum_b C_b + B separate positions.
 // Wider matrices (granular mode, B up to 65535) run in column chunks of at
 // most 16383 whose counts are added in the epilogue of the next chunk.
-// A lane gets its 16-byte MFMA fragment for slot (b, s) from its row's label
-// through a 34-entry LDS pattern table (at most two non-zero bytes), so the
-// one-hot matrix never exists -- not in HBM, not in LDS.  Labels are staged
-// per block of COF_SLOTS slots (<= COF_SLOTS columns x 384 rows: 128 A-rows +
-// 256 B-rows) in LDS, double-buffered through registers.  Columns with no
-// label (never sampled) own no slot and are skipped: stages index the
-// compacted list of non-empty columns.
+// A lane gets its 16-byte MFMA fragment for slot (b, s) from a 36-entry LDS
+// pattern table (at most two non-zero bytes), so the one-hot matrix never
+// exists -- not in HBM, not in LDS.  The table index of every (slot, row)
+// is one byte, computed once per chunk by cof_entries_kernel into the entry
+// matrix E (slots x rows, 1/16 of the one-hot bytes; the same bytes per
+// slot as a uint8 label column).  The GEMM stages E per block of COF_SLOTS
+// slots x 384 rows (128 A-rows + 256 B-rows) in LDS, double-buffered
+// through registers, so its inner loop is two LDS reads and one shift per
+// fragment: no per-slot descriptor, label offset or clamp.  Columns with no
+// label (never sampled) own no slot.
 #define COF_BM 128          // output rows per block (2 waves x 64)
 #define COF_BN 256          // output cols per block (2 waves x 128)
 #ifndef COF_SLOTS
@@ -63,6 +66,8 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 #define COF_ROWS (COF_BM + COF_BN)
 #define COF_CHUNK 16383     // columns per accumulation chunk
 #define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
+#define COF_EMAX (4LL << 30)  // bytes of the entry matrix E of one column chunk
+#define COF_ENT_GRID 8192   // blocks of the entry-matrix kernel
 #ifndef COF_EXP
 #define COF_EXP 0           // tools only: 1 = no epilogue stores
 #endif
@@ -88,13 +93,11 @@ __device__ __forceinline__ int block_excl_scan1024(int v, int* sh, int* total) {
 
 // Slot tables of one chunk of Bc columns (colC = the chunk's column maxima):
 // ccol[c] = chunk column of the c-th non-empty column; desc[k] = c << COF_SB
-// | s for k < K (K padded to a multiple of COF_SLOTS with -1); stage_lo[st] /
-// stage_nc[st] = the stage's range of compacted columns (nc <= COF_SLOTS since
-// every non-empty column owns at least one slot).
+// | s for k < K (K padded to a multiple of COF_SLOTS with -1); *nslot = the
+// padded K.
 __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__ colC, int64_t Bc,
                                                          int* __restrict__ ccol, int* __restrict__ nslot,
-                                                         int* __restrict__ desc, int* __restrict__ stage_lo,
-                                                         int* __restrict__ stage_nc) {
+                                                         int* __restrict__ desc) {
     __shared__ int sh[16];
     const int t = threadIdx.x;
     int kcar = 0, ccar = 0;
@@ -116,27 +119,43 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
     const int Kp = (K + COF_SLOTS - 1) / COF_SLOTS * COF_SLOTS;
     if (t == 0) *nslot = Kp;
     for (int k = K + t; k < Kp; k += 1024) desc[k] = -1;
-    __syncthreads();
-    for (int st = t; st < Kp / COF_SLOTS; st += 1024) {
-        const int k0 = st * COF_SLOTS;
-        const int k1 = min(k0 + COF_SLOTS, K) - 1;
-        const int lo = desc[k0] >> COF_SB;
-        const int hi = desc[k1] >> COF_SB;
-        stage_lo[st] = lo;
-        stage_nc[st] = hi - lo + 1;
-    }
 }
 
-// Fragment table (LDS, 36 x 16 B), indexed by off + med3(lab - 16 sub, -1, 16):
-//   slots sub >= 1 (off 1):  entry 0 / 17 = zero (label below / above the
-//       slot), 1 + x = one-hot byte x (x = 0..15);
-//   slot 0 (off 19):  entry 19 = zero (lab 0, not sampled), 19 + lab = flag
-//       (-128 in byte 0) + one-hot byte lab (lab = 1..15), 35 = flag only.
-// A fragment is one ds_read_b128 after 3 VALU (sub, med3, shift-add); the
-// per-slot 16 sub and entry offset are computed once per K-step.
-#define COF_TAB 36
-__device__ __forceinline__ int cof_entry(int lab, int sub16, int off) {
-    return off + min(max(lab - sub16, -1), 16);
+// Fragment table (LDS, 33 x 16 B): entry 0 = zero (label outside the slot,
+// or not sampled); 1 + x = one-hot byte x (x = 0..15, slots sub >= 1: label
+// 16 sub + x); 17 = the flag only (slot 0, label >= 16); 17 + lab = flag +
+// one-hot byte lab (slot 0, lab = 1..15).  The flag is int8 -128 in byte 0.
+// A wave's 16-byte reads spread over 16 bank groups (256 B); the common
+// vectors (zero, flag only, the one-hot bytes) sit in distinct groups.
+#define COF_TAB 33
+
+// Entry matrix of one chunk: E[k * Npad + i] = the table entry of row i in
+// slot k (desc[k] = column c << COF_SB | sub; -1 = padding slot: entry 0),
+// entry 0 for rows i >= N.  One dword (4 rows) per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ A, int64_t N, int64_t Npad,
+                                                          const int* __restrict__ desc, const int* __restrict__ ccol,
+                                                          const int* __restrict__ nslot_p, uint8_t* __restrict__ E) {
+    const int64_t nd = Npad / 4;
+    const int64_t tot = (int64_t)(*nslot_p) * nd;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = t / nd, r4 = 4 * (t - k * nd);
+        const int d = desc[k];
+        unsigned out = 0;
+        if (d >= 0) {
+            const int sub = d & ((1 << COF_SB) - 1);
+            const T* col = A + (int64_t)ccol[d >> COF_SB] * N;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (r4 + e >= N) continue;
+                const int lab = (int)col[r4 + e];
+                const int x = lab - 16 * sub;
+                const int en = sub == 0 ? (lab == 0 ? 0 : (lab < 16 ? 17 + lab : 17)) : ((unsigned)x < 16u ? 1 + x : 0);
+                out |= (unsigned)en << (8 * e);
+            }
+        }
+        *reinterpret_cast<unsigned*>(E + k * Npad + r4) = out;
+    }
 }
 
 // Output modes: packed upper triangle of rows [r0, r1) (R "dist" order), or
@@ -206,21 +225,16 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
     if (__any(nan) && lane == 0) cc.flags[0] = 1;
 }
 
-// T: label type (uint8_t / uint16_t); VEC: N is a multiple of 4/sizeof(T),
-// so a dword load covers 4/sizeof(T) consecutive rows of a column.
-template <typename T, bool VEC, int MODE>
+// E: the chunk's entry matrix (cof_entries_kernel), Npad bytes per slot.
+template <int MODE>
 __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
-    const T* __restrict__ A, int64_t N, int64_t r0, int64_t r1, int64_t TC, int64_t I0,
-    const int* __restrict__ desc, const int* __restrict__ stage_lo, const int* __restrict__ stage_nc,
-    const int* __restrict__ ccol, const int* __restrict__ nslot_p, const uint16_t* co_prev,
-    const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* __restrict__ dist,
-    const uint32_t* cb_prev, uint32_t* cb, int64_t NB, CofCand cc) {
-    constexpr int RPD = 4 / (int)sizeof(T);             // rows per dword
-    constexpr int ROWD = COF_ROWS / RPD;                // dwords per staged column
+    const uint8_t* __restrict__ E, int64_t Npad, int64_t N, int64_t r0, int64_t r1, int64_t TC, int64_t I0,
+    const int* __restrict__ nslot_p, const uint16_t* co_prev, const uint16_t* both_prev, uint16_t* co, uint16_t* both,
+    double* __restrict__ dist, const uint32_t* cb_prev, uint32_t* cb, int64_t NB, CofCand cc) {
+    constexpr int ROWD = COF_ROWS / 4;                  // dwords per staged slot
     constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
-    __shared__ __attribute__((aligned(16))) T panel[2][COF_SLOTS][COF_ROWS];
+    __shared__ __attribute__((aligned(16))) uint8_t panel[2][COF_SLOTS][COF_ROWS];
     __shared__ __attribute__((aligned(16))) v4i ftab[COF_TAB];
-    __shared__ __attribute__((aligned(16))) int sdesc[2][2][COF_SLOTS / 2];  // [buf][half][k-step]
     const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     int64_t I, J;
@@ -254,131 +268,74 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0;
 
-    // stage loader: dword p of the panel = (column c, row dword rd); rows past
-    // N read clamped rows (their outputs are masked in the epilogue).  The
-    // column indices of stage st+1 are fetched while stage st is issued, so
-    // a stage's label loads never wait on the column table; every load is
-    // unconditional (ccol has >= COF_SLOTS readable entries past any stage
-    // start; columns c >= nc are zeroed after the load).
-    // Stage loader.  Every value loaded in an iteration is first used at that
-    // iteration's commit, after the stage's MFMAs: the labels of stage st+1
-    // (from the column list scol[(st+1) & 1] in LDS) and the column list of
-    // stage st+2 (a 32-entry slice of ccol, masked to the stage's nc at
-    // commit; ccol has >= COF_SLOTS readable entries past any stage start).
-    // Dword p of the panel = (column c, row dword rd); rows past N read
-    // clamped rows (their outputs are masked in the epilogue); panel columns
-    // c >= nc hold column 0's labels and are never read by a descriptor.
-    __shared__ int scol[2][COF_SLOTS];
+    // Stage loader: dword p of the panel = (slot c, row dword rd) of E; rows
+    // past Npad read the last dword (their outputs are masked in the
+    // epilogue).  Every value loaded in an iteration is first used at that
+    // iteration's commit, after the stage's MFMAs.
     unsigned pf[LOADS];
-    int pdesc = -1, pclo = 0, pcol = 0, pcolok = 0;
     auto issue = [&](int st) {
-        const int* sc = scol[st & 1];
+        const uint8_t* Es = E + (int64_t)st * COF_SLOTS * Npad;
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) {
             const int p = i * 256 + tid;
             const int c = p / ROWD, rd = p - c * ROWD;
-            int64_t row = rd < COF_BM / RPD ? rowA0 + RPD * rd : rowB0 + RPD * (rd - COF_BM / RPD);
-            const T* colp = A + (int64_t)sc[c] * N;
-            unsigned v = 0u;
-            if (VEC) {
-                row = row + RPD <= N ? row : N - RPD;
-                v = *reinterpret_cast<const unsigned*>(colp + row);
-            } else {
-#pragma unroll
-                for (int e = 0; e < RPD; ++e) {
-                    const int64_t rr = row + e < N ? row + e : N - 1;
-                    v |= (unsigned)colp[rr] << (8 * sizeof(T) * e);
-                }
-            }
-            pf[i] = v;
-        }
-        pclo = stage_lo[st];
-        if (tid < COF_SLOTS) pdesc = desc[(int64_t)st * COF_SLOTS + tid];
-    };
-    auto fetch_cols = [&](int st) {
-        if (tid < COF_SLOTS) {
-            pcol = ccol[stage_lo[st] + tid];
-            pcolok = tid < stage_nc[st];
+            int64_t row = rd < COF_BM / 4 ? rowA0 + 4 * rd : rowB0 + 4 * (rd - COF_BM / 4);
+            row = row + 4 <= Npad ? row : Npad - 4;
+            pf[i] = *reinterpret_cast<const unsigned*>(Es + c * Npad + row);
         }
     };
-    auto commit = [&](int bb, int stc) {
+    auto commit = [&](int bb) {
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
-        if (tid < COF_SLOTS) {
-            const int dsc = pdesc;
-            sdesc[bb][tid & 1][tid >> 1] =
-                dsc < 0 ? -1 : (((dsc >> COF_SB) - pclo) << COF_SB) | (dsc & ((1 << COF_SB) - 1));
-            if (stc >= 0) scol[stc & 1][tid] = pcolok ? pcol : 0;
-        }
     };
     if (tid < COF_TAB) {
         v4i e = {0, 0, 0, 0};
-        if (tid >= 1 && tid <= 16) {  // later slots: one-hot byte tid - 1
+        if (tid >= 1 && tid <= 16) {  // one-hot byte tid - 1
             const int x = tid - 1;
             e[x >> 2] = 1 << (8 * (x & 3));
-        } else if (tid >= 20) {  // slot 0, label tid - 19 (35: >= 16, flag only)
-            const int x = tid - 19;
-            if (x < 16) e[x >> 2] = 1 << (8 * (x & 3));
-            e[0] |= 0x80;  // the flag (int8 -128) in byte 0
+        } else if (tid >= 17) {  // slot 0: the flag (int8 -128 in byte 0), + one-hot byte tid - 17
+            const int x = tid - 17;
+            if (x > 0) e[x >> 2] = 1 << (8 * (x & 3));
+            e[0] |= 0x80;
         }
         ftab[tid] = e;
     }
     if (nstage > 0) {
-        fetch_cols(0);
-        if (tid < COF_SLOTS) scol[0][tid] = pcolok ? pcol : 0;
-        __syncthreads();
         issue(0);
-        if (nstage > 1) fetch_cols(1);
-        commit(0, nstage > 1 ? 1 : -1);
+        commit(0);
     }
     __syncthreads();
     const int ra = wr * 64 + (lane & 31);            // A rows ra, ra + 32 (panel rows 0..127)
     const int rb = COF_BM + wc * 128 + (lane & 31);  // B rows rb + 32*ni
-    const int h = lane >> 5;
+    const int h = lane >> 5;                         // K-step q: lanes of half h take slot 2q + h
     for (int st = 0; st < nstage; ++st) {
         const int bb = st & 1;
         if (st + 1 < nstage) issue(st + 1);
-        if (st + 2 < nstage) fetch_cols(st + 2);
-        // software pipeline over the stage's K-steps: labels of step q+2 and
+        // software pipeline over the stage's K-steps: entries of step q+2 and
         // the fragment-table reads of step q+1 are in flight while the MFMAs
         // of step q run
         constexpr int QN = COF_SLOTS / 2;
-        int dsc[QN];
-#pragma unroll
-        for (int q4 = 0; q4 < QN / 4; ++q4) {
-            const int4 v = *reinterpret_cast<const int4*>(&sdesc[bb][h][4 * q4]);
-            dsc[4 * q4 + 0] = v.x;
-            dsc[4 * q4 + 1] = v.y;
-            dsc[4 * q4 + 2] = v.z;
-            dsc[4 * q4 + 3] = v.w;
-        }
-        int lab[2][6];
-        // branch-free: a padding slot (desc -1) reads column 0's labels and
-        // maps every label to the zero entry (sub16 above any label)
-        auto read_labels = [&](int q, int (&L)[6]) {
-            const T* col = &panel[bb][max(dsc[q], 0) >> COF_SB][0];
+        int ent[2][6];
+        auto read_entries = [&](int q, int (&L)[6]) {
+            const uint8_t* col = &panel[bb][2 * q + h][0];
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi) L[mi] = col[ra + 32 * mi];
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) L[2 + ni] = col[rb + 32 * ni];
         };
         v4i fr[2][6];
-        auto read_frags = [&](int q, const int (&L)[6], v4i (&F)[6]) {
-            const int d = dsc[q];
-            const int sub = d & ((1 << COF_SB) - 1);
-            const int sub16 = d < 0 ? (1 << 20) : 16 * sub;
-            const int off = (d >= 0 && sub == 0) ? 19 : 1;
+        auto read_frags = [&](const int (&L)[6], v4i (&F)[6]) {
 #pragma unroll
-            for (int x = 0; x < 6; ++x) F[x] = ftab[cof_entry(L[x], sub16, off)];
+            for (int x = 0; x < 6; ++x) F[x] = ftab[L[x]];
         };
-        read_labels(0, lab[0]);
-        read_labels(1, lab[1]);
-        read_frags(0, lab[0], fr[0]);
+        read_entries(0, ent[0]);
+        read_entries(1, ent[1]);
+        read_frags(ent[0], fr[0]);
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
             const int cur = q & 1;
-            if (q + 2 < QN) read_labels(q + 2, lab[cur]);
-            if (q + 1 < QN) read_frags(q + 1, lab[cur ^ 1], fr[cur ^ 1]);
+            if (q + 2 < QN) read_entries(q + 2, ent[cur]);
+            if (q + 1 < QN) read_frags(ent[cur ^ 1], fr[cur ^ 1]);
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -388,7 +345,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         }
         if (st + 1 < nstage) {
             __syncthreads();  // every wave is done with buffer bb^1 (read in stage st-1)
-            commit(bb ^ 1, st + 2 < nstage ? st + 2 : -1);
+            commit(bb ^ 1);
             __syncthreads();
         }
     }
@@ -455,14 +412,17 @@ struct CofPlan {
     int* ccol;
     int* nslot;
     int* desc;
-    int* slo;
-    int* snc;
     int64_t maxslots;
+    uint8_t* E;                 // entry matrix of the current chunk (maxslots x Npad bytes)
+    int64_t Npad;               // rows per slot of E (N rounded up to 4)
+    std::vector<int64_t> cuts;  // column chunks [cuts[c], cuts[c + 1])
 };
 
-// Column maxima + table space.  label_bits 16 synchronises once to size the
-// slot table exactly (sum_b ceil((C_b + 1) / 16) can be large); 8 bounds it
-// by 16 slots per column.
+// Column maxima, column chunks and table space.  A chunk has at most
+// COF_CHUNK columns (the 14-bit co field) and an entry matrix of at most
+// COF_EMAX bytes.  8-bit labels bound the slots by 16 per column; when that
+// bound does not fit (and always for 16-bit labels) the column maxima are
+// read back once to size the chunks exactly.
 static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, hipStream_t st,
                     CofPlan* pl) {
     int* colC = (int*)ccg_ws(ctx, WS_COC_A, sizeof(int) * (B + 8));
@@ -472,49 +432,63 @@ static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int6
     if (label_bits == 8) coc_colmax_kernel<uint8_t><<<g, 256, 0, st>>>((const uint8_t*)A, N, colC);
     else coc_colmax_kernel<uint16_t><<<g, 256, 0, st>>>((const uint16_t*)A, N, colC);
     CCG_HIP(hipGetLastError());
+    const int64_t Npad = (N + 3) / 4 * 4;
     const int64_t Bc = std::min<int64_t>(B, COF_CHUNK);
+    pl->cuts.clear();
     int64_t maxslots = Bc * 16 + COF_SLOTS;
-    if (label_bits == 16) {
+    if (label_bits == 8 && maxslots * Npad <= COF_EMAX) {
+        for (int64_t c0 = 0; c0 < B; c0 += COF_CHUNK) pl->cuts.push_back(c0);
+        pl->cuts.push_back(B);
+    } else {
         std::vector<int> h(B);
         CCG_HIP(hipMemcpyAsync(h.data(), colC, sizeof(int) * B, hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
-        int64_t worst = 0;
-        for (int64_t c0 = 0; c0 < B; c0 += COF_CHUNK) {
-            int64_t s = 0;
-            for (int64_t b = c0; b < std::min<int64_t>(B, c0 + COF_CHUNK); ++b) s += h[b] > 0 ? (h[b] + 16) / 16 : 0;
-            worst = std::max(worst, s);
+        const int64_t cap = std::max<int64_t>(COF_EMAX / Npad - COF_SLOTS, 4097);  // slots per chunk
+        int64_t s = 0, worst = 0, c0 = 0;
+        pl->cuts.push_back(0);
+        for (int64_t b = 0; b < B; ++b) {
+            const int64_t v = h[b] > 0 ? (h[b] + 16) / 16 : 0;
+            if (b > c0 && (b - c0 == COF_CHUNK || s + v > cap)) {
+                pl->cuts.push_back(b);
+                worst = std::max(worst, s);
+                s = 0;
+                c0 = b;
+            }
+            s += v;
         }
-        maxslots = worst + COF_SLOTS;
+        pl->cuts.push_back(B);
+        maxslots = std::max(worst, s) + COF_SLOTS;
     }
-    int* ft = (int*)ccg_ws(ctx, WS_COC_B, sizeof(int) * (Bc + 8 + maxslots + 2 * (maxslots / COF_SLOTS + 1)));
+    int* ft = (int*)ccg_ws(ctx, WS_COC_B, sizeof(int) * (Bc + 8 + maxslots));
     if (!ft) return CCG_ENOMEM;
+    uint8_t* E = (uint8_t*)ccg_ws(ctx, WS_COC_G, (size_t)(maxslots * Npad));
+    if (!E) return CCG_ENOMEM;
     pl->colC = colC;
     pl->ccol = ft;
     pl->nslot = ft + Bc;
     pl->desc = pl->nslot + 8;
-    pl->slo = pl->desc + maxslots;
-    pl->snc = pl->slo + (maxslots / COF_SLOTS + 1);
     pl->maxslots = maxslots;
+    pl->E = E;
+    pl->Npad = Npad;
     return CCG_OK;
 }
 
+// One column chunk [cb0, cb0 + Bc): slot tables, entry matrix, GEMM tiles.
 template <int MODE>
-static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t N, int64_t r0, int64_t r1, int64_t TC,
-                       int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
+static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, int64_t N, int64_t r0, int64_t r1,
+                       int64_t TC, int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
                        const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
                        uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{}) {
-#define COF_ARGS N, r0, r1, TC, I0, pl.desc, pl.slo, pl.snc, pl.ccol, pl.nslot, co_prev, both_prev, co, both, dist, \
-                 cb_prev, cb, (NB ? NB : N), cc
-    if (label_bits == 8) {
-        const uint8_t* Ac = (const uint8_t*)A + cb0 * N;
-        if (N % 4 == 0) cof_tile_kernel<uint8_t, true, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
-        else cof_tile_kernel<uint8_t, false, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
-    } else {
-        const uint16_t* Ac = (const uint16_t*)A + cb0 * N;
-        if (N % 2 == 0) cof_tile_kernel<uint16_t, true, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
-        else cof_tile_kernel<uint16_t, false, MODE><<<(unsigned)ntiles, 256, 0, st>>>(Ac, COF_ARGS);
-    }
-#undef COF_ARGS
+    cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc);
+    const unsigned eg = (unsigned)std::min<int64_t>(ccg_cdiv(pl.maxslots * (pl.Npad / 4), 256), COF_ENT_GRID);
+    if (label_bits == 8)
+        cof_entries_kernel<uint8_t><<<eg, 256, 0, st>>>((const uint8_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
+                                                        pl.nslot, pl.E);
+    else
+        cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
+                                                         pl.nslot, pl.E);
+    cof_tile_kernel<MODE><<<(unsigned)ntiles, 256, 0, st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, co_prev,
+                                                            both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
 }
 
 extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, int64_t r0,
@@ -538,7 +512,7 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
     CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_dev: too many tiles");
-    const int64_t nch = ccg_cdiv(B, COF_CHUNK);
+    const int64_t nch = (int64_t)pl.cuts.size() - 1;
     uint16_t *pco = co, *pboth = both;  // partial counts between chunks
     if (nch > 1 && (!co || !both)) {
         const int64_t P = (r1 - r0) * N - (r1 * (r1 + 1) - r0 * (r0 + 1)) / 2;
@@ -549,10 +523,9 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     }
     const int t_k = ccg_timer_start(ctx, CCG_KT_COCLUSTER, st);
     for (int64_t c = 0; c < nch; ++c) {
-        const int64_t cb0 = c * COF_CHUNK, Bc = std::min<int64_t>(COF_CHUNK, B - cb0);
-        cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
+        const int64_t cb0 = pl.cuts[c], Bc = pl.cuts[c + 1] - cb0;
         const bool last = c == nch - 1;
-        cof_launch<COF_TRI>(label_bits, A, cb0, N, r0, r1, TC, I0, ntiles, pl, c ? pco : nullptr,
+        cof_launch<COF_TRI>(label_bits, A, cb0, Bc, N, r0, r1, TC, I0, ntiles, pl, c ? pco : nullptr,
                             c ? pboth : nullptr, nch > 1 ? pco : co, nch > 1 ? pboth : both, last ? dist : nullptr,
                             nullptr, nullptr, st);
     }
@@ -575,11 +548,10 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     const int64_t ntiles = TR * TC;
     CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_rows: too many tiles");
-    const int64_t nch = ccg_cdiv(B, COF_CHUNK);
+    const int64_t nch = (int64_t)pl.cuts.size() - 1;
     for (int64_t c = 0; c < nch; ++c) {
-        const int64_t cb0 = c * COF_CHUNK, Bc = std::min<int64_t>(COF_CHUNK, B - cb0);
-        cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
-        cof_launch<COF_RECT>(label_bits, A, cb0, N, r0, r1, TC, I0, ntiles, pl, nullptr, nullptr, nullptr, nullptr,
+        const int64_t cb0 = pl.cuts[c], Bc = pl.cuts[c + 1] - cb0;
+        cof_launch<COF_RECT>(label_bits, A, cb0, Bc, N, r0, r1, TC, I0, ntiles, pl, nullptr, nullptr, nullptr, nullptr,
                              nullptr, c ? cb : nullptr, cb, st, NB);
     }
     CCG_HIP(hipGetLastError());
@@ -891,13 +863,13 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     CofPlan pl;
     int rc = cof_plan(ctx, Ap, label_bits, N, B, st, &pl);
     if (rc) return rc;
-    cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC, B, pl.ccol, pl.nslot, pl.desc, pl.slo, pl.snc);
+    if (pl.cuts.size() != 2) return CCG_OK;  // more than one column chunk: not done (the sub-slab path)
     const int64_t TC = ccg_cdiv(N, COF_BN), TR = ccg_cdiv(N, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - fl(TR);
     CCG_REQUIRE(ntiles < (1LL << 31), "consensus kNN: too many tiles");
     CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, flags};
-    cof_launch<COF_CAND>(label_bits, Ap, 0, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
+    cof_launch<COF_CAND>(label_bits, Ap, 0, B, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
                          nullptr, nullptr, st, N, cc);
     CCG_HIP(hipGetLastError());
     int hf[2] = {0, 0};
