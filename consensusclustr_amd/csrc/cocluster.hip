@@ -355,6 +355,30 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     }
     // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts).
     const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
+    if (MODE == COF_TRI && COF_EXP == 0 && co && both && !co_prev && !dist) {
+        // interior wave quarter (every column above every row, inside N and
+        // the slab): one pointer per row and immediate column offsets, no
+        // per-element masks or 64-bit offset arithmetic
+        const int64_t ia0 = rowA0 + wr * 64, jb0 = rowB0 + wc * 128;
+        if (jb0 > ia0 + 63 && jb0 + 128 <= N && ia0 + 64 <= r1) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t gi = ia0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int64_t o = gi * N - gi * (gi + 1) / 2 - gi - 1 - base + jb0 + (lane & 31);
+                    uint16_t* pc = co + o;
+                    uint16_t* pb = both + o;
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni) {
+                        const int a = acc[mi][ni][r];
+                        pc[32 * ni] = (uint16_t)(a & 16383);
+                        pb[32 * ni] = (uint16_t)(a >> 14);
+                    }
+                }
+            return;
+        }
+    }
     // Loops run row-major (mi, r outer) so each of a lane's 32 rows computes
     // its packed-triangle offset once for its 4 column groups (the 64-bit
     // offset arithmetic per element dominated the small-B epilogue).  Staging
