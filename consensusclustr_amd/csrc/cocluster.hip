@@ -200,6 +200,16 @@ __device__ __forceinline__ void cof_cand_push(const CofCand& cc, int64_t row, in
 __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64_t ia0, int64_t jb0, int64_t N,
                                                   int64_t r1, const CofCand& cc) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    // the lane's 4 columns' thresholds once (not per row); an interior
+    // quarter (every column above every row, inside N and the slab) needs no
+    // per-element masks
+    double tj[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int64_t gj = jb0 + 32 * ni + col;
+        tj[ni] = gj < N ? cc.tstar[gj] : INFINITY;
+    }
+    const bool interior = jb0 > ia0 + 63 && jb0 + 128 <= N && ia0 + 64 <= r1;
     bool nan = false;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -213,12 +223,12 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
                 const int64_t gj = jb0 + 32 * ni + col;
                 const int a = acc[mi][ni][r];
                 const int cv = a & 16383, bv = a >> 14;
-                if (row_ok && gj < N && gj > gi) {
+                if (interior || (row_ok && gj < N && gj > gi)) {
                     nan |= bv == 0;
                     const double dc = (double)cv, db = (double)bv;
                     const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
                     if (bv > 0 && dc >= ti * db) cof_cand_push(cc, gi, gj, N, val);
-                    if (bv > 0 && dc >= cc.tstar[gj] * db) cof_cand_push(cc, gj, gi, N, val);
+                    if (bv > 0 && dc >= tj[ni] * db) cof_cand_push(cc, gj, gi, N, val);
                 }
             }
         }
