@@ -176,12 +176,23 @@ struct CofCand {
     uint2* cand;
     int cap;
     int64_t pmul, padd;  // the row permutation: original id of position p = (p * pmul + padd) mod N
+    uint64_t pinv;       // floor((2^64 - 1) / N): the mod by a multiply-high (ckc_mod)
     int* flags;          // [0] a pair with both == 0, [1] a row overflowed cap
 };
 
+// x mod N for x < 2^63 by Barrett reduction with pinv = floor((2^64 - 1) / N):
+// q = mulhi(x, pinv) undershoots x / N by at most 2, so two corrections at most
+// (a 128-bit or 64-bit division is a long software loop on the GPU).
+__device__ __forceinline__ int64_t ckc_mod(uint64_t x, int64_t N, uint64_t pinv) {
+    const uint64_t q = __umul64hi(x, pinv);
+    uint64_t r = x - q * (uint64_t)N;
+    while (r >= (uint64_t)N) r -= (uint64_t)N;
+    return (int64_t)r;
+}
+
+// p * pmul + padd < N^2 + N < 2^63 for N < 2^31.
 __device__ __forceinline__ int64_t cof_orig(int64_t p, int64_t N, const CofCand& cc) {
-    return (int64_t)(((unsigned __int128)p * (unsigned __int128)cc.pmul + (unsigned __int128)cc.padd) %
-                     (unsigned __int128)N);
+    return ckc_mod((uint64_t)p * (uint64_t)cc.pmul + (uint64_t)cc.padd, N, cc.pinv);
 }
 
 // COF_CAND epilogue of one wave's 64 x 128 quarter (rows ia0.., columns
@@ -223,13 +234,27 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
                 const int64_t gj = jb0 + 32 * ni + col;
                 const int a = acc[mi][ni][r];
                 const int cv = a & 16383, bv = a >> 14;
-                if (interior || (row_ok && gj < N && gj > gi)) {
-                    nan |= bv == 0;
-                    const double dc = (double)cv, db = (double)bv;
-                    const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
-                    if (bv > 0 && dc >= ti * db) cof_cand_push(cc, gi, gj, N, val);
-                    if (bv > 0 && dc >= tj[ni] * db) cof_cand_push(cc, gj, gi, N, val);
+                const bool ok = interior || (row_ok && gj < N && gj > gi);
+                nan |= ok && bv == 0;
+                const double dc = (double)cv, db = (double)bv;
+                const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
+                // row gi is shared by the 32 lanes of this half: one counter
+                // add per half for all its passing pairs (lane order)
+                const bool pi = ok && bv > 0 && dc >= ti * db;
+                const unsigned long long m = __ballot(pi);
+                if (m) {
+                    const unsigned long long hm = h ? (m & 0xFFFFFFFF00000000ull) : (m & 0xFFFFFFFFull);
+                    const int leader = hm ? __ffsll((long long)hm) - 1 : lane;
+                    int base = 0;
+                    if (lane == leader && hm) base = atomicAdd(&cc.cnt[gi], __popcll(hm));
+                    base = __shfl(base, leader, 64);
+                    if (pi) {
+                        const int slot = base + __popcll(hm & ((1ull << lane) - 1));
+                        if (slot < cc.cap) cc.cand[gi * cc.cap + slot] = make_uint2((unsigned)cof_orig(gj, N, cc), val);
+                        else cc.flags[1] = 1;
+                    }
                 }
+                if (ok && bv > 0 && dc >= tj[ni] * db) cof_cand_push(cc, gj, gi, N, val);
             }
         }
     if (__any(nan) && lane == 0) cc.flags[0] = 1;
@@ -754,10 +779,10 @@ template <typename T>
 __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B, int64_t pmul, int64_t padd,
                                    T* __restrict__ Ap) {
     const int64_t tot = B * N;
+    const uint64_t pinv = ~0ull / (uint64_t)N;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t b = t / N, p = t - b * N;
-        const int64_t o = (int64_t)(((unsigned __int128)p * (unsigned __int128)pmul + (unsigned __int128)padd) %
-                                    (unsigned __int128)N);
+        const int64_t o = ckc_mod((uint64_t)p * (uint64_t)pmul + (uint64_t)padd, N, pinv);
         Ap[t] = A[b * N + o];
     }
 }
@@ -902,7 +927,7 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - fl(TR);
     CCG_REQUIRE(ntiles < (1LL << 31), "consensus kNN: too many tiles");
-    CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, flags};
+    CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, ~0ull / (uint64_t)N, flags};
     cof_launch<COF_CAND>(label_bits, Ap, 0, B, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
                          nullptr, nullptr, st, N, cc);
     CCG_HIP(hipGetLastError());
