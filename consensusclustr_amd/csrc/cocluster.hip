@@ -48,7 +48,7 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 // and K = 16 * sum_b S_b instead of sum_b C_b + B separate positions.
 // Wider matrices (granular mode, B up to 65535) run in column chunks of at
 // most 16383 whose counts are added in the epilogue of the next chunk.
-// A lane gets its 16-byte MFMA fragment for slot (b, s) from a 36-entry LDS
+// A lane gets its 16-byte MFMA fragment for slot (b, s) from a 33-entry LDS
 // pattern table (at most two non-zero bytes), so the one-hot matrix never
 // exists -- not in HBM, not in LDS.  The table index of every (slot, row)
 // is one byte, computed once per chunk by cof_entries_kernel into the entry
