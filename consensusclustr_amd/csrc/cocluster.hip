@@ -67,7 +67,7 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 #define COF_CHUNK 16383     // columns per accumulation chunk
 #define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
 #define COF_EMAX (4LL << 30)  // bytes of the entry matrix E of one column chunk
-#define COF_ENT_GRID 8192   // blocks of the entry-matrix kernel
+#define COF_ENT_GRID 4096   // slot blocks (grid y) of the entry-matrix kernel
 #ifndef COF_EXP
 #define COF_EXP 0           // tools only: 1 = no epilogue stores
 #endif
@@ -131,30 +131,34 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
 
 // Entry matrix of one chunk: E[k * Npad + i] = the table entry of row i in
 // slot k (desc[k] = column c << COF_SB | sub; -1 = padding slot: entry 0),
-// entry 0 for rows i >= N.  One dword (4 rows) per thread.
+// entry 0 for rows i >= N.  Slots stride over grid y, row dwords (4 rows per
+// thread) over grid x: no per-element division.
 template <typename T>
 __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ A, int64_t N, int64_t Npad,
                                                           const int* __restrict__ desc, const int* __restrict__ ccol,
                                                           const int* __restrict__ nslot_p, uint8_t* __restrict__ E) {
-    const int64_t nd = Npad / 4;
-    const int64_t tot = (int64_t)(*nslot_p) * nd;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = t / nd, r4 = 4 * (t - k * nd);
+    const int nslot = *nslot_p;
+    for (int k = blockIdx.y; k < nslot; k += gridDim.y) {
         const int d = desc[k];
-        unsigned out = 0;
-        if (d >= 0) {
-            const int sub = d & ((1 << COF_SB) - 1);
-            const T* col = A + (int64_t)ccol[d >> COF_SB] * N;
+        const int sub = d < 0 ? 0 : d & ((1 << COF_SB) - 1);
+        const T* col = A + (d < 0 ? 0 : (int64_t)ccol[d >> COF_SB] * N);
+        uint8_t* Ek = E + (int64_t)k * Npad;
+        for (int64_t r4 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); r4 < Npad;
+             r4 += 4 * (int64_t)gridDim.x * blockDim.x) {
+            unsigned out = 0;
+            if (d >= 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (r4 + e >= N) continue;
-                const int lab = (int)col[r4 + e];
-                const int x = lab - 16 * sub;
-                const int en = sub == 0 ? (lab == 0 ? 0 : (lab < 16 ? 17 + lab : 17)) : ((unsigned)x < 16u ? 1 + x : 0);
-                out |= (unsigned)en << (8 * e);
+                for (int e = 0; e < 4; ++e) {
+                    if (r4 + e >= N) continue;
+                    const int lab = (int)col[r4 + e];
+                    const int x = lab - 16 * sub;
+                    const int en =
+                        sub == 0 ? (lab == 0 ? 0 : (lab < 16 ? 17 + lab : 17)) : ((unsigned)x < 16u ? 1 + x : 0);
+                    out |= (unsigned)en << (8 * e);
+                }
             }
+            *reinterpret_cast<unsigned*>(Ek + r4) = out;
         }
-        *reinterpret_cast<unsigned*>(E + k * Npad + r4) = out;
     }
 }
 
@@ -539,7 +543,8 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
                        const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
                        uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{}) {
     cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc);
-    const unsigned eg = (unsigned)std::min<int64_t>(ccg_cdiv(pl.maxslots * (pl.Npad / 4), 256), COF_ENT_GRID);
+    const dim3 eg((unsigned)std::min<int64_t>(ccg_cdiv(pl.Npad / 4, 256), 128),
+                  (unsigned)std::min<int64_t>(pl.maxslots, COF_ENT_GRID));
     if (label_bits == 8)
         cof_entries_kernel<uint8_t><<<eg, 256, 0, st>>>((const uint8_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                         pl.nslot, pl.E);
