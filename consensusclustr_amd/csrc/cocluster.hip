@@ -418,6 +418,25 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             return;
         }
     }
+    if (MODE == COF_RECT && COF_EXP == 0 && !cb_prev) {
+        // interior wave quarter of the full rows: one pointer per row, immediate column offsets
+        const int64_t ia0 = rowA0 + wr * 64, jb0 = rowB0 + wc * 128;
+        if (jb0 + 128 <= NB && ia0 + 64 <= r1) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t gi = ia0 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    uint32_t* pr = cb + (gi - r0) * NB + jb0 + (lane & 31);
+#pragma unroll
+                    for (int ni = 0; ni < 4; ++ni) {
+                        const int a = acc[mi][ni][r];
+                        pr[32 * ni] = (uint32_t)(a & 16383) | ((uint32_t)(a >> 14) << 16);
+                    }
+                }
+            return;
+        }
+    }
     // Loops run row-major (mi, r outer) so each of a lane's 32 rows computes
     // its packed-triangle offset once for its 4 column groups (the 64-bit
     // offset arithmetic per element dominated the small-B epilogue).  Staging
