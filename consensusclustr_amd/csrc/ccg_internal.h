@@ -82,6 +82,9 @@ struct ccg_ctx {
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
     void* fx_zeroed;  // kNN radius search: the WS_FX_A buffer whose counters were zeroed at allocation
+    // kNN: the exact-search row list of the last call and its count (device; ccg_knn_last_fallback)
+    const int* last_fail_list;
+    const int* last_fail_count;
     // kernel timing (ccg_timing_*)
     int timing;
     ccg_timer_rec* timers;   // pool, grows

@@ -390,46 +390,6 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
     return x * q + min(x, r) + i;
 }
 
-// Timing attribution for tools only (tools/build_variant.sh stamps
-// "-DKNN_STAMPS=1"): s_memtime stamps split each screen wave's cycles into
-// chunk DMA issue (0), tile MFMA + max-reduce (1), enqueue (2), flushes (3),
-// union thresholds (4), the chunk's vmcnt wait (5) and barrier (6);
-// ccg_debug_knn_stamps reads the sums.  The stamps' own waits inflate the
-// tile share.
-#ifdef KNN_STAMPS
-// kst_[7..10] count events: tiles with a candidate (7), flushes (8), flush
-// insertion rounds (9), tiles (10); knn_stamp_acc[11] counts waves.
-__device__ unsigned long long knn_stamp_acc[12];
-#define KST_DECL                                                \
-    unsigned long long kst_[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
-    unsigned long long kst_t = __builtin_amdgcn_s_memtime()
-#define KST(i)                                                     \
-    do {                                                           \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        kst_[i] += t_ - kst_t;                                     \
-        kst_t = t_;                                                \
-    } while (0)
-#define KST_FLUSH_OUT()                                                             \
-    do {                                                                            \
-        if ((threadIdx.x & 63) == 0) {                                              \
-            for (int i_ = 0; i_ < 11; ++i_) atomicAdd(&knn_stamp_acc[i_], kst_[i_]); \
-            atomicAdd(&knn_stamp_acc[11], 1ull);                                    \
-        }                                                                           \
-    } while (0)
-#define KSC(i) (kst_[i] += 1)
-extern "C" int ccg_debug_knn_stamps(unsigned long long* out12) {
-    if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(knn_stamp_acc), 12 * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(knn_stamp_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#else
-#define KST_DECL
-#define KST(i)
-#define KSC(i)
-#define KST_FLUSH_OUT()
-#endif
-
 // s_waitcnt vmcnt(N) for a compile-time N (the LDS-DMA is issued as inline
 // asm, so the compiler does not track it).
 template <int N>
@@ -536,7 +496,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int Lc = c0 - cl, Rc = ch - 1 - c0, Mc = min(Lc, Rc);
     const int nck = ch - cl;
 #define chunk_at(kk_) knn_chunk_at((kk_), c0, Lc, Rc, Mc)
-    KST_DECL;
     // rejection threshold (see below); a hinted row starts at its hint's
     // threshold, which every later T keeps as a floor (T0 is itself a valid
     // rejection threshold for both halves, so certification stays exact)
@@ -546,9 +505,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     bool tdirty = false;  // lists changed since T was last set to the union threshold
 #define KNN_FLUSH()                                                                   \
     do {                                                                              \
-        KSC(8);                                                                       \
         for (int i_ = 0; __any(i_ < qc); ++i_) {                                      \
-            KSC(9);                                                                   \
             if (i_ < qc) {                                                            \
                 const uint2 e_ = qbw[i_ * 64 + lane];                                 \
                 const float v_ = __uint_as_float(e_.x);                               \
@@ -570,54 +527,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     KNN_STAGE_GLDS(0, chunk_at(0));
     if (KNN_NBUF == 3 && nck > 1) KNN_STAGE_GLDS(1, chunk_at(1));
     for (int k = 0; k < nck; ++k) {
-#ifdef KNN_EXP_NOSTAGE  // tools only: every chunk reads buffer 0 (staged once; results wrong)
-        const int b = 0;
-        const int c = chunk_at(k);
-        if (k == 0) {
-            knn_wait_vmcnt<0>();
-            __syncthreads();
-        }
-        if (false) {
-#else
         const int b = k % KNN_NBUF;
         const int c = chunk_at(k);
-        {
-#endif
-        KST(1);
         if constexpr (knn_nbuf(KSTEPS) == 3) {
             if (k + 1 < nck) knn_wait_vmcnt<LOADS>();
             else knn_wait_vmcnt<0>();
         } else {
             knn_wait_vmcnt<0>();
         }
-        KST(5);
         __syncthreads();
-        KST(6);
         if (k + KNN_NBUF - 1 < nck) KNN_STAGE_GLDS((k + KNN_NBUF - 1) % KNN_NBUF, chunk_at(k + KNN_NBUF - 1));
-        }
-        KST(0);
         // After the MFMA chain of a tile (accumulator ACC_, first ref RB_):
         // self / padding masking, the tile maximum, and -- when some lane's
         // value beats its threshold -- the branch-free enqueue (per half-tile
         // of 8 registers: flush first if its candidates could overflow a
         // queue).  After a flush both halves move to the union threshold;
         // between flushes T only rises.
-#if defined(KNN_EXP_NOMAX)  // tools only: MFMA + staging alone (results wrong)
-#define KNN_TILE_TEST(ACC_) asm volatile("; exp keep acc" ::"v"(ACC_)); if (false)
-#elif defined(KNN_EXP_NOCAND)  // tools only: no candidate is ever queued (results wrong)
 #define KNN_TILE_TEST(ACC_)                                                                 \
     float vmax = ACC_[0];                                                                   \
     _Pragma("unroll") for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, ACC_[reg]);     \
-    if (__any(vmax > T)) asm volatile("; exp cand" ::"v"(vmax));                            \
-    if (false)
-#else
-#define KNN_TILE_TEST(ACC_)                                                                 \
-    float vmax = ACC_[0];                                                                   \
-    _Pragma("unroll") for (int reg = 1; reg < 16; ++reg) vmax = fmaxf(vmax, ACC_[reg]);     \
-    KST(1);                                                                                 \
-    KSC(10);                                                                                \
     if (__any(vmax > T))
-#endif
 #define KNN_TILE_POST(ACC_, RB_)                                                            \
     do {                                                                                    \
         const int rbase = (RB_);                                                            \
@@ -628,13 +557,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }                                                                               \
         }                                                                                   \
         KNN_TILE_TEST(ACC_) {                                                               \
-            KSC(7);                                                                         \
             _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                              \
                 int c8 = 0;                                                                 \
                 _Pragma("unroll") for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) c8 += ACC_[reg] > T ? 1 : 0; \
-                KST(2);                                                                     \
                 if (__any(qc + c8 > QC)) KNN_FLUSH();                                       \
-                KST(3);                                                                     \
                 _Pragma("unroll") for (int reg = 8 * hh; reg < 8 * hh + 8; ++reg) {         \
                     const float v = ACC_[reg];                                              \
                     qbw[qc * 64 + lane] =                                                   \
@@ -642,12 +568,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     qc += v > T ? 1 : 0;                                                    \
                 }                                                                           \
             }                                                                               \
-            KST(2);                                                                         \
         }                                                                                   \
         if (tdirty) {                                                                       \
             T = fmaxf(T0, union_kth<KP, R>(lv));                                            \
             tdirty = false;                                                                 \
-            KST(4);                                                                         \
         }                                                                                   \
     } while (0)
         static_assert(QC >= 8, "queue must hold a half tile");
@@ -701,12 +625,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #undef KNN_TILE_POST
 #undef KNN_TILE_TEST
     }
-    KST(1);
     KNN_FLUSH();
-    KST(3);
     T = fmaxf(T0, union_kth<KP, R>(lv));
-    KST(4);
-    KST_FLUSH_OUT();
 #undef KNN_FLUSH
 #undef KNN_STAGE_GLDS
 #undef chunk_at
@@ -1447,10 +1367,6 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         }
 #undef CCG_SCREEN16
         ccg_timer_stop(ctx, t_scr, st);
-#ifdef KNN_EXP_SCREEN_ONLY  // tools only: time the screen alone (outputs undefined)
-        ccg_timer_stop(ctx, t_all, st);
-        return CCG_OK;
-#endif
     }
     const int64_t* seg_off = sg ? sg->seg_off : nullptr;
     const int nseg = sg ? sg->nseg : 1;
@@ -1471,6 +1387,8 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, seg_off, nseg, st,
                              dist_sq, fail_tau);
     if (rc) return rc;
+    ctx->last_fail_list = fail_list;
+    ctx->last_fail_count = fail_count;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {
@@ -2076,10 +1994,6 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         if (cell_hint)
             kb_hint_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, kq, ustart, srow, idx, ud2, cell_hint);
     }
-#ifdef KNN_EXP_SCREEN_ONLY
-    ccg_timer_stop(ctx, t_all, st);
-    return CCG_OK;
-#endif
     // 4. expansion to rows; ties cut by the list go to the exact search over all rows
     if (kq < 1) CCG_HIP(hipMemsetAsync(fail_count, 0, 3 * sizeof(int), st));  // (the table path zeroed it above)
     // one wave per distinct cell; cells whose list holds an equal-d2 tie
@@ -2101,6 +2015,8 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st, false,
                              KNN_EXPAND_RADIUS ? ftau : nullptr);
     if (rc) return rc;
+    ctx->last_fail_list = fail_list;
+    ctx->last_fail_count = fail_count;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     if (stats) {
@@ -2111,6 +2027,20 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         stats->fallback = us.fallback + nf;
         ctx->last_stats = *stats;
     }
+    return CCG_OK;
+}
+
+extern "C" int ccg_knn_last_fallback(ccg_ctx* ctx, int32_t* rows, int64_t cap, int64_t* count) {
+    CCG_REQUIRE(ctx && count && (rows || cap == 0), "ccg_knn_last_fallback: NULL argument");
+    *count = 0;
+    if (!ctx->last_fail_list) return CCG_OK;
+    CCG_HIP(hipSetDevice(ctx->device));
+    CCG_HIP(hipDeviceSynchronize());
+    int nf = 0;
+    CCG_HIP(hipMemcpy(&nf, ctx->last_fail_count, sizeof(int), hipMemcpyDeviceToHost));
+    *count = nf;
+    const int64_t m = std::min<int64_t>(nf, cap);
+    if (m > 0) CCG_HIP(hipMemcpy(rows, ctx->last_fail_list, sizeof(int32_t) * m, hipMemcpyDeviceToHost));
     return CCG_OK;
 }
 

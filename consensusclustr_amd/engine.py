@@ -348,6 +348,14 @@ class Engine:
             return self.last_knn_stats
         return None
 
+    def knn_last_fallback(self):
+        """Rows the last kNN call sent to the exact search (ccg_knn_last_fallback)."""
+        cnt = ctypes.c_int64(0)
+        check(self.lib.ccg_knn_last_fallback(self.ctx, None, 0, ctypes.byref(cnt)))
+        out = np.empty(max(cnt.value, 1), np.int32)
+        check(self.lib.ccg_knn_last_fallback(self.ctx, _ptr(out), out.size, ctypes.byref(cnt)))
+        return out[:cnt.value].copy()
+
     def knn_boot_table_t(self, pcs_cm, N, d, idx, n_unique, rows, kmax, tab_idx, tab_d2, out_idx, out_dist=None,
                          stats=False):
         """knn_boot_t from a cell table of the same PCs (ccg_knn_boot_table_dev)."""

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 3
+#define CCG_ABI_VERSION 4
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -194,6 +194,16 @@ int ccg_knn_boot_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                            const int32_t* tab_idx, const double* tab_d2, int K,
                            int32_t* out_idx, double* out_dist,
                            ccg_knn_stats* stats, void* stream);
+
+/* Diagnostics: the rows that the last kNN call on this context sent to the
+ * exact fp64 search -- certification failures of ccg_knn_rows_dev /
+ * ccg_knn_table_dev (cells, for the table), and in the bootstrap paths the
+ * rows whose kmax-th entry was a tie the distinct-cell list may cut (not the
+ * distinct cells searched exactly for lack of table entries).  *count gets
+ * their number, the first min(count, cap) go to rows (host).  Synchronises
+ * the device.  Lets a test check exactly the rows the fast paths did not
+ * settle. */
+int ccg_knn_last_fallback(ccg_ctx* ctx, int32_t* rows, int64_t cap, int64_t* count);
 
 /* Batched kNN over independent segments: the iterate=TRUE subclustering
  * (R/consensusClust.R:541-566, BASELINE config 5) runs one bootstrap loop per
