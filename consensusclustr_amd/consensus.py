@@ -193,14 +193,19 @@ def bootstrap_knn_batches(pca, boots, kmax, engine=None, group=None, batch=32):
 
 def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRange=RES_RANGE, kNum=K_NUM,
                       mode="robust", seed=123, engine=None, boot_indices=None, return_matrix=None,
-                      merge=False, minStability=0.175, group=None):
+                      merge=False, minStability=0.175, group=None, boot_seed=None, boot_knn=None):
     """The bootstrap + consensus core of consensusClust (R/consensusClust.R:388-456).
 
     The bootstrap loop runs as the R drop-in does (R/ccg.R ccgConsensusCore):
     every bootstrap's indices are drawn first, the kNN of a batch of
     bootstraps is one engine call (a DeviceGroup `group` splits each batch
     over its GPUs), then per bootstrap the SNN graphs, host clustering and
-    one batched silhouette.
+    one batched silhouette.  seed is the clustering seed (getClustAssignments'
+    and cluster_leiden's `seed`); boot_seed (default: seed) seeds the
+    bootstrap draws, as BPPARAM = SerialParam(RNGseed = seed) does in the
+    reference -- iterate=TRUE forwards BPPARAM but not seed (:562-566).
+    boot_knn: (nboots, n, max(kNum)) neighbour rows of every bootstrap when a
+    caller already searched them (the level-batched iterate driver).
     Returns dict(assignments=<chosen consensus labels>, clustAssignments=<B x N
     uint8/uint16>, scores=<consensus scores>, choice=<index>, candidates,
     consensus_knn=<N x max(kNum)>) and, when return_matrix (default: N <=
@@ -213,10 +218,16 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
     eng = engine or default_engine()
     pca = np.asarray(pca, dtype=np.float64)
     N = pca.shape[0]
-    boots = bootstrap_indices(N, nboots, bootSize, seed) if boot_indices is None else np.asarray(boot_indices)
+    if boot_seed is None:
+        boot_seed = seed
+    boots = bootstrap_indices(N, nboots, bootSize, boot_seed) if boot_indices is None else np.asarray(boot_indices)
     fn = _cluster_fn(clusterFun)
     columns = []
-    for b0, b1, knn in bootstrap_knn_batches(pca, boots, max(kNum), eng, group):  # bplapply(1:nboots), :391-400
+    if boot_knn is not None:
+        batches = [(0, boots.shape[0], boot_knn)]
+    else:
+        batches = bootstrap_knn_batches(pca, boots, max(kNum), eng, group)
+    for b0, b1, knn in batches:  # bplapply(1:nboots), :391-400
         for b in range(b0, b1):
             try:
                 columns.append(getClustAssignments(pca, boots[b], clusterFun=fn, resRange=resRange, kNum=kNum,

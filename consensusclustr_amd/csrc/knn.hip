@@ -1013,9 +1013,75 @@ struct KnnSegs {
     int nseg;
     const int64_t* seg_off;  // device, nseg + 1 row offsets
     int64_t npos;            // padded positions
-    const int* perm;         // device, position -> row (-1: padding)
+    int* perm;               // device, position -> row (-1: padding); knn_run writes each segment's Morton order
     const int4* blk;         // device, per query block: chunk range [x, y), query limit z
+    const int64_t* pos_off;  // device, nseg + 1 position offsets (multiples of KNN_QPB)
 };
+
+// (segment << 15 | Morton code, row) pairs: rows grouped by segment, each
+// segment in the spatial order of its leading coordinates
+__global__ void knn_seg_morton_keys_kernel(const double* __restrict__ rows, int64_t n, int d,
+                                           const unsigned* __restrict__ bnd, const int64_t* __restrict__ seg_off,
+                                           int nseg, int32_t* __restrict__ keys, int32_t* __restrict__ ids) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const unsigned sg = (unsigned)knn_seg_of(seg_off, nseg, r);
+    keys[r] = (int32_t)((sg << (KNN_MD * KNN_MORTON_BITS)) | morton_key(rows + r * d, d, bnd));
+    ids[r] = (int32_t)r;
+}
+
+// sorted rank t (rows grouped by segment) -> the segment's padded position
+__global__ void knn_seg_perm_kernel(int64_t n, const int32_t* __restrict__ sorted_ids,
+                                    const int64_t* __restrict__ seg_off, const int64_t* __restrict__ pos_off, int nseg,
+                                    int* __restrict__ perm) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int s = knn_seg_of(seg_off, nseg, t);
+    perm[pos_off[s] + (t - seg_off[s])] = sorted_ids[t];
+}
+
+// Host plan of a segmented run: segment s occupies positions [po_s, po_s +
+// n_s), po_s a multiple of KNN_QPB; each query block scans its segment's
+// chunks.  Uploads seg_off, the position offsets, the blocks and an identity
+// permutation (-1 padding; knn_run reorders each segment spatially) into
+// WS_SEGS on st.  The host vectors must outlive the uploads: the caller
+// synchronises st before they go out of scope.
+static int knn_seg_plan(ccg_ctx* ctx, const int64_t* seg_off, int nseg, int d, int kmax, hipStream_t st,
+                        std::vector<int64_t>& po, std::vector<int>& hperm, std::vector<int4>& hblk, KnnSegs* out) {
+    po.assign(nseg + 1, 0);
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t ns = seg_off[s + 1] - seg_off[s];
+        CCG_REQUIRE(ns >= kmax + 1, "kNN segments: segment %d has %lld rows, needs >= kmax+1 = %d", s,
+                    (long long)ns, kmax + 1);
+        po[s + 1] = po[s] + ccg_cdiv(ns, KNN_QPB) * KNN_QPB;
+    }
+    const int64_t npos = po[nseg];
+    CCG_REQUIRE(npos < (1LL << 30), "kNN segments: too many positions");
+    const int64_t nblk = npos / KNN_QPB;
+    const int KNN_CHUNK = knn_chunk(knn_ksteps(d));
+    hperm.assign(npos, -1);
+    hblk.resize(nblk);
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t ns = seg_off[s + 1] - seg_off[s];
+        for (int64_t i = 0; i < ns; ++i) hperm[po[s] + i] = (int)(seg_off[s] + i);
+        const int cl = (int)(po[s] / KNN_CHUNK), ch = (int)((po[s] + ns + KNN_CHUNK - 1) / KNN_CHUNK);
+        for (int64_t b = po[s] / KNN_QPB; b < po[s + 1] / KNN_QPB; ++b)
+            hblk[b] = make_int4(cl, ch, (int)(po[s] + ns), 0);
+    }
+    const size_t offb = ccg_cdiv(sizeof(int64_t) * (nseg + 1), 16) * 16;
+    char* tab = (char*)ccg_ws(ctx, WS_SEGS, 2 * offb + sizeof(int4) * nblk + sizeof(int) * npos + 64);
+    if (!tab) return CCG_ENOMEM;
+    int64_t* d_off = (int64_t*)tab;
+    int64_t* d_po = (int64_t*)(tab + offb);
+    int4* d_blk = (int4*)(tab + 2 * offb);
+    int* d_perm = (int*)(d_blk + nblk);
+    CCG_HIP(hipMemcpyAsync(d_off, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(d_po, po.data(), sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(d_blk, hblk.data(), sizeof(int4) * nblk, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(d_perm, hperm.data(), sizeof(int) * npos, hipMemcpyHostToDevice, st));
+    *out = KnnSegs{nseg, d_off, npos, d_perm, d_blk, d_po};
+    return CCG_OK;
+}
 
 // ------------------------------------------ exact search by a radius --
 // The exact search of the rows certification (or a cell table) could not
@@ -1310,7 +1376,22 @@ static int knn_run(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax,
         knn_rowstats_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(n * d, 1024), 256), 256, 0, st>>>(rows, n, d,
                                                                                                     mbits, bnd);
         if (sg) {
-            order_perm = sg->perm;  // segments keep their rows in input order
+            // each segment in the Morton order of its rows (radix sort on segment << 15 | code)
+            int sbits = 0;
+            while ((1 << sbits) < sg->nseg) ++sbits;
+            if (!KNN_NO_MORTON && sbits + KNN_MORTON_DIMS * KNN_MORTON_BITS <= 31) {
+                int32_t* kk = (int32_t*)ccg_ws(ctx, WS_ORDER, sizeof(int32_t) * 4 * n + 64);
+                if (!kk) return CCG_ENOMEM;
+                int32_t* ids = kk + n;
+                int32_t* skeys = ids + n;
+                int32_t* sids = skeys + n;
+                const unsigned gn = (unsigned)ccg_cdiv(n, 256);
+                knn_seg_morton_keys_kernel<<<gn, 256, 0, st>>>(rows, n, d, bnd, sg->seg_off, sg->nseg, kk, ids);
+                rc = ccg_sort_pairs_i32(ctx, kk, skeys, ids, sids, n, sbits + KNN_MORTON_DIMS * KNN_MORTON_BITS, st);
+                if (rc) return rc;
+                knn_seg_perm_kernel<<<gn, 256, 0, st>>>(n, sids, sg->seg_off, sg->pos_off, sg->nseg, sg->perm);
+            }
+            order_perm = sg->perm;
         } else if (KNN_NO_MORTON) {
             order_perm = nullptr;  // tools only: input order
         } else if (buckets) {
@@ -1422,37 +1503,13 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
     CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG, "ccg_knn_segments_dev: kmax=%d must be in [1, %d]", kmax,
                 KNN_KP_BIG);
     CCG_REQUIRE(seg_off[0] == 0 && seg_off[nseg] == n, "ccg_knn_segments_dev: seg_off must run from 0 to n");
-    // host plan: segment s occupies positions [po_s, po_s + n_s), po_s a multiple of KNN_QPB
-    std::vector<int64_t> po(nseg + 1, 0);
-    for (int s = 0; s < nseg; ++s) {
-        const int64_t ns = seg_off[s + 1] - seg_off[s];
-        CCG_REQUIRE(ns >= kmax + 1, "ccg_knn_segments_dev: segment %d has %lld rows, needs >= kmax+1 = %d", s,
-                    (long long)ns, kmax + 1);
-        po[s + 1] = po[s] + ccg_cdiv(ns, KNN_QPB) * KNN_QPB;
-    }
-    const int64_t npos = po[nseg];
-    CCG_REQUIRE(npos < (1LL << 30), "ccg_knn_segments_dev: too many positions");
-    const int64_t nblk = npos / KNN_QPB;
-    const int KNN_CHUNK = knn_chunk(knn_ksteps(d));
-    std::vector<int> hperm(npos, -1);
-    std::vector<int4> hblk(nblk);
-    for (int s = 0; s < nseg; ++s) {
-        const int64_t ns = seg_off[s + 1] - seg_off[s];
-        for (int64_t i = 0; i < ns; ++i) hperm[po[s] + i] = (int)(seg_off[s] + i);
-        const int cl = (int)(po[s] / KNN_CHUNK), ch = (int)((po[s] + ns + KNN_CHUNK - 1) / KNN_CHUNK);
-        for (int64_t b = po[s] / KNN_QPB; b < po[s + 1] / KNN_QPB; ++b)
-            hblk[b] = make_int4(cl, ch, (int)(po[s] + ns), 0);
-    }
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    char* tab = (char*)ccg_ws(ctx, WS_SEGS, sizeof(int64_t) * (nseg + 1) + sizeof(int) * npos + sizeof(int4) * nblk + 64);
-    if (!tab) return CCG_ENOMEM;
-    int64_t* d_off = (int64_t*)tab;
-    int4* d_blk = (int4*)(tab + ccg_cdiv(sizeof(int64_t) * (nseg + 1), 16) * 16);
-    int* d_perm = (int*)(d_blk + nblk);
-    CCG_HIP(hipMemcpyAsync(d_off, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(d_blk, hblk.data(), sizeof(int4) * nblk, hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(d_perm, hperm.data(), sizeof(int) * npos, hipMemcpyHostToDevice, st));
-    KnnSegs sg{nseg, d_off, npos, d_perm, d_blk};
+    std::vector<int64_t> po;
+    std::vector<int> hperm;
+    std::vector<int4> hblk;
+    KnnSegs sg;
+    int rc0 = knn_seg_plan(ctx, seg_off, nseg, d, kmax, st, po, hperm, hblk, &sg);
+    if (rc0) return rc0;
     const int rc = knn_run(ctx, rows, n, d, kmax, out_idx, out_dist, stats, st, &sg);
     CCG_HIP(hipStreamSynchronize(st));  // the host plan buffers must outlive the uploads
     return rc;
@@ -1548,8 +1605,13 @@ __device__ void kb_expand_row(int64_t i, int u, int kq, const int* __restrict__ 
                               const int* __restrict__ ustart, const int* __restrict__ srow,
                               const int* __restrict__ row2u, int kmax, int32_t* __restrict__ out_idx,
                               double* __restrict__ out_dist, int* __restrict__ fail_list, int* __restrict__ fail_count,
-                              double* __restrict__ fail_tau) {
+                              double* __restrict__ fail_tau, const int64_t* __restrict__ useg = nullptr,
+                              int nseg = 1) {
     const int uc = row2u[i];
+    if (useg) {  // segmented run: the distinct cells of the row's own segment
+        const int sg = knn_seg_of(useg, nseg, uc);
+        u = (int)(useg[sg + 1] - useg[sg]);
+    }
     // the distinct cell's kq nearest distinct cells with their certified d2
     // (fp64, unfused, dimension order: the oracle's sums; copies share them)
     const int* nbl = uidx + (int64_t)uc * kq;
@@ -1660,13 +1722,15 @@ __global__ __launch_bounds__(256) void kb_expand_ties_kernel(int u, int kq, cons
                                                              double* __restrict__ out_dist, int* __restrict__ fail_list,
                                                              int* __restrict__ fail_count, double* __restrict__ fail_tau,
                                                              const int* __restrict__ tie_list,
-                                                             const int* __restrict__ tie_count) {
+                                                             const int* __restrict__ tie_count,
+                                                             const int64_t* __restrict__ useg = nullptr,
+                                                             int nseg = 1) {
     const int nt = *tie_count;
     for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nt; f += gridDim.x * blockDim.x) {
         const int uc = tie_list[f];
         for (int z = ustart[uc]; z < ustart[uc + 1]; ++z)
             kb_expand_row(srow[z], u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
-                          fail_count, fail_tau);
+                          fail_count, fail_tau, useg, nseg);
     }
 }
 
@@ -1685,10 +1749,16 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
                                                               double* __restrict__ out_dist, int* __restrict__ fail_list,
                                                               int* __restrict__ fail_count,
                                                               double* __restrict__ fail_tau,
-                                                              int* __restrict__ tie_list, int* __restrict__ tie_count) {
+                                                              int* __restrict__ tie_list, int* __restrict__ tie_count,
+                                                              const int64_t* __restrict__ useg = nullptr,
+                                                              int nseg = 1) {
     const int lane = threadIdx.x & 63;
     const int uc = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (uc >= u) return;
+    if (useg) {  // segmented run: the cut test counts the distinct cells of the cell's own segment
+        const int sg = knn_seg_of(useg, nseg, uc);
+        u = (int)(useg[sg + 1] - useg[sg]);
+    }
     const int oa = ustart[uc], ob = ustart[uc + 1], oc = ob - oa;  // the own cell's rows (sorted positions)
     const bool has = lane < kq;
     const int v = has ? uidx[(int64_t)uc * kq + lane] : 0;
@@ -2027,6 +2097,191 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         stats->fallback = us.fallback + nf;
         ctx->last_stats = *stats;
     }
+    return CCG_OK;
+}
+
+// --------------------------------------------- batched bootstrap segments --
+// iterate=TRUE (R/consensusClust.R:541-567) re-runs the bootstrap loop
+// (:391-400) on every subcluster: many small bootstraps of many small PC
+// matrices.  ccg_knn_boot_segments_dev runs all of them -- one segment per
+// (subcluster, bootstrap) -- through ONE distinct-cell pipeline: rows grouped
+// by (segment, cell) with one radix sort, one segmented screen / certify /
+// fallback over every segment's distinct cells (each segment in its own
+// Morton order), one expansion back to rows, one exact search for cut ties.
+__global__ void kbs_keys_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t Ntot,
+                                const int64_t* __restrict__ seg_off, int nseg, int32_t* __restrict__ keys,
+                                int32_t* __restrict__ rid, int* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int c = idx[t];
+    if (c < 0 || c >= Ntot) {
+        atomicOr(err, CCG_DERR_KNN_UNIQUE);
+        c = 0;
+    }
+    keys[t] = (int32_t)((int64_t)knn_seg_of(seg_off, nseg, t) * Ntot + c);
+    rid[t] = (int32_t)t;
+}
+
+// the distinct-cell search returns segment-local distinct ids: back to global ids
+__global__ void kbs_uglobal_kernel(int64_t u, int kq, const int64_t* __restrict__ useg, int nseg,
+                                   int32_t* __restrict__ uidx) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= u * kq) return;
+    uidx[t] += (int32_t)useg[knn_seg_of(useg, nseg, t / kq)];
+}
+
+// neighbour rows: subtract (sign -1) or add (+1) the row's segment start
+__global__ void kbs_rebase_kernel(int64_t n, int kmax, const int64_t* __restrict__ seg_off, int nseg, int sign,
+                                  int32_t* __restrict__ out_idx) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kmax) return;
+    out_idx[t] += sign * (int32_t)seg_off[knn_seg_of(seg_off, nseg, t / kmax)];
+}
+
+extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int64_t Ntot, int d, const int32_t* idx,
+                                         int64_t n, const int64_t* seg_off, const int* seg_unique, int nseg, int kmax,
+                                         int local_ids, int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                                         void* stream) {
+    CCG_REQUIRE(ctx && cells && idx && seg_off && seg_unique && out_idx, "ccg_knn_boot_segments_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boot_segments_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(nseg >= 1 && n >= 2 && n < (1LL << 30) && Ntot >= 1 && Ntot < (1LL << 30),
+                "ccg_knn_boot_segments_dev: bad sizes");
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG, "ccg_knn_boot_segments_dev: kmax=%d must be in [1, %d]", kmax,
+                KNN_KP_BIG);
+    CCG_REQUIRE(seg_off[0] == 0 && seg_off[nseg] == n, "ccg_knn_boot_segments_dev: seg_off must run from 0 to n");
+    CCG_REQUIRE((int64_t)nseg * Ntot < (1LL << 31),
+                "ccg_knn_boot_segments_dev: nseg x Ntot = %lld must be below 2^31 (split the batch)",
+                (long long)nseg * Ntot);
+    std::vector<int64_t> uoff(nseg + 1, 0);
+    for (int s = 0; s < nseg; ++s) {
+        const int64_t ns = seg_off[s + 1] - seg_off[s];
+        CCG_REQUIRE(ns >= 2 && seg_unique[s] >= kmax + 1 && seg_unique[s] <= ns,
+                    "ccg_knn_boot_segments_dev: segment %d has %d distinct cells in %lld rows (needs >= kmax+1 = %d)",
+                    s, seg_unique[s], (long long)ns, kmax + 1);
+        uoff[s + 1] = uoff[s] + seg_unique[s];
+    }
+    const int64_t u = uoff[nseg];
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    double* ftau = nullptr;
+    int* fail_list = knn_fail_ws(ctx, n, &ftau);
+    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (n + 1) + sizeof(int32_t) * (4 * n + (size_t)u + 1));
+    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * (d + kmax) +
+                                                      sizeof(int32_t) * (size_t)u * kmax + 64);
+    double* rows = (double*)ccg_ws(ctx, WS_SEG_ROWS, sizeof(double) * (size_t)n * d);
+    int64_t* dso = (int64_t*)ccg_ws(ctx, WS_SEG_TAB, sizeof(int64_t) * 2 * (size_t)(nseg + 1));
+    unsigned int* misc = (unsigned int*)ccg_ws(ctx, WS_MISC, 256);
+    if (!fail_list || !ta || !urows || !rows || !dso || !misc) return CCG_ENOMEM;
+    int64_t* duo = dso + nseg + 1;
+    int64_t* head = (int64_t*)ta;
+    int32_t* keys = (int32_t*)(head + n + 1);
+    int32_t* skeys = keys + n;
+    int32_t* rid = skeys + n;
+    int32_t* srow = rid + n;
+    int32_t* ustart = srow + n;
+    int32_t* row2u = keys;
+    double* ud2 = urows + (size_t)u * d;
+    int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kmax);
+    int* fail_count = (int*)(misc + 4);
+    CCG_HIP(hipMemcpyAsync(dso, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(duo, uoff.data(), sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
+    const unsigned ng = (unsigned)ccg_cdiv(n, 256);
+    // 1. the rows, and (segment, cell) keys sorted stably: each segment's cells, each cell's rows ascending
+    gather_rows_rm_kernel<<<(unsigned)ccg_cdiv((d & 1) == 0 ? n * (d / 2) : n * d, 256), 256, 0, st>>>(
+        cells, Ntot, d, idx, n, rows);
+    kbs_keys_kernel<<<ng, 256, 0, st>>>(idx, n, Ntot, dso, nseg, keys, rid, ctx->d_err);
+    int bits = 1;
+    while (bits < 31 && (1LL << bits) < (int64_t)nseg * Ntot) ++bits;
+    int rc = ccg_sort_pairs_i32(ctx, keys, skeys, rid, srow, n, bits, st);
+    if (rc) return rc;
+    // 2. distinct (segment, cell) ids: ids of a segment are contiguous, in cell order
+    kb_heads_kernel<<<ng, 256, 0, st>>>(skeys, n, head, ustart, u + 1);
+    rc = ccg_scan_i64(ctx, head, head, n, st);
+    if (rc) return rc;
+    kb_tables_kernel<<<ng, 256, 0, st>>>(skeys, srow, n, head, (int)u, ustart, row2u, ctx->d_err);
+    kb_urows_kernel<<<(unsigned)ccg_cdiv(u * d, 256), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
+                                                                      nullptr);
+    // 3. every segment's distinct cells among themselves (kq = kmax: each has >= kmax + 1)
+    std::vector<int64_t> po;
+    std::vector<int> hperm;
+    std::vector<int4> hblk;
+    KnnSegs sg;
+    rc = knn_seg_plan(ctx, uoff.data(), nseg, d, kmax, st, po, hperm, hblk, &sg);
+    if (rc) return rc;
+    ccg_knn_stats us = {0, 0};
+    rc = knn_run(ctx, urows, u, d, kmax, uidx, ud2, stats ? &us : nullptr, st, &sg, true);
+    if (rc) return rc;
+    kbs_uglobal_kernel<<<(unsigned)ccg_cdiv(u * kmax, 256), 256, 0, st>>>(u, kmax, duo, nseg, uidx);
+    // 4. expansion to rows (global row ids), then segment-local ids; cut ties: the exact search in the segment
+    CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));
+    int* tie_count = (int*)(misc + 6);
+    int* tie_list = (int*)head;  // the heads' scan is consumed (kb_tables_kernel)
+    kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(n, (int)u, kmax, uidx, ud2, ustart, srow, row2u,
+                                                                     kmax, out_idx, out_dist, fail_list, fail_count,
+                                                                     ftau, tie_list, tie_count, duo, nseg);
+    kb_expand_ties_kernel<<<64, 256, 0, st>>>((int)u, kmax, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
+                                              fail_list, fail_count, ftau, tie_list, tie_count, duo, nseg);
+    const unsigned gk = (unsigned)ccg_cdiv(n * kmax, 256);
+    kbs_rebase_kernel<<<gk, 256, 0, st>>>(n, kmax, dso, nseg, -1, out_idx);
+    rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, dso, nseg, st, false,
+                             nullptr);
+    if (rc) return rc;
+    if (!local_ids) kbs_rebase_kernel<<<gk, 256, 0, st>>>(n, kmax, dso, nseg, 1, out_idx);
+    ctx->last_fail_list = fail_list;
+    ctx->last_fail_count = fail_count;
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    int nf = 0;
+    if (stats) CCG_HIP(hipMemcpyAsync(&nf, fail_count, sizeof(int), hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));  // the host plan vectors must outlive their uploads
+    if (stats) {
+        stats->queries = n;
+        stats->fallback = us.fallback + nf;
+        ctx->last_stats = *stats;
+    }
+    return CCG_OK;
+}
+
+extern "C" int ccg_knn_boot_segments(ccg_ctx* ctx, const double* cells, int64_t Ntot, int d, const int32_t* idx,
+                                     int64_t n, const int64_t* seg_off, const int* seg_unique, int nseg, int kmax,
+                                     int32_t* out_idx, double* out_dist, ccg_knn_stats* stats) {
+    CCG_REQUIRE(ctx && cells && idx && seg_off && out_idx, "ccg_knn_boot_segments: NULL argument");
+    CCG_REQUIRE(Ntot >= 1 && n >= 2 && d >= 1 && nseg >= 1 && seg_off[0] == 0 && seg_off[nseg] == n,
+                "ccg_knn_boot_segments: bad sizes");
+    for (int64_t t = 0; t < n; ++t)
+        CCG_REQUIRE(idx[t] >= 0 && idx[t] < Ntot, "ccg_knn_boot_segments: idx[%lld] out of range", (long long)t);
+    std::vector<int> su(nseg);
+    if (seg_unique) {
+        std::copy(seg_unique, seg_unique + nseg, su.begin());
+    } else {  // length(unique(...)) of every segment
+        std::vector<int> stamp(Ntot, -1);
+        for (int s = 0; s < nseg; ++s) {
+            int c = 0;
+            for (int64_t t = seg_off[s]; t < seg_off[s + 1]; ++t)
+                if (stamp[idx[t]] != s) {
+                    stamp[idx[t]] = s;
+                    ++c;
+                }
+            su[s] = c;
+        }
+    }
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    double* dcells = (double*)ccg_ws(ctx, WS_HOST_A, sizeof(double) * Ntot * d);
+    int32_t* didx = (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * n);
+    int32_t* dout = (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * n * kmax);
+    double* ddist = out_dist ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * n * kmax) : nullptr;
+    if (!dcells || !didx || !dout || (out_dist && !ddist)) return CCG_ENOMEM;
+    CCG_HIP(hipMemcpyAsync(dcells, cells, sizeof(double) * Ntot * d, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(didx, idx, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    int rc = ccg_knn_boot_segments_dev(ctx, dcells, Ntot, d, didx, n, seg_off, su.data(), nseg, kmax, 1, dout, ddist,
+                                       stats, st);
+    if (rc) return rc;
+    rc = ccg_take_device_error(ctx);
+    if (rc) return rc;
+    CCG_HIP(hipMemcpyAsync(out_idx, dout, sizeof(int32_t) * n * kmax, hipMemcpyDeviceToHost, st));
+    if (out_dist) CCG_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(double) * n * kmax, hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
     return CCG_OK;
 }
 

@@ -141,6 +141,56 @@ class Engine:
         return [(out[off[s]:off[s + 1]], None if dist is None else dist[off[s]:off[s + 1]])
                 for s in range(len(mats))]
 
+    def knn_boot_segments(self, pcas, boots, kmax=20, want_dist=True):
+        """The bootstrap kNN of many PC matrices in one engine call
+        (ccg_knn_boot_segments): pcas a list of (N_s, d_s) matrices (zero-
+        padded to a common d), boots a list of (nb_s, n_s) or (n_s,) index
+        arrays into them.  Returns, per matrix, (idx (nb_s, n_s, kmax) int32
+        bootstrap-row indices, dist or None): each bootstrap exactly as
+        knn_boot gives it."""
+        d = max(p.shape[1] for p in pcas)
+        Nof = np.zeros(len(pcas) + 1, np.int64)
+        for s, p in enumerate(pcas):
+            Nof[s + 1] = Nof[s] + p.shape[0]
+        cells = np.zeros((int(Nof[-1]), d), np.float64)
+        for s, p in enumerate(pcas):
+            cells[Nof[s]:Nof[s + 1], :p.shape[1]] = p
+        bl = [np.atleast_2d(np.asarray(b, np.int64)) for b in boots]
+        segs = [(s, b) for s, bb in enumerate(bl) for b in range(bb.shape[0])]
+        off = np.zeros(len(segs) + 1, np.int64)
+        for t, (s, b) in enumerate(segs):
+            off[t + 1] = off[t] + bl[s].shape[1]
+        idx = np.concatenate([bl[s][b] + Nof[s] for s, b in segs]).astype(np.int32)
+        n = idx.size
+        out = np.empty((n, kmax), np.int32)
+        dist = np.empty((n, kmax), np.float64) if want_dist else None
+        st = _lib.ccg_knn_stats()
+        check(self.lib.ccg_knn_boot_segments(self.ctx, _ptr(cells), cells.shape[0], d, _ptr(idx), n, _ptr(off),
+                                             None, len(segs), kmax, _ptr(out), _ptr(dist), ctypes.byref(st)))
+        self.last_knn_stats = (st.queries, st.fallback)
+        res, t = [], 0
+        for s, bb in enumerate(bl):
+            nb, ns = bb.shape
+            a, b = off[t], off[t + nb]
+            res.append((out[a:b].reshape(nb, ns, kmax),
+                        None if dist is None else dist[a:b].reshape(nb, ns, kmax)))
+            t += nb
+        return res
+
+    def knn_boot_segments_t(self, cells, idx, seg_off, seg_unique, kmax, out_idx, out_dist=None, local_ids=True,
+                            stats=False):
+        """Device flavour (ccg_knn_boot_segments_dev): cells (Ntot, d) row-major
+        tensor, idx (n,) int32 tensor, seg_off / seg_unique host arrays."""
+        Ntot, d = cells.shape
+        off = np.ascontiguousarray(seg_off, dtype=np.int64)
+        su = np.ascontiguousarray(seg_unique, dtype=np.int32)
+        st = _lib.ccg_knn_stats()
+        check(self.lib.ccg_knn_boot_segments_dev(self.ctx, _ptr(cells), Ntot, d, _ptr(idx), idx.numel(), _ptr(off),
+                                                 _ptr(su), off.size - 1, kmax, 1 if local_ids else 0, _ptr(out_idx),
+                                                 _ptr(out_dist), ctypes.byref(st), _stream()))
+        self.last_knn_stats = (st.queries, st.fallback)
+        return self.last_knn_stats if stats else None
+
     def snn(self, knn_idx, k, type="number"):
         """SNN edges i<j sorted by (i, j) with weights (ccg_snn)."""
         knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)

@@ -195,6 +195,37 @@ int ccg_knn_boot_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                            int32_t* out_idx, double* out_dist,
                            ccg_knn_stats* stats, void* stream);
 
+/* The bootstrap kNN of many small PC matrices in one set of launches:
+ * iterate=TRUE (R/consensusClust.R:541-567, BASELINE config 5) re-runs the
+ * bootstrap loop (:391-400) on every subcluster of a level.  One segment =
+ * one bootstrap of one subcluster; every segment gets ccg_knn_boot_dev's
+ * result (the distinct-cell search, bit for bit), all segments together:
+ *   cells      : Ntot x d float64 ROW-major (device): the subclusters' PC
+ *                matrices stacked (zero-pad a smaller pcNum: padding dims do
+ *                not change distances)
+ *   idx        : n int32 (device): segment s's rows are idx[seg_off[s] ..
+ *                seg_off[s+1]), each a row of `cells` (its subcluster's block;
+ *                R's sample() - 1 plus the block start)
+ *   seg_off    : HOST, nseg + 1 offsets (0 .. n)
+ *   seg_unique : HOST, nseg: the distinct values of each segment (R:
+ *                length(unique(...))); each must be >= kmax + 1
+ *   local_ids  : 1 = out_idx holds segment-local bootstrap-row indices
+ *                (ccg_knn_boot_dev's), 0 = rows of the concatenation (the
+ *                disjoint union graph, ready for one ccg_snn_rows_dev call)
+ * Requires nseg * Ntot < 2^31 (split larger batches).  Synchronises the stream
+ * before returning (a small host plan is uploaded). */
+int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int64_t Ntot, int d,
+                              const int32_t* idx, int64_t n, const int64_t* seg_off,
+                              const int* seg_unique, int nseg, int kmax, int local_ids,
+                              int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                              void* stream);
+/* Host flavour (cells, idx, outputs host; segment-local ids); seg_unique may
+ * be NULL (counted on the host). */
+int ccg_knn_boot_segments(ccg_ctx* ctx, const double* cells, int64_t Ntot, int d,
+                          const int32_t* idx, int64_t n, const int64_t* seg_off,
+                          const int* seg_unique, int nseg, int kmax, int32_t* out_idx,
+                          double* out_dist, ccg_knn_stats* stats);
+
 /* Diagnostics: the rows that the last kNN call on this context sent to the
  * exact fp64 search -- certification failures of ccg_knn_rows_dev /
  * ccg_knn_table_dev (cells, for the table), and in the bootstrap paths the

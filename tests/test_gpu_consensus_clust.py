@@ -97,3 +97,22 @@ def test_consensus_clust_iterates_into_subclusters(engine):
     for t in np.unique(top_of):  # a subclustered cluster's members all carry its prefix
         parts = {x for x in lab if x.split("_")[0] == t}
         assert len(parts) == 1 or all("_" in x for x in parts)
+
+
+def test_level_batched_iterate_equals_depth_first_recursion(engine):
+    """BASELINE config 5: iterate=TRUE walked level by level with ONE batched
+    bootstrap kNN per level (ccg_knn_boot_segments) returns exactly what the
+    depth-first recursion of :546-567 returns, on a 4-subcluster case."""
+    from consensusclustr_amd.pipeline import consensusClust
+    rng = np.random.default_rng(4)
+    groups = [(t, s, 180) for t in (1, 2, 3, 4) for s in (1, 2)]
+    counts, sf, top, sub = _counts(rng, groups, boost=5.0)
+    genes = np.flatnonzero(counts.std(1) > 0).astype(np.int32)
+    kw = dict(pcNum=10, nboots=60, clusterFun=_components, engine=engine, silhouetteThresh=0.0, iterate=True,
+              minSize=50, seed=7)
+    a = consensusClust(counts, sf, genes, batch_levels=True, **kw)
+    b = consensusClust(counts, sf, genes, batch_levels=False, **kw)
+    assert a["assignments"] == b["assignments"]
+    assert a["silhouette"] == b["silhouette"] and a["pcNum"] == b["pcNum"]
+    lab = np.array(a["assignments"])
+    assert len({x.split("_")[0] for x in lab}) >= 2

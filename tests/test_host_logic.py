@@ -271,3 +271,36 @@ def test_allgather_plan_unequal_and_equal_counts(G):
         assert np.array_equal(buf, full)
     with pytest.raises(Exception):
         allgather_plan([1, -1])
+
+
+@pytest.mark.parametrize("batch_levels", [True, False])
+def test_iterate_forwards_bootstrap_seed_and_resets_clustering_seed(monkeypatch, batch_levels):
+    """R/consensusClust.R:562-566 forwards BPPARAM (SerialParam(RNGseed =
+    seed): the bootstrap streams) to the recursive call but not `seed`, which
+    falls back to 123 there.  Subclusters therefore draw their bootstraps
+    from the caller's seed and cluster with seed 123."""
+    import consensusclustr_amd.pipeline as P
+    calls = []
+
+    def fake_pcs(counts, sf, vf, cells, depth, pcNum, pcVar, nboots, eng):
+        return "pca", (np.zeros((cells.size, 5)), np.arange(3, dtype=np.int32))
+
+    def fake_consensus(pca, **kw):
+        calls.append((pca.shape[0], kw["seed"], kw["boot_seed"], kw.get("boot_knn") is None))
+        n = pca.shape[0]
+        fin = np.where(np.arange(n) < n // 2, 1, 2) if n >= 400 else np.ones(n, np.int64)
+        return {"final_assignments": fin}
+
+    monkeypatch.setattr(P, "_node_pcs", fake_pcs)
+    monkeypatch.setattr(P, "consensus_cluster", fake_consensus)
+    monkeypatch.setattr(P, "_silhouette_mean", lambda eng, pca, f: 0.9)
+    monkeypatch.setattr(P, "level_bootstrap_knn", lambda pcas, *a, **k: [None] * len(pcas))
+    for top_seed in (7, 11):
+        calls.clear()
+        out = P.consensusClust(np.ones((3, 800)), np.ones(800), np.arange(3), nboots=5, seed=top_seed,
+                               iterate=True, engine=object(), batch_levels=batch_levels)
+        assert len(out["assignments"]) == 800
+        top = [c for c in calls if c[0] == 800]
+        subs = [c for c in calls if c[0] == 400]
+        assert top == [(800, top_seed, top_seed, True)]
+        assert len(subs) == 2 and all(c[1] == 123 and c[2] == top_seed for c in subs)
