@@ -13,6 +13,21 @@ flips, generated on the device before timing.  Inputs are resident in HBM
 when the timed region starts.  Weak scaling: B bootstraps per GPU per step
 (default 125 -> 1000 bootstraps = BASELINE config 3 at 8 GPUs).
 
+Workloads (--workload; the default cfg3 line is the metric line):
+  cfg3    : the metric -- 100k cells x 30 PCs, 125 bootstraps per GPU per step,
+            robust, the co-cluster row slab of this rank over all ranks' columns;
+  cfg3job : cfg3 as one whole 1-GPU job: 1000 bootstraps per step and one
+            co-cluster over the 1000 columns;
+  cfg2    : 20k cells x 20 PCs, 500 bootstraps, robust, one whole 1-GPU job;
+  cfg4    : 250k cells x 30 PCs, granular (60 map-back columns per bootstrap,
+            no silhouettes, :688): one GPU's share of the 8-GPU job -- 125
+            bootstraps and rank 0's pair-balanced slab of the 60 000-column
+            co-cluster (the other ranks' columns are synthetic copies);
+  cfg5    : iterate=TRUE on 100k cells: every subcluster (5k-20k cells, d_c
+            5-15 PCs) of one level through the batched segment kNN
+            (ccg_knn_boot_segments_dev), one SNN pass over the disjoint union,
+            per-segment silhouettes, map-back and per-subcluster co-clusters.
+
 Usage: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1
 and no WORLD_SIZE in the environment, this process (which never touches the
 GPU) starts N ranks through torch.distributed.run (127.0.0.1) and exits with
@@ -39,6 +54,14 @@ PEAK_HBM_GBS = 8000.0
 PEAK_F64_TFLOPS = 78.6     # dense fp64 MFMA (MI355X spec; not in the guide)
 K_NUM = (10, 15, 20)
 N_RES = 20
+# BASELINE.json configs: shapes per workload (weak scaling: bootstraps per GPU)
+WORKLOADS = {
+    "cfg3": dict(cells=100000, pcs=30, boots_per_gpu=125, mode="robust", emul_ranks=0, cmax=40),
+    "cfg3job": dict(cells=100000, pcs=30, boots_per_gpu=1000, mode="robust", emul_ranks=0, cmax=40),
+    "cfg2": dict(cells=20000, pcs=20, boots_per_gpu=500, mode="robust", emul_ranks=0, cmax=40),
+    "cfg4": dict(cells=250000, pcs=30, boots_per_gpu=125, mode="granular", emul_ranks=8, cmax=60),
+    "cfg5": dict(cells=100000, pcs=30, boots_per_gpu=125, mode="robust", emul_ranks=0, cmax=40),
+}
 
 
 def parse():
@@ -46,18 +69,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cells", type=int, default=100000)
-    ap.add_argument("--pcs", type=int, default=30)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
+    ap.add_argument("--cells", type=int, default=None)
+    ap.add_argument("--pcs", type=int, default=None)
     ap.add_argument("--genes", type=int, default=2000)
-    ap.add_argument("--boots-per-gpu", type=int, default=125)
+    ap.add_argument("--boots-per-gpu", type=int, default=None)
+    ap.add_argument("--check", action="store_true",
+                    help="with the CPU baseline leg: also check one bootstrap's outputs against the oracle "
+                         "(on by default with the CPU baseline)")
     ap.add_argument("--boot-size", type=float, default=0.9)
     ap.add_argument("--cpu-sample-rows", type=int, default=6000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=3,
                     help="bootstraps in flight per GPU (one engine context + HIP stream each)")
-    ap.add_argument("--pipeline", default="",
-                    help="NK,NS: stage-split schedule instead of --streams: NK kNN streams feed NS "
-                         "SNN+silhouette streams through a ring of bootstrap buffers")
+    ap.add_argument("--seg-batch", type=int, default=16,
+                    help="cfg5: bootstraps of every subcluster per segmented launch set")
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
                     help="table: one cell table per step (ccg_knn_table_dev) filtered per bootstrap; "
                          "screen: a screen per bootstrap (warm-started)")
@@ -69,7 +95,12 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WORKLOADS[a.workload]
+    for k in ("cells", "pcs", "boots_per_gpu"):
+        if getattr(a, k) is None:
+            setattr(a, k, w[k])
+    return a
 
 
 def _free_port():
@@ -143,8 +174,8 @@ def synth_pcs(torch, N, d, G, seed, dev):
     return pcs, pop
 
 
-def synth_labels(torch, pop, boot, L, dev, seed):
-    """60 clusterings of one bootstrap: C rising with resolution (2..40),
+def synth_labels(torch, pop, boot, L, dev, seed, chi=40):
+    """60 clusterings of one bootstrap: C rising with resolution (2..chi),
     permuted true populations, 5% uniform flips; codes 1..C.  Labels are
     drawn per cell and gathered to the bootstrap rows: a cell's copies are
     identical points with the same neighbours, which community detection puts
@@ -153,7 +184,7 @@ def synth_labels(torch, pop, boot, L, dev, seed):
     N = pop.numel()
     li = torch.arange(L, device=dev)
     ki = (li // N_RES)[:, None]
-    Cl = (2 + (38 * (li % N_RES)) // (N_RES - 1))[:, None]
+    Cl = (2 + ((chi - 2) * (li % N_RES)) // (N_RES - 1))[:, None]
     lab = (pop[None, :] * 7 + ki) % Cl + 1
     flip = torch.rand(L, N, device=dev, generator=g) < 0.05
     rnd = (torch.rand(L, N, device=dev, generator=g) * Cl).long() + 1
@@ -161,10 +192,10 @@ def synth_labels(torch, pop, boot, L, dev, seed):
 
 
 def _cpu_boot_worker(a):
-    """One bootstrap's per-bootstrap CPU work (kNN k=20, SNN k=10/15/20, 6
-    silhouettes) on a single core, as one BiocParallel MulticoreParam worker
-    runs getClustAssignments.  Returns its seconds."""
-    X, seed = a
+    """One bootstrap's per-bootstrap CPU work (kNN k=20, SNN k=10/15/20, and
+    in robust mode 6 silhouettes) on a single core, as one BiocParallel
+    MulticoreParam worker runs getClustAssignments.  Returns its seconds."""
+    X, seed, n_sil = a
     sys.path.insert(0, ROOT)
     import oracle as O
     rng = np.random.default_rng(seed)
@@ -174,37 +205,49 @@ def _cpu_boot_worker(a):
     for k in K_NUM:
         O.snn(idx, k, "number")
     t2 = time.perf_counter()
-    for l_ in rng.integers(1, 21, (6, X.shape[0])).astype(np.int32):  # 6 of the 60 clusterings, C ~ 20
+    for l_ in rng.integers(1, 21, (n_sil, X.shape[0])).astype(np.int32):  # n_sil of the 60 clusterings, C ~ 20
         O.silhouette(X, l_)
     t3 = time.perf_counter()
     return t1 - t0, t2 - t1, t3 - t2
 
 
-def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
+def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0, robust=True, coc_cols=None, coc_pairs=None,
+                 seg_rows=None):
     """The CPU restatement (oracle/, C) timed bootstrap-parallel on the host's
     cores, as the reference fans bootstraps over bplapply(MulticoreParam):
     `cores` single-threaded workers each run one bootstrap sample of
     `sample_rows` rows concurrently (so memory contention is included); the
     per-bootstrap seconds are extrapolated to n rows (kNN n^2, SNN and
-    silhouette n, 60 clusterings) and divided over the cores.  The co-cluster
-    runs OpenMP over the same cores on 2000 cells, extrapolated by N^2."""
+    silhouette n, 60 clusterings; granular mode scores none) and divided over
+    the cores.  The co-cluster runs OpenMP over the same cores on 2000 cells
+    x min(B, 1000) columns, extrapolated by pairs and columns.  seg_rows
+    (cfg5): the per-bootstrap work is the sum over subclusters of n_s rows."""
     import multiprocessing as mp
     import oracle as O
     cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     rng = np.random.default_rng(seed)
     ns = min(sample_rows, n)
-    samples = [(O.gather_rows(pcs_np, rng.integers(0, N, ns).astype(np.int32)), seed + w) for w in range(cores)]
+    n_sil = 6 if robust else 0
+    samples = [(O.gather_rows(pcs_np, rng.integers(0, N, ns).astype(np.int32)), seed + w, n_sil)
+               for w in range(cores)]
     with mp.get_context("spawn").Pool(cores) as pool:
         res = pool.map(_cpu_boot_worker, samples)
-    t_knn = float(np.mean([r[0] for r in res])) * (n / ns) ** 2
-    t_snn = float(np.mean([r[1] for r in res])) * (n / ns)
-    t_sil = float(np.mean([r[2] for r in res])) * (60 / 6) * (n / ns)
+    segs = [n] if seg_rows is None else list(seg_rows)
+    k1 = float(np.mean([r[0] for r in res]))
+    k2 = float(np.mean([r[1] for r in res]))
+    k3 = float(np.mean([r[2] for r in res]))
+    t_knn = sum(k1 * (m / ns) ** 2 for m in segs)
+    t_snn = sum(k2 * (m / ns) for m in segs)
+    t_sil = sum(k3 * (60 / 6) * (m / ns) for m in segs) if robust else 0.0
     Nc = 2000
-    A = rng.integers(1, 13, (B, Nc)).astype(np.int32)
-    A[rng.random((B, Nc)) < 0.35] = -1
+    Bc = B if coc_cols is None else coc_cols
+    Bs = min(Bc, 1000)
+    P = N * (N - 1) / 2 if coc_pairs is None else coc_pairs
+    A = rng.integers(1, 13, (Bs, Nc)).astype(np.int32)
+    A[rng.random((Bs, Nc)) < 0.35] = -1
     t0 = time.perf_counter()
     O.cocluster(A, nthreads=cores, want=("co", "both"))
-    t_coc = (time.perf_counter() - t0) * (N * (N - 1) / (Nc * (Nc - 1)))
+    t_coc = (time.perf_counter() - t0) * (P / (Nc * (Nc - 1) / 2)) * (Bc / Bs)
     t_step = B * (t_knn + t_snn + t_sil) / cores + t_coc
     return {
         "value": B / t_step,
@@ -212,10 +255,322 @@ def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0):
         "cores": cores,
         "kind": "port",
         "sample": (f"oracle (C) bootstrap-parallel: {cores} single-threaded workers, one {ns}-row bootstrap each "
-                   f"(kNN x (n/{ns})^2, SNN k=10/15/20 x n/{ns}, silhouette of 6 clusterings x 10 x n/{ns}), "
-                   f"per-bootstrap core-seconds knn {t_knn:.1f}, snn {t_snn:.2f}, silhouette {t_sil:.2f}; "
-                   f"co-cluster OpenMP x{cores} on {B} columns x {Nc} cells x (N/{Nc})^2 = {t_coc:.1f} s per step"),
+                   f"(kNN x (n/{ns})^2, SNN k=10/15/20 x n/{ns}" +
+                   (f", silhouette of 6 clusterings x 10 x n/{ns}" if robust else ", no silhouettes (granular)") +
+                   (f"; summed over {len(segs)} subclusters of {min(segs)}-{max(segs)} rows" if seg_rows else "") +
+                   f"), per-bootstrap core-seconds knn {t_knn:.1f}, snn {t_snn:.2f}, silhouette {t_sil:.2f}; "
+                   f"co-cluster OpenMP x{cores} on {Bs} columns x {Nc} cells, x (pairs {P:.3g} / sample pairs) x "
+                   f"(columns {Bc} / {Bs}) = {t_coc:.1f} s per step"),
     }
+
+
+def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, robust, A_full=None, co=None,
+                       both=None, r0=0, r1=0, sample=256):
+    """Part of the cpu_baseline leg: the oracle as the CHECKER of one timed
+    bootstrap.  Bootstrap 0 runs again through the step's calls (gather, kNN
+    from the cell table, SNN rows, silhouette) into fresh buffers; sampled kNN
+    rows (plus every row the fast paths sent to the exact search) must be
+    bit-exact, all three SNN graphs must equal the oracle's edge lists, the
+    60 silhouette means must agree within 1e-5, and sampled rows of the
+    step's co/both slab must equal orc_cocluster_rows."""
+    import concurrent.futures as cf
+    import oracle as O
+    N, d = pcs.shape
+    n = boot.numel()
+    dev = pcs.device
+    rows = torch.empty((n, d), dtype=torch.float64, device=dev)
+    knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
+    eng.gather_rows_rm_t(pcs, N, d, boot, rows)
+    if tab is not None:
+        eng.knn_boot_table_t(pcs_cm, N, d, boot, u, rows, 20, tab[0], tab[1], knn)
+    else:
+        eng.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, knn)
+    cut = eng.knn_last_fallback()
+    ro = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    rl = torch.zeros(n, dtype=torch.int32, device=dev)
+    cap = 700 * n
+    nbr = torch.empty(cap, dtype=torch.int32, device=dev)
+    wpk = torch.empty(cap, dtype=torch.int32, device=dev)
+    ne = torch.zeros(3, dtype=torch.int64, device=dev)
+    eng.snn_rows_t(knn, K_NUM, "number", ro, rl, nbr, wpk, ne)
+    L = labels0.shape[0]
+    mean = torch.empty(L, dtype=torch.float64, device=dev)
+    ncl = torch.empty(L, dtype=torch.int32, device=dev)
+    mns = torch.empty(L, dtype=torch.int32, device=dev)
+    if robust:
+        eng.silhouette_cells_t(rows, labels0, cmax, boot, N, mean, ncl, mns)
+    torch.cuda.synchronize()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    out = {}
+    X = rows.cpu().numpy()
+    kn = knn.cpu().numpy()
+    rng = np.random.default_rng(5)
+    q = np.unique(np.concatenate([cut[:4096], rng.choice(n, min(sample, n), replace=False)])).astype(np.int32)
+    oi, _ = O.knn_queries(X, 20, q, nthreads=threads)
+    out["knn_rows_checked"] = int(q.size)
+    out["knn_exact"] = bool(np.array_equal(kn[q], oi))
+    used = int(ro[-1].item()) if ne.min().item() >= 0 else 0
+    ok = used > 0
+    if ok:
+        ln = rl.cpu().numpy().astype(np.int64)
+        off = ro.cpu().numpy()
+        i = np.repeat(np.arange(n, dtype=np.int64), ln)
+        pos = np.repeat(off[:-1], ln) + (np.arange(i.size) - np.repeat(np.cumsum(ln) - ln, ln))
+        j = nbr[:used].cpu().numpy()[pos]
+        w = wpk[:used].cpu().numpy().view(np.uint32)[pos]
+        for g, k in enumerate(K_NUM):
+            b = (w >> np.uint32(8 * g)) & np.uint32(0xFF)
+            m = b != 0
+            ei, ej, ew = O.snn(kn, k, "number")
+            ok = ok and np.array_equal(i[m], ei) and np.array_equal(j[m], ej) and np.array_equal(
+                b[m].astype(np.float64), ew)
+    out["snn_graphs_exact"] = bool(ok)
+    if robust:
+        labs = labels0.cpu().numpy()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            ref = list(ex.map(lambda l_: O.silhouette(X, labs[l_])[1], range(L)))
+        got = mean.cpu().numpy()
+        rel = np.abs(got - np.asarray(ref)) / np.maximum(np.abs(np.asarray(ref)), 1e-300)
+        out["silhouette_max_rel_err"] = float(rel.max())
+        out["silhouette_within_1e-5"] = bool(rel.max() <= 1e-5)
+    if A_full is not None and A_full.numel() <= (1 << 31):
+        An = A_full.cpu().numpy()
+        rsel = np.unique(np.clip(np.array([r0, r0 + 1, (r0 + r1) // 2, r1 - 2]), r0, r1 - 2)).astype(np.int32)
+        rco, rb = O.cocluster_rows(An, rsel, nthreads=threads)
+        good = True
+        for t, i_ in enumerate(rsel):
+            o = int(i_) * N - int(i_) * (int(i_) + 1) // 2 - (r0 * N - r0 * (r0 + 1) // 2)
+            m_ = N - 1 - int(i_)
+            good = good and np.array_equal(co[o:o + m_].cpu().numpy().view(np.uint16), rco[t, i_ + 1:]) and \
+                np.array_equal(both[o:o + m_].cpu().numpy().view(np.uint16), rb[t, i_ + 1:])
+        out["cocluster_rows_checked"] = int(rsel.size)
+        out["cocluster_exact"] = bool(good)
+    out["ok"] = all(v for k_, v in out.items() if isinstance(v, bool))
+    return out
+
+
+def workload_text(name, N, d, B, G, emul):
+    if name == "cfg3":
+        return ("BASELINE cfg3 shapes: 100k cells x 30 PCs, robust mode, kNum 10/15/20 x 20 resolutions; "
+                f"{B} bootstraps per GPU per step ({G * B} total) + co-cluster row slab over all columns")
+    if name == "cfg3job":
+        return (f"BASELINE cfg3 as one whole job: {N} cells x {d} PCs, robust, {B * G} bootstraps per step, "
+                "one co-cluster over all their columns")
+    if name == "cfg2":
+        return f"BASELINE cfg2: {N} cells x {d} PCs, robust, {B * G} bootstraps, whole job incl. co-cluster"
+    if name == "cfg4":
+        return (f"BASELINE cfg4 granular, one GPU's share of the {emul or G}-GPU job: {N} cells x {d} PCs, {B} "
+                f"bootstraps (60 map-back columns each, C 2..60, no silhouettes, :688) + this rank's pair-balanced "
+                f"row slab of the {(emul or G) * B * 60}-column co-cluster"
+                + (" (the other ranks' columns synthetic)" if emul else ""))
+    return name
+
+
+def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen):
+    """BASELINE cfg5: one iterate=TRUE level on 100k cells (R/consensusClust.R:
+    541-567).  The cells fall into 10 subclusters of 5k-20k cells with pcNum
+    d_c = 5..15 (the :356 rule's range); each subcluster's bootstrap loop
+    (:391-400, :650-692) runs B bootstraps.  A step batches `--seg-batch`
+    bootstraps of EVERY subcluster per launch set: the segmented distinct-cell
+    kNN (ccg_knn_boot_segments_dev, one segment per (subcluster, bootstrap),
+    neighbour ids of the concatenation), ONE SNN rows pass over the disjoint
+    union of all the batch's graphs, then per segment the silhouettes of its
+    60 clusterings; per subcluster the selection + map-back and its co-cluster
+    triangle.  The subclusters' PC matrices are slices of synthetic PCs (the
+    per-subset PCA, f4, is timed on its own)."""
+    eng = engs[0]
+    S = len(engs)
+    N, B, G = args.cells, args.boots_per_gpu, world
+    L = len(K_NUM) * N_RES
+    pcs, pop = synth_pcs(torch, N, args.pcs, args.genes, 20241024 + 5, dev)
+    sizes = [5000, 6000, 7000, 8000, 9000, 10000, 11000, 12000, 12000, 20000]
+    sizes[-1] += N - sum(sizes)
+    nsub = len(sizes)
+    dcs = [5 + (10 * c) // (nsub - 1) for c in range(nsub)]
+    dpad = max(dcs)
+    perm = torch.from_numpy(np.random.default_rng(55).permutation(N)).to(dev)
+    Nof = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    cells = torch.zeros((N, dpad), dtype=torch.float64, device=dev)  # the subclusters' PCs stacked, zero-padded
+    for c in range(nsub):
+        cells[Nof[c]:Nof[c + 1], :dcs[c]] = pcs[perm[Nof[c]:Nof[c + 1]], :dcs[c]]
+    popc = pop[perm]
+    ns = [int(0.9 * m) for m in sizes]
+    bids = [rank * B + j for j in range(B)]
+    # bootstrap b of subcluster c: default_rng(123 + b) draws (the same stream seed for every subcluster:
+    # BPPARAM is forwarded, :562-566)
+    boots = [[np.random.default_rng(123 + b).integers(0, sizes[c], ns[c]).astype(np.int32) for b in bids]
+             for c in range(nsub)]
+    uniq = [[int(np.count_nonzero(np.bincount(x, minlength=sizes[c]))) for x in boots[c]] for c in range(nsub)]
+    boots_t = [torch.from_numpy(np.stack(boots[c])).to(dev) for c in range(nsub)]  # (B, n_c) local cells
+    labels = [torch.empty((B, L, ns[c]), dtype=torch.int32, device=dev) for c in range(nsub)]
+    for c in range(nsub):
+        for j in range(B):
+            labels[c][j] = synth_labels(torch, popc[Nof[c]:Nof[c + 1]], boots_t[c][j], L, dev, 1000 + bids[j], chi=20)
+    cmax = max(int(lb.max().item()) for lb in labels)
+    SB = max(1, min(args.seg_batch, B))
+    batches = [(b0, min(B, b0 + SB)) for b0 in range(0, B, SB)]
+
+    def seg_plan(b0, b1):
+        segs = [(c, j) for j in range(b0, b1) for c in range(nsub)]
+        off = np.concatenate([[0], np.cumsum([ns[c] for c, _ in segs])]).astype(np.int64)
+        su = np.array([uniq[c][j] for c, j in segs], np.int32)
+        idx = torch.cat([boots_t[c][j] + int(Nof[c]) for c, j in segs])
+        return segs, off, su, idx
+
+    plans = [seg_plan(b0, b1) for b0, b1 in batches]
+    nmax = max(int(p[1][-1]) for p in plans)
+    rows_s = [torch.empty((nmax, dpad), dtype=torch.float64, device=dev) for _ in range(S)]
+    knn_s = [torch.empty((nmax, 20), dtype=torch.int32, device=dev) for _ in range(S)]
+    rcap = 700 * nmax
+    snn_s = [(torch.zeros(nmax + 1, dtype=torch.int64, device=dev), torch.zeros(nmax, dtype=torch.int32, device=dev),
+              torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
+             for _ in range(S)]
+    nedges = torch.zeros((len(batches), len(K_NUM)), dtype=torch.int64, device=dev)
+    means = [torch.empty((B, L), dtype=torch.float64, device=dev) for _ in range(nsub)]
+    nclust = [torch.empty((B, L), dtype=torch.int32, device=dev) for _ in range(nsub)]
+    minsize = [torch.empty((B, L), dtype=torch.int32, device=dev) for _ in range(nsub)]
+    A = [torch.zeros((B, sizes[c]), dtype=torch.uint8, device=dev) for c in range(nsub)]
+    P = [sizes[c] * (sizes[c] - 1) // 2 for c in range(nsub)]
+    co = [torch.empty(P[c], dtype=torch.int16, device=dev) for c in range(nsub)]
+    both = [torch.empty(P[c], dtype=torch.int16, device=dev) for c in range(nsub)]
+    streams = [e.torch_stream() for e in engs]
+
+    def run_batch(t, si):
+        segs, off, su, idx = plans[t]
+        e = engs[si]
+        n = int(off[-1])
+        rows, knn = rows_s[si][:n], knn_s[si][:n]
+        e.knn_boot_segments_t(cells, idx, off, su, 20, knn, local_ids=False)
+        e.snn_rows_t(knn, K_NUM, "number", snn_s[si][0][:n + 1], snn_s[si][1][:n], snn_s[si][2], snn_s[si][3],
+                     nedges[t])
+        e.gather_rows_rm_t(cells, N, dpad, idx, rows)
+        for q, (c, j) in enumerate(segs):
+            a, b = int(off[q]), int(off[q + 1])
+            e.silhouette_cells_t(rows[a:b], labels[c][j], cmax, boots_t[c][j], sizes[c], means[c][j], nclust[c][j],
+                                 minsize[c][j])
+
+    def step():
+        cur = torch.cuda.current_stream()
+        for st_ in streams:
+            st_.wait_stream(cur)
+        for t in range(len(batches)):
+            si = t % S
+            with torch.cuda.stream(streams[si]):
+                run_batch(t, si)
+        for st_ in streams:
+            cur.wait_stream(st_)
+        for c in range(nsub):
+            eng.select_mapback_t("robust", labels[c], boots_t[c], sizes[c], A[c], 0, means=means[c],
+                                 nclust=nclust[c], minsize=minsize[c])
+            eng.cocluster_t(A[c], 0, sizes[c], co=co[c], both=both[c])
+
+    def barrier():
+        if G > 1:
+            dist.barrier()
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if int(nedges.min().item()) < 0:
+        raise RuntimeError(f"SNN row capacity too small: {rcap}")
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    # kernel times (library timers) over one more step, then the segmented kNN in isolation
+    for e in engs:
+        e.timing(True)
+        for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
+            e.timing_read(w)
+    step()
+    torch.cuda.synchronize()
+    kt = {}
+    for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
+        r = [e.timing_read(w) for e in engs]
+        kt[w] = (sum(x[0] for x in r), sum(x[1] for x in r))
+    for e in engs:
+        e.timing(False)
+    eng.timing(True)
+    eng.timing_read("knn_screen")
+    eng.timing_read("knn_total")
+    fbk = 0
+    with torch.cuda.stream(streams[0]):
+        for t in range(len(batches)):
+            segs, off, su, idx = plans[t]
+            n = int(off[-1])
+            fbk += eng.knn_boot_segments_t(cells, idx, off, su, 20, knn_s[0][:n], local_ids=False, stats=True)[1]
+    iso_scr = eng.timing_read("knn_screen")
+    iso_tot = eng.timing_read("knn_total")
+    eng.timing(False)
+    if G > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = tt.item()
+    value = G * B * args.steps / el
+    # the screen's algorithmic work: 2 u_s^2 d_c per segment (the distinct cells it searches)
+    flops = sum(2.0 * uniq[c][j] ** 2 * dcs[c] for c in range(nsub) for j in range(B))
+    scr_ms = iso_scr[0]
+    roof = {
+        "kernel": "knn_screen16_kernel over every (subcluster, bootstrap) segment's distinct cells "
+                  "(ccg_knn_boot_segments_dev; fp16 hi/lo split, v_mfma_f32_32x32x16_f16)",
+        "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_F16_TFLOPS,
+        "achieved": round(flops / (scr_ms * 1e-3) / 1e12, 2),
+        "frac": round(flops / (scr_ms * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
+        "traffic": None,
+        "algorithmic_per_launch": f"sum over segments of 2 u_s^2 d_c = {flops:.3e} flop per step over "
+                                  f"{iso_scr[1]} launches ({nsub} subclusters x {B} bootstraps)",
+        "avg_launch_ms": round(scr_ms / max(iso_scr[1], 1), 4),
+        "knn_total_ms_per_step": round(iso_tot[0], 3),
+        "exact_search_rows_per_step": int(fbk),
+    }
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "bootstraps/s",
+        "n_gpus": G,
+        "ranks_seen": ranks_seen,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1000, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "dtype_detail": "kNN order exact in f64 (segmented distinct-cell screen: fp16 hi/lo x3 MFMA, f64 certify, "
+                        "exact f64 expansion); silhouette f64 fixed-point sums; co-cluster int8 MFMA",
+        "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA, subclusters = random cell blocks of "
+                "5k-20k cells with the first d_c PCs; synthetic clusterings (C 2..20) in place of host Leiden",
+        "config": {
+            "workload": f"BASELINE cfg5: one iterate=TRUE level on {N} cells -- {nsub} subclusters "
+                        f"({min(sizes)}-{max(sizes)} cells, pcNum {min(dcs)}-{max(dcs)}), {B} bootstraps of every "
+                        f"subcluster per GPU per step (value = level bootstraps/s; x{nsub} subcluster-bootstraps), "
+                        f"{SB} bootstraps x {nsub} subclusters per segmented launch set",
+            "name": "cfg5", "cells": N, "subcluster_cells": sizes, "subcluster_pcs": dcs, "boots_per_gpu": B,
+            "segments_per_launch": SB * nsub, "streams_per_gpu": S,
+        },
+        "subcluster_bootstraps_per_s": round(value * nsub, 3),
+        "roofline": roof,
+        "kernel_ms_per_step": {w: round(v[0], 3) for w, v in kt.items()},
+        "kernel_launches_per_step": {w: int(v[1]) for w, v in kt.items()},
+    }
+    if rank == 0 and G == 1 and not args.no_cpu_baseline:
+        dm = int(round(float(np.mean(dcs))))
+        out["cpu_baseline"] = cpu_baseline(pcs[:, :dm].contiguous().cpu().numpy(), B, max(ns), N, dm,
+                                           args.cpu_sample_rows, coc_cols=B, coc_pairs=float(sum(P)),
+                                           seg_rows=ns)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    for e in engs[1:]:
+        e.close()
+    grp.close()
+    if G > 1:
+        dist.destroy_process_group()
 
 
 def visible_gpus():
@@ -275,16 +630,20 @@ def main():
     else:
         grp = DeviceGroup.open([local])
     S = max(1, args.streams)
-    NK = NS = 0
-    if args.pipeline:
-        NK, NS = (max(1, int(v)) for v in args.pipeline.split(","))
-        S = NK + NS
+    W = WORKLOADS[args.workload]
+    if args.workload == "cfg5":
+        return run_cfg5(args, torch, dist, grp, [grp.engines[0]] + [Engine(local) for _ in range(S - 1)], dev, world,
+                        rank, json_fd, ranks_seen)
+    robust = W["mode"] == "robust"
+    emul = W["emul_ranks"] if world == 1 else 0  # one GPU's share of an emul-rank job (synthetic other columns)
     engs = [grp.engines[0]] + [Engine(local) for _ in range(S - 1)]  # own workspaces per in-flight bootstrap
     eng = engs[0]
     N, d, B = args.cells, args.pcs, args.boots_per_gpu
     n = int(args.boot_size * N)
     L = len(K_NUM) * N_RES
     G = world
+    Gc = emul or G  # ranks whose columns the co-cluster counts
+    cpr = B if robust else B * L  # assignment columns per rank per step (granular: all 60, :688)
 
     # ---------------- inputs, resident in HBM before timing
     pcs, pop = synth_pcs(torch, N, d, args.genes, 20241024 + 3, dev)
@@ -314,10 +673,10 @@ def main():
 
     labels = torch.empty((B, L, n), dtype=torch.int32, device=dev)
     for j in range(B):
-        labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j])
+        labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j], chi=W["cmax"])
     cmax = int(labels.max().item())
 
-    RING = NK + NS + 1 if NK else S  # bootstrap buffers (gathered rows, kNN) in flight
+    RING = S  # bootstrap buffers (gathered rows, kNN) in flight
     rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(RING)]
     knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(RING)]
     rows, knn = rows_s[0], knn_s[0]
@@ -338,9 +697,9 @@ def main():
     nclust = torch.empty((B, L), dtype=torch.int32, device=dev)
     minsize = torch.empty((B, L), dtype=torch.int32, device=dev)
     choice = torch.empty(B, dtype=torch.int32, device=dev)
-    A_full = torch.zeros((G * B, N), dtype=torch.uint8, device=dev)  # all ranks' columns
-    A_local = A_full[rank * B:(rank + 1) * B]  # this rank's block, all-gathered in place
-    cuts = row_slabs(N, G)
+    A_full = torch.zeros((Gc * cpr, N), dtype=torch.uint8, device=dev)  # all ranks' columns
+    A_local = A_full[rank * cpr:(rank + 1) * cpr]  # this rank's block, all-gathered in place
+    cuts = row_slabs(N, Gc)
     r0, r1 = cuts[rank], cuts[rank + 1]
     P = max(slab_pairs(N, r0, r1), 1)
     co = torch.empty(P, dtype=torch.int16, device=dev)      # uint16 counts (viewed as int16)
@@ -349,40 +708,22 @@ def main():
     ev_k = [torch.cuda.Event() for _ in range(B)]
     ev_s = [torch.cuda.Event() for _ in range(B)]
 
-    def step_pipeline():
-        # stage split: kNN streams (MFMA-bound screen) run ahead of the
-        # SNN + silhouette streams (issue/LDS-bound) by up to RING bootstraps,
-        # so the two kinds of work always share the GPU
-        cur = torch.cuda.current_stream()
-        if use_table:
-            eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
-        for st_ in streams:
-            st_.wait_stream(cur)
-        for j in range(B):
-            slot, ks, ss = j % RING, j % NK, NK + j % NS
-            with torch.cuda.stream(streams[ks]):
-                if j >= RING:
-                    streams[ks].wait_event(ev_s[j - RING])  # the slot's previous bootstrap is consumed
-                engs[ks].gather_rows_rm_t(pcs, N, d, boots[j], rows_s[slot])
-                boot_knn(engs[ks], j, rows_s[slot], knn_s[slot])
-                ev_k[j].record(streams[ks])
-            with torch.cuda.stream(streams[ss]):
-                streams[ss].wait_event(ev_k[j])
-                engs[ss].snn_rows_t(knn_s[slot], K_NUM, "number", *snn_out[ss - NK], nedges[j])
-                engs[ss].silhouette_cells_t(rows_s[slot], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
-                ev_s[j].record(streams[ss])
-        for st_ in streams:
-            cur.wait_stream(st_)
-        eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
-                             minsize=minsize, out_choice=choice)
-        grp.allgather_columns_t([A_local], [B] * G, [A_full])
-        grp.cocluster_sharded_t([A_full], co=[co], both=[both])
+    def step_tail():
+        # selection + map-back into this rank's columns, the all-gather, this rank's co/both slab
+        if robust:
+            eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
+                                 minsize=minsize, out_choice=choice)
+        else:
+            eng.select_mapback_t("granular", labels, boots, N, A_local, 0)
+        if emul:  # one rank of an emul-rank job: the other ranks' columns are already in place
+            eng.cocluster_t(A_full, r0, r1, co=co, both=both)
+        else:
+            grp.allgather_columns_t([A_local], [cpr] * G, [A_full])
+            grp.cocluster_sharded_t([A_full], co=[co], both=[both])
 
     host_t = [0.0]  # host time spent enqueueing the bootstrap loop (the launches are asynchronous)
 
     def step():
-        if NK:
-            return step_pipeline()
         th = time.perf_counter()
         # S bootstraps in flight: bootstrap j runs on stream j % S with its own
         # engine context (workspaces), so one bootstrap's latency-bound SNN
@@ -399,14 +740,12 @@ def main():
                 e.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[si])
                 boot_knn(e, j, rows_s[si], knn_s[si])
                 e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
-                e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+                if robust:  # granular mode scores no clustering (:688)
+                    e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_t[0] += time.perf_counter() - th
         for st_ in streams:
             cur.wait_stream(st_)
-        eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
-                             minsize=minsize, out_choice=choice)
-        grp.allgather_columns_t([A_local], [B] * G, [A_full])
-        grp.cocluster_sharded_t([A_full], co=[co], both=[both])
+        step_tail()
 
     def barrier():
         if G > 1:
@@ -425,6 +764,10 @@ def main():
         if int(nedges.min().item()) < 0:
             raise RuntimeError(f"SNN row capacity too small: {rcap}")
     need = nedges.max(0).values.tolist()
+    if emul:  # the other ranks' column blocks: this rank's columns with the cells rotated (same label counts)
+        for k in range(1, emul):
+            A_full[k * cpr:(k + 1) * cpr] = torch.roll(A_local, shifts=k * 7919, dims=1)
+        torch.cuda.synchronize()
     eng.gather_rows_rm_t(pcs, N, d, boots[0], rows)
     fb = eng.knn_boot_hint_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, hint, stats=True)  # certification statistics
     fb_cold = eng.knn_boot_t(pcs_cm, N, d, boots[0], uniq[0], rows, 20, knn, stats=True)
@@ -466,7 +809,8 @@ def main():
             eng.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[0])
             boot_knn(eng, j, rows_s[0], knn_s[0])
             eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
-            eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+            if robust:
+                eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_idle.append(time.perf_counter() - th)
         torch.cuda.synchronize()
     host_idle_ms = 1000 * float(np.median(host_idle))
@@ -505,7 +849,8 @@ def main():
         eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         boot_knn(eng, j, rows, knn)
         eng.snn_rows_t(knn, K_NUM, "number", *snn_out[0], nedges[j])
-        eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+        if robust:
+            eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
     iso_snn = eng.timing_read("snn")
     iso_sil = eng.timing_read("silhouette")
     torch.cuda.synchronize()
@@ -534,7 +879,7 @@ def main():
     mfma_exec_table = 3 * 2.0 * N * N * kpad
     # co-cluster roofline: OPS = 2 * P * (sum_b C_b + B) over this rank's slab
     colC = int(A_full.max(dim=1).values.to(torch.int64).sum().item())  # sum_b C_b over all ranks' columns
-    coc_ops = 2.0 * P * (colC + G * B)
+    coc_ops = 2.0 * P * (colC + Gc * cpr)
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
@@ -584,6 +929,8 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             coc_traffic = json.load(f).get("cocluster_bytes_per_launch_B125")
+    if args.workload != "cfg3":
+        coc_traffic = None  # the committed PMC traffic is the cfg3 (N = 100k, B = 125) launch
     roof_coc = {
         "kernel": "cof_tile_kernel (one-hot int8 co/both GEMM, v_mfma_i32_32x32x32_i8), this rank's row slab",
         "bound": "mfma",
@@ -593,7 +940,7 @@ def main():
         "frac": round(coc_ops / (coc_ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
         "traffic": coc_traffic,
         "algorithmic_per_launch": f"2*P*(sum C_b + B) = {coc_ops:.3e} int8 ops (P={P} pairs in this slab, "
-                                  f"sum C_b={colC}, B={G * B}), SURVEY 8(d); one launch per step",
+                                  f"sum C_b={colC}, B={Gc * cpr}), SURVEY 8(d); one launch per step",
         "avg_launch_ms": round(coc_ms, 4),
         "avg_launch_ms_note": "library hipEvent timer on the launch stream, the timer step after the timed region",
         "output_bytes_per_launch": 4 * P,
@@ -605,6 +952,8 @@ def main():
     sil_ms = iso_sil[0] / max(iso_sil[1], 1)
     snn_bytes = sum(n * k * 4 for k in K_NUM) + 16 * sum(iso_edges) / max(nis, 1)
     sil_flop = 2.0 * d * u_iso * iso_npres / max(nis, 1)
+    if not robust:
+        sil_ms = 0.0
     roof_snn = {
         "kernel": "SNN union-graph rows (ccg_snn_rows_dev: host lists, bitonic build tiers, copy rows)",
         "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
@@ -618,8 +967,8 @@ def main():
     roof_sil = {
         "kernel": "silhouette of the 60 clusterings (ccg_silhouette_cells_dev; widths on v_mfma_f64_16x16x4f64)",
         "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_F64_TFLOPS,
-        "achieved": round(sil_flop / (sil_ms * 1e-3) / 1e12, 2),
-        "frac": round(sil_flop / (sil_ms * 1e-3) / 1e12 / PEAK_F64_TFLOPS, 4),
+        "achieved": round(sil_flop / (sil_ms * 1e-3) / 1e12, 2) if robust else None,
+        "frac": round(sil_flop / (sil_ms * 1e-3) / 1e12 / PEAK_F64_TFLOPS, 4) if robust else None,
         "traffic": None,
         "algorithmic_per_launch": f"2 d u sum_l C_l = {sil_flop:.3e} flop per bootstrap (x.mu of the u distinct "
                                   f"cells against every present centroid of the 60 labelings)",
@@ -647,8 +996,9 @@ def main():
                         "silhouette f64 with fixed-point sums; co-cluster int8 MFMA, int32 counts",
         "data": "synthetic: NB counts (12 populations, 2000 genes) -> PCA; synthetic clusterings in place of host Leiden",
         "config": {
-            "workload": "BASELINE cfg3 shapes: 100k cells x 30 PCs, robust mode, kNum 10/15/20 x 20 resolutions; "
-                        f"{B} bootstraps per GPU per step ({G * B} total) + co-cluster row slab over all columns",
+            "workload": workload_text(args.workload, N, d, B, G, emul),
+            "name": args.workload,
+            "mode": W["mode"], "assignment_columns": Gc * cpr, "slab_rows": [int(r0), int(r1)],
             "cells": N, "pcs": d, "bootstrap_rows": n, "distinct_cells_mean": round(float(np.mean(uniq)), 1),
             "boots_per_gpu": B, "clusterings_per_boot": L,
             "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}", "streams_per_gpu": S,
@@ -660,7 +1010,7 @@ def main():
         "roofline_knn_table" if use_table else "roofline_knn_screen": (roof_table if use_table else roof_screen),
         "roofline_knn_screen_path" if use_table else "roofline_knn_table_path": (roof_screen if use_table else roof_table),
         "roofline_snn": roof_snn,
-        "roofline_silhouette": roof_sil,
+        "roofline_silhouette": roof_sil if robust else None,
         "kernel_ms_per_step": per_step,
         "kernel_ms_per_step_note": "library hipEvent timers over one extra step after the timed region "
                                    "(bootstraps overlap, so kernel times sum to more than the step)",
@@ -672,7 +1022,11 @@ def main():
         "snn_edges_max_per_boot": [int(e) for e in need],
     }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pcs.cpu().numpy(), B, n, N, d, args.cpu_sample_rows)
+        out["cpu_baseline"] = cpu_baseline(pcs.cpu().numpy(), B, n, N, d, args.cpu_sample_rows, robust=robust,
+                                           coc_cols=Gc * cpr, coc_pairs=P)
+        out["cpu_baseline"]["check"] = cpu_baseline_check(
+            eng, torch, pcs, pcs_cm, boots[0], uniq[0], labels[0], (tab_idx, tab_d2) if use_table else None, cmax,
+            robust, A_full, co, both, int(r0), int(r1))
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
