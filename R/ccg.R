@@ -81,8 +81,18 @@ ccgEngine <- function(devices = getOption("ccg.devices", 0L)) {
 # random step picks the initial centres -- sample.int(m, k), and when those
 # rows repeat (bootstrap copies) sample.int(nrow(unique(x)), k) again.
 # nunique() returns nrow(unique(x)) (computed at most once per bootstrap).
-.ccg_replay_findknn_draws <- function(x, nunique) {
-  if (!.ccg_kmknn_draws()) return(invisible(NULL))
+# options(ccg.replay_findknn = ): "replay" (default) replays the draws as
+# above; "findKNN" calls the installed BiocNeighbors::findKNN itself for its
+# side effects on the stream (exact whatever the installed version does, at
+# the cost of the CPU search); "none" draws nothing (BiocNeighbors >= 1.99, or
+# when bit-exact Leiden streams are not needed).
+.ccg_replay_findknn_draws <- function(x, nunique, k = 10L) {
+  mode <- getOption("ccg.replay_findknn", "replay")
+  if (identical(mode, "none") || !.ccg_kmknn_draws()) return(invisible(NULL))
+  if (identical(mode, "findKNN")) {
+    BiocNeighbors::findKNN(x, k = k)
+    return(invisible(NULL))
+  }
   m <- nrow(x)
   k <- ceiling(sqrt(m))
   if (k >= m) return(invisible(NULL))
@@ -93,10 +103,14 @@ ccgEngine <- function(devices = getOption("ccg.devices", 0L)) {
 
 #' mean(approxSilhouette(x, l)[, 3], na.rm = TRUE) for every clustering in
 #' the list `labs` in one batched call (:447, :518, :664, :811).
-ccgSilhouetteMeans <- function(x, labs, eng = ccgEngine()) {
+#' cell: for a bootstrap matrix whose rows repeat cells, the 1-based cell of
+#' each row (match(rownames(x), unique(rownames(x)))): widths are then
+#' computed once per (cell, label) and weighted (ccg_silhouette_cells).
+ccgSilhouetteMeans <- function(x, labs, eng = ccgEngine(), cell = NULL) {
   codes <- vapply(labs, function(l) as.integer(factor(l)), integer(nrow(x)))
   if (!is.matrix(codes)) codes <- matrix(codes, nrow = nrow(x))
-  .Call(C_ccg_r_silhouette, eng, x, codes)
+  if (is.null(cell)) return(.Call(C_ccg_r_silhouette, eng, x, codes))
+  .Call(C_ccg_r_silhouette_cells, eng, x, codes, as.integer(cell))
 }
 
 #' Drop-in for getClustAssignments (R/consensusClust.R:650-692): one exact
@@ -124,17 +138,21 @@ getClustAssignments <- function(pca, clusterFun = "leiden", resRange, kNum, mode
     if (is.null(nu)) nu <<- nrow(unique(pca))
     nu
   }
+  # every graph of kNum from one SNN pass over the max(kNum) lists
+  ks <- sort(unique(as.integer(kNum)))
+  graphs <- .Call(C_ccg_r_snn_multi, eng, knn, ks, 0L)
   labs <- list()
   for (k in kNum) {
-    g <- .ccg_graph(.Call(C_ccg_r_snn, eng, knn, as.integer(k), 0L), nrow(pca))
+    g <- .ccg_graph(graphs[[match(as.integer(k), ks)]], nrow(pca))
     for (res in resRange) {
-      .ccg_replay_findknn_draws(pca, nunique)  # the reference's findKNN for this (k, res), :656
+      .ccg_replay_findknn_draws(pca, nunique, k)  # the reference's findKNN for this (k, res), :656
       labs[[length(labs) + 1L]] <- .ccg_cluster_graph(g, clusterFun, res)
     }
   }
   mapback <- function(l) setNames(l, rownames(pca))[match(cellOrder, rownames(pca))]
   if (mode == "robust") {
-    s <- ccgSilhouetteMeans(pca, labs, eng)
+    # copies of a cell share a row name: widths once per (cell, label)
+    s <- ccgSilhouetteMeans(pca, labs, eng, cell = match(rownames(pca), unique(rownames(pca))))
     score <- ifelse(s$nclust > 1 & s$minsize > minSize, s$mean, ifelse(s$minsize > minSize, 0, 0.15))
     r <- rank(score, ties.method = "first")
     return(mapback(labs[[which(r == max(r))]]))
@@ -188,31 +206,72 @@ ccgStabilityMatrix <- function(clustAssignments, finalAssignments, eng = ccgEngi
 #' The bootstrap + consensus core of consensusClust (R/consensusClust.R:388-497)
 #' over the engine: call it from consensusClust in place of those lines.
 #' Returns list(assignments, clustAssignments).
-ccgConsensusCore <- function(pca, nboots, bootSize, clusterFun, resRange, kNum, mode, seed, minStability,
-                             BPPARAM = BiocParallel::SerialParam(RNGseed = seed), batch = 32L) {
-  eng <- ccgEngine()
-  if (!inherits(BPPARAM, "SerialParam")) {
-    # HIP cannot run in forked workers; the same RNG streams come from a
-    # SerialParam with the same seed
-    BPPARAM <- BiocParallel::SerialParam(RNGseed = BiocParallel::bpRNGseed(BPPARAM))
-  }
-  cells <- rownames(pca)
-  n <- bootSize * nrow(pca)
-  # pass 1 (:391-394): every bootstrap's sample() in its own stream, and the
-  # stream's state on entry (the global state is restored after bplapply)
-  draws <- BiocParallel::bplapply(seq_len(nboots), function(boot) {
+.ccg_serial <- function(BPPARAM) {
+  if (inherits(BPPARAM, "SerialParam")) return(BPPARAM)
+  # HIP cannot run in forked workers; the same RNG streams come from a
+  # SerialParam with the same seed
+  BiocParallel::SerialParam(RNGseed = BiocParallel::bpRNGseed(BPPARAM))
+}
+
+# pass 1 (:391-394): every bootstrap's sample() in its own stream, and the
+# stream's state on entry (the global state is restored after bplapply)
+.ccg_draw_bootstraps <- function(cells, n, nboots, BPPARAM) {
+  BiocParallel::bplapply(seq_len(nboots), function(boot) {
     st <- get(".Random.seed", envir = globalenv())
     list(idx = match(sample(cells, n, replace = TRUE), cells), seed = st)
   }, BPPARAM = BPPARAM)
+}
+
+#' iterate=TRUE, one level at a time (BASELINE config 5): the bootstrap
+#' draws of every subcluster PC matrix in `pcas` (each from the forwarded
+#' BPPARAM's streams, as the recursive consensusClust call of :562-566 draws
+#' them) and their kNN in batched ccg_r_knn_boot_segments calls -- every
+#' subcluster's bootstraps in one set of GPU launches.  Pass element s of the
+#' result as ccgConsensusCore(pcas[[s]], ..., prefetched = result[[s]]).  A
+#' maintainer restructures :546-567 into three lapply passes: PCs of every
+#' subcluster, ccgLevelBootstrapKNN, then each subcluster's consensus core.
+ccgLevelBootstrapKNN <- function(pcas, nboots, bootSize, kNum, BPPARAM, batch = 32L) {
+  eng <- ccgEngine()
+  BPPARAM <- .ccg_serial(BPPARAM)
+  draws <- lapply(pcas, function(p) {
+    d <- .ccg_draw_bootstraps(rownames(p), bootSize * nrow(p), nboots, BPPARAM)
+    list(draws = d, knns = vector("list", nboots))
+  })
+  for (b0 in seq(1L, nboots, by = batch)) {
+    bs <- b0:min(nboots, b0 + batch - 1L)
+    boots <- lapply(draws, function(x) {
+      vapply(x$draws[bs], function(d) d$idx, integer(length(x$draws[[1L]]$idx)))
+    })
+    boots <- lapply(boots, function(b) if (is.matrix(b)) b else matrix(b, ncol = length(bs)))
+    res <- tryCatch(.Call(C_ccg_r_knn_boot_segments, eng, pcas, boots, as.integer(max(kNum))),
+                    error = function(e) NULL)  # e.g. a subcluster too small for a segment: searched per core
+    if (!is.null(res)) for (s in seq_along(pcas)) draws[[s]]$knns[bs] <- res[[s]]
+  }
+  draws
+}
+
+ccgConsensusCore <- function(pca, nboots, bootSize, clusterFun, resRange, kNum, mode, seed, minStability,
+                             BPPARAM = BiocParallel::SerialParam(RNGseed = seed), batch = 32L,
+                             prefetched = NULL) {
+  eng <- ccgEngine()
+  BPPARAM <- .ccg_serial(BPPARAM)
+  cells <- rownames(pca)
+  n <- bootSize * nrow(pca)
+  draws <- if (is.null(prefetched)) .ccg_draw_bootstraps(cells, n, nboots, BPPARAM) else prefetched$draws
   after <- get0(".Random.seed", envir = globalenv(), inherits = FALSE)
   clustAssignments <- vector("list", nboots)
   for (b0 in seq(1L, nboots, by = batch)) {
     bs <- b0:min(nboots, b0 + batch - 1L)
     # the batch's kNN in one engine call: the distinct-cell search per
-    # bootstrap, bootstraps split over the GPUs of a device group
-    boot <- vapply(draws[bs], function(d) d$idx, integer(length(draws[[1L]]$idx)))
-    knns <- tryCatch(.Call(C_ccg_r_knn_boot, eng, pca, matrix(boot, ncol = length(bs)), as.integer(max(kNum))),
-                     error = function(e) NULL)
+    # bootstrap, bootstraps split over the GPUs of a device group (or the
+    # level's batched search, ccgLevelBootstrapKNN)
+    knns <- if (!is.null(prefetched) && !any(vapply(prefetched$knns[bs], is.null, logical(1)))) {
+      prefetched$knns[bs]
+    } else {
+      boot <- vapply(draws[bs], function(d) d$idx, integer(length(draws[[1L]]$idx)))
+      tryCatch(.Call(C_ccg_r_knn_boot, eng, pca, matrix(boot, ncol = length(bs)), as.integer(max(kNum))),
+               error = function(e) NULL)
+    }
     # pass 2: re-enter each stream, re-draw sample() (the same indices: the
     # stream then stands where the reference's getClustAssignments starts)
     for (t in seq_along(bs)) {

@@ -124,14 +124,18 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
         raise ValueError(f"knn must be {n} x {kmax}, got {knn.shape}")
     fn = _cluster_fn(clusterFun)
     labels = []
+    order = np.argsort(kNum, kind="stable")
+    graphs = eng.snn_multi(knn, [int(kNum[t]) for t in order], "number")  # every k in one pass, :656-658
+    graph_of = {int(kNum[t]): graphs[g] for g, t in enumerate(order)}
     for k in kNum:  # :653-654, k outer, resolution inner
-        ei, ej, w = eng.snn(knn, k, "number")  # SNNGraphParam(type="number"), :656-658
+        ei, ej, w = graph_of[int(k)]
         for res in resRange:
             labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
     lab = np.stack(labels)
     if mode == "robust":
         X = pca[boot_idx]
-        means, nclust, minsize, _ = eng.silhouette(X, lab)  # :664 on the bootstrap rows
+        # :664 on the bootstrap rows: widths once per (cell, label), copies weighted
+        means, nclust, minsize = eng.silhouette_cells(X, lab, boot_idx, N)
         scores = robust_scores(means, nclust, minsize, minSize)
         choice = robust_choice(scores)
         out = mapback(boot_idx, lab[choice], N)
@@ -443,8 +447,11 @@ def null_statistics(pca_nulls, kNum=K_NUM, clusterFun="leiden", resRange=NULL_RE
     for t, X, (knn, _) in zip(ok, mats, knns):
         n = X.shape[0]
         labels = []
+        order = np.argsort(kNum, kind="stable")
+        graphs = eng.snn_multi(np.ascontiguousarray(knn), [int(kNum[t]) for t in order], "number")
+        graph_of = {int(kNum[t]): graphs[g] for g, t in enumerate(order)}
         for k in kNum:  # getClustAssignments' k-outer / resolution-inner loop (:653-654)
-            ei, ej, w = eng.snn(np.ascontiguousarray(knn), k, "number")
+            ei, ej, w = graph_of[int(k)]
             for res in resRange:
                 labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
         lab = np.stack(labels)

@@ -1036,7 +1036,7 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     // cell, the other rows, per-labeling disagreements, exceptions
     char* tb = (char*)ccg_ws(ctx, WS_SIL_C, sizeof(int) * (size_t)ncell + sizeof(int64_t) * (size_t)(m + 1) +
                                                 3 * sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
-                                                sizeof(unsigned long long) * (size_t)L * m + 256);
+                                                sizeof(unsigned long long) * (size_t)L * m + 512);
     if (!tb) return CCG_ENOMEM;
     int* first = (int*)tb;
     int64_t* scan = (int64_t*)(tb + ccg_cdiv(sizeof(int) * ncell, 16) * 16);
@@ -1045,7 +1045,9 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     int* nexc = nonrep + m;             // [0] exception count; then cnt and the disagreements (zeroed together)
     int* cnt = nexc + 4;                // [m] (first mw used)
     int* mult = cnt + m;                // [L][m] (first mw columns used)
-    unsigned long long* exc = (unsigned long long*)(mult + ccg_cdiv((int64_t)L * m, 2) * 2);
+    // the u64 exceptions start on an 8-byte boundary whatever the parity of m
+    unsigned long long* exc =
+        (unsigned long long*)(tb + ccg_cdiv((int64_t)((char*)(mult + (int64_t)L * m) - tb), 16) * 16);
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
     const unsigned gm = (unsigned)ccg_cdiv(m, 256);
@@ -1101,6 +1103,39 @@ extern "C" int ccg_silhouette(ccg_ctx* ctx, const double* x, int64_t m, int d, c
     if (out_nclust) CCG_HIP(hipMemcpyAsync(out_nclust, dnc, sizeof(int32_t) * L, hipMemcpyDeviceToHost, st));
     if (out_minsize) CCG_HIP(hipMemcpyAsync(out_minsize, dms, sizeof(int32_t) * L, hipMemcpyDeviceToHost, st));
     if (out_width) CCG_HIP(hipMemcpyAsync(out_width, dw, sizeof(double) * m * L, hipMemcpyDeviceToHost, st));
+    CCG_HIP(hipStreamSynchronize(st));
+    return CCG_OK;
+}
+
+extern "C" int ccg_silhouette_cells(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels, int L,
+                                    int cmax, const int32_t* cell, int64_t ncell, double* out_mean,
+                                    int32_t* out_nclust, int32_t* out_minsize) {
+    CCG_REQUIRE(ctx && x && labels && cell && out_mean, "ccg_silhouette_cells: NULL argument");
+    CCG_REQUIRE(m >= 1 && d >= 1 && L >= 1 && ncell >= 1, "ccg_silhouette_cells: bad sizes");
+    for (int64_t t = 0; t < (int64_t)L * m; ++t)
+        if (labels[t] < 1 || labels[t] > cmax) {
+            ccg_set_error("ccg_silhouette_cells: label %d at %lld outside [1, %d]", labels[t], (long long)t, cmax);
+            return CCG_ERANGE;
+        }
+    for (int64_t r = 0; r < m; ++r)
+        CCG_REQUIRE(cell[r] >= 0 && cell[r] < ncell, "ccg_silhouette_cells: cell[%lld] out of range", (long long)r);
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    double* dx = (double*)ccg_ws(ctx, WS_HOST_A, sizeof(double) * m * d);
+    int32_t* dl = (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * m * L);
+    double* dmean = (double*)ccg_ws(ctx, WS_HOST_C, sizeof(double) * L + 2 * sizeof(int32_t) * L + 64);
+    int32_t* dc = (int32_t*)ccg_ws(ctx, WS_HOST_D, sizeof(int32_t) * m);
+    if (!dx || !dl || !dmean || !dc) return CCG_ENOMEM;
+    int32_t* dnc = (int32_t*)(dmean + L);
+    int32_t* dms = dnc + L;
+    CCG_HIP(hipMemcpyAsync(dx, x, sizeof(double) * m * d, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(dl, labels, sizeof(int32_t) * m * L, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipMemcpyAsync(dc, cell, sizeof(int32_t) * m, hipMemcpyHostToDevice, st));
+    int rc = ccg_silhouette_cells_dev(ctx, dx, m, d, dl, L, cmax, dc, ncell, dmean, dnc, dms, st);
+    if (rc) return rc;
+    CCG_HIP(hipMemcpyAsync(out_mean, dmean, sizeof(double) * L, hipMemcpyDeviceToHost, st));
+    if (out_nclust) CCG_HIP(hipMemcpyAsync(out_nclust, dnc, sizeof(int32_t) * L, hipMemcpyDeviceToHost, st));
+    if (out_minsize) CCG_HIP(hipMemcpyAsync(out_minsize, dms, sizeof(int32_t) * L, hipMemcpyDeviceToHost, st));
     CCG_HIP(hipStreamSynchronize(st));
     return CCG_OK;
 }

@@ -1327,3 +1327,65 @@ extern "C" int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
     }
     return CCG_OK;
 }
+
+extern "C" int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk, int type,
+                             int32_t* const* out_i, int32_t* const* out_j, double* const* out_w, const int64_t* caps,
+                             int64_t* nedges) {
+    CCG_REQUIRE(ctx && knn && ks && nedges, "ccg_snn_multi: NULL argument");
+    CCG_REQUIRE(n >= 1 && kstride >= 1 && nk >= 1 && nk <= SNN_MAXK, "ccg_snn_multi: bad sizes");
+    CCG_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    for (int64_t t = 0; t < n * kstride; ++t)
+        CCG_REQUIRE(knn[t] >= 0 && knn[t] < n && knn[t] != t / kstride,
+                    "ccg_snn_multi: neighbour index out of range or self at %lld", (long long)t);
+    int64_t tot = 0;
+    for (int t = 0; t < nk; ++t) tot += caps ? std::max<int64_t>(caps[t], 0) : 0;
+    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
+    int64_t* dne = (int64_t*)ccg_ws(ctx, WS_HOST_E, 64);
+    int32_t* di = tot > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * tot) : nullptr;
+    int32_t* dj = tot > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * tot) : nullptr;
+    double* dw = tot > 0 ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * tot) : nullptr;
+    if (!dknn || !dne || (tot > 0 && (!di || !dj || !dw))) return CCG_ENOMEM;
+    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
+    int32_t* oi[SNN_MAXK];
+    int32_t* oj[SNN_MAXK];
+    double* ow[SNN_MAXK];
+    int64_t dc[SNN_MAXK];
+    int64_t* dn[SNN_MAXK];
+    int64_t o = 0;
+    for (int t = 0; t < nk; ++t) {
+        dc[t] = caps ? std::max<int64_t>(caps[t], 0) : 0;
+        oi[t] = dc[t] ? di + o : nullptr;
+        oj[t] = dc[t] ? dj + o : nullptr;
+        ow[t] = dc[t] ? dw + o : nullptr;
+        dn[t] = dne + t;
+        o += dc[t];
+    }
+    int64_t ne[SNN_MAXK];
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        int rc = ccg_snn_multi_dev(ctx, dknn, n, kstride, ks, nk, type, oi, oj, ow, dc, dn, st);
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(ne, dne, sizeof(int64_t) * nk, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        if (ne[0] >= 0) break;
+        ctx->snn_row_reserve = -ne[0] + (-ne[0]) / 8;  // rows did not fit the reservation: grow and rerun
+    }
+    CCG_REQUIRE(ne[0] >= 0, "ccg_snn_multi: row reservation could not be satisfied");
+    bool short_cap = false;
+    for (int t = 0; t < nk; ++t) {
+        nedges[t] = ne[t];
+        short_cap |= ne[t] > dc[t];
+    }
+    if (short_cap) {
+        ccg_set_error("ccg_snn_multi: capacities smaller than the edge counts (reported in nedges)");
+        return CCG_ECAP;
+    }
+    for (int t = 0; t < nk; ++t)
+        if (ne[t] > 0) {
+            CCG_HIP(hipMemcpyAsync(out_i[t], oi[t], sizeof(int32_t) * ne[t], hipMemcpyDeviceToHost, st));
+            CCG_HIP(hipMemcpyAsync(out_j[t], oj[t], sizeof(int32_t) * ne[t], hipMemcpyDeviceToHost, st));
+            CCG_HIP(hipMemcpyAsync(out_w[t], ow[t], sizeof(double) * ne[t], hipMemcpyDeviceToHost, st));
+        }
+    CCG_HIP(hipStreamSynchronize(st));
+    return CCG_OK;
+}

@@ -208,6 +208,45 @@ class Engine:
                                ctypes.byref(ne)))
         return ei, ej, w
 
+    def snn_multi(self, knn_idx, ks, type="number"):
+        """Every graph of ks (ascending) from one pass (ccg_snn_multi):
+        a list of (i, j, w) edge lists, one per k."""
+        knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
+        n, kst = knn_idx.shape
+        nk = len(ks)
+        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        karr = (ctypes.c_int * nk)(*ks)
+        ne = (ctypes.c_int64 * nk)()
+        P = _vp * nk
+        zero = (ctypes.c_int64 * nk)()
+        rc = self.lib.ccg_snn_multi(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, P(), P(), P(), zero, ne)
+        if rc not in (_lib.CCG_OK, _lib.CCG_ECAP):
+            check(rc)
+        outs = [(np.empty(ne[g], np.int32), np.empty(ne[g], np.int32), np.empty(ne[g], np.float64))
+                for g in range(nk)]
+        caps = (ctypes.c_int64 * nk)(*[ne[g] for g in range(nk)])
+        check(self.lib.ccg_snn_multi(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t,
+                                     P(*[_ptr(o[0]) for o in outs]), P(*[_ptr(o[1]) for o in outs]),
+                                     P(*[_ptr(o[2]) for o in outs]), caps, ne))
+        return outs
+
+    def silhouette_cells(self, x, labels, cell, ncell, cmax=None):
+        """ccg_silhouette_cells: means over bootstrap rows x whose cells are
+        `cell` (copies identical), widths once per (cell, label).  Returns
+        (mean[L], nclust[L], minsize[L])."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        m, d = x.shape
+        lab = np.ascontiguousarray(np.atleast_2d(labels), dtype=np.int32)
+        L = lab.shape[0]
+        cmax = int(lab.max()) if cmax is None else cmax
+        cell = np.ascontiguousarray(cell, dtype=np.int32)
+        mean = np.empty(L, np.float64)
+        nc = np.empty(L, np.int32)
+        ms = np.empty(L, np.int32)
+        check(self.lib.ccg_silhouette_cells(self.ctx, _ptr(x), m, d, _ptr(lab), L, cmax, _ptr(cell), int(ncell),
+                                            _ptr(mean), _ptr(nc), _ptr(ms)))
+        return mean, nc, ms
+
     def silhouette(self, x, labels, cmax=None, want_width=False):
         """Batched approxSilhouette means (ccg_silhouette).
 

@@ -286,6 +286,14 @@ int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n,
                       double* const* out_w, const int64_t* caps,
                       int64_t* const* d_nedges, void* stream);
 
+/* Host flavour of ccg_snn_multi_dev (knn, outputs and caps host; nedges a
+ * host array of nk counts).  If some caps[t] < nedges[t] (call with caps all
+ * 0 to size) returns CCG_ECAP with every nedges[t] set and no edges copied. */
+int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
+                  const int* ks, int nk, int type, int32_t* const* out_i,
+                  int32_t* const* out_j, double* const* out_w, const int64_t* caps,
+                  int64_t* nedges);
+
 /* The same graphs as rows (CSR of the union graph = the largest k, built in
  * one pass): row j = partners p > j of node j in ascending order,
  * nbr[row_off[j] .. row_off[j] + row_len[j]) with wpk = per-graph packed
@@ -333,6 +341,14 @@ int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
                              const int32_t* labels, int L, int cmax,
                              const int32_t* cell, int64_t ncell, double* out_mean,
                              int32_t* out_nclust, int32_t* out_minsize, void* stream);
+
+/* Host flavour of ccg_silhouette_cells_dev (all pointers host): what an R
+ * getClustAssignments calls with the bootstrap matrix pca[sample(...), ] and
+ * cell = match(rownames, unique(rownames)) - 1. */
+int ccg_silhouette_cells(ccg_ctx* ctx, const double* x, int64_t m, int d,
+                         const int32_t* labels, int L, int cmax, const int32_t* cell,
+                         int64_t ncell, double* out_mean, int32_t* out_nclust,
+                         int32_t* out_minsize);
 
 /* ----------------------------------------------- selection + map-back -- */
 /* For nb bootstraps with L clusterings each (labels nb x L x n int32,

@@ -217,6 +217,65 @@ SEXP ccg_r_knn_segments(SEXP e, SEXP mats, SEXP kmax) {
     return out;
 }
 
+/* iterate=TRUE, one level (BASELINE config 5): pcas a list of N_s x d_s
+ * matrices (the level's subclusters), boots a list of n_s x nb 1-based index
+ * matrices (one column per bootstrap, like ccg_r_knn_boot).  Every bootstrap
+ * of every subcluster in ONE call (ccg_knn_boot_segments); returns a list
+ * (per subcluster) of lists (per bootstrap) of n_s x kmax 1-based
+ * neighbour matrices, each equal to ccg_r_knn_boot's. */
+SEXP ccg_r_knn_boot_segments(SEXP e, SEXP pcas, SEXP boots, SEXP kmax) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    const int nsub = Rf_length(pcas), k = Rf_asInteger(kmax);
+    if (Rf_length(boots) != nsub) Rf_error("one bootstrap matrix per PC matrix");
+    int d = 0;
+    int64_t Ntot = 0, n = 0;
+    int nseg = 0;
+    int64_t* Nof = (int64_t*)R_alloc((size_t)nsub + 1, sizeof(int64_t));
+    Nof[0] = 0;
+    for (int s = 0; s < nsub; ++s) {
+        SEXP p = VECTOR_ELT(pcas, s), b = VECTOR_ELT(boots, s);
+        if (Rf_ncols(p) > d) d = Rf_ncols(p);
+        Nof[s + 1] = Nof[s] + Rf_nrows(p);
+        nseg += Rf_ncols(b);
+        n += (int64_t)Rf_nrows(b) * Rf_ncols(b);
+    }
+    Ntot = Nof[nsub];
+    double* cells = (double*)R_alloc((size_t)Ntot * d, sizeof(double)); /* row-major, zero-padded dims */
+    int32_t* idx = (int32_t*)R_alloc((size_t)n, sizeof(int32_t));
+    int64_t* off = (int64_t*)R_alloc((size_t)nseg + 1, sizeof(int64_t));
+    off[0] = 0;
+    int q = 0;
+    for (int s = 0; s < nsub; ++s) {
+        SEXP p = VECTOR_ELT(pcas, s), b = VECTOR_ELT(boots, s);
+        const int r = Rf_nrows(p), c = Rf_ncols(p), ns = Rf_nrows(b), nb = Rf_ncols(b);
+        const double* v = REAL(p);
+        for (int i = 0; i < r; ++i)
+            for (int j = 0; j < d; ++j) cells[(Nof[s] + i) * d + j] = j < c ? v[i + (R_xlen_t)j * r] : 0.0;
+        for (int t = 0; t < nb; ++t, ++q) {
+            for (int i = 0; i < ns; ++i) idx[off[q] + i] = (int32_t)(INTEGER(b)[i + (R_xlen_t)t * ns] - 1 + Nof[s]);
+            off[q + 1] = off[q] + ns;
+        }
+    }
+    int32_t* out = (int32_t*)R_alloc((size_t)n * k, sizeof(int32_t));
+    ccg_knn_stats st;
+    CALL("ccg_knn_boot_segments", ccg_knn_boot_segments(ctx, cells, Ntot, d, idx, n, off, NULL, nseg, k, out, NULL,
+                                                        &st));
+    SEXP res = PROTECT(Rf_allocVector(VECSXP, nsub));
+    q = 0;
+    for (int s = 0; s < nsub; ++s) {
+        SEXP b = VECTOR_ELT(boots, s);
+        const int ns = Rf_nrows(b), nb = Rf_ncols(b);
+        SEXP lst = PROTECT(Rf_allocVector(VECSXP, nb));
+        for (int t = 0; t < nb; ++t, ++q) SET_VECTOR_ELT(lst, t, knn_matrix(out + off[q] * k, ns, k));
+        SET_VECTOR_ELT(res, s, lst);
+        UNPROTECT(1);
+    }
+    UNPROTECT(1);
+    return res;
+}
+
 /* ---------------------------------------------------------------- SNN -- */
 /* knn: n x ks 1-based; first k columns used; type 0 = "number", 1 = "rank".
  * Returns list(from, to, weight), 1-based, from < to. */
@@ -255,6 +314,61 @@ SEXP ccg_r_snn(SEXP e, SEXP knn, SEXP k, SEXP type) {
     return res;
 }
 
+/* Every graph of kNum in one pass (ccg_snn_multi): knn n x ks 1-based, ks
+ * the ascending k values; returns a list (one per k) of list(from, to,
+ * weight), 1-based, from < to. */
+static SEXP edge_list(const int32_t* ei, const int32_t* ej, const double* w, int64_t ne) {
+    SEXP from = PROTECT(Rf_allocVector(INTSXP, ne));
+    SEXP to = PROTECT(Rf_allocVector(INTSXP, ne));
+    SEXP wt = PROTECT(Rf_allocVector(REALSXP, ne));
+    for (int64_t t = 0; t < ne; ++t) {
+        INTEGER(from)[t] = ei[t] + 1;
+        INTEGER(to)[t] = ej[t] + 1;
+        REAL(wt)[t] = w[t];
+    }
+    SEXP res = PROTECT(Rf_allocVector(VECSXP, 3));
+    SET_VECTOR_ELT(res, 0, from);
+    SET_VECTOR_ELT(res, 1, to);
+    SET_VECTOR_ELT(res, 2, wt);
+    SEXP nm = PROTECT(Rf_allocVector(STRSXP, 3));
+    SET_STRING_ELT(nm, 0, Rf_mkChar("from"));
+    SET_STRING_ELT(nm, 1, Rf_mkChar("to"));
+    SET_STRING_ELT(nm, 2, Rf_mkChar("weight"));
+    Rf_setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(5);
+    return res;
+}
+
+SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    int64_t n;
+    int kst;
+    int32_t* kn = knn_from_r(knn, &n, &kst);
+    const int nk = Rf_length(ks);
+    if (nk < 1 || nk > 4) Rf_error("ccg_r_snn_multi: 1 to 4 values of k");
+    int kv[4];
+    for (int t = 0; t < nk; ++t) kv[t] = INTEGER(ks)[t];
+    int64_t ne[4] = {0, 0, 0, 0}, caps[4] = {0, 0, 0, 0};
+    int32_t* oi[4] = {NULL, NULL, NULL, NULL};
+    int32_t* oj[4] = {NULL, NULL, NULL, NULL};
+    double* ow[4] = {NULL, NULL, NULL, NULL};
+    int rc = ccg_snn_multi(ctx, kn, n, kst, kv, nk, Rf_asInteger(type), oi, oj, ow, caps, ne);
+    if (rc != CCG_OK && rc != CCG_ECAP) fail("ccg_snn_multi", rc);
+    for (int t = 0; t < nk; ++t) {
+        caps[t] = ne[t];
+        oi[t] = (int32_t*)R_alloc((size_t)ne[t] + 1, sizeof(int32_t));
+        oj[t] = (int32_t*)R_alloc((size_t)ne[t] + 1, sizeof(int32_t));
+        ow[t] = (double*)R_alloc((size_t)ne[t] + 1, sizeof(double));
+    }
+    CALL("ccg_snn_multi", ccg_snn_multi(ctx, kn, n, kst, kv, nk, Rf_asInteger(type), oi, oj, ow, caps, ne));
+    SEXP out = PROTECT(Rf_allocVector(VECSXP, nk));
+    for (int t = 0; t < nk; ++t) SET_VECTOR_ELT(out, t, edge_list(oi[t], oj[t], ow[t], ne[t]));
+    UNPROTECT(1);
+    return out;
+}
+
 /* --------------------------------------------------------- silhouette -- */
 /* mean(approxSilhouette(x, labels[, l])[, 3], na.rm = TRUE) for every column
  * l of an m x L integer matrix of codes 1..cmax (factor codes).  Returns
@@ -281,6 +395,51 @@ SEXP ccg_r_silhouette(SEXP e, SEXP x, SEXP labels) {
     if (rc != CCG_OK) {
         UNPROTECT(3);
         fail("ccg_silhouette", rc);
+    }
+    SEXP res = PROTECT(Rf_allocVector(VECSXP, 3));
+    SET_VECTOR_ELT(res, 0, mean);
+    SET_VECTOR_ELT(res, 1, ncl);
+    SET_VECTOR_ELT(res, 2, mns);
+    SEXP nm = PROTECT(Rf_allocVector(STRSXP, 3));
+    SET_STRING_ELT(nm, 0, Rf_mkChar("mean"));
+    SET_STRING_ELT(nm, 1, Rf_mkChar("nclust"));
+    SET_STRING_ELT(nm, 2, Rf_mkChar("minsize"));
+    Rf_setAttrib(res, R_NamesSymbol, nm);
+    UNPROTECT(5);
+    return res;
+}
+
+/* The same means for the bootstrap matrix x = pca[sample(...), ] whose rows
+ * repeat cells: cell = match(rownames(x), unique(rownames(x))) (1-based), so
+ * widths are computed once per (cell, label) (ccg_silhouette_cells). */
+SEXP ccg_r_silhouette_cells(SEXP e, SEXP x, SEXP labels, SEXP cell) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    const int64_t m = Rf_nrows(x);
+    const int d = Rf_ncols(x);
+    if (Rf_nrows(labels) != m || XLENGTH(cell) != m) Rf_error("labels and cell need one row per row of x");
+    const int L = Rf_ncols(labels);
+    const int* lab = INTEGER(labels);
+    int cmax = 1;
+    for (R_xlen_t t = 0; t < (R_xlen_t)m * L; ++t) {
+        if (lab[t] == NA_INTEGER || lab[t] < 1) Rf_error("labels must be codes >= 1");
+        if (lab[t] > cmax) cmax = lab[t];
+    }
+    int32_t* c0 = (int32_t*)R_alloc((size_t)m, sizeof(int32_t));
+    int ncell = 1;
+    for (int64_t r = 0; r < m; ++r) {
+        c0[r] = INTEGER(cell)[r] - 1;
+        if (c0[r] + 1 > ncell) ncell = c0[r] + 1;
+    }
+    SEXP mean = PROTECT(Rf_allocVector(REALSXP, L));
+    SEXP ncl = PROTECT(Rf_allocVector(INTSXP, L));
+    SEXP mns = PROTECT(Rf_allocVector(INTSXP, L));
+    int rc = ccg_silhouette_cells(ctx, REAL(x), m, d, lab, L, cmax, c0, ncell, REAL(mean), INTEGER(ncl),
+                                  INTEGER(mns));
+    if (rc != CCG_OK) {
+        UNPROTECT(3);
+        fail("ccg_silhouette_cells", rc);
     }
     SEXP res = PROTECT(Rf_allocVector(VECSXP, 3));
     SET_VECTOR_ELT(res, 0, mean);
@@ -478,8 +637,11 @@ static const R_CallMethodDef call_methods[] = {
     {"ccg_r_abi_version", (DL_FUNC)&ccg_r_abi_version, 0},
     {"ccg_r_knn_boot", (DL_FUNC)&ccg_r_knn_boot, 4},
     {"ccg_r_knn_segments", (DL_FUNC)&ccg_r_knn_segments, 3},
+    {"ccg_r_knn_boot_segments", (DL_FUNC)&ccg_r_knn_boot_segments, 4},
     {"ccg_r_snn", (DL_FUNC)&ccg_r_snn, 4},
+    {"ccg_r_snn_multi", (DL_FUNC)&ccg_r_snn_multi, 4},
     {"ccg_r_silhouette", (DL_FUNC)&ccg_r_silhouette, 3},
+    {"ccg_r_silhouette_cells", (DL_FUNC)&ccg_r_silhouette_cells, 4},
     {"ccg_r_cocluster_dist", (DL_FUNC)&ccg_r_cocluster_dist, 2},
     {"ccg_r_consensus_knn", (DL_FUNC)&ccg_r_consensus_knn, 3},
     {"ccg_r_block_dist", (DL_FUNC)&ccg_r_block_dist, 4},

@@ -87,7 +87,9 @@ def test_r_bootstrap_loop_is_batched_and_keeps_the_rng_sequence():
     :650-692)."""
     code = open(RCODE).read()
     core = code[code.index("ccgConsensusCore <- function("):code.index("ccgNullStatistics <- function(")]
-    assert core.count("bplapply(seq_len(nboots)") == 1
+    draw = code[code.index(".ccg_draw_bootstraps <- function("):code.index("ccgLevelBootstrapKNN <- function(")]
+    assert draw.count("bplapply(seq_len(nboots)") == 1 and ".Random.seed" in draw
+    assert ".ccg_draw_bootstraps(cells, n, nboots, BPPARAM)" in core
     assert ".Random.seed" in core and "draws[[b]]$seed" in core
     assert "C_ccg_r_knn_boot" in core and "knn = if (is.null(knns))" in core
     gca = code[code.index("getClustAssignments <- function("):code.index("#' kNN(jaccardDist, k)$id")]
@@ -96,3 +98,41 @@ def test_r_bootstrap_loop_is_batched_and_keeps_the_rng_sequence():
     assert loop.index(".ccg_replay_findknn_draws") < loop.index(".ccg_cluster_graph")
     assert 'simplify(g, edge.attr.comb = "first")' in code
     assert 'packageVersion("BiocNeighbors") < "1.99.0"' in code
+
+
+def test_r_getclustassignments_runs_the_bench_kernels():
+    """The R drop-in reaches the kernels bench.py times: every kNum graph from
+    ONE SNN pass (ccg_snn_multi) and the silhouettes over the bootstrap's
+    distinct cells (ccg_silhouette_cells, cell = the row-name match)."""
+    code = open(RCODE).read()
+    gca = code[code.index("getClustAssignments <- function("):code.index("#' kNN(jaccardDist, k)$id")]
+    assert "C_ccg_r_snn_multi" in gca and "C_ccg_r_snn," not in gca
+    assert "cell = match(rownames(pca), unique(rownames(pca)))" in gca
+    sil = code[code.index("ccgSilhouetteMeans <- function("):code.index("#' Drop-in for getClustAssignments")]
+    assert "C_ccg_r_silhouette_cells" in sil
+    assert re.search(r"ccg_silhouette_cells\(ctx,", _glue()) and re.search(r"ccg_snn_multi\(ctx,", _glue())
+
+
+def test_r_level_batching_uses_the_segment_search():
+    """iterate=TRUE levels (BASELINE config 5): ccgLevelBootstrapKNN draws
+    each subcluster's bootstraps from the forwarded BPPARAM streams and
+    searches all of them through ccg_r_knn_boot_segments; ccgConsensusCore
+    consumes them (prefetched) without drawing again."""
+    code = open(RCODE).read()
+    lvl = code[code.index("ccgLevelBootstrapKNN <- function("):code.index("ccgConsensusCore <- function(")]
+    assert "C_ccg_r_knn_boot_segments" in lvl and ".ccg_draw_bootstraps(" in lvl
+    core = code[code.index("ccgConsensusCore <- function("):code.index("ccgNullStatistics <- function(")]
+    assert "prefetched$draws" in core and "prefetched$knns[bs]" in core
+    assert "ccg_knn_boot_segments(ctx, cells, Ntot, d, idx, n, off, NULL" in _glue()
+
+
+def test_r_findknn_replay_is_optional_and_skipped_when_k_covers_the_rows():
+    """The BiocNeighbors 1.x draw replay (parity unpinned) sits behind
+    options(ccg.replay_findknn): "replay" (default), "findKNN" (the installed
+    findKNN for its side effects), "none"; kmeans is not run (no draw) when
+    ceiling(sqrt(m)) >= m."""
+    code = open(RCODE).read()
+    rep = code[code.index(".ccg_replay_findknn_draws <- function("):code.index("#' mean(approxSilhouette")]
+    assert 'getOption("ccg.replay_findknn", "replay")' in rep
+    assert 'identical(mode, "none")' in rep and "BiocNeighbors::findKNN(x, k = k)" in rep
+    assert rep.index("if (k >= m) return(invisible(NULL))") < rep.index("sample.int(m, k)")
