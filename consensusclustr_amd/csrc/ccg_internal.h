@@ -57,6 +57,7 @@ enum ccg_ws_slot {
     WS_TAB,          // kNN cell table of a host call (ccg_knn_boot): ids then squared distances
     WS_FX_A,         // kNN exact search of failed rows: radii, candidate counts, overflow list
     WS_FX_B,         // kNN exact search of failed rows: candidate (d2, row) buffers
+    WS_FX_C,         // kNN exact search of failed rows: the references' fp32 image and fp64 norms
     WS_SEG_ROWS,     // batched bootstrap segments: the gathered rows of every segment
     WS_SEG_TAB,      // batched bootstrap segments: row and distinct-cell segment offsets
     WS_NSLOTS

@@ -1148,86 +1148,92 @@ __device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
 // pairs within it take the exact fp64 sum.  So the candidates are exactly the
 // plain scan's.  (The exact form costs three fp64 operations per dimension;
 // the filter one packed fp32 FMA per two.)
-#ifndef KNN_FX_FILTER
-#define KNN_FX_FILTER 1  // tools only: 0 = exact fp64 for every pair (A/B)
-#endif
+//
+// The references' fp32 image and fp64 norms are made once per call
+// (knn_fx_prep_kernel, skipped when no row failed; a failed row's own image
+// row is its query).  The scan gives each wave 64 references, one per lane,
+// held in registers, and walks a group of 64 failed rows at wave-uniform
+// addresses (scalar loads, served from the scalar cache to every wave of the
+// group): per (row, reference) pair one packed fp32 FMA per two dimensions,
+// no LDS staging and no barriers.
+#define KNN_FX_QG 64  // failed rows per group
 template <int DMAX>
-__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, int n, int d,
+__global__ __launch_bounds__(256) void knn_fx_prep_kernel(const double* __restrict__ rows, int n, int d,
+                                                          const int* __restrict__ fail_count,
+                                                          float* __restrict__ ref32, double* __restrict__ nrm) {
+    if (*fail_count == 0) return;
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    float v[DMAX];
+    double ny = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) {
+        const double y = k < d ? rows[j * d + k] : 0.0;
+        ny = fma(y, y, ny);
+        v[k] = (float)y;
+    }
+    float4* o = reinterpret_cast<float4*>(ref32 + j * DMAX);
+#pragma unroll
+    for (int k4 = 0; k4 < DMAX / 4; ++k4) o[k4] = make_float4(v[4 * k4], v[4 * k4 + 1], v[4 * k4 + 2], v[4 * k4 + 3]);
+    nrm[j] = ny;
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, const float* __restrict__ ref32,
+                                                          const double* __restrict__ nrm, int n, int d,
                                                           const int* __restrict__ fail_list,
                                                           const int* __restrict__ fail_count,
                                                           const double* __restrict__ fail_tau, int* __restrict__ cnt,
                                                           double* __restrict__ bd, int* __restrict__ bi,
                                                           int* __restrict__ ovf_count) {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    __shared__ double sy[KNN_FX_CHUNK * DMAX];
-    __shared__ f2 syf[KNN_FX_CHUNK * DMAX / 2];
-    __shared__ double sny[KNN_FX_CHUNK];
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
     const int nf = min(*fail_count, KNN_FX_ROWS);
-    // reference ranges: about 2 units per block of the grid whatever the row count
-    const int ng = (nf + 63) / 64;
-    const int want = max(1, 2 * (int)gridDim.x / max(ng, 1));
-    const int range = (((n + want - 1) / want) + KNN_FX_CHUNK - 1) / KNN_FX_CHUNK * KNN_FX_CHUNK;
-    const int nr = (n + range - 1) / range;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int64_t w = blockIdx.x; w < (int64_t)ng * nr; w += gridDim.x) {
-        const int g = (int)(w / nr), r = (int)(w - (int64_t)g * nr);
-        const int f = g * 64 + lane;
-        const double tf = f < nf ? fail_tau[f] : -1.0;
-        const bool valid = f < nf && tf < INFINITY;  // no radius: the per-thread-list kernels
-        const int q = valid ? fail_list[f] : -1;
-        const double t = valid ? tf : -1.0;
-        double xq[DMAX];
-        f2 xf[DMAX / 2];
-        double nx = 0.0;
+    const int ng = (nf + KNN_FX_QG - 1) / KNN_FX_QG;
+    const int nrw = (n + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * 4;
+    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
+    for (int64_t w = w0; w < (int64_t)ng * nrw; w += nw) {
+        const int g = (int)(w / nrw), r = (int)(w - (int64_t)g * nrw);
+        const int j = r * 64 + lane;
+        const int jc = j < n ? j : n - 1;
+        f2 yf[DMAX / 2];
+        {
+            const float4* yp = reinterpret_cast<const float4*>(ref32 + (int64_t)jc * DMAX);
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) {
-            xq[k] = (valid && k < d) ? rows[(int64_t)q * d + k] : 0.0;
-            nx = fma(xq[k], xq[k], nx);
+            for (int k4 = 0; k4 < DMAX / 4; ++k4) {
+                const float4 y = yp[k4];
+                yf[2 * k4] = f2{y.x, y.y};
+                yf[2 * k4 + 1] = f2{y.z, y.w};
+            }
         }
+        const double ny = nrm[jc];
+        const int f1 = __builtin_amdgcn_readfirstlane(min(nf, (g + 1) * KNN_FX_QG));
+        for (int f = g * KNN_FX_QG; f < f1; ++f) {  // wave-uniform
+            const double t = fail_tau[f];
+            if (!(t < INFINITY)) continue;  // no radius: the per-thread-list kernels
+            const int q = __builtin_amdgcn_readfirstlane(fail_list[f]);
+            const double nx = nrm[q];
+            const float4* xp = reinterpret_cast<const float4*>(ref32 + (int64_t)q * DMAX);
+            f2 acc = {0.f, 0.f};
 #pragma unroll
-        for (int k2 = 0; k2 < DMAX / 2; ++k2) xf[k2] = f2{(float)xq[2 * k2], (float)xq[2 * k2 + 1]};
-        const int j0 = r * range, j1 = min(n, j0 + range);
-        for (int c0 = j0; c0 < j1; c0 += KNN_FX_CHUNK) {
-            const int cn = min(KNN_FX_CHUNK, j1 - c0);
-            __syncthreads();
-            for (int e = threadIdx.x; e < cn * d; e += 256) {  // the chunk's rows are contiguous
-                const int jj = e / d, k = e - jj * d;
-                sy[jj * DMAX + k] = rows[(int64_t)c0 * d + e];
+            for (int k4 = 0; k4 < DMAX / 4; ++k4) {
+                const float4 x = xp[k4];
+                acc = __builtin_elementwise_fma(f2{x.x, x.y}, yf[2 * k4], acc);
+                acc = __builtin_elementwise_fma(f2{x.z, x.w}, yf[2 * k4 + 1], acc);
             }
-            if (d < DMAX)
-                for (int e = threadIdx.x; e < cn * DMAX; e += 256) {  // zero the padding dims
-                    const int jj = e / DMAX, k = e - jj * DMAX;
-                    if (k >= d) sy[e] = 0.0;
-                }
-            __syncthreads();
-            for (int jj = threadIdx.x; jj < cn; jj += 256) {
-                double ny = 0.0;
-                for (int k = 0; k < DMAX; ++k) ny = fma(sy[jj * DMAX + k], sy[jj * DMAX + k], ny);
-                sny[jj] = ny;
-            }
-            for (int e = threadIdx.x; e < cn * DMAX / 2; e += 256)
-                syf[e] = f2{(float)sy[2 * e], (float)sy[2 * e + 1]};
-            __syncthreads();
-            for (int jj = wv; jj < cn; jj += 4) {
-                const int j = c0 + jj;
-                bool maybe = true;
-                if (KNN_FX_FILTER) {
-                    f2 acc = {0.f, 0.f};
+            const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
+            if (j < n && j != q && approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60) {
+                double xq[DMAX];
 #pragma unroll
-                    for (int k2 = 0; k2 < DMAX / 2; ++k2) acc = __builtin_elementwise_fma(xf[k2], syf[jj * DMAX / 2 + k2], acc);
-                    const double ny = sny[jj];
-                    const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
-                    maybe = approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60;
-                }
-                if (maybe) {
-                    const double v = knn_exact_d2<DMAX>(xq, sy + jj * DMAX, d);
-                    if (v <= t && j != q) {
-                        const int slot = atomicAdd(&cnt[f], 1);
-                        if (slot < KNN_FX_CAP) {
-                            bd[(int64_t)f * KNN_FX_CAP + slot] = v;
-                            bi[(int64_t)f * KNN_FX_CAP + slot] = j;
-                        }
+                for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
+                const double v = knn_exact_d2<DMAX>(xq, rows + (int64_t)j * d, d);
+                if (v <= t) {
+                    const int slot = atomicAdd(&cnt[f], 1);
+                    if (slot < KNN_FX_CAP) {
+                        bd[(int64_t)f * KNN_FX_CAP + slot] = v;
+                        bi[(int64_t)f * KNN_FX_CAP + slot] = j;
                     }
                 }
             }
@@ -1298,9 +1304,17 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         int* ovf_list = ovf_count + 64;
         double* bd = (double*)buf;
         int* bi = (int*)(bd + (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-#define CCG_FX(DM_)                                                                                                \
-    knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, bd, bi, \
-                                                         ovf_count)
+        char* img32 = (char*)ccg_ws(ctx, WS_FX_C, (sizeof(float) * 64 + sizeof(double)) * (size_t)n + 64);
+        if (!img32) return CCG_ENOMEM;
+        double* nrm = (double*)img32;
+        float* ref32 = (float*)(nrm + n);
+#define CCG_FX(DM_)                                                                                              \
+    do {                                                                                                         \
+        knn_fx_prep_kernel<DM_><<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, (int)n, d, fail_count, ref32,  \
+                                                                             nrm);                                \
+        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, ref32, nrm, (int)n, d, fail_list, fail_count,  \
+                                                             fail_tau, cnt, bd, bi, ovf_count);                   \
+    } while (0)
         if (d <= 16) CCG_FX(16);
         else if (d <= 32) CCG_FX(32);
         else CCG_FX(64);
