@@ -85,6 +85,9 @@ struct ccg_ctx {
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
     void* fx_zeroed;  // kNN radius search: the WS_FX_A buffer whose counters were zeroed at allocation
+    void* scan_zeroed;  // one-pass scan: the WS_SCAN buffer whose ticket and flags were zeroed
+    int64_t scan_cap;   // tiles its status arrays hold
+    unsigned scan_seq;  // call sequence stamped into the status words
     // kNN: the exact-search row list of the last call and its count (device; ccg_knn_last_fallback)
     const int* last_fail_list;
     const int* last_fail_count;
