@@ -30,6 +30,7 @@
 //      rows when the caller wants them (ccg_snn_multi_dev).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "ccg_internal.h"
 
@@ -460,101 +461,19 @@ struct SnnBitonicLds {
     long long wc4[W][SNN_MAXK];
 };
 
-// One node, W waves (W = 1: one wave; W = 4: a 256-thread block for the
-// hubs); wave w holds sorted elements 64*E*w .. 64*E*(w+1) - 1.
-template <int E, int W, typename K>
-__device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, const SnnSpec& sp, int64_t n, int64_t j,
-                                                 const SnnMember& m, int wv, int lane,
-                                                 const int2* __restrict__ hosts_s, const SnnRows& rows,
-                                                 int64_t* __restrict__ cnt) {
+// The node's sorted keys x (lane-major, padding ~0 last) -> its row: runs of
+// equal partner are combined (sum / bytewise min of the per-graph values) and
+// the last key of each run writes (partner, packed values); per-graph counts.
+// W > 1 (the hub tier) joins the waves' runs through L's wave summaries.
+template <int E, int W, typename K, typename LDS>
+__device__ __forceinline__ void snn_emit_sorted(LDS& L, const SnnSpec& sp, int64_t n, int64_t j, int wv, int lane,
+                                                K (&x)[E], const SnnRows& rows, int64_t* __restrict__ cnt) {
     constexpr int PS = SnnKeyT<K>::PS;
-    constexpr int S = 64 * E;  // elements per wave
-    const int kmax = sp.kk[sp.nk - 1];
-    const int incl = snn_scan_add(m.len);
-    const int M = __builtin_amdgcn_readlane(incl, 63);
-    const int pre = incl - m.len;
-    const int base = S * wv;  // this wave's first item / element
 #define SNN_SYNC()                            \
     do {                                      \
         if constexpr (W == 1) WAVE_LDS_SYNC(); \
         else __syncthreads();                 \
     } while (0)
-    // gather (element-major within the wave's slice)
-#pragma unroll
-    for (int e = 0; e < E; ++e) L.u.mark[base + 64 * e + lane] = -1;
-    if (wv == 0 && lane <= kmax) L.mem[lane] = make_int4((int)m.h0, (int)m.hend, m.cur, pre);
-    SNN_SYNC();
-    if (wv == 0 && lane <= kmax && m.len > 0) L.u.mark[pre] = lane;
-    SNN_SYNC();
-    int mi[E];
-    // the member of the slice's first item when its run starts in an earlier slice
-    const unsigned long long started = __ballot(lane <= kmax && m.len > 0 && pre < base);
-    int carry = started ? 63 - __clzll(started) : INT_MIN;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int v = snn_scan_max(max(L.u.mark[base + 64 * e + lane], carry));
-        carry = __builtin_amdgcn_readlane(v, 63);
-        mi[e] = v;
-    }
-    int2 hv[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int t = base + 64 * e + lane;
-        hv[e] = make_int2(0, 0);
-        if (t < M) {
-            const int4 md = L.mem[mi[e]];
-            const int q = md.x + (t - md.w);
-            hv[e] = q < md.y ? hosts_s[q] : make_int2(md.z, 0);
-        }
-    }
-    K x[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-        x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
-    SNN_SYNC();  // every mark is read
-#pragma unroll
-    for (int e = 0; e < E; ++e) L.u.buf[base + 64 * e + lane] = x[e];
-    SNN_SYNC();
-#pragma unroll
-    for (int e = 0; e < E; ++e) x[e] = L.u.buf[base + E * lane + e];
-    snn_bitonic<E, K>(x, lane);
-    if constexpr (W > 1) {
-        // merges across waves through LDS: mirror stage, then the cross-wave
-        // xor stages, then the in-wave xor stages
-#pragma unroll
-        for (int k = 2 * S; k <= W * S; k <<= 1) {
-            SNN_SYNC();
-#pragma unroll
-            for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
-            SNN_SYNC();
-            {
-                const int pw = wv ^ (k / S - 1);
-                const bool lower = (wv & (k / (2 * S))) == 0;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const K o = L.u.buf[S * pw + E * (63 - lane) + (E - 1 - e)];
-                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
-                    x[e] = lower ? lo : hi;
-                }
-            }
-#pragma unroll
-            for (int jj = k / 4; jj >= S; jj >>= 1) {
-                SNN_SYNC();
-#pragma unroll
-                for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
-                SNN_SYNC();
-                const int pw = wv ^ (jj / S);
-                const bool lower = (wv & (jj / S)) == 0;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const K o = L.u.buf[S * pw + E * lane + e];
-                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
-                    x[e] = lower ? lo : hi;
-                }
-            }
-            snn_bitonic_xor<E, K, S / 2>(x, lane);
-        }
-    }
     // runs of equal p: forward segmented combine inside the lane
     int p[E];
     unsigned agg[E];
@@ -665,13 +584,246 @@ __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, cons
 #undef SNN_SYNC
 }
 
+// One node, W waves (W = 1: one wave; W = 4: a 256-thread block for the
+// hubs); wave w holds sorted elements 64*E*w .. 64*E*(w+1) - 1.
+template <int E, int W, typename K>
+__device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, const SnnSpec& sp, int64_t n, int64_t j,
+                                                 const SnnMember& m, int wv, int lane,
+                                                 const int2* __restrict__ hosts_s, const SnnRows& rows,
+                                                 int64_t* __restrict__ cnt) {
+    constexpr int S = 64 * E;  // elements per wave
+    const int kmax = sp.kk[sp.nk - 1];
+    const int incl = snn_scan_add(m.len);
+    const int M = __builtin_amdgcn_readlane(incl, 63);
+    const int pre = incl - m.len;
+    const int base = S * wv;  // this wave's first item / element
+#define SNN_SYNC()                            \
+    do {                                      \
+        if constexpr (W == 1) WAVE_LDS_SYNC(); \
+        else __syncthreads();                 \
+    } while (0)
+    // gather (element-major within the wave's slice)
+#pragma unroll
+    for (int e = 0; e < E; ++e) L.u.mark[base + 64 * e + lane] = -1;
+    if (wv == 0 && lane <= kmax) L.mem[lane] = make_int4((int)m.h0, (int)m.hend, m.cur, pre);
+    SNN_SYNC();
+    if (wv == 0 && lane <= kmax && m.len > 0) L.u.mark[pre] = lane;
+    SNN_SYNC();
+    int mi[E];
+    // the member of the slice's first item when its run starts in an earlier slice
+    const unsigned long long started = __ballot(lane <= kmax && m.len > 0 && pre < base);
+    int carry = started ? 63 - __clzll(started) : INT_MIN;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int v = snn_scan_max(max(L.u.mark[base + 64 * e + lane], carry));
+        carry = __builtin_amdgcn_readlane(v, 63);
+        mi[e] = v;
+    }
+    int2 hv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = base + 64 * e + lane;
+        hv[e] = make_int2(0, 0);
+        if (t < M) {
+            const int4 md = L.mem[mi[e]];
+            const int q = md.x + (t - md.w);
+            hv[e] = q < md.y ? hosts_s[q] : make_int2(md.z, 0);
+        }
+    }
+    K x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
+    SNN_SYNC();  // every mark is read
+#pragma unroll
+    for (int e = 0; e < E; ++e) L.u.buf[base + 64 * e + lane] = x[e];
+    SNN_SYNC();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = L.u.buf[base + E * lane + e];
+    snn_bitonic<E, K>(x, lane);
+    if constexpr (W > 1) {
+        // merges across waves through LDS: mirror stage, then the cross-wave
+        // xor stages, then the in-wave xor stages
+#pragma unroll
+        for (int k = 2 * S; k <= W * S; k <<= 1) {
+            SNN_SYNC();
+#pragma unroll
+            for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
+            SNN_SYNC();
+            {
+                const int pw = wv ^ (k / S - 1);
+                const bool lower = (wv & (k / (2 * S))) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const K o = L.u.buf[S * pw + E * (63 - lane) + (E - 1 - e)];
+                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+                    x[e] = lower ? lo : hi;
+                }
+            }
+#pragma unroll
+            for (int jj = k / 4; jj >= S; jj >>= 1) {
+                SNN_SYNC();
+#pragma unroll
+                for (int e = 0; e < E; ++e) L.u.buf[base + E * lane + e] = x[e];
+                SNN_SYNC();
+                const int pw = wv ^ (jj / S);
+                const bool lower = (wv & (jj / S)) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const K o = L.u.buf[S * pw + E * lane + e];
+                    const K lo = x[e] < o ? x[e] : o, hi = x[e] < o ? o : x[e];
+                    x[e] = lower ? lo : hi;
+                }
+            }
+            snn_bitonic_xor<E, K, S / 2>(x, lane);
+        }
+    }
+    snn_emit_sorted<E, W, K>(L, sp, n, j, wv, lane, x, rows, cnt);
+#undef SNN_SYNC
+}
+
+
+// ---------------------------------------------------------- merge tier --
+// NUMBER graphs (32-bit keys p << 6 | m), one wave per node: a node's items
+// are <= kmax + 2 runs that are ALREADY sorted by partner -- each member's
+// hosts above j (ascending host lists), plus one run of the members
+// themselves (s > j, sorted across lanes) -- so instead of a full bitonic sort
+// of the padded 64 E slots the wave merges the runs pairwise, ceil(log2(kmax +
+// 2)) levels of merge path: each lane emits ceil(M / 64) consecutive outputs of
+// a level after a binary search for its start on the merge diagonal.  Work per
+// level is O(M), not O(64 E log^2).  The sorted keys then go through the same
+// combine / row write as the bitonic tier.
+template <int E>
+struct SnnMergeLds {
+    int4 mem[64];
+    int off[2][64];  // run offsets (ping-pong): nr + 1 entries
+    uint32_t a[64 * E];
+    union {
+        int mark[64 * E];  // gather: item t -> member whose run starts at t (-1 elsewhere)
+        uint32_t b[64 * E];
+    } u;
+};
+
+// One level: runs [off[r], off[r+1]) of src, pairs (2i, 2i+1) merged into dst
+// (ties: the left run first); lane emits outputs [lane VT, lane VT + VT).
+__device__ __forceinline__ void snn_merge_level(const uint32_t* src, uint32_t* dst, const int* off, int nr, int M,
+                                                int VT, int lane) {
+    int o = lane * VT;
+    const int oend = min(M, o + VT);
+    if (o >= oend) return;
+    const int np = (nr + 1) >> 1;
+    int P = 0;  // the last pair starting at or before o (it contains o)
+    while (P + 1 < np && off[2 * (P + 1)] <= o) ++P;
+    int a0 = off[2 * P], a1 = off[min(2 * P + 1, nr)], b1 = off[min(2 * P + 2, nr)];
+    const int dd = o - a0, la = a1 - a0, lb = b1 - a1;
+    int lo = max(0, dd - lb), hi = min(dd, la);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (src[a0 + mid] <= src[a1 + dd - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int ia = a0 + lo, ib = a1 + dd - lo;
+    for (; o < oend; ++o) {
+        while (ia == a1 && ib == b1) {  // this lane's outputs continue in the next pair
+            ++P;
+            a0 = off[2 * P];
+            a1 = off[min(2 * P + 1, nr)];
+            b1 = off[min(2 * P + 2, nr)];
+            ia = a0;
+            ib = a1;
+        }
+        const uint32_t va = ia < a1 ? src[ia] : 0xFFFFFFFFu;
+        const uint32_t vb = ib < b1 ? src[ib] : 0xFFFFFFFFu;
+        const bool ta = ia < a1 && (ib >= b1 || va <= vb);
+        dst[o] = ta ? va : vb;
+        ia += ta ? 1 : 0;
+        ib += ta ? 0 : 1;
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void snn_merge_node(SnnMergeLds<E>& L, const SnnSpec& sp, int64_t n, int64_t j,
+                                               const SnnMember& m, int lane, const int2* __restrict__ hosts_s,
+                                               const SnnRows& rows, int64_t* __restrict__ cnt) {
+    using K = uint32_t;
+    const int kmax = sp.kk[sp.nk - 1];
+    // member lane's host items (ascending hosts above j) and its own item (s > j)
+    const bool selfi = lane >= 1 && lane <= kmax && m.len > 0 && m.cur > (int)j;
+    const int hl = m.len - (selfi ? 1 : 0);
+    const int incl = snn_scan_add(hl);
+    const int MH = __builtin_amdgcn_readlane(incl, 63);
+    const int pre = incl - hl;
+    K sk[1] = {selfi ? SnnKeyT<K>::make(m.cur, lane, 0) : ~(K)0};
+    snn_bitonic<1, K>(sk, lane);  // the self run, sorted across lanes
+    const int ns = __popcll(__ballot(selfi));
+    const int M = MH + ns;
+#pragma unroll
+    for (int e = 0; e < E; ++e) L.u.mark[64 * e + lane] = -1;
+    if (lane <= kmax) L.mem[lane] = make_int4((int)m.h0, (int)m.hend, m.cur, pre);
+    WAVE_LDS_SYNC();
+    if (lane <= kmax && hl > 0) L.u.mark[pre] = lane;
+    WAVE_LDS_SYNC();
+    int mi[E];
+    int carry = INT_MIN;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int v = snn_scan_max(max(L.u.mark[64 * e + lane], carry));
+        carry = __builtin_amdgcn_readlane(v, 63);
+        mi[e] = v;
+    }
+    int2 hv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = 64 * e + lane;
+        hv[e] = make_int2(0, 0);
+        if (t < MH) {
+            const int4 md = L.mem[mi[e]];
+            hv[e] = hosts_s[md.x + (t - md.w)];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = 64 * e + lane;
+        if (t < MH) L.a[t] = SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y);
+    }
+    if (lane < ns) L.a[MH + lane] = sk[0];
+    if (lane <= kmax) L.off[0][lane] = pre;
+    if (lane == kmax + 1) L.off[0][lane] = MH;
+    if (lane == kmax + 2) L.off[0][lane] = M;
+    int nr = kmax + 2;
+    WAVE_LDS_SYNC();
+    const int VT = (M + 63) >> 6;
+    uint32_t* src = L.a;
+    uint32_t* dst = L.u.b;
+    int cur = 0;
+    while (nr > 1) {
+        snn_merge_level(src, dst, L.off[cur], nr, M, VT, lane);
+        const int nr2 = (nr + 1) >> 1;
+        if (lane < nr2) L.off[cur ^ 1][lane] = L.off[cur][2 * lane];
+        if (lane == nr2) L.off[cur ^ 1][nr2] = M;
+        WAVE_LDS_SYNC();
+        uint32_t* t = src;
+        src = dst;
+        dst = t;
+        cur ^= 1;
+        nr = nr2;
+    }
+    K x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int idx = E * lane + e;
+        x[e] = idx < M ? src[idx] : ~(K)0;
+    }
+    snn_emit_sorted<E, 1, K>(L, sp, n, j, 0, lane, x, rows, cnt);
+}
+
 // Size classes (items M of a node): 0: M <= 512 (E = 4 or 8 per node),
 // 1: <= 1024 (E = 16), 2: <= 2048 (E = 32), 3: <= 4096 (the hubs: 4 waves x
 // E = 16 per node), larger: the block tier.  Classes 0..2 run one node per
 // wave (4 waves per block, 2 for class 2: its LDS stage is 8-16 KB per wave);
 // class 3 runs one node per 256-thread block over a fixed grid.
 __host__ __device__ constexpr int snn_bitonic_wpb(int cls) { return cls == 2 ? 2 : 4; }
-template <int CLS, typename K>
+template <int CLS, typename K, bool MERGE = false>
 __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
@@ -693,6 +845,22 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
             snn_bitonic_node<16, 4, K>(lds3, sp, n, j, m, wv, lane, hosts_s, rows, cnt);
             __syncthreads();
         }
+    } else if constexpr (MERGE) {
+        constexpr int EM = CLS == 0 ? 8 : (CLS == 1 ? 16 : 32);
+        constexpr int WPB = snn_bitonic_wpb(CLS);
+        __shared__ SnnMergeLds<EM> ldsm[WPB];
+        const int64_t f = (int64_t)blockIdx.x * WPB + wv;
+        if (f >= *count) return;
+        const int64_t j = list[f];
+        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        if constexpr (CLS == 0) {
+            if (__builtin_amdgcn_readlane(snn_scan_add(m.len), 63) <= 256) {
+                snn_merge_node<4>(*reinterpret_cast<SnnMergeLds<4>*>(&ldsm[wv]), sp, n, j, m, lane, hosts_s, rows,
+                                  cnt);
+                return;
+            }
+        }
+        snn_merge_node<EM>(ldsm[wv], sp, n, j, m, lane, hosts_s, rows, cnt);
     } else {
         constexpr int EM = CLS == 0 ? 8 : (CLS == 1 ? 16 : 32);
         constexpr int WPB = snn_bitonic_wpb(CLS);
@@ -1089,6 +1257,15 @@ static bool snn_no_copy() {
     return v;
 }
 
+// CCG_SNN_SORT=bitonic: the full bitonic tier for NUMBER graphs too (A/B checks of the merge tier)
+static bool snn_sort_bitonic() {
+    static const bool v = [] {
+        const char* e = getenv("CCG_SNN_SORT");
+        return e && strcmp(e, "bitonic") == 0;
+    }();
+    return v;
+}
+
 static int snn_spec(const int* ks, int nk, int type, int kstride, SnnSpec* sp) {
     CCG_REQUIRE(ks, "SNN: NULL ks");
     CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "SNN: 1 <= nk <= %d", SNN_MAXK);
@@ -1162,19 +1339,23 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     if (rc) return rc;
     snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
     int* ov_list = ov + 3 * n;
-#define SNN_BITONIC(CLS_, K_, GRID_)                                                                           \
-    snn_bitonic_build_kernel<CLS_, K_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                       \
+#define SNN_BITONIC(CLS_, K_, GRID_, MG_)                                                                      \
+    snn_bitonic_build_kernel<CLS_, K_, MG_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                  \
         knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
         ov_count + 1, src)
-#define SNN_BITONIC_ALL(K_)                                                       \
+#define SNN_BITONIC_ALL(K_, MG_)                                                  \
     do {                                                                          \
-        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)));             \
-        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)));             \
-        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)));             \
-        SNN_BITONIC(3, K_, 1024u);                                                 \
+        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), MG_);        \
+        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), MG_);        \
+        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), MG_);        \
+        SNN_BITONIC(3, K_, 1024u, false);                                          \
     } while (0)
-    if (sp.type == CCG_SNN_NUMBER) SNN_BITONIC_ALL(uint32_t);
-    else SNN_BITONIC_ALL(unsigned long long);
+    if (sp.type == CCG_SNN_NUMBER) {
+        if (snn_sort_bitonic()) SNN_BITONIC_ALL(uint32_t, false);
+        else SNN_BITONIC_ALL(uint32_t, true);  // the merge tier (sorted host runs)
+    } else {
+        SNN_BITONIC_ALL(unsigned long long, false);
+    }
 #undef SNN_BITONIC_ALL
 #undef SNN_BITONIC
     // nodes with more than SNN_BITONIC_MAX items: the block tier, then dense
