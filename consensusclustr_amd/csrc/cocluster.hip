@@ -68,9 +68,6 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 #define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
 #define COF_EMAX (4LL << 30)  // bytes of the entry matrix E of one column chunk
 #define COF_ENT_GRID 4096   // slot blocks (grid y) of the entry-matrix kernel
-#ifndef COF_EXP
-#define COF_EXP 0           // tools only: 1 = no epilogue stores
-#endif
 
 __device__ __forceinline__ int block_excl_scan1024(int v, int* sh, int* total) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -394,7 +391,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     }
     // ---- epilogue: acc = co + 16384 * both (+ the previous chunks' counts).
     const int64_t base = r0 * N - r0 * (r0 + 1) / 2;
-    if (MODE == COF_TRI && COF_EXP == 0 && co && both && !co_prev && !dist) {
+    if (MODE == COF_TRI && co && both && !co_prev && !dist) {
         // interior wave quarter (every column above every row, inside N and
         // the slab): one pointer per row and immediate column offsets, no
         // per-element masks or 64-bit offset arithmetic
@@ -418,7 +415,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             return;
         }
     }
-    if (MODE == COF_RECT && COF_EXP == 0 && !cb_prev) {
+    if (MODE == COF_RECT && !cb_prev) {
         // interior wave quarter of the full rows: one pointer per row, immediate column offsets
         const int64_t ia0 = rowA0 + wr * 64, jb0 = rowB0 + wc * 128;
         if (jb0 + 128 <= NB && ia0 + 64 <= r1) {
@@ -456,10 +453,6 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
                 const int a = acc[mi][ni][r];
                 int cv = a & 16383, bv = a >> 14;
                 if (MODE == COF_TRI) {
-#if COF_EXP == 1  // tools only: no epilogue stores (timing variant)
-                    asm volatile("" ::"v"(cv), "v"(bv), "v"(rb));
-                    continue;
-#endif
                     if (row_ok && gj < N && gj > gi) {
                         const int64_t o = rb + gj;
                         if (co_prev) {

@@ -26,9 +26,6 @@
 #include "ccg_internal.h"
 
 #define SIL_T 256
-#ifndef SIL_EXP
-#define SIL_EXP 0  // tools only: 1 = no width epilogue, 2 = no MFMA, 3 = no row widths (timing variants)
-#endif
 #ifndef SIL_LG
 #define SIL_LG 5
 #endif
@@ -643,19 +640,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
 #pragma unroll
                 for (int t = 0; t < RT; ++t) {
                     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#if SIL_EXP == 2
-                    acc[0] = a[0] * xb[t][0];
-                    acc[1] = a[1] * xb[t][1];
-                    acc[2] = a[2] * xb[t][2];
-                    acc[3] = a[3] * xb[t][3];
-#else
 #pragma unroll
                     for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], xb[t][s], acc, 0, 0, 0);
-#endif
-#if SIL_EXP == 1
-                    oth[t] = fmin(oth[t], (acc[0] + acc[1]) + (acc[2] + acc[3]));
-                    continue;
-#endif
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const double tv = fma(-2.0, acc[i], mv[i]);
@@ -690,13 +676,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         const int wt = (rep && iw) ? cnt[pw] - mult[(int64_t)l * mw + pw] : 1;
         long long wq = 0;
         unsigned wn = 0;
-#if SIL_EXP == 3
-        wq = (long long)ow + (long long)sw;
-        wn = iw;
-#else
         sil_row_width(sw, ow, iw, np, wsc,
                       (out_width && !rep) ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn, wt);
-#endif
         // integer reductions (order-independent): wave, then block; one
         // partial per (labeling, block) -- same-line global atomics from every
         // wave serialised at the L2
