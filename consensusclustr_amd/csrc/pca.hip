@@ -12,9 +12,11 @@
 //      relative residual below 1e-11 (irlba stops at 1e-5; this is the exact
 //      PCA up to rounding)
 //   5. scores x = Z V, sdev = sqrt(eigenvalues of C)
-// The small dense factorisations (p x p Cholesky and symmetric eigen, p <=
-// npc + 16) run on the host in plain C; everything of size genes or cells
-// runs on the GPU.  Signs: a component is oriented so that its
+// The small dense factorisations (p <= npc + 16): the Cholesky and
+// triangular inverse of every CholeskyQR step in one device block (no host
+// round trip per power step; the host C code for p > 88), the Rayleigh-Ritz
+// eigenproblem every 8 steps on the host in plain C; everything of size genes
+// or cells runs on the GPU.  Signs: a component is oriented so that its
 // largest-|loading| gene is positive (irlba's signs depend on its random
 // start vector, so parity on the scores is up to sign per component).
 #include <algorithm>
@@ -275,6 +277,51 @@ static std::vector<double> host_inv_upper_from_lower(const std::vector<double>& 
     return Ri;
 }
 
+// The same Cholesky and upper-factor inverse on the device, one 256-thread
+// block with L in LDS (p <= PCA_DEV_CHOL), so a CholeskyQR step needs no host
+// round trip: S (p x p, row-major) -> Ri = (L^T)^{-1} (row-major, upper).  A
+// non-positive pivot sets *flag (the subspace lost rank; the host reports it
+// at its next check) and the factor continues with pivot 1.
+#define PCA_DEV_CHOL 88
+__global__ __launch_bounds__(256) void pca_cholinv_kernel(const double* __restrict__ S, double* __restrict__ Ri, int p,
+                                                          int* __restrict__ flag) {
+    extern __shared__ double La[];  // [p][p]
+    for (int t = threadIdx.x; t < p * p; t += 256) La[t] = S[t];
+    __syncthreads();
+    for (int j = 0; j < p; ++j) {
+        __shared__ double d_s;
+        if (threadIdx.x == 0) {
+            double s = La[j * p + j];
+            for (int k = 0; k < j; ++k) s -= La[j * p + k] * La[j * p + k];
+            if (!(s > 0.0)) {
+                atomicOr(flag, 1);
+                s = 1.0;
+            }
+            d_s = sqrt(s);
+            La[j * p + j] = d_s;
+        }
+        __syncthreads();
+        const double d = d_s;
+        for (int i = j + 1 + threadIdx.x; i < p; i += 256) {
+            double t = La[i * p + j];
+            for (int k = 0; k < j; ++k) t -= La[i * p + k] * La[j * p + k];
+            La[i * p + j] = t / d;
+        }
+        __syncthreads();
+    }
+    // column j of R^{-1} (R = L^T upper) by back substitution, one thread per column
+    for (int j = threadIdx.x; j < p; j += 256) {
+        for (int i = 0; i < p; ++i)
+            if (i > j) Ri[i * p + j] = 0.0;
+        Ri[j * p + j] = 1.0 / La[j * p + j];
+        for (int i = j - 1; i >= 0; --i) {
+            double s = 0.0;
+            for (int k = i + 1; k <= j; ++k) s += La[k * p + i] * Ri[k * p + j];
+            Ri[i * p + j] = -s / La[i * p + i];
+        }
+    }
+}
+
 // Cyclic Jacobi eigen-decomposition of a symmetric p x p matrix (row-major):
 // eigenvalues in w, eigenvectors as the columns of Q.
 static void host_jacobi(std::vector<double> a, int p, std::vector<double>& w, std::vector<double>& Q) {
@@ -356,7 +403,7 @@ static int pca_from_z(ccg_ctx* ctx, const PcaWs& ws, int64_t nc, int ng, int npc
     double *Z = ws.Z, *C = ws.C, *V = ws.V, *W = ws.W, *T1 = ws.T1, *T2 = ws.T2, *S = ws.S, *S2 = ws.S2;
     int* flag = ws.flag;
     // per-gene mean and sample sd (two passes, deterministic slice order), standardise
-    CCG_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
+    CCG_HIP(hipMemsetAsync(flag, 0, 2 * sizeof(int), st));  // [0] zero variance, [1] lost rank (device Cholesky)
     const dim3 gs((unsigned)ccg_cdiv(ng, 256), PCA_SLICES);
     const unsigned gf = (unsigned)ccg_cdiv(ng, 256);
     pca_colstat_kernel<<<gs, 256, 0, st>>>(Z, nc, ng, ws.mean, 0, ws.part);
@@ -376,10 +423,16 @@ static int pca_from_z(ccg_ctx* ctx, const PcaWs& ws, int64_t nc, int ng, int npc
     int rc = pca_gemm(ng, ng, nc, Z, 1, ng, Z, ng, 1, C, ng, 1.0 / (double)(nc - 1), 0.0, st, true);
     if (rc) return rc;
     std::vector<double> hS(np), w, Q;
-    // one CholeskyQR step: S = src^T src = L L^T, dst = src L^{-T}
+    // one CholeskyQR step: S = src^T src = L L^T, dst = src L^{-T}; the small
+    // factorisation on the device (no host round trip) when p allows
+    const bool dev_chol = p <= PCA_DEV_CHOL;
     auto cholqr = [&](const double* src, double* dst) -> int {
         int r2 = pca_gemm(p, p, ng, src, 1, p, src, p, 1, S, p, 1.0, 0.0, st);
         if (r2) return r2;
+        if (dev_chol) {
+            pca_cholinv_kernel<<<1, 256, sizeof(double) * p * p, st>>>(S, S2, p, flag + 1);
+            return pca_gemm(ng, p, p, src, p, 1, S2, p, 1, dst, p, 1.0, 0.0, st);
+        }
         CCG_HIP(hipMemcpyAsync(hS.data(), S, sizeof(double) * np, hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
         if (!host_cholesky(hS, p)) {
@@ -411,7 +464,13 @@ static int pca_from_z(ccg_ctx* ctx, const PcaWs& ws, int64_t nc, int ng, int npc
         rc = pca_gemm(p, p, ng, V, 1, p, W, p, 1, S, p, 1.0, 0.0, st);
         if (rc) return rc;
         CCG_HIP(hipMemcpyAsync(hS.data(), S, sizeof(double) * np, hipMemcpyDeviceToHost, st));
+        int lost = 0;
+        if (dev_chol) CCG_HIP(hipMemcpyAsync(&lost, flag + 1, sizeof(int), hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
+        if (lost) {
+            ccg_set_error("ccg_pca: the iterated subspace lost rank (%d vectors, %d genes)", p, ng);
+            return CCG_EINVAL;
+        }
         for (int a = 0; a < p; ++a)
             for (int b = 0; b < a; ++b) hS[a * p + b] = hS[b * p + a] = 0.5 * (hS[a * p + b] + hS[b * p + a]);
         host_jacobi(hS, p, w, Q);
