@@ -1898,18 +1898,26 @@ __global__ __launch_bounds__(256) void kt_tau_kernel(int kq, int K, int d, const
                                                      const double* __restrict__ tab_d2, const double* __restrict__ urows,
                                                      const int* __restrict__ fail_list,
                                                      const int* __restrict__ fail_count, double* __restrict__ tau) {
-    __shared__ int srow_[4][64];
+    __shared__ int hset_[4][128];  // the cell's own table row as an open-addressing set (K <= 48 of 128 slots)
     __shared__ int pick_[4][64];
     __shared__ double val_[4][128];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int nf = *fail_count;
+    auto hslot = [](int x) { return (int)(((unsigned)x * 2654435761u) >> 25); };
     for (int f = blockIdx.x * 4 + wv; f < nf; f += gridDim.x * 4) {
         const int uid = fail_list[f];
         const int64_t c = scell[ustart[uid]];
         const int v = lane < K ? tab_idx[c * K + lane] : -1;
-        srow_[wv][lane] = v;
+        hset_[wv][lane] = -1;
+        hset_[wv][64 + lane] = -1;
         const int u1 = v >= 0 ? cell2u[v] : -1;
         const double val1 = u1 >= 0 ? tab_d2[c * K + lane] : INFINITY;
+        KT_SYNC();
+        if (v >= 0)
+            for (int h = hslot(v);; h = (h + 1) & 127) {
+                const int prev = atomicCAS(&hset_[wv][h], -1, v);
+                if (prev == -1 || prev == v) break;
+            }
         KT_SYNC();
         int w = -1;
         if (v >= 0) {
@@ -1917,7 +1925,14 @@ __global__ __launch_bounds__(256) void kt_tau_kernel(int kq, int K, int d, const
                 const int x = tab_idx[(int64_t)v * K + s];
                 if (x < 0 || x == (int)c || cell2u[x] < 0) continue;
                 bool in_row = false;
-                for (int t = 0; t < K; ++t) in_row |= srow_[wv][t] == x;
+                for (int h = hslot(x);; h = (h + 1) & 127) {
+                    const int y = hset_[wv][h];
+                    if (y == x) {
+                        in_row = true;
+                        break;
+                    }
+                    if (y == -1) break;
+                }
                 if (!in_row) w = x;
             }
         }
