@@ -4,8 +4,6 @@
 #include <stdio.h>
 #include <string.h>
 
-#include <algorithm>
-
 #include "ccg_internal.h"
 
 static thread_local char g_err[1024] = "";
@@ -235,36 +233,41 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64
     return woff + x - v;
 }
 
-// One-pass scan (decoupled look-back): every block takes the next tile id
-// from a ticket (so a tile's predecessors are always running or done),
-// publishes its tile sum, looks back over the predecessors' published sums
-// until one carries its inclusive prefix, publishes its own inclusive prefix
-// and writes its outputs.  One launch per scan instead of two.  A status word
-// holds (call sequence << 2 | state), state 1 = tile sum, 2 = inclusive
-// prefix, so no reset is needed between calls; the value is stored before
-// the word (release) and read after it (acquire).  The block that takes the
-// last id returns the ticket to 0 for the next call.
-struct ScanStatus {
-    unsigned* ticket;
-    unsigned* flag;
-    int64_t* aggr;
-    int64_t* incl;
-};
-
-__global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_t* out, int64_t n, int64_t nb,
-                                                       ScanStatus ss, unsigned seq) {
+__global__ __launch_bounds__(SCAN_T) void scan_tile_sums(const int64_t* __restrict__ in,
+                                                         int64_t n, int64_t* __restrict__ bsum) {
     __shared__ int64_t sh[SCAN_T / 64];
-    __shared__ int64_t sh_pre;
-    __shared__ unsigned sh_tile;
-    if (threadIdx.x == 0) {
-        const unsigned t = atomicAdd(ss.ticket, 1u);
-        if (t == (unsigned)nb - 1) __hip_atomic_store(ss.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh_tile = t;
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    int64_t s = 0;
+#pragma unroll
+    for (int e = 0; e < SCAN_TILE / SCAN_T; ++e) {
+        int64_t i = base + threadIdx.x * (SCAN_TILE / SCAN_T) + e;
+        if (i < n) s += in[i];
     }
-    __syncthreads();
-    const int64_t tile = sh_tile;
+    int64_t tot;
+    block_excl_scan(s, sh, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_block_sums(int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
+        int64_t i = b0 + threadIdx.x;
+        int64_t v = i < nb ? bsum[i] : 0;
+        int64_t tot;
+        int64_t ex = block_excl_scan(v, sh, &tot);
+        if (i < nb) bsum[i] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tiles(const int64_t* in, int64_t* out, int64_t n,
+                                                     const int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
     constexpr int E = SCAN_TILE / SCAN_T;
-    const int64_t base = tile * SCAN_TILE + threadIdx.x * E;
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * E;
     int64_t v[E];
     int64_t s = 0;
 #pragma unroll
@@ -273,41 +276,43 @@ __global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_
         s += v[e];
     }
     int64_t tot;
-    const int64_t ex = block_excl_scan(s, sh, &tot);
-    if (threadIdx.x == 0) {
-        int64_t pre = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&ss.incl[0], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ss.flag[0], (seq << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&ss.aggr[tile], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ss.flag[tile], (seq << 2) | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t p = tile - 1; p >= 0;) {
-                const unsigned f = __hip_atomic_load(&ss.flag[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if ((f >> 2) != seq) {  // not published yet in this call
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                if ((f & 3u) == 2u) {
-                    pre += __hip_atomic_load(&ss.incl[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                pre += __hip_atomic_load(&ss.aggr[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                --p;
-            }
-            __hip_atomic_store(&ss.incl[tile], pre + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ss.flag[tile], (seq << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        sh_pre = pre;
-    }
-    __syncthreads();
-    int64_t x = ex + sh_pre;
+    int64_t ex = block_excl_scan(s, sh, &tot) + bsum[blockIdx.x];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        if (base + e < n) out[base + e] = x;
-        x += v[e];
+        if (base + e < n) out[base + e] = ex;
+        ex += v[e];
     }
-    if (tile == nb - 1 && threadIdx.x == 0) out[n] = sh_pre + tot;
+    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = bsum[nb];
+}
+
+// Second pass for up to SCAN_DIRECT_MAX tiles: each block adds up the raw
+// sums of the tiles before it itself (<= 1024 loads), so the single-block
+// pass over the tile sums -- a launch on the critical path -- is skipped.
+#define SCAN_DIRECT_MAX 1024
+__global__ __launch_bounds__(SCAN_T) void scan_tiles_direct(const int64_t* in, int64_t* out, int64_t n,
+                                                            const int64_t* __restrict__ bsum, int64_t nb) {
+    __shared__ int64_t sh[SCAN_T / 64];
+    constexpr int E = SCAN_TILE / SCAN_T;
+    int64_t pre = 0;
+    for (int64_t b = threadIdx.x; b < blockIdx.x; b += SCAN_T) pre += bsum[b];
+    int64_t prefix;
+    block_excl_scan(pre, sh, &prefix);
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * E;
+    int64_t v[E];
+    int64_t s = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        v[e] = (base + e < n) ? in[base + e] : 0;
+        s += v[e];
+    }
+    int64_t tot;
+    int64_t ex = block_excl_scan(s, sh, &tot) + prefix;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (base + e < n) out[base + e] = ex;
+        ex += v[e];
+    }
+    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = prefix + tot;
 }
 
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
@@ -315,21 +320,17 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipSt
         CCG_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), st));
         return CCG_OK;
     }
-    const int64_t nb = ccg_cdiv(n, SCAN_TILE);
-    // status of up to max(nb, 2^16) tiles: ticket, flags, tile sums, inclusive prefixes
-    const int64_t cap = std::max<int64_t>(nb, 1 << 16);
-    const size_t fb = (size_t)ccg_cdiv(sizeof(unsigned) * (cap + 4), 16) * 16;
-    char* ws = (char*)ccg_ws(ctx, WS_SCAN, fb + 2 * sizeof(int64_t) * (size_t)cap);
-    if (!ws) return CCG_ENOMEM;
-    if (ctx->scan_zeroed != (void*)ws || ctx->scan_cap < cap) {  // fresh buffer: ticket and flags zero
-        CCG_HIP(hipMemsetAsync(ws, 0, fb, st));
-        ctx->scan_zeroed = (void*)ws;
-        ctx->scan_cap = (ctx->ws_bytes[WS_SCAN] - fb) / (2 * sizeof(int64_t));
-        ctx->scan_seq = 0;
+    int64_t nb = ccg_cdiv(n, SCAN_TILE);
+    int64_t* bsum = (int64_t*)ccg_ws(ctx, WS_SCAN, sizeof(int64_t) * (nb + 1));
+    if (!bsum) return CCG_ENOMEM;
+    scan_tile_sums<<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
+    if (nb <= SCAN_DIRECT_MAX) {
+        scan_tiles_direct<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
+        CCG_HIP(hipGetLastError());
+        return CCG_OK;
     }
-    ctx->scan_seq = (ctx->scan_seq % 0x3FFFFFFFu) + 1;  // 30-bit call sequence, never 0
-    ScanStatus ss{(unsigned*)ws, (unsigned*)ws + 4, (int64_t*)(ws + fb), (int64_t*)(ws + fb) + cap};
-    scan_onepass<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, nb, ss, ctx->scan_seq);
+    scan_block_sums<<<1, SCAN_T, 0, st>>>(bsum, nb);
+    scan_tiles<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }

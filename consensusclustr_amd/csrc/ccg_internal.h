@@ -57,7 +57,6 @@ enum ccg_ws_slot {
     WS_TAB,          // kNN cell table of a host call (ccg_knn_boot): ids then squared distances
     WS_FX_A,         // kNN exact search of failed rows: radii, candidate counts, overflow list
     WS_FX_B,         // kNN exact search of failed rows: candidate (d2, row) buffers
-    WS_FX_C,         // kNN exact search of failed rows: the references' fp32 image and fp64 norms
     WS_SEG_ROWS,     // batched bootstrap segments: the gathered rows of every segment
     WS_SEG_TAB,      // batched bootstrap segments: row and distinct-cell segment offsets
     WS_NSLOTS
@@ -85,9 +84,6 @@ struct ccg_ctx {
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
     void* fx_zeroed;  // kNN radius search: the WS_FX_A buffer whose counters were zeroed at allocation
-    void* scan_zeroed;  // one-pass scan: the WS_SCAN buffer whose ticket and flags were zeroed
-    int64_t scan_cap;   // tiles its status arrays hold
-    unsigned scan_seq;  // call sequence stamped into the status words
     // kNN: the exact-search row list of the last call and its count (device; ccg_knn_last_fallback)
     const int* last_fail_list;
     const int* last_fail_count;

@@ -1149,73 +1149,70 @@ __device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
 // plain scan's.  (The exact form costs three fp64 operations per dimension;
 // the filter one packed fp32 FMA per two.)
 //
-// The references' fp32 image and fp64 norms are made once per call
-// (knn_fx_prep_kernel, skipped when no row failed; a failed row's own image
-// row is its query).  The scan gives each wave 64 references, one per lane,
-// held in registers, and walks a group of 64 failed rows at wave-uniform
-// addresses (scalar loads, served from the scalar cache to every wave of the
-// group): per (row, reference) pair one packed fp32 FMA per two dimensions,
-// no LDS staging and no barriers.
+// A block takes 64 failed rows (a group) and 256 references, one per lane
+// of its 4 waves, held in registers as fp32 pairs with their fp64 norms
+// (converted on the fly from the fp64 rows).  The group's rows are staged once
+// in LDS as fp32 with their norms and radii; every wave then walks them at
+// wave-uniform LDS addresses (broadcast reads): per (row, reference) pair one
+// packed fp32 FMA per two dimensions.  An empty failed list exits at once.
 #define KNN_FX_QG 64  // failed rows per group
 template <int DMAX>
-__global__ __launch_bounds__(256) void knn_fx_prep_kernel(const double* __restrict__ rows, int n, int d,
-                                                          const int* __restrict__ fail_count,
-                                                          float* __restrict__ ref32, double* __restrict__ nrm) {
-    if (*fail_count == 0) return;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    float v[DMAX];
-    double ny = 0.0;
-#pragma unroll
-    for (int k = 0; k < DMAX; ++k) {
-        const double y = k < d ? rows[j * d + k] : 0.0;
-        ny = fma(y, y, ny);
-        v[k] = (float)y;
-    }
-    float4* o = reinterpret_cast<float4*>(ref32 + j * DMAX);
-#pragma unroll
-    for (int k4 = 0; k4 < DMAX / 4; ++k4) o[k4] = make_float4(v[4 * k4], v[4 * k4 + 1], v[4 * k4 + 2], v[4 * k4 + 3]);
-    nrm[j] = ny;
-}
-
-template <int DMAX>
-__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, const float* __restrict__ ref32,
-                                                          const double* __restrict__ nrm, int n, int d,
+__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, int n, int d,
                                                           const int* __restrict__ fail_list,
                                                           const int* __restrict__ fail_count,
                                                           const double* __restrict__ fail_tau, int* __restrict__ cnt,
                                                           double* __restrict__ bd, int* __restrict__ bi,
                                                           int* __restrict__ ovf_count) {
     typedef float f2 __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) float sx[KNN_FX_QG][DMAX];
+    __shared__ double snx[KNN_FX_QG], stau[KNN_FX_QG];
+    __shared__ int sq[KNN_FX_QG];
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
     const int nf = min(*fail_count, KNN_FX_ROWS);
     const int ng = (nf + KNN_FX_QG - 1) / KNN_FX_QG;
-    const int nrw = (n + 63) / 64;
-    const int lane = threadIdx.x & 63;
-    const int nw = gridDim.x * 4;
-    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
-    for (int64_t w = w0; w < (int64_t)ng * nrw; w += nw) {
-        const int g = (int)(w / nrw), r = (int)(w - (int64_t)g * nrw);
-        const int j = r * 64 + lane;
+    const int nrb = (n + 255) / 256;
+    for (int64_t u = blockIdx.x; u < (int64_t)ng * nrb; u += gridDim.x) {
+        const int g = (int)(u / nrb), r = (int)(u - (int64_t)g * nrb);
+        const int f0 = g * KNN_FX_QG, nq = min(KNN_FX_QG, nf - f0);
+        __syncthreads();  // the previous unit's reads of the stage are done
+        for (int e = threadIdx.x; e < KNN_FX_QG * DMAX; e += 256) {
+            const int i = e / DMAX, k = e - i * DMAX;
+            float v = 0.f;
+            if (i < nq && k < d) v = (float)rows[(int64_t)fail_list[f0 + i] * d + k];
+            sx[i][k] = v;
+        }
+        if (threadIdx.x < KNN_FX_QG) {
+            const int i = threadIdx.x;
+            double nx = 0.0, t = -1.0;
+            int q = -1;
+            if (i < nq) {
+                q = fail_list[f0 + i];
+                t = fail_tau[f0 + i];
+                if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
+                for (int k = 0; k < DMAX; ++k) {
+                    const double y = k < d ? rows[(int64_t)q * d + k] : 0.0;
+                    nx = fma(y, y, nx);
+                }
+            }
+            snx[i] = nx;
+            stau[i] = t;
+            sq[i] = q;
+        }
+        __syncthreads();
+        const int j = r * 256 + threadIdx.x;
         const int jc = j < n ? j : n - 1;
         f2 yf[DMAX / 2];
-        {
-            const float4* yp = reinterpret_cast<const float4*>(ref32 + (int64_t)jc * DMAX);
+        double ny = 0.0;
 #pragma unroll
-            for (int k4 = 0; k4 < DMAX / 4; ++k4) {
-                const float4 y = yp[k4];
-                yf[2 * k4] = f2{y.x, y.y};
-                yf[2 * k4 + 1] = f2{y.z, y.w};
-            }
+        for (int k2 = 0; k2 < DMAX / 2; ++k2) {
+            const double y0 = 2 * k2 < d ? rows[(int64_t)jc * d + 2 * k2] : 0.0;
+            const double y1 = 2 * k2 + 1 < d ? rows[(int64_t)jc * d + 2 * k2 + 1] : 0.0;
+            ny = fma(y0, y0, ny);
+            ny = fma(y1, y1, ny);
+            yf[k2] = f2{(float)y0, (float)y1};
         }
-        const double ny = nrm[jc];
-        const int f1 = __builtin_amdgcn_readfirstlane(min(nf, (g + 1) * KNN_FX_QG));
-        for (int f = g * KNN_FX_QG; f < f1; ++f) {  // wave-uniform
-            const double t = fail_tau[f];
-            if (!(t < INFINITY)) continue;  // no radius: the per-thread-list kernels
-            const int q = __builtin_amdgcn_readfirstlane(fail_list[f]);
-            const double nx = nrm[q];
-            const float4* xp = reinterpret_cast<const float4*>(ref32 + (int64_t)q * DMAX);
+        for (int i = 0; i < nq; ++i) {  // block-uniform
+            const float4* xp = reinterpret_cast<const float4*>(&sx[i][0]);
             f2 acc = {0.f, 0.f};
 #pragma unroll
             for (int k4 = 0; k4 < DMAX / 4; ++k4) {
@@ -1223,17 +1220,19 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                 acc = __builtin_elementwise_fma(f2{x.x, x.y}, yf[2 * k4], acc);
                 acc = __builtin_elementwise_fma(f2{x.z, x.w}, yf[2 * k4 + 1], acc);
             }
+            const double nx = snx[i], t = stau[i];
             const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
+            const int q = sq[i];
             if (j < n && j != q && approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60) {
                 double xq[DMAX];
 #pragma unroll
                 for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
                 const double v = knn_exact_d2<DMAX>(xq, rows + (int64_t)j * d, d);
                 if (v <= t) {
-                    const int slot = atomicAdd(&cnt[f], 1);
+                    const int slot = atomicAdd(&cnt[f0 + i], 1);
                     if (slot < KNN_FX_CAP) {
-                        bd[(int64_t)f * KNN_FX_CAP + slot] = v;
-                        bi[(int64_t)f * KNN_FX_CAP + slot] = j;
+                        bd[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = v;
+                        bi[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = j;
                     }
                 }
             }
@@ -1304,17 +1303,9 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         int* ovf_list = ovf_count + 64;
         double* bd = (double*)buf;
         int* bi = (int*)(bd + (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-        char* img32 = (char*)ccg_ws(ctx, WS_FX_C, (sizeof(float) * 64 + sizeof(double)) * (size_t)n + 64);
-        if (!img32) return CCG_ENOMEM;
-        double* nrm = (double*)img32;
-        float* ref32 = (float*)(nrm + n);
 #define CCG_FX(DM_)                                                                                              \
-    do {                                                                                                         \
-        knn_fx_prep_kernel<DM_><<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(rows, (int)n, d, fail_count, ref32,  \
-                                                                             nrm);                                \
-        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, ref32, nrm, (int)n, d, fail_list, fail_count,  \
-                                                             fail_tau, cnt, bd, bi, ovf_count);                   \
-    } while (0)
+    knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, bd, bi, \
+                                                         ovf_count)
         if (d <= 16) CCG_FX(16);
         else if (d <= 32) CCG_FX(32);
         else CCG_FX(64);

@@ -692,7 +692,10 @@ __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, cons
 // 2)) levels of merge path: each lane emits ceil(M / 64) consecutive outputs of
 // a level after a binary search for its start on the merge diagonal.  Work per
 // level is O(M), not O(64 E log^2).  The sorted keys then go through the same
-// combine / row write as the bitonic tier.
+// combine / row write as the bitonic tier.  Measured slower than the bitonic
+// tier on MI355X (cfg3: classes 0/1/2 136/251/249 against 97/170/156 us per
+// bootstrap): each merge step is a dependent LDS read per lane, while the
+// register network is pure VALU issue.  Kept behind CCG_SNN_SORT=merge.
 template <int E>
 struct SnnMergeLds {
     int4 mem[64];
@@ -1257,11 +1260,13 @@ static bool snn_no_copy() {
     return v;
 }
 
-// CCG_SNN_SORT=bitonic: the full bitonic tier for NUMBER graphs too (A/B checks of the merge tier)
+// CCG_SNN_SORT=merge: the merge tier for NUMBER graphs (bit-identical rows;
+// measured slower than the bitonic tier at cfg3: 1.01 against 0.81 ms per
+// bootstrap for the SNN stage, so the bitonic tier is the default)
 static bool snn_sort_bitonic() {
     static const bool v = [] {
         const char* e = getenv("CCG_SNN_SORT");
-        return e && strcmp(e, "bitonic") == 0;
+        return !(e && strcmp(e, "merge") == 0);
     }();
     return v;
 }
@@ -1352,7 +1357,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     } while (0)
     if (sp.type == CCG_SNN_NUMBER) {
         if (snn_sort_bitonic()) SNN_BITONIC_ALL(uint32_t, false);
-        else SNN_BITONIC_ALL(uint32_t, true);  // the merge tier (sorted host runs)
+        else SNN_BITONIC_ALL(uint32_t, true);  // the merge tier (sorted host runs; CCG_SNN_SORT=merge)
     } else {
         SNN_BITONIC_ALL(unsigned long long, false);
     }
