@@ -1161,8 +1161,7 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                                                           const int* __restrict__ fail_list,
                                                           const int* __restrict__ fail_count,
                                                           const double* __restrict__ fail_tau, int* __restrict__ cnt,
-                                                          double* __restrict__ bd, int* __restrict__ bi,
-                                                          int* __restrict__ ovf_count) {
+                                                          int* __restrict__ bi, int* __restrict__ ovf_count) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     __shared__ __attribute__((aligned(16))) float sx[KNN_FX_QG][DMAX];
     __shared__ double snx[KNN_FX_QG], stau[KNN_FX_QG];
@@ -1222,52 +1221,75 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
             }
             const double nx = snx[i], t = stau[i];
             const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
-            const int q = sq[i];
-            if (j < n && j != q && approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60) {
-                double xq[DMAX];
-#pragma unroll
-                for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
-                const double v = knn_exact_d2<DMAX>(xq, rows + (int64_t)j * d, d);
-                if (v <= t) {
-                    const int slot = atomicAdd(&cnt[f0 + i], 1);
-                    if (slot < KNN_FX_CAP) {
-                        bd[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = v;
-                        bi[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = j;
-                    }
-                }
+            // a pair within radius + margin joins the row's candidates; its
+            // exact distance is taken in knn_fx_select_kernel (no fp64 row
+            // loads inside this loop: they stall the whole wave for one lane)
+            if (j < n && j != sq[i] && approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60) {
+                const int slot = atomicAdd(&cnt[f0 + i], 1);
+                if (slot < KNN_FX_CAP) bi[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = j;
             }
         }
     }
 }
 
-__global__ __launch_bounds__(256) void knn_fx_select_kernel(int kmax, const int* __restrict__ fail_list,
+// One block per failed row: the exact fp64 d2 (the contract's arithmetic)
+// of every candidate, those within the radius bitonic-sorted by (d2, row)
+// in LDS, the first kmax written.
+template <int DMAX>
+__global__ __launch_bounds__(256) void knn_fx_select_kernel(const double* __restrict__ rows, int d, int kmax,
+                                                            const int* __restrict__ fail_list,
                                                             const int* __restrict__ fail_count,
                                                             const double* __restrict__ fail_tau,
-                                                            int* __restrict__ cnt, const double* __restrict__ bd,
-                                                            const int* __restrict__ bi, int32_t* __restrict__ out_idx,
+                                                            int* __restrict__ cnt, const int* __restrict__ bi,
+                                                            int32_t* __restrict__ out_idx,
                                                             double* __restrict__ out_dist, bool dist_sq,
                                                             int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
     __shared__ double kd[KNN_FX_CAP];
     __shared__ int ki[KNN_FX_CAP];
+    __shared__ int nin;
     const int nf = *fail_count;
     for (int f = blockIdx.x; f < nf; f += gridDim.x) {
         const int q = fail_list[f];
         int c = KNN_FX_CAP + 1;
+        double t = INFINITY;
         if (f < KNN_FX_ROWS) {
             c = cnt[f];
-            if (!(fail_tau[f] < INFINITY)) c = KNN_FX_CAP + 1;
+            t = fail_tau[f];
+            if (!(t < INFINITY)) c = KNN_FX_CAP + 1;
         }
         __syncthreads();
         if (f < KNN_FX_ROWS && threadIdx.x == 0) cnt[f] = 0;  // zero for the next call
+        if (threadIdx.x == 0) nin = 0;
+        __syncthreads();
         if (c > KNN_FX_CAP || c < kmax) {  // the per-thread-list kernels take it
             if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
             continue;
         }
+        double xq[DMAX];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
         int m = 1;
         while (m < c) m <<= 1;
         for (int s = threadIdx.x; s < m; s += blockDim.x) {
-            kd[s] = s < c ? bd[(int64_t)f * KNN_FX_CAP + s] : INFINITY;
-            ki[s] = s < c ? bi[(int64_t)f * KNN_FX_CAP + s] : 0x7fffffff;
+            double v = INFINITY;
+            int j = 0x7fffffff;
+            if (s < c) {
+                const int jj = bi[(int64_t)f * KNN_FX_CAP + s];
+                const double e = knn_exact_d2<DMAX>(xq, rows + (int64_t)jj * d, d);
+                if (e <= t) {
+                    v = e;
+                    j = jj;
+                    atomicAdd(&nin, 1);
+                }
+            }
+            kd[s] = v;
+            ki[s] = j;
+        }
+        __syncthreads();
+        if (nin < kmax) {  // (cannot happen: tau bounds kmax exact distances) the per-thread-list kernels
+            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
+            __syncthreads();
+            continue;
         }
         knn_lds_bitonic(kd, ki, m);
         for (int r = threadIdx.x; r < kmax; r += blockDim.x) {
@@ -1293,25 +1315,25 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
     if (!seg_off && fail_tau) {
         // the radius search; its leftovers (overflow) continue below
         int* cnt = (int*)ccg_ws(ctx, WS_FX_A, sizeof(int) * (KNN_FX_ROWS + 64 + n));
-        char* buf = (char*)ccg_ws(ctx, WS_FX_B, (sizeof(double) + sizeof(int)) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-        if (!cnt || !buf) return CCG_ENOMEM;
+        int* bi = (int*)ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
+        if (!cnt || !bi) return CCG_ENOMEM;
         if (ctx->fx_zeroed != (void*)cnt) {  // fresh buffer: the select kernel keeps the counters zero afterwards
             CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * KNN_FX_ROWS, st));
             ctx->fx_zeroed = (void*)cnt;
         }
         int* ovf_count = cnt + KNN_FX_ROWS;
         int* ovf_list = ovf_count + 64;
-        double* bd = (double*)buf;
-        int* bi = (int*)(bd + (size_t)KNN_FX_ROWS * KNN_FX_CAP);
 #define CCG_FX(DM_)                                                                                              \
-    knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, bd, bi, \
-                                                         ovf_count)
+    do {                                                                                                         \
+        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, \
+                                                             bi, ovf_count);                                      \
+        knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, fail_list, fail_count, fail_tau, cnt, bi,     \
+                                                       out_idx, out_dist, dist_sq, ovf_list, ovf_count);          \
+    } while (0)
         if (d <= 16) CCG_FX(16);
         else if (d <= 32) CCG_FX(32);
         else CCG_FX(64);
 #undef CCG_FX
-        knn_fx_select_kernel<<<256, 256, 0, st>>>(kmax, fail_list, fail_count, fail_tau, cnt, bd, bi, out_idx,
-                                                          out_dist, dist_sq, ovf_list, ovf_count);
         fail_list = ovf_list;
         fail_count = ovf_count;
     }
