@@ -40,24 +40,27 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 }
 
 // ------------------------------------------------- fused one-hot path --
-// co and both in ONE int32 accumulator: every column b gets a K range of
-// S_b = ceil((C_b + 1) / 16) 16-position slots; position 0 holds the
-// "sampled" flag as int8 -128 on both sides (product 16384), positions
-// 1..C_b the one-hot label (product 1), so
+// co and both in ONE int32 accumulator.  The K dimension is cut into 8-byte
+// halves: column b owns H_b = ceil((C_b + 1) / 8) consecutive halves; its
+// first half holds the "sampled" flag as int8 -128 in byte 0 (product 16384
+// on both sides) and labels 1..7 in bytes 1..7, half s >= 1 labels 8s..8s+7
+// (product 1), so
 //     acc = co + 16384 * both      (co <= B_chunk <= 16383, so the fields split)
-// and K = 16 * sum_b S_b instead of sum_b C_b + B separate positions.
+// and K = 8 * sum_b H_b instead of sum_b C_b + B separate positions (C = 37:
+// 40 positions for 38 -- 16-byte granularity took 48).
 // Wider matrices (granular mode, B up to 65535) run in column chunks of at
 // most 16383 whose counts are added in the epilogue of the next chunk.
-// A lane gets its 16-byte MFMA fragment for slot (b, s) from a 33-entry LDS
-// pattern table (at most two non-zero bytes), so the one-hot matrix never
-// exists -- not in HBM, not in LDS.  The table index of every (slot, row)
-// is one byte, computed once per chunk by cof_entries_kernel into the entry
-// matrix E (slots x rows, 1/16 of the one-hot bytes; the same bytes per
-// slot as a uint8 label column).  The GEMM stages E per block of COF_SLOTS
-// slots x 384 rows (128 A-rows + 256 B-rows) in LDS, double-buffered
-// through registers, so its inner loop is two LDS reads and one shift per
-// fragment: no per-slot descriptor, label offset or clamp.  Columns with no
-// label (never sampled) own no slot.
+// A 16-byte MFMA fragment (one slot = two halves, possibly of two columns)
+// comes from an LDS pattern table: a half's state is one of 9 (zero, or the
+// one-hot byte / flag pattern), a slot's entry sigma_lo + 9 sigma_hi (< 81),
+// and the slot's type (which of its halves is a first half) picks one of
+// four 81-entry tables -- the types of a stage's 32 slots are one 64-bit
+// word.  So the one-hot matrix never exists -- not in HBM, not in LDS.  The
+// entry of every (slot, row) is one byte, computed once per chunk by
+// cof_entries_kernel into the entry matrix E (slots x rows).  The GEMM stages
+// E per block of COF_SLOTS slots x 384 rows (128 A-rows + 256 B-rows) in LDS,
+// double-buffered through registers, so its inner loop is two LDS reads per
+// fragment.  Columns with no label (never sampled) own no half.
 #define COF_BM 128          // output rows per block (2 waves x 64)
 #define COF_BN 256          // output cols per block (2 waves x 128)
 #ifndef COF_SLOTS
@@ -65,7 +68,7 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 #endif
 #define COF_ROWS (COF_BM + COF_BN)
 #define COF_CHUNK 16383     // columns per accumulation chunk
-#define COF_SB 13           // desc = column << COF_SB | slot-in-column (slot < 4097)
+#define COF_SB 14           // desc = column << COF_SB | half-in-column (half < 8193)
 #define COF_EMAX (4LL << 30)  // bytes of the entry matrix E of one column chunk
 #define COF_ENT_GRID 4096   // slot blocks (grid y) of the entry-matrix kernel
 
@@ -88,20 +91,23 @@ __device__ __forceinline__ int block_excl_scan1024(int v, int* sh, int* total) {
     return woff + x - v;
 }
 
-// Slot tables of one chunk of Bc columns (colC = the chunk's column maxima):
-// ccol[c] = chunk column of the c-th non-empty column; desc[k] = c << COF_SB
-// | s for k < K (K padded to a multiple of COF_SLOTS with -1); *nslot = the
-// padded K.
+// Half tables of one chunk of Bc columns (colC = the chunk's column maxima):
+// ccol[c] = chunk column of the c-th non-empty column; desc[h] = c << COF_SB
+// | s for the halves h < Kh (padded with -1 to 2 * nslot); *nslot = the slots
+// ceil(Kh / 2) padded to a multiple of COF_SLOTS; tmask[st] = the types of
+// stage st's slots, 2 bits per slot (bit 0: its low half is a column's first
+// half, bit 1: its high half).
 __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__ colC, int64_t Bc,
                                                          int* __restrict__ ccol, int* __restrict__ nslot,
-                                                         int* __restrict__ desc) {
+                                                         int* __restrict__ desc,
+                                                         unsigned long long* __restrict__ tmask) {
     __shared__ int sh[16];
     const int t = threadIdx.x;
     int kcar = 0, ccar = 0;
     for (int64_t b0 = 0; b0 < Bc; b0 += 1024) {
         const int64_t b = b0 + t;
         const int C = b < Bc ? colC[b] : 0;
-        const int v = C > 0 ? (C + 16) / 16 : 0;  // ceil((C + 1) / 16)
+        const int v = C > 0 ? (C + 8) / 8 : 0;  // ceil((C + 1) / 8)
         int ktot, ctot;
         const int koff = kcar + block_excl_scan1024(v, sh, &ktot);
         const int coff = ccar + block_excl_scan1024(C > 0 ? 1 : 0, sh, &ctot);
@@ -112,45 +118,63 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
         kcar += ktot;
         ccar += ctot;
     }
-    const int K = kcar;
-    const int Kp = (K + COF_SLOTS - 1) / COF_SLOTS * COF_SLOTS;
+    const int Kh = kcar;
+    const int Kp = ((Kh + 1) / 2 + COF_SLOTS - 1) / COF_SLOTS * COF_SLOTS;
     if (t == 0) *nslot = Kp;
-    for (int k = K + t; k < Kp; k += 1024) desc[k] = -1;
+    for (int k = Kh + t; k < 2 * Kp; k += 1024) desc[k] = -1;
+    __syncthreads();  // the block's desc writes are visible to the block
+    for (int st = t; st < Kp / COF_SLOTS; st += 1024) {
+        unsigned long long m = 0;
+        for (int j = 0; j < 2 * COF_SLOTS; ++j) {
+            const int d = desc[2 * COF_SLOTS * st + j];
+            if (d >= 0 && (d & ((1 << COF_SB) - 1)) == 0) m |= 1ull << j;
+        }
+        tmask[st] = m;
+    }
 }
 
-// Fragment table (LDS, 33 x 16 B): entry 0 = zero (label outside the slot,
-// or not sampled); 1 + x = one-hot byte x (x = 0..15, slots sub >= 1: label
-// 16 sub + x); 17 = the flag only (slot 0, label >= 16); 17 + lab = flag +
-// one-hot byte lab (slot 0, lab = 1..15).  The flag is int8 -128 in byte 0.
-// A wave's 16-byte reads spread over 16 bank groups (256 B); the common
-// vectors (zero, flag only, the one-hot bytes) sit in distinct groups.
-#define COF_TAB 33
+// Fragment table (LDS, 4 x 81 x 16 B): entry type * 81 + sigma_lo + 9 sigma_hi.
+// Half state sigma: 0 = zero (not sampled, or the label outside the half);
+// normal half 1 + x = one-hot byte x (label 8s + x); first half 1 = the flag
+// only (label >= 8), 1 + x = flag + one-hot byte x (label x = 1..7).  The flag
+// is int8 -128 in byte 0.  The zero entries of the four types sit in distinct
+// 16-byte bank groups.
+#define COF_TAB (4 * 81)
+
+__device__ __forceinline__ int cof_sigma(int d, int lab) {
+    if (d < 0 || lab == 0) return 0;
+    const int s = d & ((1 << COF_SB) - 1);
+    if (s == 0) return lab < 8 ? 1 + lab : 1;
+    const int x = lab - 8 * s;
+    return (unsigned)x < 8u ? 1 + x : 0;
+}
 
 // Entry matrix of one chunk: E[k * Npad + i] = the table entry of row i in
-// slot k (desc[k] = column c << COF_SB | sub; -1 = padding slot: entry 0),
-// entry 0 for rows i >= N.  Slots stride over grid y, row dwords (4 rows per
-// thread) over grid x: no per-element division.
+// slot k (halves 2k, 2k + 1; -1 = padding: state 0), entry 0 for rows i >= N.
+// Slots stride over grid y, row dwords (4 rows per thread) over grid x: no
+// per-element division.
 template <typename T>
 __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ A, int64_t N, int64_t Npad,
                                                           const int* __restrict__ desc, const int* __restrict__ ccol,
                                                           const int* __restrict__ nslot_p, uint8_t* __restrict__ E) {
     const int nslot = *nslot_p;
     for (int k = blockIdx.y; k < nslot; k += gridDim.y) {
-        const int d = desc[k];
-        const int sub = d < 0 ? 0 : d & ((1 << COF_SB) - 1);
-        const T* col = A + (d < 0 ? 0 : (int64_t)ccol[d >> COF_SB] * N);
+        const int dl = desc[2 * k], dh = desc[2 * k + 1];
+        const T* cl = A + (dl < 0 ? 0 : (int64_t)ccol[dl >> COF_SB] * N);
+        const T* chh = A + (dh < 0 ? 0 : (int64_t)ccol[dh >> COF_SB] * N);
         uint8_t* Ek = E + (int64_t)k * Npad;
         for (int64_t r4 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); r4 < Npad;
              r4 += 4 * (int64_t)gridDim.x * blockDim.x) {
             unsigned out = 0;
-            if (d >= 0) {
+            if (dl >= 0) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (r4 + e >= N) continue;
-                    const int lab = (int)col[r4 + e];
-                    const int x = lab - 16 * sub;
-                    const int en =
-                        sub == 0 ? (lab == 0 ? 0 : (lab < 16 ? 17 + lab : 17)) : ((unsigned)x < 16u ? 1 + x : 0);
+#ifdef COF_HALFTAB
+                    const int en = cof_sigma(dl, (int)cl[r4 + e]) | (cof_sigma(dh, (int)chh[r4 + e]) << 4);
+#else
+                    const int en = cof_sigma(dl, (int)cl[r4 + e]) + 9 * cof_sigma(dh, (int)chh[r4 + e]);
+#endif
                     out |= (unsigned)en << (8 * e);
                 }
             }
@@ -265,12 +289,17 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     const uint8_t* __restrict__ E, int64_t Npad, int64_t N, int64_t r0, int64_t r1, int64_t TC, int64_t I0,
-    const int* __restrict__ nslot_p, const uint16_t* co_prev, const uint16_t* both_prev, uint16_t* co, uint16_t* both,
-    double* __restrict__ dist, const uint32_t* cb_prev, uint32_t* cb, int64_t NB, CofCand cc) {
+    const int* __restrict__ nslot_p, const unsigned long long* __restrict__ tmask, const uint16_t* co_prev,
+    const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* __restrict__ dist, const uint32_t* cb_prev,
+    uint32_t* cb, int64_t NB, CofCand cc) {
     constexpr int ROWD = COF_ROWS / 4;                  // dwords per staged slot
     constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
     __shared__ __attribute__((aligned(16))) uint8_t panel[2][COF_SLOTS][COF_ROWS];
+#ifdef COF_HALFTAB
+    __shared__ __attribute__((aligned(16))) uint2 htab[18];  // [first][sigma]: one 144-byte span, no bank conflicts
+#else
     __shared__ __attribute__((aligned(16))) v4i ftab[COF_TAB];
+#endif
     const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     int64_t I, J;
@@ -324,18 +353,31 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
     };
-    if (tid < COF_TAB) {
-        v4i e = {0, 0, 0, 0};
-        if (tid >= 1 && tid <= 16) {  // one-hot byte tid - 1
-            const int x = tid - 1;
-            e[x >> 2] = 1 << (8 * (x & 3));
-        } else if (tid >= 17) {  // slot 0: the flag (int8 -128 in byte 0), + one-hot byte tid - 17
-            const int x = tid - 17;
-            if (x > 0) e[x >> 2] = 1 << (8 * (x & 3));
-            e[0] |= 0x80;
-        }
-        ftab[tid] = e;
+#ifdef COF_HALFTAB
+    if (tid < 18) {
+        const bool first = tid >= 9;
+        const int sg = tid % 9;
+        unsigned w[2] = {0u, 0u};
+        if (sg >= 1 && first) w[0] |= 0x80u;
+        const int ob = first ? (sg >= 2 ? sg - 1 : -1) : sg - 1;
+        if (ob >= 0) w[ob >> 2] |= 1u << (8 * (ob & 3));
+        htab[tid] = make_uint2(w[0], w[1]);
     }
+#else
+    for (int x = tid; x < COF_TAB; x += 256) {
+        const int ty = x / 81, en = x - ty * 81;
+        int w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {  // half hf: dwords 2 hf, 2 hf + 1
+            const int sg = hf ? en / 9 : en % 9;
+            const bool first = (ty >> hf) & 1;
+            if (sg >= 1 && first) w[2 * hf] |= 0x80;  // the flag
+            const int ob = first ? (sg >= 2 ? sg - 1 : -1) : sg - 1;  // one-hot byte
+            if (ob >= 0) w[2 * hf + (ob >> 2)] |= 1 << (8 * (ob & 3));
+        }
+        ftab[x] = (v4i){w[0], w[1], w[2], w[3]};
+    }
+#endif
     if (nstage > 0) {
         issue(0);
         commit(0);
@@ -360,18 +402,32 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
             for (int ni = 0; ni < 4; ++ni) L[2 + ni] = col[rb + 32 * ni];
         };
         v4i fr[2][6];
-        auto read_frags = [&](const int (&L)[6], v4i (&F)[6]) {
+        // the type of slot 2q + h picks its table: ftab + 81 * type
+        const unsigned long long tm = tmask[st];
+        auto read_frags = [&](int q, const int (&L)[6], v4i (&F)[6]) {
+#ifdef COF_HALFTAB
+            const int ty = (int)((tm >> (4 * q + 2 * h)) & 3);
+            const uint2* blo = htab + 9 * (ty & 1);
+            const uint2* bhi = htab + 9 * (ty >> 1);
 #pragma unroll
-            for (int x = 0; x < 6; ++x) F[x] = ftab[L[x]];
+            for (int x = 0; x < 6; ++x) {
+                const uint2 lo = blo[L[x] & 15], hi = bhi[L[x] >> 4];
+                F[x] = (v4i){(int)lo.x, (int)lo.y, (int)hi.x, (int)hi.y};
+            }
+#else
+            const v4i* tb = ftab + 81 * (int)((tm >> (4 * q + 2 * h)) & 3);
+#pragma unroll
+            for (int x = 0; x < 6; ++x) F[x] = tb[L[x]];
+#endif
         };
         read_entries(0, ent[0]);
         read_entries(1, ent[1]);
-        read_frags(ent[0], fr[0]);
+        read_frags(0, ent[0], fr[0]);
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
             const int cur = q & 1;
             if (q + 2 < QN) read_entries(q + 2, ent[cur]);
-            if (q + 1 < QN) read_frags(ent[cur ^ 1], fr[cur ^ 1]);
+            if (q + 1 < QN) read_frags(q + 1, ent[cur ^ 1], fr[cur ^ 1]);
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -486,7 +542,8 @@ struct CofPlan {
     int* colC;
     int* ccol;
     int* nslot;
-    int* desc;
+    int* desc;                  // 2 * maxslots halves
+    unsigned long long* tmask;  // maxslots / COF_SLOTS stages
     int64_t maxslots;
     uint8_t* E;                 // entry matrix of the current chunk (maxslots x Npad bytes)
     int64_t Npad;               // rows per slot of E (N rounded up to 4)
@@ -495,7 +552,7 @@ struct CofPlan {
 
 // Column maxima, column chunks and table space.  A chunk has at most
 // COF_CHUNK columns (the 14-bit co field) and an entry matrix of at most
-// COF_EMAX bytes.  8-bit labels bound the slots by 16 per column; when that
+// COF_EMAX bytes.  8-bit labels bound the halves by 32 (slots by 16) per column; when that
 // bound does not fit (and always for 16-bit labels) the column maxima are
 // read back once to size the chunks exactly.
 static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64_t B, hipStream_t st,
@@ -518,11 +575,11 @@ static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int6
         std::vector<int> h(B);
         CCG_HIP(hipMemcpyAsync(h.data(), colC, sizeof(int) * B, hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
-        const int64_t cap = std::max<int64_t>(COF_EMAX / Npad - COF_SLOTS, 4097);  // slots per chunk
+        const int64_t cap = 2 * std::max<int64_t>(COF_EMAX / Npad - COF_SLOTS, 4097);  // halves per chunk
         int64_t s = 0, worst = 0, c0 = 0;
         pl->cuts.push_back(0);
         for (int64_t b = 0; b < B; ++b) {
-            const int64_t v = h[b] > 0 ? (h[b] + 16) / 16 : 0;
+            const int64_t v = h[b] > 0 ? (h[b] + 8) / 8 : 0;
             if (b > c0 && (b - c0 == COF_CHUNK || s + v > cap)) {
                 pl->cuts.push_back(b);
                 worst = std::max(worst, s);
@@ -532,16 +589,20 @@ static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int6
             s += v;
         }
         pl->cuts.push_back(B);
-        maxslots = std::max(worst, s) + COF_SLOTS;
+        maxslots = (std::max(worst, s) + 1) / 2 + COF_SLOTS;
     }
-    int* ft = (int*)ccg_ws(ctx, WS_COC_B, sizeof(int) * (Bc + 8 + maxslots));
-    if (!ft) return CCG_ENOMEM;
+    const int64_t nstg = maxslots / COF_SLOTS + 1;
+    unsigned long long* ftm = (unsigned long long*)ccg_ws(
+        ctx, WS_COC_B, sizeof(unsigned long long) * nstg + sizeof(int) * (Bc + 8 + 2 * maxslots));
+    if (!ftm) return CCG_ENOMEM;
+    int* ft = (int*)(ftm + nstg);
     uint8_t* E = (uint8_t*)ccg_ws(ctx, WS_COC_G, (size_t)(maxslots * Npad));
     if (!E) return CCG_ENOMEM;
     pl->colC = colC;
     pl->ccol = ft;
     pl->nslot = ft + Bc;
     pl->desc = pl->nslot + 8;
+    pl->tmask = ftm;
     pl->maxslots = maxslots;
     pl->E = E;
     pl->Npad = Npad;
@@ -554,7 +615,7 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
                        int64_t TC, int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
                        const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
                        uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{}) {
-    cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc);
+    cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.tmask);
     const dim3 eg((unsigned)std::min<int64_t>(ccg_cdiv(pl.Npad / 4, 256), 128),
                   (unsigned)std::min<int64_t>(pl.maxslots, COF_ENT_GRID));
     if (label_bits == 8)
@@ -563,7 +624,7 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
     else
         cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                          pl.nslot, pl.E);
-    cof_tile_kernel<MODE><<<(unsigned)ntiles, 256, 0, st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, co_prev,
+    cof_tile_kernel<MODE><<<(unsigned)ntiles, 256, 0, st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
                                                             both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
 }
 

@@ -42,8 +42,12 @@ def main():
     ms, cnt = eng.timing_read("cocluster")
     ms /= cnt
     ops = 2.0 * P * (int(C.sum()) + B)
+    w = (torch.arange(P, device="cuda") % 1009).to(torch.int64)
+    digest = [int(co.to(torch.int64).sum()), int(both.to(torch.int64).sum()), int((co.to(torch.int64) * w).sum()),
+              int((both.to(torch.int64) * w).sum())]  # compares library variants
     print(json.dumps({"N": N, "B": B, "sumC": int(C.sum()), "coc_ms": ms, "tops": ops / (ms * 1e-3) / 1e12,
-                      "frac_of_5000": ops / (ms * 1e-3) / 5e15, "out_GBs": 4.0 * P / (ms * 1e-3) / 1e9}))
+                      "frac_of_5000": ops / (ms * 1e-3) / 5e15, "out_GBs": 4.0 * P / (ms * 1e-3) / 1e9,
+                      "digest": digest}))
 
 
 if __name__ == "__main__":
