@@ -170,11 +170,7 @@ __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (r4 + e >= N) continue;
-#ifdef COF_HALFTAB
-                    const int en = cof_sigma(dl, (int)cl[r4 + e]) | (cof_sigma(dh, (int)chh[r4 + e]) << 4);
-#else
                     const int en = cof_sigma(dl, (int)cl[r4 + e]) + 9 * cof_sigma(dh, (int)chh[r4 + e]);
-#endif
                     out |= (unsigned)en << (8 * e);
                 }
             }
@@ -295,11 +291,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     constexpr int ROWD = COF_ROWS / 4;                  // dwords per staged slot
     constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
     __shared__ __attribute__((aligned(16))) uint8_t panel[2][COF_SLOTS][COF_ROWS];
-#ifdef COF_HALFTAB
-    __shared__ __attribute__((aligned(16))) uint2 htab[18];  // [first][sigma]: one 144-byte span, no bank conflicts
-#else
     __shared__ __attribute__((aligned(16))) v4i ftab[COF_TAB];
-#endif
     const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     int64_t I, J;
@@ -353,17 +345,6 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
     };
-#ifdef COF_HALFTAB
-    if (tid < 18) {
-        const bool first = tid >= 9;
-        const int sg = tid % 9;
-        unsigned w[2] = {0u, 0u};
-        if (sg >= 1 && first) w[0] |= 0x80u;
-        const int ob = first ? (sg >= 2 ? sg - 1 : -1) : sg - 1;
-        if (ob >= 0) w[ob >> 2] |= 1u << (8 * (ob & 3));
-        htab[tid] = make_uint2(w[0], w[1]);
-    }
-#else
     for (int x = tid; x < COF_TAB; x += 256) {
         const int ty = x / 81, en = x - ty * 81;
         int w[4] = {0, 0, 0, 0};
@@ -377,7 +358,6 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         }
         ftab[x] = (v4i){w[0], w[1], w[2], w[3]};
     }
-#endif
     if (nstage > 0) {
         issue(0);
         commit(0);
@@ -405,20 +385,9 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
         // the type of slot 2q + h picks its table: ftab + 81 * type
         const unsigned long long tm = tmask[st];
         auto read_frags = [&](int q, const int (&L)[6], v4i (&F)[6]) {
-#ifdef COF_HALFTAB
-            const int ty = (int)((tm >> (4 * q + 2 * h)) & 3);
-            const uint2* blo = htab + 9 * (ty & 1);
-            const uint2* bhi = htab + 9 * (ty >> 1);
-#pragma unroll
-            for (int x = 0; x < 6; ++x) {
-                const uint2 lo = blo[L[x] & 15], hi = bhi[L[x] >> 4];
-                F[x] = (v4i){(int)lo.x, (int)lo.y, (int)hi.x, (int)hi.y};
-            }
-#else
             const v4i* tb = ftab + 81 * (int)((tm >> (4 * q + 2 * h)) & 3);
 #pragma unroll
             for (int x = 0; x < 6; ++x) F[x] = tb[L[x]];
-#endif
         };
         read_entries(0, ent[0]);
         read_entries(1, ent[1]);

@@ -518,12 +518,12 @@ __device__ __forceinline__ void sil_row_width(double selfsq, double oth2, bool i
 
 // LDS stage of sil_width: ch centroids ([ch][DMAX + 2] f64: the 16-byte row
 // pad spreads the 16 lanes of a fragment read over distinct banks), [ch] f64
-// |mu|^2 + v and [ch] codes; ch = min(sil_chunk, cmax rounded up to 16) keeps
-// the stage within 64 KB and, for the usual cmax <= 64, small enough for
-// several blocks per CU.
+// |mu|^2 + v and [ch] codes; ch = min(sil_chunk, SIL_LG x cmax rounded up to
+// 16): a group of SIL_LG labelings with up to ~50 clusters each is staged at
+// once, and the stage (<= 73 KB) leaves room for two blocks per CU.
 template <int DMAX>
 constexpr int sil_chunk() {
-    return DMAX <= 16 ? 256 : (DMAX <= 32 ? 208 : 112);
+    return DMAX <= 16 ? 384 : (DMAX <= 32 ? 256 : 112);
 }
 template <int DMAX>
 constexpr int sil_sp() {
@@ -581,83 +581,62 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         xx[t] = p;
     }
     const double wsc = ldexp(1.0, scale_exp((double)m));
-    const int l1 = min(L, (int)(blockIdx.y + 1) * SIL_LG);
-    // the next labeling's labels and cluster count are loaded a labeling ahead
-    // (their latency hides behind the current labeling's MFMA work)
-    int labn[RT];
-    int npn = 0;
-    {
-        const int l = blockIdx.y * SIL_LG;
+    const int lg0 = blockIdx.y * SIL_LG, l1 = min(L, lg0 + SIL_LG);
+    // x.mu of one staged 16-centroid tile against the RT row tiles, folded into
+    // the rows' running own / other minima
+    auto tile = [&](int c0, const int (&lab)[RT], double (&oth)[RT], double (&self)[RT]) {
+        double a[KS];
+        const double* ap = smu + (c0 + j) * SP + g * KS;
 #pragma unroll
-        for (int t = 0; t < RT; ++t) labn[t] = (l < l1 && in[t]) ? labels[(int64_t)l * m + rowof[t]] : 0;
-        npn = l < l1 ? npres[l] : 0;
-    }
-    for (int l = blockIdx.y * SIL_LG; l < l1; ++l) {
-        const int np = npn;
-        int lab[RT];
-        double oth[RT], self[RT];
+        for (int s = 0; s < KS; s += 2) {
+            const double2 v = *reinterpret_cast<const double2*>(ap + s);
+            a[s] = v.x;
+            a[s + 1] = v.y;
+        }
+        double mv[4];
+        int code[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            mv[i] = smv[c0 + g + 4 * i];
+            code[i] = scode[c0 + g + 4 * i];
+        }
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            lab[t] = labn[t];
-            oth[t] = INFINITY;
-            self[t] = INFINITY;
-        }
-        if (l + 1 < l1) {
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < RT; ++t) labn[t] = in[t] ? labels[(int64_t)(l + 1) * m + rowof[t]] : 0;
-            npn = npres[l + 1];
-        }
-        const double* ml = muc + (int64_t)l * cmax * DMAX;
-        const double* al = auxc + (int64_t)l * cmax * 2;
-        for (int p0 = 0; p0 < np; p0 += CH) {
-            const int nc = min(CH, np - p0);
-            const int nct = (nc + 15) & ~15;  // whole 16-centroid tiles; padding: zero centroid, +inf offset
-            for (int t = threadIdx.x; t < nct * DMAX; t += SIL_T) {
-                const int c = t / DMAX, p = t - c * DMAX;
-                smu[c * SP + p] = t < nc * DMAX ? ml[(int64_t)p0 * DMAX + t] : 0.0;
+            for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], xb[t][s], acc, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double tv = fma(-2.0, acc[i], mv[i]);
+                const bool own = code[i] == lab[t];
+                self[t] = own ? tv : self[t];
+                // the own cluster leaves the minimum by a high word of +DBL_MAX
+                const double cand = __hiloint2double(own ? 0x7fefffff : __double2hiint(tv), __double2loint(tv));
+                oth[t] = __builtin_fmin(oth[t], cand);
             }
-            for (int t = threadIdx.x; t < nct; t += SIL_T) {
-                smv[t] = t < nc ? al[2 * (int64_t)(p0 + t)] + al[2 * (int64_t)(p0 + t) + 1] : INFINITY;
-                scode[t] = t < nc ? codes[(int64_t)l * cmax + p0 + t] : -1;
-            }
-            __syncthreads();
-            for (int c0 = 0; c0 < nct; c0 += 16) {
-                double a[KS];
-                const double* ap = smu + (c0 + j) * SP + g * KS;
-#pragma unroll
-                for (int s = 0; s < KS; s += 2) {
-                    const double2 v = *reinterpret_cast<const double2*>(ap + s);
-                    a[s] = v.x;
-                    a[s + 1] = v.y;
-                }
-                double mv[4];
-                int code[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    mv[i] = smv[c0 + g + 4 * i];
-                    code[i] = scode[c0 + g + 4 * i];
-                }
-#pragma unroll
-                for (int t = 0; t < RT; ++t) {
-                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], xb[t][s], acc, 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const double tv = fma(-2.0, acc[i], mv[i]);
-                        const bool own = code[i] == lab[t];
-                        self[t] = own ? tv : self[t];
-                        // the own cluster leaves the minimum by a high word of +DBL_MAX
-                        const double cand = __hiloint2double(own ? 0x7fefffff : __double2hiint(tv), __double2loint(tv));
-                        oth[t] = __builtin_fmin(oth[t], cand);
-                    }
-                }
-            }
-            __syncthreads();  // before the next chunk (or labeling) overwrites the stage
         }
-        // merge the four lane groups (each saw every fourth centroid of a
-        // tile); lane group g then finishes row tile t = g, so every lane
-        // takes one row's square roots and division
+    };
+    // stage centroids [p0, p0 + nc) of labeling l at LDS position off (whole
+    // 16-centroid tiles; padding: zero centroid, +inf offset)
+    auto stage = [&](int l, int p0, int nc, int off) {
+        const int nct = (nc + 15) & ~15;
+        const double* ml = muc + ((int64_t)l * cmax + p0) * DMAX;
+        const double* al = auxc + ((int64_t)l * cmax + p0) * 2;
+        for (int t = threadIdx.x; t < nct * DMAX; t += SIL_T) {
+            const int c = t / DMAX, p = t - c * DMAX;
+            smu[(off + c) * SP + p] = t < nc * DMAX ? ml[t] : 0.0;
+        }
+        for (int t = threadIdx.x; t < nct; t += SIL_T) {
+            smv[off + t] = t < nc ? al[2 * t] + al[2 * t + 1] : INFINITY;
+            scode[off + t] = t < nc ? codes[(int64_t)l * cmax + p0 + t] : -1;
+        }
+    };
+    // one labeling's widths from the rows' minima: the four lane groups
+    // (each saw every fourth centroid of a tile) merged; lane group g then
+    // finishes row tile t = g, so every lane takes one row's square roots and
+    // division.  The wave's integer sums go to its own partial (no block
+    // barrier): wsum[l][4 block + wave].
+    auto finish = [&](int l, int np, double (&oth)[RT], double (&self)[RT]) {
         double ow = 0.0, sw = 0.0;
         bool iw = false;
         int64_t pw = 0;
@@ -678,25 +657,71 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         unsigned wn = 0;
         sil_row_width(sw, ow, iw, np, wsc,
                       (out_width && !rep) ? out_width + (int64_t)l * m + r0 + g * 16 + j : nullptr, wq, wn, wt);
-        // integer reductions (order-independent): wave, then block; one
-        // partial per (labeling, block) -- same-line global atomics from every
-        // wave serialised at the L2
         for (int o = 32; o > 0; o >>= 1) {
             wq += __shfl_xor(wq, o, 64);
             wn += __shfl_xor(wn, o, 64);
         }
-        __shared__ long long red_q[4];
-        __shared__ unsigned red_n[4];
         if (lane == 0) {
-            red_q[wave] = wq;
-            red_n[wave] = wn;
+            wsum[(int64_t)l * nbw + 4 * blockIdx.x + wave] = (unsigned long long)wq;
+            wcnt[(int64_t)l * nbw + 4 * blockIdx.x + wave] = (unsigned long long)wn;
+        }
+    };
+    int tot = 0;  // staged centroids of the whole group (uniform)
+    for (int l = lg0; l < l1; ++l) tot += (npres[l] + 15) & ~15;
+    if (tot <= CH) {
+        // the group's centroids in one stage, one barrier; the labels of all its
+        // labelings loaded up front
+        int labg[SIL_LG][RT], npg[SIL_LG];
+#pragma unroll
+        for (int li = 0; li < SIL_LG; ++li) {
+            const int l = lg0 + li;
+            npg[li] = l < l1 ? npres[l] : 0;
+#pragma unroll
+            for (int t = 0; t < RT; ++t) labg[li][t] = (l < l1 && in[t]) ? labels[(int64_t)l * m + rowof[t]] : 0;
+        }
+        int off = 0;
+#pragma unroll
+        for (int li = 0; li < SIL_LG; ++li) {
+            if (lg0 + li < l1) stage(lg0 + li, 0, npg[li], off);
+            off += (npg[li] + 15) & ~15;
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            wsum[(int64_t)l * nbw + blockIdx.x] = (unsigned long long)(red_q[0] + red_q[1] + red_q[2] + red_q[3]);
-            wcnt[(int64_t)l * nbw + blockIdx.x] = (unsigned long long)(red_n[0] + red_n[1] + red_n[2] + red_n[3]);
+        off = 0;
+#pragma unroll
+        for (int li = 0; li < SIL_LG; ++li) {
+            if (lg0 + li >= l1) break;
+            double oth[RT], self[RT];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                oth[t] = INFINITY;
+                self[t] = INFINITY;
+            }
+            const int nct = (npg[li] + 15) & ~15;
+            for (int c0 = 0; c0 < nct; c0 += 16) tile(off + c0, labg[li], oth, self);
+            off += nct;
+            finish(lg0 + li, npg[li], oth, self);
         }
-        __syncthreads();  // red_q / red_n are rewritten by the next labeling
+        return;
+    }
+    // a group larger than the stage: each labeling in chunks of CH centroids
+    for (int l = lg0; l < l1; ++l) {
+        const int np = npres[l];
+        int lab[RT];
+        double oth[RT], self[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            lab[t] = in[t] ? labels[(int64_t)l * m + rowof[t]] : 0;
+            oth[t] = INFINITY;
+            self[t] = INFINITY;
+        }
+        for (int p0 = 0; p0 < np; p0 += CH) {
+            const int nc = min(CH, np - p0);
+            __syncthreads();  // the previous chunk's reads are done
+            stage(l, p0, nc, 0);
+            __syncthreads();
+            for (int c0 = 0; c0 < nc; c0 += 16) tile(c0, lab, oth, self);
+        }
+        finish(l, np, oth, self);
     }
 }
 
@@ -750,14 +775,15 @@ __global__ __launch_bounds__(256) void sil_final(int64_t m, int L, int cmax, int
     }
 }
 
-// rows per sil_width block and the number of such blocks (partials per labeling)
+// rows per sil_width block, and the width partials per labeling (one per
+// wave of every block)
 template <int DMAX>
 constexpr int sil_width_rows() {
     return 4 * sil_rt<DMAX>() * 16;
 }
 static int sil_width_blocks(int64_t m, int d) {
     const int rb = d <= 16 ? sil_width_rows<16>() : (d <= 32 ? sil_width_rows<32>() : sil_width_rows<64>());
-    return (int)ccg_cdiv(m, rb);
+    return 4 * (int)ccg_cdiv(m, rb);
 }
 
 // ---------------------------------------------- distinct-cell widths --
@@ -859,7 +885,7 @@ __global__ void sil_width_exc(const double* __restrict__ x, int64_t m, int d, co
     sil_row_width(fmax(xx + self, 0.0), fmax(xx + oth, 0.0), true, np, ldexp(1.0, scale_exp((double)m)), nullptr,
                   wq, wn);
     if (wn) {
-        atomicAdd(&wsum[(int64_t)l * nbw], (unsigned long long)wq);
+        atomicAdd(&wsum[(int64_t)l * nbw], (unsigned long long)wq);  // the first partial of the labeling
         atomicAdd(&wcnt[(int64_t)l * nbw], 1ull);
     }
     }
@@ -903,9 +929,10 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
     // the representative grid uses its first blocks
     const int64_t nrows = rep ? mw : m;
     dim3 grid2((unsigned)ccg_cdiv(nrows, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
-    const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), ((int64_t)cmax + 15) / 16 * 16);
+    // the stage holds a whole group of SIL_LG labelings when it can
+    const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), (int64_t)SIL_LG * (((int64_t)cmax + 15) / 16 * 16));
     const size_t lds5 = (size_t)CH * sil_sp<DMAX>() * 8 + (size_t)CH * 8 + (size_t)CH * 4;
-    const int nbw = (int)ccg_cdiv(m, sil_width_rows<DMAX>());
+    const int nbw = 4 * (int)ccg_cdiv(m, sil_width_rows<DMAX>());
     if (rep) {
         // partials of blocks past the representative grid stay 0 (zeroed with the buffer)
         sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
