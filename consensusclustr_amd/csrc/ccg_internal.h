@@ -59,6 +59,7 @@ enum ccg_ws_slot {
     WS_FX_B,         // kNN exact search of failed rows: candidate (d2, row) buffers
     WS_SEG_ROWS,     // batched bootstrap segments: the gathered rows of every segment
     WS_SEG_TAB,      // batched bootstrap segments: row and distinct-cell segment offsets
+    WS_KB_C,         // distinct-cell kNN: per-cell counts / offsets / cursors / cell -> distinct id (counting grouping)
     WS_NSLOTS
 };
 
@@ -84,6 +85,8 @@ struct ccg_ctx {
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
     void* fx_zeroed;  // kNN radius search: the WS_FX_A buffer whose counters were zeroed at allocation
+    void* kb_zeroed;  // kNN row grouping: the WS_KB_C buffer whose counts / cursors are zero for N = kb_zero_n
+    int64_t kb_zero_n;
     // kNN: the exact-search row list of the last call and its count (device; ccg_knn_last_fallback)
     const int* last_fail_list;
     const int* last_fail_count;

@@ -1556,19 +1556,107 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
 // computed distinct neighbour (a tie that may continue past the list) is
 // re-searched exactly over all rows by the fallback kernels.
 
-// keys = the cells (clamped into [0, N): an index outside sets the sticky
-// error), values = the rows
-__global__ void kb_iota_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N, int32_t* __restrict__ cells,
-                               int32_t* __restrict__ rid, int* __restrict__ err) {
+// Rows grouped by cell with a counting sort over the N cells (ccg_knn_boot
+// and its table flavour; the segments keep the radix sort): per-cell counts
+// with a presence bit, pk[c] = present << 32 | count, so ONE exclusive scan
+// gives every present cell its distinct id (high word) and its first sorted
+// position (low word).  pk and the cursors are zero between calls (each call
+// clears what it used).  The cells' rows are then scattered by per-cell
+// atomic cursors and each cell's few rows sorted ascending, so the result is
+// exactly the stable sort's.
+// (also zeroes the ucap + 1 words of ustart, so a wrong caller u leaves no
+// garbage offsets behind)
+__global__ void kb_count_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N,
+                                unsigned long long* __restrict__ pk, int* __restrict__ err,
+                                int32_t* __restrict__ ztab, int64_t nz) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t; i < nz; i += (int64_t)gridDim.x * blockDim.x) ztab[i] = 0;
     if (t >= n) return;
     int c = idx[t];
     if (c < 0 || c >= N) {
         atomicOr(err, CCG_DERR_KNN_UNIQUE);
         c = 0;
     }
-    cells[t] = c;
-    rid[t] = (int32_t)t;
+    const unsigned long long old = atomicAdd(&pk[c], 1ull);
+    if ((old & 0xffffffffull) == 0ull) atomicAdd(&pk[c], 1ull << 32);  // the first row: the presence bit
+}
+
+// Per cell c (and c = N): cell2u[c] (-1: absent), ustart[uid]; pk[c] back to
+// 0 and the scatter cursor zeroed (for every cell, whatever the caller's u).
+// A caller's u that differs from the count sets the sticky error; ids are
+// clamped into [0, ucap) so every later access stays in bounds.
+__global__ void kb_cells_kernel(unsigned long long* __restrict__ pk, const int64_t* __restrict__ pko, int64_t N,
+                                int64_t n, int ucap, int u_given, int* __restrict__ cell2u,
+                                int* __restrict__ ustart, int* __restrict__ cursor, int* __restrict__ err) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < N) {
+        const unsigned long long a = (unsigned long long)pko[c], b = (unsigned long long)pko[c + 1];
+        const bool present = (b >> 32) > (a >> 32);
+        const int uid = min((int)(a >> 32), ucap - 1);
+        cell2u[c] = present ? uid : -1;
+        if (present) ustart[uid] = (int)(a & 0xffffffffull);
+        pk[c] = 0ull;
+        cursor[c] = 0;
+    } else if (c == N) {
+        const int u = (int)((unsigned long long)pko[N] >> 32);
+        if (u_given >= 0 && u != u_given) atomicOr(err, CCG_DERR_KNN_UNIQUE);
+        ustart[min(u, ucap)] = (int)n;
+    }
+}
+
+__global__ void kb_scatter_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N,
+                                  const int* __restrict__ cell2u, const int* __restrict__ ustart,
+                                  int* __restrict__ cursor, int32_t* __restrict__ srow, int32_t* __restrict__ scell) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int c = idx[t];
+    if (c < 0 || c >= N) c = 0;  // (flagged by the count kernel)
+    const int64_t pos = min((int64_t)ustart[max(cell2u[c], 0)] + atomicAdd(&cursor[c], 1), n - 1);
+    srow[pos] = (int32_t)t;
+    scell[pos] = c;
+}
+
+// One wave per distinct cell: its rows sorted ascending (a wave bitonic sort
+// up to 64 rows; ranks by counting beyond, through tmp), row2u.
+__global__ __launch_bounds__(256) void kb_fixup_kernel(int u, int64_t n, const int* __restrict__ ustart,
+                                                       int32_t* __restrict__ srow, int* __restrict__ row2u,
+                                                       int32_t* __restrict__ tmp) {
+    const int uid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (uid >= u) return;
+    const int s = min(max(ustart[uid], 0), (int)n), e = min(max(ustart[uid + 1], s), (int)n);
+    const int k = e - s;
+    if (k <= 0) return;
+    if (k == 1) {
+        if (lane == 0) row2u[srow[s]] = uid;
+        return;
+    }
+    if (k <= 64) {
+        int v = lane < k ? srow[s + lane] : 0x7fffffff;
+        for (int kk = 2; kk <= 64; kk <<= 1)
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                const int o = __shfl_xor(v, j, 64);
+                const bool up = (lane & kk) == 0, lo = (lane & j) == 0;
+                v = (lo == up) ? min(v, o) : max(v, o);
+            }
+        if (lane < k) {
+            srow[s + lane] = v;
+            row2u[v] = uid;
+        }
+        return;
+    }
+    for (int i = lane; i < k; i += 64) {  // a cell drawn more than 64 times (tiny N): ranks by counting
+        const int v = srow[s + i];
+        int r = 0;
+        for (int j = 0; j < k; ++j) r += srow[s + j] < v ? 1 : 0;
+        tmp[s + r] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    for (int i = lane; i < k; i += 64) {
+        const int v = tmp[s + i];
+        srow[s + i] = v;
+        row2u[v] = uid;
+    }
 }
 
 // (cell, row) pairs sorted by cell (stable: each cell's rows ascending)
@@ -1869,12 +1957,6 @@ __global__ void kt_transpose_kernel(const double* __restrict__ pcs, int64_t N, i
     rows[i * d + k] = pcs[t];
 }
 
-__global__ void kt_cellmap_kernel(int u, const int* __restrict__ ustart, const int32_t* __restrict__ scell,
-                                  int* __restrict__ cell2u) {
-    const int uid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (uid < u) cell2u[scell[ustart[uid]]] = uid;
-}
-
 // one wave per distinct cell: the first kq present entries of its table row
 __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, const int* __restrict__ ustart,
                                                         const int32_t* __restrict__ scell,
@@ -2050,31 +2132,41 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     int32_t* row2u = cells;
     int* fail_count = (int*)(misc + 4);  // zeroed by knn_run's init kernel (or below when u == 1)
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
-    // 1. rows grouped by cell (stable radix sort on the cell index bits)
-    int bits = 1;
-    while (bits < 31 && (1LL << bits) < N) ++bits;
+    // 1-2. rows grouped by cell: a counting sort over the N cells (one scan
+    // gives the distinct ids and the cells' first positions)
     const unsigned ng = (unsigned)ccg_cdiv(n, 256);
-    kb_iota_kernel<<<ng, 256, 0, st>>>(idx, n, N, cells, rid, ctx->d_err);
-    int rc = ccg_sort_pairs_i32(ctx, cells, scell, rid, srow, n, bits, st);
-    if (rc) return rc;
-    // 2. distinct cells: heads -> scan -> tables (zeroed first: see kb_tables_kernel)
-    int32_t* ustart0 = srow + n;
-    kb_heads_kernel<<<ng, 256, 0, st>>>(scell, n, head, n_unique >= 0 ? ustart0 : nullptr, (int64_t)n_unique + 1);
-    rc = ccg_scan_i64(ctx, head, head, n, st);
-    if (rc) return rc;
+    char* tc = (char*)ccg_ws(ctx, WS_KB_C, 2 * sizeof(int64_t) * (size_t)(N + 1) + 2 * sizeof(int) * (size_t)N + 64);
+    if (!tc) return CCG_ENOMEM;
+    unsigned long long* pk = (unsigned long long*)tc;    // [N + 1] counts | presence (zero between calls)
+    int64_t* pko = (int64_t*)(pk + N + 1);               // [N + 1] their exclusive scan
+    int* cursor = (int*)(pko + N + 1);                   // [N] scatter cursors (zeroed by kb_cells_kernel)
+    int* cell2u = cursor + N;                            // [N] cell -> distinct id (-1: absent)
+    if (ctx->kb_zeroed != (void*)tc || ctx->kb_zero_n != N) {
+        CCG_HIP(hipMemsetAsync(pk, 0, sizeof(int64_t) * (size_t)(N + 1), st));
+        ctx->kb_zeroed = (void*)tc;
+        ctx->kb_zero_n = N;
+    }
+    kb_count_kernel<<<ng, 256, 0, st>>>(idx, n, N, pk, ctx->d_err, srow + n, (int64_t)ucap + 1);
+    int rc = ccg_scan_i64(ctx, (const int64_t*)pk, pko, N, st);
+    if (rc) {
+        ctx->kb_zeroed = nullptr;  // the counts were not cleared: the next call zeroes them
+        return rc;
+    }
     int u = n_unique;
     if (u < 0) {
         int64_t hu = 0;
-        CCG_HIP(hipMemcpyAsync(&hu, head + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipMemcpyAsync(&hu, pko + N, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         CCG_HIP(hipStreamSynchronize(st));
-        u = (int)hu;
-        CCG_HIP(hipMemsetAsync(ustart0, 0, sizeof(int32_t) * ((size_t)u + 1), st));
+        u = (int)((uint64_t)hu >> 32);
     }
     const int kq = std::min(kmax, u - 1);
-    int32_t* ustart = ustart0;                   // [u + 1]
+    int32_t* ustart = srow + n;                  // [u + 1]
     double* ud2 = urows + (size_t)u * d;         // [u][kq] certified squared distances
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
-    kb_tables_kernel<<<ng, 256, 0, st>>>(scell, srow, n, head, u, ustart, row2u, ctx->d_err);
+    kb_cells_kernel<<<(unsigned)ccg_cdiv(N + 1, 256), 256, 0, st>>>(pk, pko, N, n, u, n_unique, cell2u, ustart,
+                                                                    cursor, ctx->d_err);
+    kb_scatter_kernel<<<ng, 256, 0, st>>>(idx, n, N, cell2u, ustart, cursor, srow, scell);
+    kb_fixup_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, n, ustart, srow, row2u, rid);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
@@ -2082,12 +2174,8 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     ccg_knn_stats us = {0, 0};
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
-        int* cell2u = (int*)ccg_ws(ctx, WS_TAB_MAP, sizeof(int) * (size_t)N);
-        if (!cell2u) return CCG_ENOMEM;
         int* ufail = (int*)(misc + 5);
-        CCG_HIP(hipMemsetAsync(cell2u, 0xff, sizeof(int) * (size_t)N, st));
         CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));  // fail counts, expansion tie count
-        kt_cellmap_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, ustart, scell, cell2u);
         kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, ustart, scell, cell2u, tab_idx, tab_d2,
                                                                    uidx, ud2, fail_list, ufail);
         kt_tau_kernel<<<256, 256, 0, st>>>(kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, fail_list, ufail,
