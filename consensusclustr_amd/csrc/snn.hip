@@ -445,6 +445,89 @@ __device__ __forceinline__ void snn_bitonic(K (&x)[E], int lane) {
     snn_bitonic_merge<E, K, 2>(x, lane);
 }
 
+// Ascending bitonic network over N keys in one lane's registers (compile-
+// time indices: min/max pairs only).
+template <int N, typename K>
+__device__ __forceinline__ void snn_sort_regs(K (&y)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int jj = k >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const K a = y[i], b = y[l];
+                    const K lo = a < b ? a : b, hi = a < b ? b : a;
+                    y[i] = (i & k) == 0 ? lo : hi;
+                    y[l] = (i & k) == 0 ? hi : lo;
+                }
+            }
+}
+
+// Bucket tier of the sort (one wave, W = 1): the node's M keys (element-major
+// in x, item t = 64 e + lane) are split by partner into 64 buckets of equal
+// partner range (lane b owns bucket b; a node's partners are spread evenly
+// over (j, n)), ranked by LDS atomics, scattered to LDS, and every lane sorts
+// its bucket (<= CAP keys) in registers; x then holds the sorted keys lane-
+// major (element E lane + e), padding ~0 last, as the bitonic tier leaves
+// them.  A wave-level bitonic sort of 64 E slots costs ~log^2(64 E) / 2
+// exchange stages per key, most across lanes; this is one register network
+// of CAP keys per lane plus a few LDS passes.  Returns false (x untouched)
+// when a bucket holds more than CAP keys: the caller sorts bitonically.
+template <int E, int CAP, typename K>
+__device__ __forceinline__ bool snn_bucket_sort(K (&x)[E], int M, int lane, int* hist, K* buf) {
+    constexpr int PS = SnnKeyT<K>::PS;
+    K kmin = ~(K)0, kmax = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (64 * e + lane < M) {
+            kmin = x[e] < kmin ? x[e] : kmin;
+            kmax = x[e] > kmax ? x[e] : kmax;
+        }
+    int pmin = (int)(kmin >> PS), pmax = (int)(kmax >> PS);
+    if (64 * 0 + lane >= M) pmin = INT_MAX, pmax = INT_MIN;  // (M >= 1: lane 0 holds a key)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        pmin = min(pmin, __shfl_xor(pmin, o, 64));
+        pmax = max(pmax, __shfl_xor(pmax, o, 64));
+    }
+    const float sc = 64.0f / (float)(pmax - pmin + 1);
+    hist[lane] = 0;
+    WAVE_LDS_SYNC();
+    int b[E], r[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        b[e] = 0;
+        r[e] = 0;
+        if (64 * e + lane < M) {
+            b[e] = min(63, (int)((float)((int)(x[e] >> PS) - pmin) * sc));
+            r[e] = atomicAdd(&hist[b[e]], 1);
+        }
+    }
+    WAVE_LDS_SYNC();
+    const int c = hist[lane];
+    if (__any(c > CAP)) return false;
+    const int off = snn_scan_add(c) - c;
+    hist[64 + lane] = off;
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (64 * e + lane < M) buf[hist[64 + b[e]] + r[e]] = x[e];
+    WAVE_LDS_SYNC();
+    K y[CAP];
+#pragma unroll
+    for (int i = 0; i < CAP; ++i) y[i] = i < c ? buf[off + i] : ~(K)0;
+    snn_sort_regs<CAP, K>(y);
+#pragma unroll
+    for (int i = 0; i < CAP; ++i)
+        if (i < c) buf[off + i] = y[i];  // the lane's own range: no other lane reads it before the barrier
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = E * lane + e < M ? buf[E * lane + e] : ~(K)0;
+    return true;
+}
+
 // LDS of one node: the member table (lane i <= kmax holds member i; packed
 // for one 16-byte read per item: first host position, end, the member, first
 // item), the item -> member marks / transpose stage, and the W waves'
@@ -586,7 +669,7 @@ __device__ __forceinline__ void snn_emit_sorted(LDS& L, const SnnSpec& sp, int64
 
 // One node, W waves (W = 1: one wave; W = 4: a 256-thread block for the
 // hubs); wave w holds sorted elements 64*E*w .. 64*E*(w+1) - 1.
-template <int E, int W, typename K>
+template <int E, int W, typename K, bool BK = false>
 __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, const SnnSpec& sp, int64_t n, int64_t j,
                                                  const SnnMember& m, int wv, int lane,
                                                  const int2* __restrict__ hosts_s, const SnnRows& rows,
@@ -635,6 +718,12 @@ __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, cons
     for (int e = 0; e < E; ++e)
         x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
     SNN_SYNC();  // every mark is read
+    if constexpr (BK && W == 1) {
+        if (snn_bucket_sort<E, (E >= 32 ? 64 : 32), K>(x, M, lane, reinterpret_cast<int*>(L.mem), L.u.buf)) {
+            snn_emit_sorted<E, W, K>(L, sp, n, j, wv, lane, x, rows, cnt);
+            return;
+        }
+    }
 #pragma unroll
     for (int e = 0; e < E; ++e) L.u.buf[base + 64 * e + lane] = x[e];
     SNN_SYNC();
@@ -826,7 +915,7 @@ __device__ __forceinline__ void snn_merge_node(SnnMergeLds<E>& L, const SnnSpec&
 // wave (4 waves per block, 2 for class 2: its LDS stage is 8-16 KB per wave);
 // class 3 runs one node per 256-thread block over a fixed grid.
 __host__ __device__ constexpr int snn_bitonic_wpb(int cls) { return cls == 2 ? 2 : 4; }
-template <int CLS, typename K, bool MERGE = false>
+template <int CLS, typename K, bool MERGE = false, bool BUCKET = false>
 __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
@@ -879,7 +968,7 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
                 return;
             }
         }
-        snn_bitonic_node<EM, 1, K>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
+        snn_bitonic_node<EM, 1, K, BUCKET && CLS >= 1>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
     }
 }
 
@@ -1260,13 +1349,18 @@ static bool snn_no_copy() {
     return v;
 }
 
-// CCG_SNN_SORT=merge: the merge tier for NUMBER graphs (bit-identical rows;
-// measured slower than the bitonic tier at cfg3: 1.01 against 0.81 ms per
-// bootstrap for the SNN stage, so the bitonic tier is the default)
-static bool snn_sort_bitonic() {
-    static const bool v = [] {
+// Sort tier of size classes 1-2 (bit-identical rows in every mode):
+// CCG_SNN_SORT=bucket (default; 64 partner-range buckets, one register network
+// per lane: classes 1 / 2 172.5 -> 162.6 / 156.4 -> 154.7 us isolated at
+// cfg3), =bitonic (the wave-wide register bitonic sort), =merge (the merge
+// tier of the sorted host runs, NUMBER only: measured slower, SNN 1.01 against
+// 0.81 ms per bootstrap).  Returns 0 bitonic, 1 merge, 2 bucket.
+static int snn_sort_mode() {
+    static const int v = [] {
         const char* e = getenv("CCG_SNN_SORT");
-        return !(e && strcmp(e, "merge") == 0);
+        if (e && strcmp(e, "merge") == 0) return 1;
+        if (e && strcmp(e, "bitonic") == 0) return 0;
+        return 2;
     }();
     return v;
 }
@@ -1344,22 +1438,25 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     if (rc) return rc;
     snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
     int* ov_list = ov + 3 * n;
-#define SNN_BITONIC(CLS_, K_, GRID_, MG_)                                                                      \
-    snn_bitonic_build_kernel<CLS_, K_, MG_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                  \
+#define SNN_BITONIC(CLS_, K_, GRID_, MG_, BK_)                                                                 \
+    snn_bitonic_build_kernel<CLS_, K_, MG_, BK_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(             \
         knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
         ov_count + 1, src)
-#define SNN_BITONIC_ALL(K_, MG_)                                                  \
+#define SNN_BITONIC_ALL(K_, MG_, BK_)                                             \
     do {                                                                          \
-        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), MG_);        \
-        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), MG_);        \
-        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), MG_);        \
-        SNN_BITONIC(3, K_, 1024u, false);                                          \
+        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), MG_, false); \
+        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), MG_, BK_);   \
+        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), MG_, BK_);   \
+        SNN_BITONIC(3, K_, 1024u, false, false);                                   \
     } while (0)
+    const int mode = snn_sort_mode();
     if (sp.type == CCG_SNN_NUMBER) {
-        if (snn_sort_bitonic()) SNN_BITONIC_ALL(uint32_t, false);
-        else SNN_BITONIC_ALL(uint32_t, true);  // the merge tier (sorted host runs; CCG_SNN_SORT=merge)
+        if (mode == 1) SNN_BITONIC_ALL(uint32_t, true, false);  // the merge tier (sorted host runs)
+        else if (mode == 2) SNN_BITONIC_ALL(uint32_t, false, true);
+        else SNN_BITONIC_ALL(uint32_t, false, false);
     } else {
-        SNN_BITONIC_ALL(unsigned long long, false);
+        if (mode == 2) SNN_BITONIC_ALL(unsigned long long, false, true);
+        else SNN_BITONIC_ALL(unsigned long long, false, false);
     }
 #undef SNN_BITONIC_ALL
 #undef SNN_BITONIC
