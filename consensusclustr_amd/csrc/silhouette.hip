@@ -37,6 +37,9 @@ __device__ __forceinline__ int scale_exp(double bound) {
     return e > 52 ? 52 : e;
 }
 
+// one atomic per block on one word: a small grid (a 1024-block grid spent
+// ~10 us serialising its atomics at the L2)
+#define SIL_MAXABS_GRID 128
 __global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, int64_t tot,
                                                   unsigned* __restrict__ bits) {
     __shared__ unsigned red[4];
@@ -814,33 +817,35 @@ __global__ void sil_isrep_kernel(const int32_t* __restrict__ cell, int64_t m, co
 
 // rep[pos] = the representative rows in row order (pos = exclusive scan);
 // cnt[pos] = the cell's rows; the other rows listed in row order (r - scan[r]
-// of them come before r)
+// of them come before r) as (row, its representative, the representative's
+// position): sil_mult_kernel reads them per labeling without a dependent
+// chain of gathers
 __global__ void sil_rep_kernel(const int32_t* __restrict__ cell, int64_t m, const int* __restrict__ first,
                                const int64_t* __restrict__ scan, int* __restrict__ rep, int* __restrict__ cnt,
-                               int* __restrict__ nonrep) {
+                               int3* __restrict__ nonrep) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= m) return;
     const int rp = first[cell[r]];
-    atomicAdd(&cnt[scan[rp]], 1);
-    if (rp == (int)r) rep[scan[r]] = (int)r;
-    else nonrep[r - scan[r]] = (int)r;
+    const int pp = (int)scan[rp];
+    atomicAdd(&cnt[pp], 1);
+    if (rp == (int)r) rep[pp] = (int)r;
+    else nonrep[r - scan[r]] = make_int3((int)r, rp, pp);
 }
 
 // Per labeling (blockIdx.y strides), every non-representative row whose
 // label differs from its representative's: dis[l][pos] += 1 (the weight is
 // cnt - dis) and the row joins the exception list (l << 32 | row).
-__global__ void sil_mult_kernel(const int32_t* __restrict__ cell, int64_t m, int L, const int32_t* __restrict__ labels,
-                                const int* __restrict__ first, const int64_t* __restrict__ scan,
-                                const int* __restrict__ nonrep, int64_t mw, int* __restrict__ dis,
-                                unsigned long long* __restrict__ exc, int* __restrict__ nexc) {
+__global__ void sil_mult_kernel(int64_t m, int L, const int32_t* __restrict__ labels,
+                                const int64_t* __restrict__ scan, const int3* __restrict__ nonrep, int64_t mw,
+                                int* __restrict__ dis, unsigned long long* __restrict__ exc, int* __restrict__ nexc) {
     const int64_t nn = m - scan[m];
     for (int l = blockIdx.y; l < L; l += gridDim.y) {
         const int32_t* lab = labels + (int64_t)l * m;
         for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nn; j += (int64_t)gridDim.x * blockDim.x) {
-            const int r = nonrep[j];
-            const int rp = first[cell[r]];
+            const int3 e = nonrep[j];
+            const int r = e.x, rp = e.y;
             if (lab[r] != lab[rp]) {
-                atomicAdd(&dis[(int64_t)l * mw + scan[rp]], 1);
+                atomicAdd(&dis[(int64_t)l * mw + e.z], 1);
                 const int e = atomicAdd(nexc, 1);
                 exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
             }
@@ -985,7 +990,7 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     }
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 1024), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
     if (d <= 16)
         sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         out_width, st);
@@ -1043,14 +1048,14 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     // distinct-cell tables: first row per cell, representative list, rows per
     // cell, the other rows, per-labeling disagreements, exceptions
     char* tb = (char*)ccg_ws(ctx, WS_SIL_C, sizeof(int) * (size_t)ncell + sizeof(int64_t) * (size_t)(m + 1) +
-                                                3 * sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
+                                                5 * sizeof(int) * (size_t)m + sizeof(int) * (size_t)L * m +
                                                 sizeof(unsigned long long) * (size_t)L * m + 512);
     if (!tb) return CCG_ENOMEM;
     int* first = (int*)tb;
     int64_t* scan = (int64_t*)(tb + ccg_cdiv(sizeof(int) * ncell, 16) * 16);
     int* rep = (int*)(scan + m + 1);
-    int* nonrep = rep + m;
-    int* nexc = nonrep + m;             // [0] exception count; then cnt and the disagreements (zeroed together)
+    int3* nonrep = (int3*)(rep + m);    // [m] (row, representative, its position)
+    int* nexc = (int*)(nonrep + m);     // [0] exception count; then cnt and the disagreements (zeroed together)
     int* cnt = nexc + 4;                // [m] (first mw used)
     int* mult = cnt + m;                // [L][m] (first mw columns used)
     // the u64 exceptions start on an 8-byte boundary whatever the parity of m
@@ -1069,8 +1074,8 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     // mw = the number of representatives (the distinct cells): device-side
     // only, so the width grid covers m positions and the weights' stride is m
     dim3 gx((unsigned)std::min<int64_t>(ccg_cdiv(m, 256), 32), (unsigned)std::min(L, 65535));
-    sil_mult_kernel<<<gx, 256, 0, st>>>(cell, m, L, labels, first, scan, nonrep, m, mult, exc, nexc);
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 1024), 1024), 256, 0, st>>>(x, m * d, maxabs);
+    sil_mult_kernel<<<gx, 256, 0, st>>>(m, L, labels, scan, nonrep, m, mult, exc, nexc);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
 #define SIL_CELLS(DM_)                                                                                              \
     sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
                     auxc, q, nullptr, st, rep, mult, cnt, m, exc, nexc, scan + m)
