@@ -1587,7 +1587,8 @@ __global__ void kb_count_kernel(const int32_t* __restrict__ idx, int64_t n, int6
 // clamped into [0, ucap) so every later access stays in bounds.
 __global__ void kb_cells_kernel(unsigned long long* __restrict__ pk, const int64_t* __restrict__ pko, int64_t N,
                                 int64_t n, int ucap, int u_given, int* __restrict__ cell2u,
-                                int* __restrict__ ustart, int* __restrict__ cursor, int* __restrict__ err) {
+                                int* __restrict__ ustart, int* __restrict__ cursor, int* __restrict__ nbig,
+                                int* __restrict__ err) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c < N) {
         const unsigned long long a = (unsigned long long)pko[c], b = (unsigned long long)pko[c + 1];
@@ -1601,6 +1602,7 @@ __global__ void kb_cells_kernel(unsigned long long* __restrict__ pk, const int64
         const int u = (int)((unsigned long long)pko[N] >> 32);
         if (u_given >= 0 && u != u_given) atomicOr(err, CCG_DERR_KNN_UNIQUE);
         ustart[min(u, ucap)] = (int)n;
+        *nbig = 0;
     }
 }
 
@@ -1616,46 +1618,73 @@ __global__ void kb_scatter_kernel(const int32_t* __restrict__ idx, int64_t n, in
     scell[pos] = c;
 }
 
-// One wave per distinct cell: its rows sorted ascending (a wave bitonic sort
-// up to 64 rows; ranks by counting beyond, through tmp), row2u.
+// One thread per distinct cell: its rows sorted ascending (an insertion sort
+// in place: a cell has ~1.5 rows), row2u.  A cell drawn more than 32 times
+// (tiny N) goes to kb_fixup_big_kernel's list.
+#define KB_FIX_SMALL 32
 __global__ __launch_bounds__(256) void kb_fixup_kernel(int u, int64_t n, const int* __restrict__ ustart,
                                                        int32_t* __restrict__ srow, int* __restrict__ row2u,
-                                                       int32_t* __restrict__ tmp) {
-    const int uid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+                                                       int* __restrict__ big, int* __restrict__ nbig) {
+    const int uid = blockIdx.x * blockDim.x + threadIdx.x;
     if (uid >= u) return;
     const int s = min(max(ustart[uid], 0), (int)n), e = min(max(ustart[uid + 1], s), (int)n);
     const int k = e - s;
     if (k <= 0) return;
-    if (k == 1) {
-        if (lane == 0) row2u[srow[s]] = uid;
+    if (k > KB_FIX_SMALL) {
+        big[atomicAdd(nbig, 1)] = uid;
         return;
     }
-    if (k <= 64) {
-        int v = lane < k ? srow[s + lane] : 0x7fffffff;
-        for (int kk = 2; kk <= 64; kk <<= 1)
-            for (int j = kk >> 1; j > 0; j >>= 1) {
-                const int o = __shfl_xor(v, j, 64);
-                const bool up = (lane & kk) == 0, lo = (lane & j) == 0;
-                v = (lo == up) ? min(v, o) : max(v, o);
+    for (int i = 1; i < k; ++i) {
+        const int v = srow[s + i];
+        int q = i - 1;
+        while (q >= 0 && srow[s + q] > v) {
+            srow[s + q + 1] = srow[s + q];
+            --q;
+        }
+        srow[s + q + 1] = v;
+    }
+    for (int p = s; p < e; ++p) row2u[srow[p]] = uid;
+}
+
+// The listed cells, one wave each: a wave bitonic sort up to 64 rows, ranks
+// by counting beyond (through tmp).
+__global__ __launch_bounds__(256) void kb_fixup_big_kernel(int64_t n, const int* __restrict__ ustart,
+                                                           int32_t* __restrict__ srow, int* __restrict__ row2u,
+                                                           const int* __restrict__ big, const int* __restrict__ nbig,
+                                                           int32_t* __restrict__ tmp) {
+    const int lane = threadIdx.x & 63;
+    const int nb = *nbig;
+    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nb; w += gridDim.x * 4) {
+        const int uid = big[w];
+        const int s = min(max(ustart[uid], 0), (int)n), e = min(max(ustart[uid + 1], s), (int)n);
+        const int k = e - s;
+        if (k <= 64) {
+            int v = lane < k ? srow[s + lane] : 0x7fffffff;
+            for (int kk = 2; kk <= 64; kk <<= 1)
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    const int o = __shfl_xor(v, j, 64);
+                    const bool up = (lane & kk) == 0, lo = (lane & j) == 0;
+                    v = (lo == up) ? min(v, o) : max(v, o);
+                }
+            if (lane < k) {
+                srow[s + lane] = v;
+                row2u[v] = uid;
             }
-        if (lane < k) {
-            srow[s + lane] = v;
+            continue;
+        }
+        for (int i = lane; i < k; i += 64) {
+            const int v = srow[s + i];
+            int r = 0;
+            for (int j = 0; j < k; ++j) r += srow[s + j] < v ? 1 : 0;
+            tmp[s + r] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
+        for (int i = lane; i < k; i += 64) {
+            const int v = tmp[s + i];
+            srow[s + i] = v;
             row2u[v] = uid;
         }
-        return;
-    }
-    for (int i = lane; i < k; i += 64) {  // a cell drawn more than 64 times (tiny N): ranks by counting
-        const int v = srow[s + i];
-        int r = 0;
-        for (int j = 0; j < k; ++j) r += srow[s + j] < v ? 1 : 0;
-        tmp[s + r] = v;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __threadfence_block();
-    for (int i = lane; i < k; i += 64) {
-        const int v = tmp[s + i];
-        srow[s + i] = v;
-        row2u[v] = uid;
     }
 }
 
@@ -2135,12 +2164,15 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     // 1-2. rows grouped by cell: a counting sort over the N cells (one scan
     // gives the distinct ids and the cells' first positions)
     const unsigned ng = (unsigned)ccg_cdiv(n, 256);
-    char* tc = (char*)ccg_ws(ctx, WS_KB_C, 2 * sizeof(int64_t) * (size_t)(N + 1) + 2 * sizeof(int) * (size_t)N + 64);
+    char* tc = (char*)ccg_ws(ctx, WS_KB_C, 2 * sizeof(int64_t) * (size_t)(N + 1) +
+                                               sizeof(int) * (2 * (size_t)N + (size_t)ucap + 8));
     if (!tc) return CCG_ENOMEM;
     unsigned long long* pk = (unsigned long long*)tc;    // [N + 1] counts | presence (zero between calls)
     int64_t* pko = (int64_t*)(pk + N + 1);               // [N + 1] their exclusive scan
     int* cursor = (int*)(pko + N + 1);                   // [N] scatter cursors (zeroed by kb_cells_kernel)
     int* cell2u = cursor + N;                            // [N] cell -> distinct id (-1: absent)
+    int* nbig = cell2u + N;                              // [1] cells with more than KB_FIX_SMALL rows
+    int* big = nbig + 4;                                 // [ucap] their ids
     if (ctx->kb_zeroed != (void*)tc || ctx->kb_zero_n != N) {
         CCG_HIP(hipMemsetAsync(pk, 0, sizeof(int64_t) * (size_t)(N + 1), st));
         ctx->kb_zeroed = (void*)tc;
@@ -2164,9 +2196,10 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     double* ud2 = urows + (size_t)u * d;         // [u][kq] certified squared distances
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kq);
     kb_cells_kernel<<<(unsigned)ccg_cdiv(N + 1, 256), 256, 0, st>>>(pk, pko, N, n, u, n_unique, cell2u, ustart,
-                                                                    cursor, ctx->d_err);
+                                                                    cursor, nbig, ctx->d_err);
     kb_scatter_kernel<<<ng, 256, 0, st>>>(idx, n, N, cell2u, ustart, cursor, srow, scell);
-    kb_fixup_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, n, ustart, srow, row2u, rid);
+    kb_fixup_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, n, ustart, srow, row2u, big, nbig);
+    kb_fixup_big_kernel<<<16, 256, 0, st>>>(n, ustart, srow, row2u, big, nbig, rid);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,

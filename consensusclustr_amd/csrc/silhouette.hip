@@ -39,14 +39,21 @@ __device__ __forceinline__ int scale_exp(double bound) {
 
 // one atomic per block on one word: a small grid (a 1024-block grid spent
 // ~10 us serialising its atomics at the L2)
-#define SIL_MAXABS_GRID 128
+#define SIL_MAXABS_GRID 256
 __global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, int64_t tot,
                                                   unsigned* __restrict__ bits) {
     __shared__ unsigned red[4];
-    double mx = 0.0;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
-         t += (int64_t)gridDim.x * blockDim.x)
+    double mx = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;  // four loads in flight per step
+    const int64_t stp = (int64_t)gridDim.x * blockDim.x;
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; t + 3 * stp < tot; t += 4 * stp) {
         mx = fmax(mx, fabs(x[t]));
+        m1 = fmax(m1, fabs(x[t + stp]));
+        m2 = fmax(m2, fabs(x[t + 2 * stp]));
+        m3 = fmax(m3, fabs(x[t + 3 * stp]));
+    }
+    for (; t < tot; t += stp) mx = fmax(mx, fabs(x[t]));
+    mx = fmax(fmax(mx, m1), fmax(m2, m3));
     // a float at or above max|x| (rounded up)
     unsigned local = __float_as_uint(nextafterf((float)mx, INFINITY));
     for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));

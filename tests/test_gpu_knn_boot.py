@@ -84,6 +84,18 @@ def test_knn_boot_dev_cell_copies_beyond_kmax(engine, path):
     _check(engine, pcs, idx, 20, path)
 
 
+def test_knn_boot_dev_cells_drawn_over_64_times(engine, path):
+    """Cells drawn 150 and 70 times (the grouping's big-cell path: ranks by
+    counting beyond 64 rows, a wave sort up to 64) among ordinary cells."""
+    rng = np.random.default_rng(4)
+    N, d = 200, 5
+    pcs = rng.normal(size=(N, d))
+    idx = rng.integers(0, N, 1200).astype(np.int32)
+    idx[rng.choice(1200, 150, replace=False)] = 5
+    idx[rng.choice(np.flatnonzero(idx != 5), 70, replace=False)] = 7
+    _check(engine, pcs, idx, 20, path)
+
+
 @pytest.mark.parametrize("kmax", [20, 32])
 def test_knn_boot_dev_lattice_ties(engine, path, kmax):
     """Integer lattice cells (many distinct cells at exactly equal distance)
