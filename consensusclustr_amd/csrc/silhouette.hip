@@ -26,6 +26,10 @@
 #include "ccg_internal.h"
 
 #define SIL_T 256
+// centroid granularity of the width tiles (v_mfma_f64_4x4x4f64: C padded to
+// a multiple of 4; the 16x16x4 tiles of round 3 padded to 16, 1.37x at C =
+// 2..40: silhouette 0.454 -> 0.435 ms per bootstrap at cfg3)
+#define SIL_CGRP 4
 #ifndef SIL_LG
 #define SIL_LG 5
 #endif
@@ -595,41 +599,39 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     // x.mu of one staged 16-centroid tile against the RT row tiles, folded into
     // the rows' running own / other minima
     auto tile = [&](int c0, const int (&lab)[RT], double (&oth)[RT], double (&self)[RT]) {
+        // 4 centroids x 16 rows per v_mfma_f64_4x4x4f64: its 4 blocks are the
+        // row tile's 4-row groups against the same 4 centroids.  Lane (g, j)
+        // feeds A = dim 4s + g of centroid c0 + (lane & 3), B = dim 4s + g of
+        // row j (the 16x16x4 form's B), and receives x_j . mu_{c0 + g}
+        // (measured on gfx950: 18 clocks per 4x4x4 against 64 per 16x16x4,
+        // 0.89 of its rate per flop, for C padded to 4 instead of 16)
         double a[KS];
-        const double* ap = smu + (c0 + j) * SP + g * KS;
+        const double* ap = smu + (c0 + (lane & 3)) * SP + g * KS;
 #pragma unroll
         for (int s = 0; s < KS; s += 2) {
             const double2 v = *reinterpret_cast<const double2*>(ap + s);
             a[s] = v.x;
             a[s + 1] = v.y;
         }
-        double mv[4];
-        int code[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            mv[i] = smv[c0 + g + 4 * i];
-            code[i] = scode[c0 + g + 4 * i];
-        }
+        const double mv = smv[c0 + g];
+        const int code = scode[c0 + g];
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+            double acc = 0.0;
 #pragma unroll
-            for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], xb[t][s], acc, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const double tv = fma(-2.0, acc[i], mv[i]);
-                const bool own = code[i] == lab[t];
-                self[t] = own ? tv : self[t];
-                // the own cluster leaves the minimum by a high word of +DBL_MAX
-                const double cand = __hiloint2double(own ? 0x7fefffff : __double2hiint(tv), __double2loint(tv));
-                oth[t] = __builtin_fmin(oth[t], cand);
-            }
+            for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_4x4x4f64(a[s], xb[t][s], acc, 0, 0, 0);
+            const double tv = fma(-2.0, acc, mv);
+            const bool own = code == lab[t];
+            self[t] = own ? tv : self[t];
+            // the own cluster leaves the minimum by a high word of +DBL_MAX
+            const double cand = __hiloint2double(own ? 0x7fefffff : __double2hiint(tv), __double2loint(tv));
+            oth[t] = __builtin_fmin(oth[t], cand);
         }
     };
     // stage centroids [p0, p0 + nc) of labeling l at LDS position off (whole
     // 16-centroid tiles; padding: zero centroid, +inf offset)
     auto stage = [&](int l, int p0, int nc, int off) {
-        const int nct = (nc + 15) & ~15;
+        const int nct = (nc + SIL_CGRP - 1) & ~(SIL_CGRP - 1);
         const double* ml = muc + ((int64_t)l * cmax + p0) * DMAX;
         const double* al = auxc + ((int64_t)l * cmax + p0) * 2;
         for (int t = threadIdx.x; t < nct * DMAX; t += SIL_T) {
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         }
     };
     int tot = 0;  // staged centroids of the whole group (uniform)
-    for (int l = lg0; l < l1; ++l) tot += (npres[l] + 15) & ~15;
+    for (int l = lg0; l < l1; ++l) tot += (npres[l] + SIL_CGRP - 1) & ~(SIL_CGRP - 1);
     if (tot <= CH) {
         // the group's centroids in one stage, one barrier; the labels of all its
         // labelings loaded up front
@@ -693,7 +695,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
 #pragma unroll
         for (int li = 0; li < SIL_LG; ++li) {
             if (lg0 + li < l1) stage(lg0 + li, 0, npg[li], off);
-            off += (npg[li] + 15) & ~15;
+            off += (npg[li] + SIL_CGRP - 1) & ~(SIL_CGRP - 1);
         }
         __syncthreads();
         off = 0;
@@ -706,8 +708,8 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
                 oth[t] = INFINITY;
                 self[t] = INFINITY;
             }
-            const int nct = (npg[li] + 15) & ~15;
-            for (int c0 = 0; c0 < nct; c0 += 16) tile(off + c0, labg[li], oth, self);
+            const int nct = (npg[li] + SIL_CGRP - 1) & ~(SIL_CGRP - 1);
+            for (int c0 = 0; c0 < nct; c0 += SIL_CGRP) tile(off + c0, labg[li], oth, self);
             off += nct;
             finish(lg0 + li, npg[li], oth, self);
         }
@@ -729,7 +731,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
             __syncthreads();  // the previous chunk's reads are done
             stage(l, p0, nc, 0);
             __syncthreads();
-            for (int c0 = 0; c0 < nc; c0 += 16) tile(c0, lab, oth, self);
+            for (int c0 = 0; c0 < nc; c0 += SIL_CGRP) tile(c0, lab, oth, self);
         }
         finish(l, np, oth, self);
     }
