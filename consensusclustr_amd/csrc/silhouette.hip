@@ -494,10 +494,10 @@ __global__ void sil_vfin(int64_t m, int d, int L, int cmax, const unsigned* __re
 
 // K5: widths and their fixed-point sum over non-NaN rows.
 //   D^2(i, c) = |x_i|^2 + (|mu_c|^2 + v_c) - 2 x_i.mu_c
-// with x.mu on the fp64 matrix core: v_mfma_f64_16x16x4f64 with A = 16
+// with x.mu on the fp64 matrix core: v_mfma_f64_4x4x4f64 with A = 4
 // centroids x 4 dims (LDS) and B = 4 dims x 16 rows (registers, loaded once
-// per block), so accumulator i of lane (g, j) = g + 4i-th centroid of the
-// tile against row j of the lane's row tile.  The epilogue is branch-free and
+// per block), so lane (g, j) receives centroid c0 + g of the group against
+// row j of the lane's row tile.  The epilogue is branch-free and
 // per value costs one fma, one compare, three selects and one min: each lane
 // keeps, per row, min over the other clusters of (|mu|^2 + v - 2 x.mu) and the
 // own cluster's value; |x|^2 is added once per row, then clamped at 0 (the
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
         }
     };
     // stage centroids [p0, p0 + nc) of labeling l at LDS position off (whole
-    // 16-centroid tiles; padding: zero centroid, +inf offset)
+    // 4-centroid groups; padding: zero centroid, +inf offset)
     auto stage = [&](int l, int p0, int nc, int off) {
         const int nct = (nc + SIL_CGRP - 1) & ~(SIL_CGRP - 1);
         const double* ml = muc + ((int64_t)l * cmax + p0) * DMAX;
