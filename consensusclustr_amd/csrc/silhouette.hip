@@ -596,7 +596,7 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     }
     const double wsc = ldexp(1.0, scale_exp((double)m));
     const int lg0 = blockIdx.y * SIL_LG, l1 = min(L, lg0 + SIL_LG);
-    // x.mu of one staged 16-centroid tile against the RT row tiles, folded into
+    // x.mu of one staged 4-centroid group against the RT row tiles, folded into
     // the rows' running own / other minima
     auto tile = [&](int c0, const int (&lab)[RT], double (&oth)[RT], double (&self)[RT]) {
         // 4 centroids x 16 rows per v_mfma_f64_4x4x4f64: its 4 blocks are the
