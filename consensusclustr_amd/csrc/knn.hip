@@ -1232,9 +1232,18 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
     }
 }
 
-// One block per failed row: the exact fp64 d2 (the contract's arithmetic)
-// of every candidate, those within the radius bitonic-sorted by (d2, row)
-// in LDS, the first kmax written.
+#ifndef WAVE_LDS_SYNC
+// a wave's LDS writes are visible to its other lanes' later LDS reads (the
+// LDS pipeline is in order per wave); the clobber stops compiler reordering
+#define WAVE_LDS_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
+#endif
+
+// One wave per failed row: the exact fp64 d2 (the contract's arithmetic)
+// of every candidate, those within the radius sorted by (d2, row) -- a wave
+// bitonic sort in registers for <= 64 candidates (the usual ~26), a wave
+// bitonic sort in the wave's LDS slice beyond -- and the first kmax written.
+// (Round 3's block per row ran its LDS sort with two block barriers per
+// stage and took two rounds of the grid for ~270 rows.)
 template <int DMAX>
 __global__ __launch_bounds__(256) void knn_fx_select_kernel(const double* __restrict__ rows, int d, int kmax,
                                                             const int* __restrict__ fail_list,
@@ -1244,11 +1253,13 @@ __global__ __launch_bounds__(256) void knn_fx_select_kernel(const double* __rest
                                                             int32_t* __restrict__ out_idx,
                                                             double* __restrict__ out_dist, bool dist_sq,
                                                             int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
-    __shared__ double kd[KNN_FX_CAP];
-    __shared__ int ki[KNN_FX_CAP];
-    __shared__ int nin;
+    __shared__ double kd_all[4][KNN_FX_CAP];
+    __shared__ int ki_all[4][KNN_FX_CAP];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* kd = kd_all[wv];
+    int* ki = ki_all[wv];
     const int nf = *fail_count;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+    for (int f = blockIdx.x * 4 + wv; f < nf; f += gridDim.x * 4) {
         const int q = fail_list[f];
         int c = KNN_FX_CAP + 1;
         double t = INFINITY;
@@ -1257,46 +1268,94 @@ __global__ __launch_bounds__(256) void knn_fx_select_kernel(const double* __rest
             t = fail_tau[f];
             if (!(t < INFINITY)) c = KNN_FX_CAP + 1;
         }
-        __syncthreads();
-        if (f < KNN_FX_ROWS && threadIdx.x == 0) cnt[f] = 0;  // zero for the next call
-        if (threadIdx.x == 0) nin = 0;
-        __syncthreads();
-        if (c > KNN_FX_CAP || c < kmax) {  // the per-thread-list kernels take it
-            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
+        const bool ovf = c > KNN_FX_CAP || c < kmax;  // (c is in a register before the counter is cleared)
+        if (f < KNN_FX_ROWS && lane == 0) cnt[f] = 0;    // zero for the next call
+        if (ovf) {  // the per-thread-list kernels take it
+            if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
             continue;
         }
         double xq[DMAX];
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) xq[k] = k < d ? rows[(int64_t)q * d + k] : 0.0;
-        int m = 1;
-        while (m < c) m <<= 1;
-        for (int s = threadIdx.x; s < m; s += blockDim.x) {
+        if (c <= 64) {
             double v = INFINITY;
-            int j = 0x7fffffff;
+            int jx = 0x7fffffff;
+            if (lane < c) {
+                const int jj = bi[(int64_t)f * KNN_FX_CAP + lane];
+                const double e = knn_exact_d2<DMAX>(xq, rows + (int64_t)jj * d, d);
+                if (e <= t) {
+                    v = e;
+                    jx = jj;
+                }
+            }
+            if (__popcll(__ballot(jx != 0x7fffffff)) < kmax) {  // (cannot happen: tau bounds kmax exact distances)
+                if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
+                continue;
+            }
+            for (int k = 2; k <= 64; k <<= 1)
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const double ov = __shfl_xor(v, j, 64);
+                    const int oj = __shfl_xor(jx, j, 64);
+                    const bool up = (lane & k) == 0, lo = (lane & j) == 0;
+                    const bool take = (lo == up) ? key_less(ov, oj, v, jx) : key_less(v, jx, ov, oj);
+                    if (take) {
+                        v = ov;
+                        jx = oj;
+                    }
+                }
+            if (lane < kmax) {
+                out_idx[(int64_t)q * kmax + lane] = jx;
+                if (out_dist) out_dist[(int64_t)q * kmax + lane] = dist_sq ? v : sqrt(v);
+            }
+            continue;
+        }
+        int m = 128;
+        while (m < c) m <<= 1;
+        int nin = 0;
+        for (int s0 = 0; s0 < m; s0 += 64) {
+            const int s = s0 + lane;
+            double v = INFINITY;
+            int jx = 0x7fffffff;
             if (s < c) {
                 const int jj = bi[(int64_t)f * KNN_FX_CAP + s];
                 const double e = knn_exact_d2<DMAX>(xq, rows + (int64_t)jj * d, d);
                 if (e <= t) {
                     v = e;
-                    j = jj;
-                    atomicAdd(&nin, 1);
+                    jx = jj;
                 }
             }
+            nin += __popcll(__ballot(jx != 0x7fffffff));
             kd[s] = v;
-            ki[s] = j;
+            ki[s] = jx;
         }
-        __syncthreads();
-        if (nin < kmax) {  // (cannot happen: tau bounds kmax exact distances) the per-thread-list kernels
-            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
-            __syncthreads();
+        if (nin < kmax) {
+            if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = q;
             continue;
         }
-        knn_lds_bitonic(kd, ki, m);
-        for (int r = threadIdx.x; r < kmax; r += blockDim.x) {
+        for (int k = 2; k <= m; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                WAVE_LDS_SYNC();
+                for (int i = lane; i < m; i += 64) {
+                    const int p = i ^ j;
+                    if (p > i) {
+                        const bool up = (i & k) == 0;
+                        const double x0 = kd[i], x1 = kd[p];
+                        const int i0 = ki[i], i1 = ki[p];
+                        if (key_less(x1, i1, x0, i0) == up) {
+                            kd[i] = x1;
+                            kd[p] = x0;
+                            ki[i] = i1;
+                            ki[p] = i0;
+                        }
+                    }
+                }
+            }
+        WAVE_LDS_SYNC();
+        for (int r = lane; r < kmax; r += 64) {
             out_idx[(int64_t)q * kmax + r] = ki[r];
             if (out_dist) out_dist[(int64_t)q * kmax + r] = dist_sq ? kd[r] : sqrt(kd[r]);
         }
-        __syncthreads();
+        WAVE_LDS_SYNC();  // the slice is rewritten by the wave's next row
     }
 }
 
