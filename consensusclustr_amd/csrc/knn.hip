@@ -1955,40 +1955,45 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
                                                               int* __restrict__ tie_list, int* __restrict__ tie_count,
                                                               const int64_t* __restrict__ useg = nullptr,
                                                               int nseg = 1) {
-    const int lane = threadIdx.x & 63;
-    const int uc = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (uc >= u) return;
-    if (useg) {  // segmented run: the cut test counts the distinct cells of the cell's own segment
+    // two distinct cells per wave, one per 32-lane half (kq <= kmax <= 32):
+    // a cell's list takes at most 32 lanes
+    const int lane = threadIdx.x & 31;
+    const int half = (threadIdx.x >> 5) & 1;
+    const int uc = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const bool live = uc < u;
+    if (__ballot(live) == 0ull) return;
+    int uu = u;
+    if (useg && live) {  // segmented run: the cut test counts the distinct cells of the cell's own segment
         const int sg = knn_seg_of(useg, nseg, uc);
-        u = (int)(useg[sg + 1] - useg[sg]);
+        uu = (int)(useg[sg + 1] - useg[sg]);
     }
-    const int oa = ustart[uc], ob = ustart[uc + 1], oc = ob - oa;  // the own cell's rows (sorted positions)
-    const bool has = lane < kq;
+    const int oa = live ? ustart[uc] : 0, ob = live ? ustart[uc + 1] : 0, oc = ob - oa;  // the own cell's rows
+    const bool has = live && lane < kq;
     const int v = has ? uidx[(int64_t)uc * kq + lane] : 0;
     const double dd = has ? ud2[(int64_t)uc * kq + lane] : INFINITY;
     const int a = has ? ustart[v] : 0, cn = has ? ustart[v + 1] - a : 0;
-    const double dprev = __shfl_up(dd, 1, 64);
+    const double dprev = __shfl_up(dd, 1, 32);
     const bool tie = has && (lane == 0 ? dd == 0.0 : dd == dprev);
-    if (__any(tie)) {  // equal-d2 groups of several cells: the per-row merge
-        if (lane == 0) tie_list[atomicAdd(tie_count, 1)] = uc;
-        return;
-    }
+    const unsigned long long bt = __ballot(tie);
+    const bool htie = ((half ? bt >> 32 : bt) & 0xffffffffull) != 0ull;
+    if (htie && lane == 0) tie_list[atomicAdd(tie_count, 1)] = uc;  // equal-d2 groups of several cells: the per-row merge
     int incl = cn;  // exclusive prefix of the neighbours' row counts
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
+    for (int o = 1; o < 32; o <<= 1) {
+        const int y = __shfl_up(incl, o, 32);
         if (lane >= o) incl += y;
     }
     const int pre = incl - cn;
     const int own = oc - 1;                    // own rows in every copy's list
     const int need = kmax - own;               // neighbour rows a list takes (<= 0: own rows only)
-    const int total = __shfl(incl, 63, 64);    // all listed neighbours' rows
+    const int total = __shfl(incl, 31, 32);    // all listed neighbours' rows
     // the last listed cell reached while the list is short: a tie may continue past it
-    const int plast = __shfl(pre, kq - 1, 64);
-    const bool cut = need > 0 && kq >= 1 && plast < need && kq < u - 1;
+    const int plast = __shfl(pre, kq - 1, 32);
+    const bool cut = need > 0 && kq >= 1 && plast < need && kq < uu - 1;
     const bool shortl = need > 0 && total < need;  // (kq = u - 1 and fewer than kmax rows: n - 1 < kmax)
-    const double glast = __shfl(dd, kq - 1, 64);
+    const double glast = __shfl(dd, kq - 1, 32);
+    if (!live || htie) return;
     for (int z = oa; z < ob; ++z) {
-        const int i = srow[z];  // a copy (wave-uniform)
+        const int i = srow[z];  // a copy (uniform in the half)
         if (cut || shortl) {
             if (lane == 0) {
                 const int p = atomicAdd(fail_count, 1);
@@ -2000,7 +2005,7 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
         int32_t* oi = out_idx + (int64_t)i * kmax;
         double* od = out_dist ? out_dist + (int64_t)i * kmax : nullptr;
         // own copies except i, ascending
-        for (int q = lane; q < oc && q - (q > z - oa ? 1 : 0) < kmax; q += 64) {
+        for (int q = lane; q < oc && q - (q > z - oa ? 1 : 0) < kmax; q += 32) {
             if (oa + q == z) continue;
             const int pos = q - (q > z - oa ? 1 : 0);
             oi[pos] = srow[oa + q];
@@ -2295,7 +2300,7 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     if (KNN_EXPAND_CELLS) {
         int* tie_count = (int*)(misc + 6);  // zeroed with the fail counts
         int* tie_list = (int*)head;         // the heads' scan is consumed (kb_tables_kernel)
-        kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u,
+        kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u,
                                                                          kmax, out_idx, out_dist, fail_list, fail_count,
                                                                          ftau, tie_list, tie_count);
         kb_expand_ties_kernel<<<64, 256, 0, st>>>(u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
@@ -2438,7 +2443,7 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));
     int* tie_count = (int*)(misc + 6);
     int* tie_list = (int*)head;  // the heads' scan is consumed (kb_tables_kernel)
-    kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(n, (int)u, kmax, uidx, ud2, ustart, srow, row2u,
+    kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(n, (int)u, kmax, uidx, ud2, ustart, srow, row2u,
                                                                      kmax, out_idx, out_dist, fail_list, fail_count,
                                                                      ftau, tie_list, tie_count, duo, nseg);
     kb_expand_ties_kernel<<<64, 256, 0, st>>>((int)u, kmax, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
