@@ -223,17 +223,24 @@ __device__ __forceinline__ SnnMember snn_member(const int32_t* __restrict__ knn,
     return m;
 }
 
-// Items M_j of every node: the row capacities.
+// Items M_j of every node: the row capacities.  kmax <= 31 (PACK): two nodes
+// per wave, one per 32-lane half (members in lanes 0..kmax of the half).
+template <bool PACK>
 __global__ __launch_bounds__(256) void snn_items_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
                                                         int kmax, const int64_t* __restrict__ hoff,
                                                         const int* __restrict__ bp, const int* __restrict__ split,
                                                         int64_t* __restrict__ cap) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
-        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+    constexpr int WL = PACK ? 32 : 64;  // lanes per node
+    constexpr int NPW = 64 / WL;        // nodes per wave
+    const int lane = threadIdx.x & (WL - 1);
+    const int64_t stride = (int64_t)gridDim.x * 4 * NPW;
+    for (int64_t jb = (int64_t)blockIdx.x * 4 * NPW; jb < n; jb += stride) {
+        const int64_t j = jb + (threadIdx.x / WL);
+        SnnMember m{0, 0, 0, 0};
+        if (j < n) m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
         int v = m.len;
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (lane == 0) cap[j] = v;
+        for (int o = WL / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, WL);
+        if (lane == 0 && j < n) cap[j] = v;
     }
 }
 
@@ -983,30 +990,41 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
 // finds r and checks the sets (any input: the test is exact set equality);
 // the build tiers skip these nodes and snn_copy_rows_kernel copies their
 // rows after them.
+template <bool PACK>
 __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
                                                       SnnSpec sp, int* __restrict__ src) {
-    const int lane = threadIdx.x & 63;
+    constexpr int WL = PACK ? 32 : 64;  // lanes per node (PACK: kmax <= 31, two nodes per wave)
+    constexpr int NPW = 64 / WL;
+    const int lane = threadIdx.x & (WL - 1);
+    const int half = PACK ? (int)((threadIdx.x >> 5) & 1) : 0;
     const int kmin = sp.kk[0], kmax = sp.kk[sp.nk - 1];
-    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+    // this node's lanes' bits of a wave ballot
+    auto mine = [&](unsigned long long b) -> unsigned long long {
+        return PACK ? ((half ? b >> 32 : b) & 0xffffffffull) : b;
+    };
+    const unsigned long long full = PACK ? 0xffffffffull : ~0ull;
+    for (int64_t jb = (int64_t)blockIdx.x * 4 * NPW; jb < n; jb += (int64_t)gridDim.x * 4 * NPW) {
+        const int64_t j = jb + (threadIdx.x / WL);
+        const bool live = j < n;
         int a = (int)j;
-        if (lane >= 1 && lane <= kmax) a = knn[j * kstride + lane - 1];
-        const bool bad = lane <= kmax && ((unsigned)a >= (unsigned)n || (lane >= 1 && a == (int)j));
+        if (live && lane >= 1 && lane <= kmax) a = knn[j * kstride + lane - 1];
+        const bool bad = live && lane <= kmax && ((unsigned)a >= (unsigned)n || (lane >= 1 && a == (int)j));
         int r = lane <= kmin ? a : 0x7fffffff;
-        for (int o = 32; o > 0; o >>= 1) r = min(r, __shfl_xor(r, o, 64));
-        bool ok = r < (int)j && !__any(bad);
-        if (ok) {
+        for (int o = WL / 2; o > 0; o >>= 1) r = min(r, __shfl_xor(r, o, WL));
+        bool ok = live && r < (int)j && mine(__ballot(bad)) == 0ull;
+        if (mine(__ballot(ok)) != 0ull) {  // (uniform in the node's lanes)
             int b = r;
-            if (lane >= 1 && lane <= kmax) b = knn[(int64_t)r * kstride + lane - 1];
+            if (ok && lane >= 1 && lane <= kmax) b = knn[(int64_t)r * kstride + lane - 1];
             // N+_k(j) == N+_k(r) for every graph: every member of j's k-prefix is in r's
             // (both hold k + 1 distinct rows)
-            for (int t = 0; t < sp.nk && ok; ++t) {
+            for (int t = 0; t < sp.nk; ++t) {
                 const int k = sp.kk[t];
                 bool found = lane > k;
-                for (int q = 0; q <= k; ++q) found |= a == __shfl(b, q, 64);
-                ok = __all(found);
+                for (int q = 0; q <= k; ++q) found |= a == __shfl(b, q, WL);
+                ok = ok && mine(__ballot(found)) == full;
             }
         }
-        if (lane == 0) src[j] = ok ? r : -1;
+        if (live && lane == 0) src[j] = ok ? r : -1;
     }
 }
 
@@ -1416,7 +1434,10 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     snn_split_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(hoff, hosts_s, n, split);
     // 2. row capacities
     const unsigned nblk = (unsigned)std::min<int64_t>(ccg_cdiv(n, SNN_WAVES), 16384);
-    snn_items_kernel<<<nblk, 256, 0, st>>>(knn, n, kstride, kmax, hoff, bp, split, roff);
+    if (kmax <= 31)
+        snn_items_kernel<true><<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 8), 16384), 256, 0, st>>>(
+            knn, n, kstride, kmax, hoff, bp, split, roff);
+    else snn_items_kernel<false><<<nblk, 256, 0, st>>>(knn, n, kstride, kmax, hoff, bp, split, roff);
     rc = ccg_scan_i64(ctx, roff, roff, n, st);
     if (rc) return rc;
     // 3. build: sort tier -> hash tier -> block tier -> dense tier
@@ -1430,8 +1451,13 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     int* lists = (int*)(ccount + 8);
     // copy nodes (NUMBER graphs only: RANK weights depend on the ranks)
     int* src = sp.type == CCG_SNN_NUMBER && !snn_no_copy() ? ov : nullptr;
-    if (src)
-        snn_src_kernel<<<nblk, 256, 0, st>>>(knn, n, kstride, sp, src);
+    if (src) {
+        if (kmax <= 31)
+            snn_src_kernel<true><<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 8), 16384), 256, 0, st>>>(knn, n, kstride,
+                                                                                                      sp, src);
+        else
+            snn_src_kernel<false><<<nblk, 256, 0, st>>>(knn, n, kstride, sp, src);
+    }
     snn_class_kernel<<<(unsigned)ccg_cdiv(std::max<int64_t>(n + 1, 64), 256), 256, 0, st>>>(roff, n, cls, cnt, sp.nk,
                                                                                            ov_count, src);
     rc = ccg_scan_i64(ctx, cls, cls, n, st);
