@@ -1028,21 +1028,37 @@ __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict_
     }
 }
 
+// Walks the class-3 list (the copy nodes and the hubs; hubs are skipped), one
+// wave per node: the first entry of r's row past j by a two-level search
+// (64 lanes sample the row, then 64 lanes scan the chunk: two dependent loads
+// instead of a ~9-step binary search), then the copy.
 __global__ __launch_bounds__(256) void snn_copy_rows_kernel(int64_t n, SnnSpec sp, const int* __restrict__ src,
-                                                            int64_t* __restrict__ cnt, SnnRows rows) {
+                                                            int64_t* __restrict__ cnt, SnnRows rows,
+                                                            const int* __restrict__ list,
+                                                            const int64_t* __restrict__ count) {
     if (rows.roff[n] > rows.cap) return;  // rows not written (the caller sizes and retries)
     const int lane = threadIdx.x & 63;
-    for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+    const int64_t nl = *count;
+    for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nl; f += (int64_t)gridDim.x * 4) {
+        const int64_t j = list[f];
         const int r = src[j];
-        if (r < 0) continue;
+        if (r < 0) continue;  // a hub (the bitonic / block tiers)
         const int64_t a = rows.roff[r];
         const int len = rows.rlen[r];
         // first entry of r's row with partner > j (partners ascending)
-        int lo = 0, hi = len;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (rows.nbr[a + mid] <= (int)j) lo = mid + 1;
-            else hi = mid;
+        const int step = (len + 63) >> 6;  // chunk per lane
+        const int s0 = lane * step;
+        const bool le0 = s0 < len && rows.nbr[a + s0] <= (int)j;
+        const int nle = __popcll(__ballot(le0));  // chunks whose first entry is <= j
+        int lo = 0;
+        if (nle > 0) {
+            const int c0 = (nle - 1) * step;  // the crossing lies in [c0, c0 + step]
+            const int c1 = min(c0 + step, len);
+            lo = c0;
+            for (int q0 = c0; q0 < c1; q0 += 64) {  // one pass unless the row exceeds 4096 entries
+                const int q = q0 + lane;
+                lo += __popcll(__ballot(q < c1 && rows.nbr[a + q] <= (int)j));
+            }
         }
         const int64_t o = rows.roff[j];
         int64_t c4[SNN_MAXK] = {0, 0, 0, 0};
@@ -1491,7 +1507,7 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
                                           ov2_list, ov_count + 2);
     snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,
                                                        dense, cnt, rows);
-    if (src) snn_copy_rows_kernel<<<nblk, 256, 0, st>>>(n, sp, src, cnt, rows);
+    if (src) snn_copy_rows_kernel<<<nblk, 256, 0, st>>>(n, sp, src, cnt, rows, lists + 3 * n, ccount + 3);
     rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)sp.nk * (n + 1), st);  // every graph's offsets in one scan
     if (rc) return rc;
     *cnt_out = cnt;
