@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-4 GPU step: selected -m gpu tests, then bench workloads (quick), each
+# One GPU round step: selected -m gpu tests (PYTEST_FILES, or "none"), then bench workloads
+# (WORKLOADS, BSTEPS, BENCH_EXTRA), each
 # step under its own time limit; stops at the first failure.
 mkdir -p gpurun_out/r4
 export TMPDIR=/tmp
