@@ -92,7 +92,7 @@ def parse():
     ap.add_argument("--table-k", type=int, default=48,
                     help="cell-table length K (<= 48): cells with fewer than 20 of their K nearest cells in a "
                          "bootstrap take the exact search")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
     a = ap.parse_args()
