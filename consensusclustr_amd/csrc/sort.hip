@@ -16,8 +16,9 @@
 //   rs_scatter : each tile ranks its pairs stably -- a wave takes a contiguous
 //                run of 64 * RS_IPT pairs, lanes along consecutive pairs, peers
 //                of equal digit found by one ballot per digit bit, running
-//                per-wave digit counts in LDS -- and writes them to their
-//                positions.
+//                per-wave digit counts in LDS -- puts the tile in digit order
+//                in LDS and writes it out with consecutive threads on
+//                consecutive positions of each digit's run.
 // Keys outside [0, 2^key_bits) are the caller's contract (only the low
 // key_bits bits are looked at).
 #include "ccg_internal.h"
@@ -62,6 +63,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
                                                          int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
     __shared__ int wcnt[RS_WAVES][1 << RS_MAXBITS];  // per-wave running digit counts, then prefixes
     __shared__ int goff[1 << RS_MAXBITS];
+    __shared__ int dstart[1 << RS_MAXBITS];  // tile-local first position of each digit
+    __shared__ int wsum[RS_WAVES];
+    __shared__ int2 stage[RS_THREADS * RS_IPT];
     const int nb = 1 << bits;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int t = threadIdx.x; t < RS_WAVES * nb; t += RS_THREADS) wcnt[t / nb][t % nb] = 0;
@@ -95,7 +99,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // per digit: exclusive prefix over the waves (tile order = wave order)
+    // per digit: exclusive prefix over the waves (tile order = wave order);
+    // the digit's tile total goes to dstart
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) {
         int s = 0;
 #pragma unroll
@@ -104,15 +109,42 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
             wcnt[ww][t] = s;
             s += c;
         }
+        dstart[t] = s;
     }
     __syncthreads();
+    {  // dstart -> exclusive prefix over the digits (two digits per thread)
+        const int d0 = 2 * threadIdx.x;
+        const int c0 = d0 < nb ? dstart[d0] : 0, c1 = d0 + 1 < nb ? dstart[d0 + 1] : 0;
+        int x = c0 + c1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int ex = x - c0 - c1;
+        for (int ww = 0; ww < w; ++ww) ex += wsum[ww];
+        if (d0 < nb) dstart[d0] = ex;
+        if (d0 + 1 < nb) dstart[d0 + 1] = ex + c0;
+    }
+    __syncthreads();
+    // the tile in digit order through LDS, then written out by consecutive
+    // threads (a digit's run of the tile is contiguous in the output)
 #pragma unroll
     for (int i = 0; i < RS_IPT; ++i) {
         if (base + 64 * i + lane >= n) continue;
         const unsigned dg = ((unsigned)kk[i] >> shift) & (unsigned)(nb - 1);
-        const int pos = goff[dg] + wcnt[w][dg] + rk[i];
-        kout[pos] = kk[i];
-        vout[pos] = vv[i];
+        stage[dstart[dg] + wcnt[w][dg] + rk[i]] = make_int2(kk[i], vv[i]);
+    }
+    __syncthreads();
+    const int64_t tbase = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT);
+    const int tn = (int)min((int64_t)(RS_THREADS * RS_IPT), n - tbase);
+    for (int j = threadIdx.x; j < tn; j += RS_THREADS) {
+        const int2 kv = stage[j];
+        const unsigned dg = ((unsigned)kv.x >> shift) & (unsigned)(nb - 1);
+        const int pos = goff[dg] + (j - dstart[dg]);
+        kout[pos] = kv.x;
+        vout[pos] = kv.y;
     }
 }
 
