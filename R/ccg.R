@@ -237,15 +237,40 @@ ccgLevelBootstrapKNN <- function(pcas, nboots, bootSize, kNum, BPPARAM, batch = 
     d <- .ccg_draw_bootstraps(rownames(p), bootSize * nrow(p), nboots, BPPARAM)
     list(draws = d, knns = vector("list", nboots))
   })
-  for (b0 in seq(1L, nboots, by = batch)) {
-    bs <- b0:min(nboots, b0 + batch - 1L)
-    boots <- lapply(draws, function(x) {
-      vapply(x$draws[bs], function(d) d$idx, integer(length(x$draws[[1L]]$idx)))
-    })
-    boots <- lapply(boots, function(b) if (is.matrix(b)) b else matrix(b, ncol = length(bs)))
-    res <- tryCatch(.Call(C_ccg_r_knn_boot_segments, eng, pcas, boots, as.integer(max(kNum))),
-                    error = function(e) NULL)  # e.g. a subcluster too small for a segment: searched per core
-    if (!is.null(res)) for (s in seq_along(pcas)) draws[[s]]$knns[bs] <- res[[s]]
+  kmax <- as.integer(max(kNum))
+  # a segment needs kmax + 1 distinct cells in every bootstrap: other
+  # subclusters are searched by their own ccgConsensusCore (prefetched knns NULL)
+  ok <- which(vapply(draws, function(x) {
+    all(vapply(x$draws, function(d) length(unique(d$idx)) > kmax, logical(1)))
+  }, logical(1)))
+  # the library's (segment, cell) keys are 31-bit: segments x stacked cells of
+  # one call < 2^31.  Subclusters go into groups that fit with one bootstrap
+  # each; each group's batch is cut to fit.
+  groups <- list()
+  cur <- integer(0)
+  for (s in ok) {
+    trial <- c(cur, s)
+    if (length(trial) * sum(vapply(pcas[trial], nrow, integer(1))) < 2^31) {
+      cur <- trial
+    } else {
+      if (length(cur)) groups[[length(groups) + 1L]] <- cur
+      cur <- s
+    }
+  }
+  if (length(cur)) groups[[length(groups) + 1L]] <- cur
+  for (grp in groups) {
+    ntot <- sum(vapply(pcas[grp], nrow, integer(1)))
+    bg <- max(1L, min(batch, floor((2^31 - 1) / (ntot * length(grp)))))
+    for (b0 in seq(1L, nboots, by = bg)) {
+      bs <- b0:min(nboots, b0 + bg - 1L)
+      boots <- lapply(draws[grp], function(x) {
+        vapply(x$draws[bs], function(d) d$idx, integer(length(x$draws[[1L]]$idx)))
+      })
+      boots <- lapply(boots, function(b) if (is.matrix(b)) b else matrix(b, ncol = length(bs)))
+      res <- tryCatch(.Call(C_ccg_r_knn_boot_segments, eng, pcas[grp], boots, kmax),
+                      error = function(e) NULL)  # on failure each subcluster's core searches its own
+      if (!is.null(res)) for (t in seq_along(grp)) draws[[grp[t]]]$knns[bs] <- res[[t]]
+    }
   }
   draws
 }

@@ -139,9 +139,15 @@ def launcher_check(args):
         seen = [mine]
     if world > 1 and world != args.gpus:
         raise SystemExit(f"world size {world} != --gpus {args.gpus}")
+    # the per-rank phase report of a real run, over the same gather (gloo, CPU
+    # tensors): a host-timed stand-in step per rank
+    t0 = time.perf_counter()
+    float(np.linalg.norm(np.random.default_rng(rank).random((256, 256)) @ np.eye(256)))
+    step_ms = 1000 * (time.perf_counter() - t0)
+    rep = per_rank_report(torch, dist, world, {"step_ms": step_ms, "boot_phase_ms": step_ms})
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "ranks_seen": [s.tolist() for s in seen], "backend": "gloo"}),
-              flush=True)
+        print(json.dumps({"n_gpus": world, "ranks_seen": [s.tolist() for s in seen], "backend": "gloo",
+                          "per_rank": rep}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -366,6 +372,148 @@ def workload_text(name, N, d, B, G, emul):
     return name
 
 
+CFG5_SIZES = [5000, 6000, 7000, 8000, 9000, 10000, 11000, 12000, 12000, 20000]
+
+
+def cfg5_inputs(torch, N, d, genes, B, rank, dev):
+    """BASELINE cfg5's level: N cells in 10 subclusters of 5k-20k cells with
+    pcNum d_c = 5..15 (the :356 rule's range), their PC matrices stacked
+    row-major and zero-padded to the largest d_c, and B bootstraps of every
+    subcluster (default_rng(123 + b): the same stream seed for every
+    subcluster, as the forwarded BPPARAM gives, :562-566)."""
+    pcs, pop = synth_pcs(torch, N, d, genes, 20241024 + 5, dev)
+    sizes = list(CFG5_SIZES)
+    sizes[-1] += N - sum(sizes)
+    nsub = len(sizes)
+    dcs = [5 + (10 * c) // (nsub - 1) for c in range(nsub)]
+    dpad = max(dcs)
+    perm = torch.from_numpy(np.random.default_rng(55).permutation(N)).to(dev)
+    Nof = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    cells = torch.zeros((N, dpad), dtype=torch.float64, device=dev)  # the subclusters' PCs stacked, zero-padded
+    for c in range(nsub):
+        cells[Nof[c]:Nof[c + 1], :dcs[c]] = pcs[perm[Nof[c]:Nof[c + 1]], :dcs[c]]
+    ns = [int(0.9 * m) for m in sizes]
+    bids = [rank * B + j for j in range(B)]
+    boots = [[np.random.default_rng(123 + b).integers(0, sizes[c], ns[c]).astype(np.int32) for b in bids]
+             for c in range(nsub)]
+    uniq = [[int(np.count_nonzero(np.bincount(x, minlength=sizes[c]))) for x in boots[c]] for c in range(nsub)]
+    boots_t = [torch.from_numpy(np.stack(boots[c])).to(dev) for c in range(nsub)]  # (B, n_c) local cells
+    return dict(pcs=pcs, pop=pop, popc=pop[perm], sizes=sizes, nsub=nsub, dcs=dcs, dpad=dpad, Nof=Nof, cells=cells,
+                ns=ns, bids=bids, boots=boots, uniq=uniq, boots_t=boots_t)
+
+
+def cfg5_seg_plan(torch, inp, b0, b1):
+    """Segments (subcluster c, bootstrap j) of bootstraps [b0, b1) of every
+    subcluster: their row offsets, distinct-cell counts and the rows' global
+    cell ids (block start + local cell)."""
+    segs = [(c, j) for j in range(b0, b1) for c in range(inp["nsub"])]
+    off = np.concatenate([[0], np.cumsum([inp["ns"][c] for c, _ in segs])]).astype(np.int64)
+    su = np.array([inp["uniq"][c][j] for c, j in segs], np.int32)
+    idx = torch.cat([inp["boots_t"][c][j] + int(inp["Nof"][c]) for c, j in segs])
+    return segs, off, su, idx
+
+
+def decode_union_rows(off, ln, nbr, wpk, nk, r0=0, r1=None):
+    """Union-graph rows (ccg_snn_rows_dev) of rows [r0, r1) -> per-graph
+    (i, j, w) NUMBER edge lists in (i, j) order (numpy, vectorised)."""
+    r1 = ln.size if r1 is None else r1
+    lens = ln[r0:r1].astype(np.int64)
+    i = np.repeat(np.arange(r0, r1, dtype=np.int64), lens)
+    start = np.repeat(off[r0:r1], lens)
+    pos = start + (np.arange(i.size, dtype=np.int64) - np.repeat(np.cumsum(lens) - lens, lens))
+    j = nbr[pos]
+    w = wpk.view(np.uint32)[pos]
+    out = []
+    for g in range(nk):
+        b = (w >> np.uint32(8 * g)) & np.uint32(0xFF)
+        m = b != 0
+        out.append((i[m], j[m].astype(np.int64), b[m].astype(np.float64)))
+    return out
+
+
+def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
+    """cfg5's cpu_baseline check leg: the oracle as the checker of the first
+    segmented launch set.  The batch runs again through the step's calls
+    (ccg_knn_boot_segments_dev with global ids, ONE ccg_snn_rows_dev over
+    the disjoint union, the per-segment cell silhouettes); for three
+    segments (the smallest and the largest subcluster's first bootstrap and
+    the batch's last segment) sampled kNN rows plus every exact-search row
+    must equal orc_knn_queries on the segment's rows (segment-local ids), the
+    segment's three SNN graphs must equal orc_snn of its neighbour rows, and
+    its 60 silhouette means must agree with orc_silhouette within 1e-5."""
+    import concurrent.futures as cf
+    import oracle as O
+    segs, off, su, idx = plan
+    dev = idx.device
+    n = int(off[-1])
+    dpad = inp["dpad"]
+    knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
+    eng.knn_boot_segments_t(inp["cells"], idx, off, su, 20, knn, local_ids=False)
+    cut = eng.knn_last_fallback()
+    ro = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    rl = torch.zeros(n, dtype=torch.int32, device=dev)
+    cap = 700 * n
+    nbr = torch.empty(cap, dtype=torch.int32, device=dev)
+    wpk = torch.empty(cap, dtype=torch.int32, device=dev)
+    ne = torch.zeros(len(K_NUM), dtype=torch.int64, device=dev)
+    eng.snn_rows_t(knn, K_NUM, "number", ro, rl, nbr, wpk, ne)
+    rows = torch.empty((n, dpad), dtype=torch.float64, device=dev)
+    eng.gather_rows_rm_t(inp["cells"], inp["cells"].shape[0], dpad, idx, rows)
+    nsub = inp["nsub"]
+    pick = sorted({0, max(range(nsub), key=lambda c: inp["sizes"][c]), len(segs) - 1})
+    L = labels[0].shape[1]
+    sil = {}
+    for q in pick:
+        c, j = segs[q]
+        a, b = int(off[q]), int(off[q + 1])
+        m_ = torch.empty(L, dtype=torch.float64, device=dev)
+        nc_ = torch.empty(L, dtype=torch.int32, device=dev)
+        ms_ = torch.empty(L, dtype=torch.int32, device=dev)
+        eng.silhouette_cells_t(rows[a:b], labels[c][j], cmax, inp["boots_t"][c][j], inp["sizes"][c], m_, nc_, ms_)
+        sil[q] = m_
+    torch.cuda.synchronize()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    kn = knn.cpu().numpy()
+    X_all = rows.cpu().numpy()
+    ok_snn = int(ne.min().item()) >= 0
+    offn, lnn = ro.cpu().numpy(), rl.cpu().numpy()
+    used = int(offn[-1]) if ok_snn else 0
+    nbn, wpn = nbr[:used].cpu().numpy(), wpk[:used].cpu().numpy()
+    rng = np.random.default_rng(11)
+    out = {"segments_checked": [], "knn_rows_checked": 0}
+    knn_ok, snn_ok, rel_max = True, ok_snn, 0.0
+    for q in pick:
+        c, j = segs[q]
+        a, b = int(off[q]), int(off[q + 1])
+        X = X_all[a:b]
+        loc = kn[a:b] - a
+        cq = cut[(cut >= a) & (cut < b)] - a
+        qs = np.unique(np.concatenate([cq[:2048], rng.choice(b - a, min(sample, b - a), replace=False),
+                                       [0, b - a - 1]])).astype(np.int32)
+        oi, _ = O.knn_queries(X, 20, qs, nthreads=threads)
+        knn_ok = knn_ok and bool(np.array_equal(loc[qs], oi))
+        out["knn_rows_checked"] += int(qs.size)
+        if ok_snn:
+            got = decode_union_rows(offn, lnn, nbn, wpn, len(K_NUM), a, b)
+            for g, k in enumerate(K_NUM):
+                ei, ej, ew = O.snn(np.ascontiguousarray(loc), k, "number")
+                gi, gj, gw = got[g]
+                snn_ok = snn_ok and np.array_equal(gi - a, ei) and np.array_equal(gj - a, ej) and \
+                    np.array_equal(gw, ew)
+        labs = labels[c][j].cpu().numpy()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            ref = np.asarray(list(ex.map(lambda l_: O.silhouette(X, labs[l_])[1], range(L))))
+        g_ = sil[q].cpu().numpy()
+        rel_max = max(rel_max, float((np.abs(g_ - ref) / np.maximum(np.abs(ref), 1e-300)).max()))
+        out["segments_checked"].append([int(c), int(j), b - a])
+    out["knn_exact"] = bool(knn_ok)
+    out["snn_graphs_exact"] = bool(snn_ok)
+    out["silhouette_max_rel_err"] = rel_max
+    out["silhouette_within_1e-5"] = bool(rel_max <= 1e-5)
+    out["ok"] = all(v for v in out.values() if isinstance(v, bool))
+    return out
+
+
 def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen):
     """BASELINE cfg5: one iterate=TRUE level on 100k cells (R/consensusClust.R:
     541-567).  The cells fall into 10 subclusters of 5k-20k cells with pcNum
@@ -382,26 +530,10 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     S = len(engs)
     N, B, G = args.cells, args.boots_per_gpu, world
     L = len(K_NUM) * N_RES
-    pcs, pop = synth_pcs(torch, N, args.pcs, args.genes, 20241024 + 5, dev)
-    sizes = [5000, 6000, 7000, 8000, 9000, 10000, 11000, 12000, 12000, 20000]
-    sizes[-1] += N - sum(sizes)
-    nsub = len(sizes)
-    dcs = [5 + (10 * c) // (nsub - 1) for c in range(nsub)]
-    dpad = max(dcs)
-    perm = torch.from_numpy(np.random.default_rng(55).permutation(N)).to(dev)
-    Nof = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    cells = torch.zeros((N, dpad), dtype=torch.float64, device=dev)  # the subclusters' PCs stacked, zero-padded
-    for c in range(nsub):
-        cells[Nof[c]:Nof[c + 1], :dcs[c]] = pcs[perm[Nof[c]:Nof[c + 1]], :dcs[c]]
-    popc = pop[perm]
-    ns = [int(0.9 * m) for m in sizes]
-    bids = [rank * B + j for j in range(B)]
-    # bootstrap b of subcluster c: default_rng(123 + b) draws (the same stream seed for every subcluster:
-    # BPPARAM is forwarded, :562-566)
-    boots = [[np.random.default_rng(123 + b).integers(0, sizes[c], ns[c]).astype(np.int32) for b in bids]
-             for c in range(nsub)]
-    uniq = [[int(np.count_nonzero(np.bincount(x, minlength=sizes[c]))) for x in boots[c]] for c in range(nsub)]
-    boots_t = [torch.from_numpy(np.stack(boots[c])).to(dev) for c in range(nsub)]  # (B, n_c) local cells
+    inp = cfg5_inputs(torch, N, args.pcs, args.genes, B, rank, dev)
+    pcs, sizes, nsub, dcs, dpad = inp["pcs"], inp["sizes"], inp["nsub"], inp["dcs"], inp["dpad"]
+    Nof, cells, popc, ns, bids = inp["Nof"], inp["cells"], inp["popc"], inp["ns"], inp["bids"]
+    uniq, boots_t = inp["uniq"], inp["boots_t"]
     labels = [torch.empty((B, L, ns[c]), dtype=torch.int32, device=dev) for c in range(nsub)]
     for c in range(nsub):
         for j in range(B):
@@ -411,11 +543,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     batches = [(b0, min(B, b0 + SB)) for b0 in range(0, B, SB)]
 
     def seg_plan(b0, b1):
-        segs = [(c, j) for j in range(b0, b1) for c in range(nsub)]
-        off = np.concatenate([[0], np.cumsum([ns[c] for c, _ in segs])]).astype(np.int64)
-        su = np.array([uniq[c][j] for c, j in segs], np.int32)
-        idx = torch.cat([boots_t[c][j] + int(Nof[c]) for c, j in segs])
-        return segs, off, su, idx
+        return cfg5_seg_plan(torch, inp, b0, b1)
 
     plans = [seg_plan(b0, b1) for b0, b1 in batches]
     nmax = max(int(p[1][-1]) for p in plans)
@@ -486,8 +614,15 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         e.timing(True)
         for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
             e.timing_read(w)
-    step()
+    evs = {}
+    step(evs)
     torch.cuda.synchronize()
+    phase = {"step_ms": el / args.steps * 1000,  # this rank's own timed steps (value uses the max over ranks)
+             "boot_phase_ms": evs["start"].elapsed_time(evs["boots_done"]),
+             "select_mapback_ms": evs["boots_done"].elapsed_time(evs["selected"]),
+             "allgather_ms": evs["selected"].elapsed_time(evs["gathered"]),
+             "slab_ms": evs["gathered"].elapsed_time(evs["slab_done"])}
+    per_rank = per_rank_report(torch, dist, G, phase, dev)
     kt = {}
     for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
         r = [e.timing_read(w) for e in engs]
@@ -506,6 +641,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     iso_scr = eng.timing_read("knn_screen")
     iso_tot = eng.timing_read("knn_total")
     eng.timing(False)
+    per_rank = per_rank_report(torch, dist, G, {"step_ms": el / args.steps * 1000}, dev)
     if G > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -553,6 +689,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
             "segments_per_launch": SB * nsub, "streams_per_gpu": S,
         },
         "subcluster_bootstraps_per_s": round(value * nsub, 3),
+        "per_rank": per_rank,
         "roofline": roof,
         "kernel_ms_per_step": {w: round(v[0], 3) for w, v in kt.items()},
         "kernel_launches_per_step": {w: int(v[1]) for w, v in kt.items()},
@@ -562,6 +699,9 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         out["cpu_baseline"] = cpu_baseline(pcs[:, :dm].contiguous().cpu().numpy(), B, max(ns), N, dm,
                                            args.cpu_sample_rows, coc_cols=B, coc_pairs=float(sum(P)),
                                            seg_rows=ns)
+        out["cpu_baseline"]["check"] = cfg5_check(eng, torch, inp, labels, cmax, plans[0])
+    elif rank == 0 and args.check:
+        out["cpu_baseline"] = {"check": cfg5_check(eng, torch, inp, labels, cmax, plans[0])}
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
@@ -571,6 +711,36 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     grp.close()
     if G > 1:
         dist.destroy_process_group()
+
+
+def group_ranks_seen(torch, dist, world, rank, local, grp, dev):
+    """[torch rank, HIP device, nranks and first rank of libccg's device
+    group (ccg_group_info)] of every rank, gathered over the process group:
+    the ranks libccg's RCCL communicator actually joined."""
+    mine = torch.tensor([rank, local, grp.nranks, grp.first_rank], dtype=torch.int64, device=dev)
+    if world == 1:
+        return [mine.tolist()]
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine)
+    return [g.tolist() for g in got]
+
+
+PHASES = ("step_ms", "boot_phase_ms", "select_mapback_ms", "allgather_ms", "slab_ms")
+
+
+def per_rank_report(torch, dist, world, values, dev=None):
+    """Every rank's PHASES values (ms) gathered to all ranks: a list of
+    dicts in rank order (the whole-job value is the max step; these say
+    where each rank spent it)."""
+    t = torch.tensor([float(values.get(k, float("nan"))) for k in PHASES], dtype=torch.float64,
+                     device=dev if dev is not None else "cpu")
+    if world > 1:
+        got = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(got, t)
+    else:
+        got = [t]
+    return [dict({"rank": r}, **{k: round(float(v), 3) for k, v in zip(PHASES, g.tolist())})
+            for r, g in enumerate(got)]
 
 
 def visible_gpus():
@@ -613,12 +783,6 @@ def main():
             raise SystemExit(f"world size {world} != --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    ranks_seen = [world]
-    if world > 1:  # the ranks RCCL actually connected: (rank, device) of each
-        mine = torch.tensor([rank, local], dtype=torch.int64, device=dev)
-        got = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(got, mine)
-        ranks_seen = [g.tolist() for g in got]
 
     from consensusclustr_amd import Engine
     from consensusclustr_amd.sharding import DeviceGroup, exchange_group_id, row_slabs, slab_pairs
@@ -629,6 +793,9 @@ def main():
         grp = DeviceGroup.open_rank(local, world, rank, exchange_group_id())
     else:
         grp = DeviceGroup.open([local])
+    # what libccg's own communicator saw (ccg_group_info), per rank:
+    # [torch rank, device, the group's nranks, the group's first rank]
+    ranks_seen = group_ranks_seen(torch, dist, world, rank, local, grp, dev)
     S = max(1, args.streams)
     W = WORKLOADS[args.workload]
     if args.workload == "cfg5":
@@ -708,22 +875,35 @@ def main():
     ev_k = [torch.cuda.Event() for _ in range(B)]
     ev_s = [torch.cuda.Event() for _ in range(B)]
 
-    def step_tail():
+    def mark(evs, k):
+        # phase events on torch's current stream (the tail's calls order their
+        # context streams after it and it after them), the timer step only
+        if evs is not None:
+            evs[k] = torch.cuda.Event(enable_timing=True)
+            evs[k].record()
+
+    def step_tail(evs=None):
         # selection + map-back into this rank's columns, the all-gather, this rank's co/both slab
+        mark(evs, "boots_done")
         if robust:
             eng.select_mapback_t("robust", labels, boots, N, A_local, 0, means=means, nclust=nclust,
                                  minsize=minsize, out_choice=choice)
         else:
             eng.select_mapback_t("granular", labels, boots, N, A_local, 0)
+        mark(evs, "selected")
         if emul:  # one rank of an emul-rank job: the other ranks' columns are already in place
+            mark(evs, "gathered")
             eng.cocluster_t(A_full, r0, r1, co=co, both=both)
         else:
             grp.allgather_columns_t([A_local], [cpr] * G, [A_full])
+            mark(evs, "gathered")
             grp.cocluster_sharded_t([A_full], co=[co], both=[both])
+        mark(evs, "slab_done")
 
     host_t = [0.0]  # host time spent enqueueing the bootstrap loop (the launches are asynchronous)
 
-    def step():
+    def step(evs=None):
+        mark(evs, "start")
         th = time.perf_counter()
         # S bootstraps in flight: bootstrap j runs on stream j % S with its own
         # engine context (workspaces), so one bootstrap's latency-bound SNN
@@ -745,7 +925,7 @@ def main():
         host_t[0] += time.perf_counter() - th
         for st_ in streams:
             cur.wait_stream(st_)
-        step_tail()
+        step_tail(evs)
 
     def barrier():
         if G > 1:
@@ -792,8 +972,15 @@ def main():
         e.timing(True)
         for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
             e.timing_read(w)
-    step()
+    evs = {}
+    step(evs)
     torch.cuda.synchronize()
+    phase = {"step_ms": el / args.steps * 1000,  # this rank's own timed steps (value uses the max over ranks)
+             "boot_phase_ms": evs["start"].elapsed_time(evs["boots_done"]),
+             "select_mapback_ms": evs["boots_done"].elapsed_time(evs["selected"]),
+             "allgather_ms": evs["selected"].elapsed_time(evs["gathered"]),
+             "slab_ms": evs["gathered"].elapsed_time(evs["slab_done"])}
+    per_rank = per_rank_report(torch, dist, G, phase, dev)
     kt = {}
     for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
         r = [e.timing_read(w) for e in engs]
@@ -945,23 +1132,39 @@ def main():
         "avg_launch_ms_note": "library hipEvent timer on the launch stream, the timer step after the timed region",
         "output_bytes_per_launch": 4 * P,
     }
-    # SNN rows (bytes = sum_K (n K 4 + E_K 16) per bootstrap) and
-    # silhouette (fp64 MFMA widths: 2 d u sum_l C_l over the distinct cells),
-    # per bootstrap in isolation
+    # SNN (the rows pass the drop-ins run too: ccg_snn_graphs = these kernels
+    # + a host decode) and silhouette (fp64 MFMA widths: 2 d u sum_l C_l over
+    # the distinct cells), per bootstrap in isolation.  SNN bytes are what the
+    # pass reads and writes as its interface: the kNN rows in, the union-graph
+    # rows out (8 B per union edge: partner + packed per-graph values), the row
+    # lengths and offsets and the per-graph edge offsets; SURVEY 8(d)'s
+    # per-graph (i, j, w) lists (16 B per edge per graph) are no longer
+    # formed on the device.
     snn_ms = iso_snn[0] / max(iso_snn[1], 1)
     sil_ms = iso_sil[0] / max(iso_sil[1], 1)
-    snn_bytes = sum(n * k * 4 for k in K_NUM) + 16 * sum(iso_edges) / max(nis, 1)
+    nk_ = len(K_NUM)
+    e_union = iso_edges[-1] / max(nis, 1)  # the largest k's graph is the union graph
+    snn_bytes = n * max(K_NUM) * 4 + 8 * e_union + n * 4 + (n + 1) * 8 + nk_ * (n + 1) * 8
+    snn_bytes_survey = sum(n * k * 4 for k in K_NUM) + 16 * sum(iso_edges) / max(nis, 1)
+    snn_traffic = None
+    if os.path.exists(args.traffic_json) and args.workload == "cfg3":
+        with open(args.traffic_json) as f:
+            snn_traffic = json.load(f).get("snn_bytes_per_boot")
     sil_flop = 2.0 * d * u_iso * iso_npres / max(nis, 1)
     if not robust:
         sil_ms = 0.0
     roof_snn = {
-        "kernel": "SNN union-graph rows (ccg_snn_rows_dev: host lists, bitonic build tiers, copy rows)",
+        "kernel": "SNN union-graph rows pass (ccg_snn_rows_dev; the same kernels ccg_snn_graphs runs for the R and "
+                  "Python drop-ins: host lists, size-class build tiers, copy rows)",
         "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
         "achieved": round(snn_bytes / (snn_ms * 1e-3) / 1e9, 1),
         "frac": round(snn_bytes / (snn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-        "traffic": None,
-        "algorithmic_per_launch": f"sum_K (n K 4 + E_K 16) = {snn_bytes:.3e} B per bootstrap (E_K the edges of "
-                                  f"graph K), SURVEY 8(d)",
+        "traffic": snn_traffic,
+        "algorithmic_per_launch": f"n kmax 4 (kNN in) + 8 E_union + 12 n + 8 nk (n+1) (rows, offsets, per-graph "
+                                  f"offsets out) = {snn_bytes:.3e} B per bootstrap (E_union = {e_union:.0f})",
+        "survey_8d_bytes_per_boot": round(snn_bytes_survey),
+        "survey_8d_note": "SURVEY 8(d)'s sum_K (n K 4 + E_K 16) counts per-graph (i, j, w) lists, which neither "
+                          "the bench nor the drop-ins write on the device (host decode from the rows)",
         "ms_per_boot": round(snn_ms, 4),
     }
     roof_sil = {
@@ -1014,6 +1217,11 @@ def main():
         "kernel_ms_per_step": per_step,
         "kernel_ms_per_step_note": "library hipEvent timers over one extra step after the timed region "
                                    "(bootstraps overlap, so kernel times sum to more than the step)",
+        "per_rank": per_rank,
+        "per_rank_note": "step_ms: each rank's own timed-region step (value uses the max over ranks); the "
+                         "phases come from torch-stream events in the extra timer step: the bootstrap loop, "
+                         "selection + map-back, the RCCL all-gather of the assignment columns, this rank's "
+                         "co/both row slab",
         "host_enqueue_ms_per_step": round(host_ms, 3),
         "host_launch_ms_per_boot_idle_gpu": round(host_idle_ms, 3),
         "cocluster_avg_ms": round(coc_ms, 3),

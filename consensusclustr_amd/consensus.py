@@ -124,11 +124,9 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
         raise ValueError(f"knn must be {n} x {kmax}, got {knn.shape}")
     fn = _cluster_fn(clusterFun)
     labels = []
-    order = np.argsort(kNum, kind="stable")
-    graphs = eng.snn_multi(knn, [int(kNum[t]) for t in order], "number")  # every k in one pass, :656-658
-    graph_of = {int(kNum[t]): graphs[g] for g, t in enumerate(order)}
-    for k in kNum:  # :653-654, k outer, resolution inner
-        ei, ej, w = graph_of[int(k)]
+    graphs = eng.snn_multi(knn, [int(k) for k in kNum], "number")  # every k in one pass, :656-658
+    for g, k in enumerate(kNum):  # :653-654, k outer, resolution inner
+        ei, ej, w = graphs[g]
         for res in resRange:
             labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
     lab = np.stack(labels)
@@ -447,11 +445,9 @@ def null_statistics(pca_nulls, kNum=K_NUM, clusterFun="leiden", resRange=NULL_RE
     for t, X, (knn, _) in zip(ok, mats, knns):
         n = X.shape[0]
         labels = []
-        order = np.argsort(kNum, kind="stable")
-        graphs = eng.snn_multi(np.ascontiguousarray(knn), [int(kNum[t]) for t in order], "number")
-        graph_of = {int(kNum[t]): graphs[g] for g, t in enumerate(order)}
-        for k in kNum:  # getClustAssignments' k-outer / resolution-inner loop (:653-654)
-            ei, ej, w = graph_of[int(k)]
+        graphs = eng.snn_multi(np.ascontiguousarray(knn), [int(k) for k in kNum], "number")
+        for g, k in enumerate(kNum):  # getClustAssignments' k-outer / resolution-inner loop (:653-654)
+            ei, ej, w = graphs[g]
             for res in resRange:
                 labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
         lab = np.stack(labels)

@@ -49,6 +49,7 @@ extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
     c->ntimers = c->cap_timers = c->used_timers = 0;
     c->d_err = nullptr;
     c->snn_row_reserve = 0;
+    c->snn_stage = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -76,6 +77,7 @@ extern "C" int ccg_close(ccg_ctx* ctx) {
         (void)hipEventDestroy(ctx->timers[t].stop);
     }
     free(ctx->timers);
+    ccg_snn_stage_free(ctx);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -129,6 +131,18 @@ void* ccg_ws(ccg_ctx* ctx, int slot, size_t bytes) {
     // Growth: let in-flight work that may still read the old buffer finish.
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
+    // state that points into the old buffer goes with it: the kNN's zeroed-
+    // counter marks (re-zeroed on the next call) and the exact-search row list
+    // of ccg_knn_last_fallback
+    const char* old = (const char*)ctx->ws[slot];
+    const size_t oldb = ctx->ws_bytes[slot];
+    auto inside = [&](const void* p) { return old && p && (const char*)p >= old && (const char*)p < old + oldb; };
+    if (inside(ctx->kb_zeroed)) ctx->kb_zeroed = nullptr;
+    if (inside(ctx->fx_zeroed)) ctx->fx_zeroed = nullptr;
+    if (inside(ctx->last_fail_list) || inside(ctx->last_fail_count)) {
+        ctx->last_fail_list = nullptr;
+        ctx->last_fail_count = nullptr;
+    }
     if (ctx->ws[slot]) (void)hipFree(ctx->ws[slot]);
     ctx->ws[slot] = nullptr;
     ctx->ws_bytes[slot] = 0;

@@ -81,6 +81,7 @@ struct ccg_ctx {
     hipStream_t stream;
     int* d_err;  // device word of CCG_DERR_* bits
     int64_t snn_row_reserve;  // SNN row entries reserved by the per-graph API (0 = default)
+    void* snn_stage;          // host-staged SNN rows of the last ccg_snn_graphs call (snn.hip)
     void* ws[WS_NSLOTS];
     size_t ws_bytes[WS_NSLOTS];
     ccg_knn_stats last_stats;
@@ -118,6 +119,9 @@ int ccg_hip_fail(hipError_t e, const char* what, const char* file, int line);
             return CCG_EINVAL;                                            \
         }                                                                 \
     } while (0)
+
+// Frees the host staging of ccg_snn_graphs (ccg_close).
+void ccg_snn_stage_free(ccg_ctx* ctx);
 
 // Reads and clears ctx->d_err (synchronising the device); returns CCG_OK or
 // the status code of the first error bit with the message set.

@@ -31,6 +31,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "ccg_internal.h"
 
@@ -985,11 +987,14 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
 // rows, and their sets N+_k = {j} u knn_k(j) coincide for every k of kNum
 // (whenever the zero-distance group fits in the smallest k + 1).  For NUMBER
 // weights |N+_k(j) n N+_k(p)| depend on those sets only, so such a node j has
-// the same weight to every partner as the node r = min N+_kmin(j) < j, and
-// its row (partners p > j) is the part of r's row past j.  snn_src_kernel
-// finds r and checks the sets (any input: the test is exact set equality);
-// the build tiers skip these nodes and snn_copy_rows_kernel copies their
-// rows after them.
+// the same weight to every partner as the node r = knn(j)[0] < j (the
+// cell's lowest other row), and its row (partners p > j) is the part of r's
+// row past j.  snn_src_kernel checks the sets (any input: the test is exact
+// set equality); the build tiers skip these nodes and snn_copy_rows_kernel
+// copies their rows after them, from the end of the src chain (the one node
+// of the chain that is built).  Round 4 took r = min N+_kmin(j), which is a
+// copy only when the cell's row is the smallest of the whole set: it caught
+// ~23% of the copies (cfg3: ~7k of ~30k nodes skipped instead of ~30k).
 template <bool PACK>
 __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
                                                       SnnSpec sp, int* __restrict__ src) {
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict_
     constexpr int NPW = 64 / WL;
     const int lane = threadIdx.x & (WL - 1);
     const int half = PACK ? (int)((threadIdx.x >> 5) & 1) : 0;
-    const int kmin = sp.kk[0], kmax = sp.kk[sp.nk - 1];
+    const int kmax = sp.kk[sp.nk - 1];
     // this node's lanes' bits of a wave ballot
     auto mine = [&](unsigned long long b) -> unsigned long long {
         return PACK ? ((half ? b >> 32 : b) & 0xffffffffull) : b;
@@ -1009,9 +1014,10 @@ __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict_
         int a = (int)j;
         if (live && lane >= 1 && lane <= kmax) a = knn[j * kstride + lane - 1];
         const bool bad = live && lane <= kmax && ((unsigned)a >= (unsigned)n || (lane >= 1 && a == (int)j));
-        int r = lane <= kmin ? a : 0x7fffffff;
-        for (int o = WL / 2; o > 0; o >>= 1) r = min(r, __shfl_xor(r, o, WL));
-        bool ok = live && r < (int)j && mine(__ballot(bad)) == 0ull;
+        // candidate: the first neighbour (a copy of j's cell sits there: copies are at
+        // distance 0, ordered by row, so it is the cell's lowest other row)
+        const int r = __shfl(a, 1, WL);
+        bool ok = live && r >= 0 && r < (int)j && mine(__ballot(bad)) == 0ull;
         if (mine(__ballot(ok)) != 0ull) {  // (uniform in the node's lanes)
             int b = r;
             if (ok && lane >= 1 && lane <= kmax) b = knn[(int64_t)r * kstride + lane - 1];
@@ -1041,8 +1047,9 @@ __global__ __launch_bounds__(256) void snn_copy_rows_kernel(int64_t n, SnnSpec s
     const int64_t nl = *count;
     for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nl; f += (int64_t)gridDim.x * 4) {
         const int64_t j = list[f];
-        const int r = src[j];
+        int r = src[j];
         if (r < 0) continue;  // a hub (the bitonic / block tiers)
+        while (src[r] >= 0) r = src[r];  // the built end of the chain (src[x] < x: no cycles)
         const int64_t a = rows.roff[r];
         const int len = rows.rlen[r];
         // first entry of r's row with partner > j (partners ascending)
@@ -1601,6 +1608,186 @@ extern "C" int ccg_snn_reserve(ccg_ctx* ctx, int64_t entries) {
     return CCG_OK;
 }
 
+// ------------------------------------------------ host consumers (R, Python) --
+// What a host clustering call (igraph::make_graph + cluster_leiden, :656-658)
+// needs is every kNum graph as an edge list.  The device builds the union
+// graph's rows once (snn_build: the same kernels ccg_snn_rows_dev runs); the
+// rows -- 8 B per union edge, partner + packed per-graph values -- and the
+// per-graph row offsets go to pinned host memory the context owns, and each
+// graph's (i, j, w) list is decoded from them on the host.  The device work is
+// the rows pass alone (no per-graph emit), and PCIe carries 8 B per union edge
+// instead of 16 B per edge per graph.
+struct SnnStage {
+    int64_t n = 0;
+    SnnSpec sp{};
+    int64_t* roff = nullptr;   // n + 1 capacity-based row offsets
+    int32_t* rlen = nullptr;   // n used lengths
+    int64_t* cnt = nullptr;    // nk (n + 1): per-graph exclusive scans of the row edge counts
+    int32_t* nbr = nullptr;    // roff[n] partners
+    uint32_t* wpk = nullptr;   // roff[n] packed per-graph values
+    size_t cap_n = 0, cap_l = 0, cap_e = 0, cap_w = 0, cap_c = 0;
+    bool valid = false;
+};
+
+static void snn_stage_release(SnnStage* s) {
+    if (s->roff) (void)hipHostFree(s->roff);
+    if (s->rlen) (void)hipHostFree(s->rlen);
+    if (s->cnt) (void)hipHostFree(s->cnt);
+    if (s->nbr) (void)hipHostFree(s->nbr);
+    if (s->wpk) (void)hipHostFree(s->wpk);
+    s->roff = nullptr;
+    s->rlen = nullptr;
+    s->cnt = nullptr;
+    s->nbr = nullptr;
+    s->wpk = nullptr;
+    s->cap_n = s->cap_l = s->cap_e = s->cap_w = s->cap_c = 0;
+}
+
+void ccg_snn_stage_free(ccg_ctx* ctx) {
+    if (!ctx || !ctx->snn_stage) return;
+    SnnStage* s = (SnnStage*)ctx->snn_stage;
+    snn_stage_release(s);
+    delete s;
+    ctx->snn_stage = nullptr;
+}
+
+template <typename T>
+static int snn_host_grow(T** p, size_t* cap, size_t want) {
+    if (*cap >= want && *p) return CCG_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t w = want + want / 8 + 64;
+    CCG_HIP(hipHostMalloc((void**)p, sizeof(T) * w, hipHostMallocDefault));
+    *cap = w;
+    return CCG_OK;
+}
+
+static double snn_host_weight(const SnnSpec& sp, unsigned v, int t) {
+    const unsigned b = (v >> (8 * t)) & 0xFFu;
+    if (sp.type == CCG_SNN_NUMBER) return (double)b;
+    const double w = (double)sp.kk[t] - 0.5 * (double)b;
+    return w < 1e-6 ? 1e-6 : w;
+}
+
+extern "C" int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk,
+                              int type, int64_t* nedges) {
+    CCG_REQUIRE(ctx && knn && ks && nedges, "ccg_snn_graphs: NULL argument");
+    CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1 && kstride >= 1, "ccg_snn_graphs: bad sizes");
+    SnnSpec sp;
+    int rc = snn_spec(ks, nk, type, kstride, &sp);
+    if (rc) return rc;
+    for (int64_t t = 0; t < n * kstride; ++t)
+        CCG_REQUIRE(knn[t] >= 0 && knn[t] < n && knn[t] != t / kstride,
+                    "ccg_snn_graphs: neighbour index out of range or self at %lld", (long long)t);
+    CCG_HIP(hipSetDevice(ctx->device));
+    if (!ctx->snn_stage) ctx->snn_stage = new SnnStage();
+    SnnStage* S = (SnnStage*)ctx->snn_stage;
+    S->valid = false;
+    hipStream_t st = ctx->stream;
+    const int kmax = ks[nk - 1];
+    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
+    if (!dknn) return CCG_ENOMEM;
+    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
+    rc = snn_host_grow(&S->roff, &S->cap_n, (size_t)n + 1);
+    if (rc) return rc;
+    rc = snn_host_grow(&S->rlen, &S->cap_l, (size_t)n);
+    if (rc) return rc;
+    rc = snn_host_grow(&S->cnt, &S->cap_c, (size_t)nk * (n + 1));
+    if (rc) return rc;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const int64_t rcap =
+            ctx->snn_row_reserve > 0 ? ctx->snn_row_reserve : (int64_t)SNN_ROW_RESERVE * n * (kmax + 1);
+        char* rbuf = (char*)ccg_ws(ctx, WS_SNN_ROWS,
+                                   (sizeof(int32_t) + sizeof(uint32_t)) * rcap + sizeof(int32_t) * (n + 64));
+        if (!rbuf) return CCG_ENOMEM;
+        int32_t* nbr = (int32_t*)rbuf;
+        uint32_t* wpk = (uint32_t*)(nbr + rcap);
+        int32_t* rlen = (int32_t*)(wpk + rcap);
+        int64_t* cnt = nullptr;
+        const int64_t* roff = nullptr;
+        rc = snn_build(ctx, dknn, n, kstride, sp, st, nbr, wpk, rcap, nullptr, rlen, &cnt, &roff);
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(S->roff, roff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        const int64_t need = S->roff[n];
+        if (need > rcap) {  // the rows did not fit the reservation: grow it and rerun
+            ctx->snn_row_reserve = need + need / 8;
+            continue;
+        }
+        rc = snn_host_grow(&S->nbr, &S->cap_e, (size_t)std::max<int64_t>(need, 1));
+        if (rc) return rc;
+        rc = snn_host_grow(&S->wpk, &S->cap_w, (size_t)std::max<int64_t>(need, 1));
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(S->rlen, rlen, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipMemcpyAsync(S->cnt, cnt, sizeof(int64_t) * nk * (n + 1), hipMemcpyDeviceToHost, st));
+        if (need > 0) {
+            CCG_HIP(hipMemcpyAsync(S->nbr, nbr, sizeof(int32_t) * need, hipMemcpyDeviceToHost, st));
+            CCG_HIP(hipMemcpyAsync(S->wpk, wpk, sizeof(uint32_t) * need, hipMemcpyDeviceToHost, st));
+        }
+        rc = ccg_take_device_error(ctx);  // synchronises; an invalid index raised on the device fails here
+        if (rc) return rc;
+        S->n = n;
+        S->sp = sp;
+        S->valid = true;
+        for (int t = 0; t < nk; ++t) nedges[t] = S->cnt[(int64_t)t * (n + 1) + n] - S->cnt[(int64_t)t * (n + 1)];
+        return CCG_OK;
+    }
+    ccg_set_error("ccg_snn_graphs: row reservation could not be satisfied");
+    return CCG_ENOMEM;
+}
+
+extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t* out_j, double* out_w,
+                                   int64_t cap) {
+    CCG_REQUIRE(ctx, "ccg_snn_graph_fetch: NULL ctx");
+    SnnStage* S = (SnnStage*)ctx->snn_stage;
+    CCG_REQUIRE(S && S->valid, "ccg_snn_graph_fetch: no graphs staged (call ccg_snn_graphs first)");
+    CCG_REQUIRE(t >= 0 && t < S->sp.nk, "ccg_snn_graph_fetch: graph %d of %d", t, S->sp.nk);
+    const int64_t n = S->n;
+    const int64_t* c = S->cnt + (int64_t)t * (n + 1);
+    const int64_t ne = c[n] - c[0];
+    if (cap < ne) {
+        ccg_set_error("ccg_snn_graph_fetch: capacity %lld < %lld edges", (long long)cap, (long long)ne);
+        return CCG_ECAP;
+    }
+    const SnnSpec sp = S->sp;
+    auto work = [&](int64_t j0, int64_t j1) {
+        for (int64_t j = j0; j < j1; ++j) {
+            int64_t e = c[j] - c[0];
+            const int64_t ro = S->roff[j];
+            const int u = S->rlen[j];
+            for (int q = 0; q < u; ++q) {
+                const unsigned v = S->wpk[ro + q];
+                const unsigned b = (v >> (8 * t)) & 0xFFu;
+                if (sp.type == CCG_SNN_NUMBER ? b == 0u : b == 0xFFu) continue;
+                if (out_i) out_i[e] = (int32_t)j;
+                if (out_j) out_j[e] = S->nbr[ro + q];
+                if (out_w) out_w[e] = snn_host_weight(sp, v, t);
+                ++e;
+            }
+        }
+    };
+    // rows split by edge count over the host's threads (each row's slots are
+    // fixed by the per-graph offsets, so the output is independent of the split)
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (ne < (1 << 16)) nt = 1;
+    if (nt == 1) {
+        work(0, n);
+        return CCG_OK;
+    }
+    std::vector<std::thread> th;
+    int64_t j0 = 0;
+    for (unsigned q = 0; q < nt; ++q) {
+        const int64_t target = c[0] + (ne * (int64_t)(q + 1)) / nt;
+        int64_t j1 = q + 1 == nt ? n : (int64_t)(std::lower_bound(c, c + n, target) - c);
+        j1 = std::max(j1, j0);
+        th.emplace_back(work, j0, j1);
+        j0 = j1;
+    }
+    for (auto& x : th) x.join();
+    return CCG_OK;
+}
+
 extern "C" int ccg_snn_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k, int type,
                            int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap, int64_t* d_nedges,
                            void* stream) {
@@ -1617,40 +1804,16 @@ extern "C" int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                        int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap, int64_t* nedges) {
     CCG_REQUIRE(ctx && knn && nedges, "ccg_snn: NULL argument");
     CCG_REQUIRE(n >= 1 && kstride >= 1, "ccg_snn: bad sizes");
-    CCG_HIP(hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    for (int64_t t = 0; t < n * kstride; ++t)
-        CCG_REQUIRE(knn[t] >= 0 && knn[t] < n && knn[t] != t / kstride,
-                    "ccg_snn: neighbour index out of range or self at %lld", (long long)t);
-    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
-    int64_t* dne = (int64_t*)ccg_ws(ctx, WS_HOST_E, 64);
-    int32_t* di = cap > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * cap) : nullptr;
-    int32_t* dj = cap > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * cap) : nullptr;
-    double* dw = cap > 0 ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * cap) : nullptr;
-    if (!dknn || !dne || (cap > 0 && (!di || !dj || !dw))) return CCG_ENOMEM;
-    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
+    CCG_REQUIRE(k >= 1 && k <= kstride, "ccg_snn: need 1 <= k <= kstride");
     int64_t ne = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        int rc = ccg_snn_dev(ctx, dknn, n, kstride, k, type, di, dj, dw, cap, dne, st);
-        if (rc) return rc;
-        CCG_HIP(hipMemcpyAsync(&ne, dne, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipStreamSynchronize(st));
-        if (ne >= 0) break;
-        ctx->snn_row_reserve = -ne + (-ne) / 8;  // rows did not fit the reservation: grow and rerun
-    }
-    CCG_REQUIRE(ne >= 0, "ccg_snn: row reservation could not be satisfied");
+    int rc = ccg_snn_graphs(ctx, knn, n, kstride, &k, 1, type, &ne);
+    if (rc) return rc;
     *nedges = ne;
     if (ne > cap) {
         ccg_set_error("ccg_snn: capacity %lld < required %lld edges", (long long)cap, (long long)ne);
         return CCG_ECAP;
     }
-    if (ne > 0) {
-        CCG_HIP(hipMemcpyAsync(out_i, di, sizeof(int32_t) * ne, hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipMemcpyAsync(out_j, dj, sizeof(int32_t) * ne, hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipMemcpyAsync(out_w, dw, sizeof(double) * ne, hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipStreamSynchronize(st));
-    }
-    return CCG_OK;
+    return ccg_snn_graph_fetch(ctx, 0, out_i, out_j, out_w, cap);
 }
 
 extern "C" int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk, int type,
@@ -1658,59 +1821,18 @@ extern "C" int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int ks
                              int64_t* nedges) {
     CCG_REQUIRE(ctx && knn && ks && nedges, "ccg_snn_multi: NULL argument");
     CCG_REQUIRE(n >= 1 && kstride >= 1 && nk >= 1 && nk <= SNN_MAXK, "ccg_snn_multi: bad sizes");
-    CCG_HIP(hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    for (int64_t t = 0; t < n * kstride; ++t)
-        CCG_REQUIRE(knn[t] >= 0 && knn[t] < n && knn[t] != t / kstride,
-                    "ccg_snn_multi: neighbour index out of range or self at %lld", (long long)t);
-    int64_t tot = 0;
-    for (int t = 0; t < nk; ++t) tot += caps ? std::max<int64_t>(caps[t], 0) : 0;
-    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
-    int64_t* dne = (int64_t*)ccg_ws(ctx, WS_HOST_E, 64);
-    int32_t* di = tot > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * tot) : nullptr;
-    int32_t* dj = tot > 0 ? (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * tot) : nullptr;
-    double* dw = tot > 0 ? (double*)ccg_ws(ctx, WS_HOST_D, sizeof(double) * tot) : nullptr;
-    if (!dknn || !dne || (tot > 0 && (!di || !dj || !dw))) return CCG_ENOMEM;
-    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
-    int32_t* oi[SNN_MAXK];
-    int32_t* oj[SNN_MAXK];
-    double* ow[SNN_MAXK];
-    int64_t dc[SNN_MAXK];
-    int64_t* dn[SNN_MAXK];
-    int64_t o = 0;
-    for (int t = 0; t < nk; ++t) {
-        dc[t] = caps ? std::max<int64_t>(caps[t], 0) : 0;
-        oi[t] = dc[t] ? di + o : nullptr;
-        oj[t] = dc[t] ? dj + o : nullptr;
-        ow[t] = dc[t] ? dw + o : nullptr;
-        dn[t] = dne + t;
-        o += dc[t];
-    }
-    int64_t ne[SNN_MAXK];
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        int rc = ccg_snn_multi_dev(ctx, dknn, n, kstride, ks, nk, type, oi, oj, ow, dc, dn, st);
-        if (rc) return rc;
-        CCG_HIP(hipMemcpyAsync(ne, dne, sizeof(int64_t) * nk, hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipStreamSynchronize(st));
-        if (ne[0] >= 0) break;
-        ctx->snn_row_reserve = -ne[0] + (-ne[0]) / 8;  // rows did not fit the reservation: grow and rerun
-    }
-    CCG_REQUIRE(ne[0] >= 0, "ccg_snn_multi: row reservation could not be satisfied");
+    int rc = ccg_snn_graphs(ctx, knn, n, kstride, ks, nk, type, nedges);
+    if (rc) return rc;
     bool short_cap = false;
-    for (int t = 0; t < nk; ++t) {
-        nedges[t] = ne[t];
-        short_cap |= ne[t] > dc[t];
-    }
+    for (int t = 0; t < nk; ++t) short_cap |= !caps || nedges[t] > caps[t];
     if (short_cap) {
         ccg_set_error("ccg_snn_multi: capacities smaller than the edge counts (reported in nedges)");
         return CCG_ECAP;
     }
-    for (int t = 0; t < nk; ++t)
-        if (ne[t] > 0) {
-            CCG_HIP(hipMemcpyAsync(out_i[t], oi[t], sizeof(int32_t) * ne[t], hipMemcpyDeviceToHost, st));
-            CCG_HIP(hipMemcpyAsync(out_j[t], oj[t], sizeof(int32_t) * ne[t], hipMemcpyDeviceToHost, st));
-            CCG_HIP(hipMemcpyAsync(out_w[t], ow[t], sizeof(double) * ne[t], hipMemcpyDeviceToHost, st));
-        }
-    CCG_HIP(hipStreamSynchronize(st));
+    for (int t = 0; t < nk; ++t) {
+        rc = ccg_snn_graph_fetch(ctx, t, out_i ? out_i[t] : nullptr, out_j ? out_j[t] : nullptr,
+                                 out_w ? out_w[t] : nullptr, caps[t]);
+        if (rc) return rc;
+    }
     return CCG_OK;
 }

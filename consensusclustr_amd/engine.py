@@ -192,43 +192,35 @@ class Engine:
         return self.last_knn_stats if stats else None
 
     def snn(self, knn_idx, k, type="number"):
-        """SNN edges i<j sorted by (i, j) with weights (ccg_snn)."""
-        knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
-        n, ks = knn_idx.shape
-        t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
-        ne = ctypes.c_int64(0)
-        rc = self.lib.ccg_snn(self.ctx, _ptr(knn_idx), n, ks, k, t, None, None, None, 0, ctypes.byref(ne))
-        if rc not in (_lib.CCG_OK, _lib.CCG_ECAP):
-            check(rc)
-        m = ne.value
+        """SNN edges i<j sorted by (i, j) with weights (ccg_snn_graphs +
+        ccg_snn_graph_fetch: one device pass, decoded on the host)."""
+        return self.snn_multi(knn_idx, [k], type)[0]
+
+    def _snn_fetch(self, t, m):
         ei = np.empty(m, np.int32)
         ej = np.empty(m, np.int32)
         w = np.empty(m, np.float64)
-        check(self.lib.ccg_snn(self.ctx, _ptr(knn_idx), n, ks, k, t, _ptr(ei), _ptr(ej), _ptr(w), m,
-                               ctypes.byref(ne)))
+        check(self.lib.ccg_snn_graph_fetch(self.ctx, t, _ptr(ei), _ptr(ej), _ptr(w), m))
         return ei, ej, w
 
     def snn_multi(self, knn_idx, ks, type="number"):
-        """Every graph of ks (ascending) from one pass (ccg_snn_multi):
-        a list of (i, j, w) edge lists, one per k."""
+        """The graph of every k in ks (any order, repeats allowed) from one
+        device pass per 4 distinct values (ccg_snn_graphs: the union-graph
+        rows, staged on the host; ccg_snn_graph_fetch decodes each graph).
+        Returns a list of (i, j, w) edge lists aligned with ks."""
         knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
         n, kst = knn_idx.shape
-        nk = len(ks)
         t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
-        karr = (ctypes.c_int * nk)(*ks)
-        ne = (ctypes.c_int64 * nk)()
-        P = _vp * nk
-        zero = (ctypes.c_int64 * nk)()
-        rc = self.lib.ccg_snn_multi(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, P(), P(), P(), zero, ne)
-        if rc not in (_lib.CCG_OK, _lib.CCG_ECAP):
-            check(rc)
-        outs = [(np.empty(ne[g], np.int32), np.empty(ne[g], np.int32), np.empty(ne[g], np.float64))
-                for g in range(nk)]
-        caps = (ctypes.c_int64 * nk)(*[ne[g] for g in range(nk)])
-        check(self.lib.ccg_snn_multi(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t,
-                                     P(*[_ptr(o[0]) for o in outs]), P(*[_ptr(o[1]) for o in outs]),
-                                     P(*[_ptr(o[2]) for o in outs]), caps, ne))
-        return outs
+        uk = sorted({int(k) for k in ks})
+        got = {}
+        for c0 in range(0, len(uk), 4):  # the library builds at most 4 graphs per pass
+            chunk = uk[c0:c0 + 4]
+            nk = len(chunk)
+            ne = (ctypes.c_int64 * nk)()
+            check(self.lib.ccg_snn_graphs(self.ctx, _ptr(knn_idx), n, kst, (ctypes.c_int * nk)(*chunk), nk, t, ne))
+            for g, k in enumerate(chunk):
+                got[k] = self._snn_fetch(g, ne[g])
+        return [got[int(k)] for k in ks]
 
     def silhouette_cells(self, x, labels, cell, ncell, cmax=None):
         """ccg_silhouette_cells: means over bootstrap rows x whose cells are

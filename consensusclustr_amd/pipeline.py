@@ -186,18 +186,31 @@ def level_bootstrap_knn(pcas, nboots, bootSize, boot_seed, kmax, engine, batch=3
     out = [None] * len(pcas)
     for s in ok:
         out[s] = np.empty((nboots, boots[s].shape[1], kmax), np.int32)
-    # keep nseg x Ntot inside the library's 31-bit (segment, cell) keys
-    Ntot = sum(pcas[s].shape[0] for s in ok)
-    if ok:
-        batch = max(1, min(batch, (2 ** 31 - 1) // max(1, Ntot * len(ok))))
-    for b0 in range(0, nboots, batch):
-        b1 = min(nboots, b0 + batch)
-        if not ok:
-            break
-        res = engine.knn_boot_segments([pcas[s] for s in ok], [boots[s][b0:b1] for s in ok], kmax=kmax,
-                                       want_dist=False)
-        for s, (idx, _) in zip(ok, res):
-            out[s][b0:b1] = idx
+    # the library's (segment, cell) keys are 31-bit: a call's segments x its
+    # stacked cells must stay below 2^31.  Subclusters go into groups that fit
+    # with one bootstrap each; each group's batch is cut to fit.
+    groups, cur = [], []
+    for s in ok:
+        trial = cur + [s]
+        if len(trial) * sum(pcas[t].shape[0] for t in trial) < 2 ** 31:
+            cur = trial
+            continue
+        if cur:
+            groups.append(cur)
+        cur = [s] if pcas[s].shape[0] < 2 ** 31 else []
+        if not cur:  # too large for any segment call: its own consensus_cluster searches it
+            out[s] = None
+    if cur:
+        groups.append(cur)
+    for grp in groups:
+        Ntot = sum(pcas[s].shape[0] for s in grp)
+        bg = max(1, min(batch, (2 ** 31 - 1) // (Ntot * len(grp))))
+        for b0 in range(0, nboots, bg):
+            b1 = min(nboots, b0 + bg)
+            res = engine.knn_boot_segments([pcas[s] for s in grp], [boots[s][b0:b1] for s in grp], kmax=kmax,
+                                           want_dist=False)
+            for s, (idx, _) in zip(grp, res):
+                out[s][b0:b1] = idx
     return out
 
 

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 4
+#define CCG_ABI_VERSION 5
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -263,7 +263,8 @@ int ccg_knn_segments(ccg_ctx* ctx, const double* rows, int64_t n, int d,
  * w = max(k - r/2, 1e-6), r = min over shared s of rank_i(s) + rank_j(s),
  * self rank 0, neighbours 1..k.
  * Host flavour: if cap < required, returns CCG_ECAP with *nedges = required
- * (call with cap = 0 to size). */
+ * (call with cap = 0 to size; the graph stays staged for
+ * ccg_snn_graph_fetch(ctx, 0, ...)). */
 int ccg_snn(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, int k,
             int type, int32_t* out_i, int32_t* out_j, double* out_w,
             int64_t cap, int64_t* nedges);
@@ -287,12 +288,32 @@ int ccg_snn_multi_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n,
                       int64_t* const* d_nedges, void* stream);
 
 /* Host flavour of ccg_snn_multi_dev (knn, outputs and caps host; nedges a
- * host array of nk counts).  If some caps[t] < nedges[t] (call with caps all
- * 0 to size) returns CCG_ECAP with every nedges[t] set and no edges copied. */
+ * host array of nk counts): ccg_snn_graphs + ccg_snn_graph_fetch of every
+ * graph.  If some caps[t] < nedges[t] (call with caps all 0 to size) returns
+ * CCG_ECAP with every nedges[t] set and no edges copied; the graphs stay
+ * staged, so a caller may fetch them (ccg_snn_graph_fetch) instead of calling
+ * again. */
 int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                   const int* ks, int nk, int type, int32_t* const* out_i,
                   int32_t* const* out_j, double* const* out_w, const int64_t* caps,
                   int64_t* nedges);
+
+/* The kNum graphs for a HOST consumer (igraph::make_graph + cluster_leiden,
+ * R/consensusClust.R:656-658): ONE device pass -- exactly the kernels of
+ * ccg_snn_rows_dev below -- builds the union graph's rows; the rows (8 B per
+ * union edge: partner + packed per-graph values) and each graph's per-row
+ * edge offsets are copied to pinned host memory owned by the context, and
+ * nedges[t] (host, nk entries) receives graph ks[t]'s edge count.  No edge
+ * list is formed on the device.  ks ascending, nk <= 4, ks <= 32.
+ * Synchronises. */
+int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk, int type,
+                   int64_t* nedges);
+/* Graph t (0 <= t < nk) of the last ccg_snn_graphs call on this context,
+ * decoded on the host from the staged rows (no device work): edges i < j
+ * sorted by (i, j), weights as ccg_snn.  Any output may be NULL; cap < the
+ * edge count returns CCG_ECAP.  May be called any number of times until the
+ * next ccg_snn_graphs / ccg_snn / ccg_snn_multi call. */
+int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t* out_j, double* out_w, int64_t cap);
 
 /* The same graphs as rows (CSR of the union graph = the largest k, built in
  * one pass): row j = partners p > j of node j in ascending order,

@@ -1,6 +1,6 @@
 /*
  * ccg_r.c -- the .Call glue a consensusClustR maintainer adds to reach
- * libccg.so (include/ccg.h, ABI version 4) from R.  Build with the package:
+ * libccg.so (include/ccg.h, ABI version 5) from R.  Build with the package:
  *   src/Makevars:  PKG_CPPFLAGS = -I$(CCG_HOME)/include
  *                  PKG_LIBS     = -L$(CCG_HOME)/consensusclustr_amd -lccg -Wl,-rpath,$(CCG_HOME)/consensusclustr_amd
  * (R is not installed in the image this repository is built in, so this file
@@ -277,54 +277,21 @@ SEXP ccg_r_knn_boot_segments(SEXP e, SEXP pcas, SEXP boots, SEXP kmax) {
 }
 
 /* ---------------------------------------------------------------- SNN -- */
-/* knn: n x ks 1-based; first k columns used; type 0 = "number", 1 = "rank".
- * Returns list(from, to, weight), 1-based, from < to. */
-SEXP ccg_r_snn(SEXP e, SEXP knn, SEXP k, SEXP type) {
-    ccg_ctx* ctx;
-    ccg_group* grp;
-    engine_of(e, &ctx, &grp);
-    int64_t n;
-    int ks;
-    int32_t* kn = knn_from_r(knn, &n, &ks);
-    int64_t ne = 0;
-    int rc = ccg_snn(ctx, kn, n, ks, Rf_asInteger(k), Rf_asInteger(type), NULL, NULL, NULL, 0, &ne);
-    if (rc != CCG_OK && rc != CCG_ECAP) fail("ccg_snn", rc);
-    SEXP from = PROTECT(Rf_allocVector(INTSXP, ne));
-    SEXP to = PROTECT(Rf_allocVector(INTSXP, ne));
-    SEXP w = PROTECT(Rf_allocVector(REALSXP, ne));
-    rc = ccg_snn(ctx, kn, n, ks, Rf_asInteger(k), Rf_asInteger(type), INTEGER(from), INTEGER(to), REAL(w), ne, &ne);
-    if (rc != CCG_OK) {
-        UNPROTECT(3);
-        fail("ccg_snn", rc);
-    }
-    for (int64_t t = 0; t < ne; ++t) {
-        INTEGER(from)[t] += 1;
-        INTEGER(to)[t] += 1;
-    }
-    SEXP res = PROTECT(Rf_allocVector(VECSXP, 3));
-    SET_VECTOR_ELT(res, 0, from);
-    SET_VECTOR_ELT(res, 1, to);
-    SET_VECTOR_ELT(res, 2, w);
-    SEXP nm = PROTECT(Rf_allocVector(STRSXP, 3));
-    SET_STRING_ELT(nm, 0, Rf_mkChar("from"));
-    SET_STRING_ELT(nm, 1, Rf_mkChar("to"));
-    SET_STRING_ELT(nm, 2, Rf_mkChar("weight"));
-    Rf_setAttrib(res, R_NamesSymbol, nm);
-    UNPROTECT(5);
-    return res;
-}
-
-/* Every graph of kNum in one pass (ccg_snn_multi): knn n x ks 1-based, ks
- * the ascending k values; returns a list (one per k) of list(from, to,
- * weight), 1-based, from < to. */
-static SEXP edge_list(const int32_t* ei, const int32_t* ej, const double* w, int64_t ne) {
+/* One graph of the staged rows of the last ccg_snn_graphs call as
+ * list(from, to, weight), 1-based, from < to: R allocates the vectors at the
+ * exact edge count and the library decodes straight into them. */
+static SEXP fetch_edge_list(ccg_ctx* ctx, int t, int64_t ne) {
     SEXP from = PROTECT(Rf_allocVector(INTSXP, ne));
     SEXP to = PROTECT(Rf_allocVector(INTSXP, ne));
     SEXP wt = PROTECT(Rf_allocVector(REALSXP, ne));
-    for (int64_t t = 0; t < ne; ++t) {
-        INTEGER(from)[t] = ei[t] + 1;
-        INTEGER(to)[t] = ej[t] + 1;
-        REAL(wt)[t] = w[t];
+    int rc = ccg_snn_graph_fetch(ctx, t, INTEGER(from), INTEGER(to), REAL(wt), ne);
+    if (rc != CCG_OK) {
+        UNPROTECT(3);
+        fail("ccg_snn_graph_fetch", rc);
+    }
+    for (int64_t q = 0; q < ne; ++q) {
+        INTEGER(from)[q] += 1;
+        INTEGER(to)[q] += 1;
     }
     SEXP res = PROTECT(Rf_allocVector(VECSXP, 3));
     SET_VECTOR_ELT(res, 0, from);
@@ -339,6 +306,25 @@ static SEXP edge_list(const int32_t* ei, const int32_t* ej, const double* w, int
     return res;
 }
 
+/* knn: n x ks 1-based; first k columns used; type 0 = "number", 1 = "rank".
+ * Returns list(from, to, weight), 1-based, from < to.  One device pass
+ * (ccg_snn_graphs), decoded on the host. */
+SEXP ccg_r_snn(SEXP e, SEXP knn, SEXP k, SEXP type) {
+    ccg_ctx* ctx;
+    ccg_group* grp;
+    engine_of(e, &ctx, &grp);
+    int64_t n;
+    int ks;
+    int32_t* kn = knn_from_r(knn, &n, &ks);
+    int kk = Rf_asInteger(k);
+    int64_t ne = 0;
+    CALL("ccg_snn_graphs", ccg_snn_graphs(ctx, kn, n, ks, &kk, 1, Rf_asInteger(type), &ne));
+    return fetch_edge_list(ctx, 0, ne);
+}
+
+/* Every graph of kNum (ccg_snn_graphs: one device pass per 4 values): knn
+ * n x kst 1-based, ks the distinct k values in ascending order; returns a
+ * list (one per k) of list(from, to, weight), 1-based, from < to. */
 SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type) {
     ccg_ctx* ctx;
     ccg_group* grp;
@@ -347,24 +333,20 @@ SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type) {
     int kst;
     int32_t* kn = knn_from_r(knn, &n, &kst);
     const int nk = Rf_length(ks);
-    if (nk < 1 || nk > 4) Rf_error("ccg_r_snn_multi: 1 to 4 values of k");
-    int kv[4];
-    for (int t = 0; t < nk; ++t) kv[t] = INTEGER(ks)[t];
-    int64_t ne[4] = {0, 0, 0, 0}, caps[4] = {0, 0, 0, 0};
-    int32_t* oi[4] = {NULL, NULL, NULL, NULL};
-    int32_t* oj[4] = {NULL, NULL, NULL, NULL};
-    double* ow[4] = {NULL, NULL, NULL, NULL};
-    int rc = ccg_snn_multi(ctx, kn, n, kst, kv, nk, Rf_asInteger(type), oi, oj, ow, caps, ne);
-    if (rc != CCG_OK && rc != CCG_ECAP) fail("ccg_snn_multi", rc);
-    for (int t = 0; t < nk; ++t) {
-        caps[t] = ne[t];
-        oi[t] = (int32_t*)R_alloc((size_t)ne[t] + 1, sizeof(int32_t));
-        oj[t] = (int32_t*)R_alloc((size_t)ne[t] + 1, sizeof(int32_t));
-        ow[t] = (double*)R_alloc((size_t)ne[t] + 1, sizeof(double));
-    }
-    CALL("ccg_snn_multi", ccg_snn_multi(ctx, kn, n, kst, kv, nk, Rf_asInteger(type), oi, oj, ow, caps, ne));
+    if (nk < 1) Rf_error("ccg_r_snn_multi: no values of k");
     SEXP out = PROTECT(Rf_allocVector(VECSXP, nk));
-    for (int t = 0; t < nk; ++t) SET_VECTOR_ELT(out, t, edge_list(oi[t], oj[t], ow[t], ne[t]));
+    for (int c0 = 0; c0 < nk; c0 += 4) {  /* the library builds up to 4 graphs per pass */
+        const int m = nk - c0 < 4 ? nk - c0 : 4;
+        int kv[4];
+        int64_t ne[4] = {0, 0, 0, 0};
+        for (int t = 0; t < m; ++t) kv[t] = INTEGER(ks)[c0 + t];
+        int rc = ccg_snn_graphs(ctx, kn, n, kst, kv, m, Rf_asInteger(type), ne);
+        if (rc != CCG_OK) {
+            UNPROTECT(1);
+            fail("ccg_snn_graphs", rc);
+        }
+        for (int t = 0; t < m; ++t) SET_VECTOR_ELT(out, c0 + t, fetch_edge_list(ctx, t, ne[t]));
+    }
     UNPROTECT(1);
     return out;
 }

@@ -436,3 +436,78 @@ def test_silhouette_cells_matches_row_path_and_oracle(engine, labels_per):
         _, m, C = O.silhouette(X, labs[l_])
         np.testing.assert_allclose(m1[l_], m, rtol=1e-5)
         assert c1[l_] == C
+
+
+@pytest.mark.parametrize("knum", [(10, 10, 15), (5, 8, 10, 15, 20), (20, 10, 15)])
+def test_snn_graphs_any_knum_vs_oracle(engine, knum):
+    """Engine.snn_multi over ccg_snn_graphs + ccg_snn_graph_fetch: kNum in
+    any order, with repeats and with more than 4 distinct values (one device
+    pass per 4 distinct k); every graph equals the oracle's, aligned with
+    kNum (getClustAssignments loops k in kNum order, :653)."""
+    rng = np.random.default_rng(41)
+    X = _mixture(rng, 4000, 10)
+    idx, _ = engine.knn_boot(X, rng.integers(0, 4000, 3600), kmax=20)
+    graphs = engine.snn_multi(idx[0], list(knum), "number")
+    assert len(graphs) == len(knum)
+    for k, got in zip(knum, graphs):
+        for a, b in zip(got, O.snn(idx[0], k, "number")):
+            assert np.array_equal(a, b)
+
+
+def test_snn_multi_ecap_keeps_graphs_staged(engine):
+    """ccg_snn_multi with too-small capacities returns CCG_ECAP with every
+    count set; the graphs stay staged, so ccg_snn_graph_fetch serves them
+    without a second device pass."""
+    import ctypes
+    from consensusclustr_amd import _lib
+    rng = np.random.default_rng(42)
+    X = _mixture(rng, 3000, 8)
+    idx, _ = engine.knn_boot(X, np.arange(3000), kmax=20)
+    knn = np.ascontiguousarray(idx[0])
+    ks = (10, 20)
+    ne = (ctypes.c_int64 * 2)()
+    P = ctypes.c_void_p * 2
+    rc = engine.lib.ccg_snn_multi(engine.ctx, knn.ctypes.data_as(ctypes.c_void_p), knn.shape[0], knn.shape[1],
+                                  (ctypes.c_int * 2)(*ks), 2, _lib.CCG_SNN_NUMBER, P(), P(), P(),
+                                  (ctypes.c_int64 * 2)(0, 0), ne)
+    assert rc == _lib.CCG_ECAP
+    for t, k in enumerate(ks):
+        got = engine._snn_fetch(t, ne[t])
+        for a, b in zip(got, O.snn(knn, k, "number")):
+            assert np.array_equal(a, b)
+    small = np.empty(1, np.int32)
+    rc = engine.lib.ccg_snn_graph_fetch(engine.ctx, 0, small.ctypes.data_as(ctypes.c_void_p), None, None, 1)
+    assert rc == _lib.CCG_ECAP
+
+
+def test_snn_copy_node_chains_of_distinct_points(engine):
+    """Copy nodes are found from each node's first neighbour; distinct points
+    with identical N+ sets for every k (a tight ball of 11 cells far from
+    the rest) chain first neighbours (src of a src), and their rows come from
+    the built end of the chain.  Graphs equal the oracle's, through the
+    device rows and through the host flavour."""
+    import torch
+    rng = np.random.default_rng(43)
+    N, d = 3000, 8
+    X = _mixture(rng, N, d)
+    X[200:211] = X[50] + 1e-7 * rng.normal(size=(11, d)) + 500.0  # an isolated tight ball of 11 cells
+    boot = np.concatenate([np.arange(N), rng.integers(0, N, 600)]).astype(np.int32)
+    idx, _ = engine.knn_boot(X, boot, kmax=20)
+    ks = (10, 15, 20)
+    for k, got in zip(ks, engine.snn_multi(idx[0], list(ks), "number")):
+        for a, b in zip(got, O.snn(idx[0], k, "number")):
+            assert np.array_equal(a, b)
+    n = idx.shape[1]
+    knn_t = torch.from_numpy(idx[0]).cuda()
+    off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    ln = torch.zeros(n, dtype=torch.int32, device="cuda")
+    nbr = torch.empty(n * 400, dtype=torch.int32, device="cuda")
+    wpk = torch.empty(n * 400, dtype=torch.int32, device="cuda")
+    ne = torch.zeros(3, dtype=torch.int64, device="cuda")
+    engine.snn_rows_t(knn_t, ks, "number", off, ln, nbr, wpk, ne)
+    torch.cuda.synchronize()
+    got = _rows_to_graphs(off.cpu().numpy(), ln.cpu().numpy(), nbr.cpu().numpy(),
+                          wpk.cpu().numpy().view(np.uint32), ks, "number")
+    for g, k in enumerate(ks):
+        for a, b in zip(got[g], O.snn(idx[0], k, "number")):
+            assert np.array_equal(a, b)

@@ -102,15 +102,22 @@ def test_r_bootstrap_loop_is_batched_and_keeps_the_rng_sequence():
 
 def test_r_getclustassignments_runs_the_bench_kernels():
     """The R drop-in reaches the kernels bench.py times: every kNum graph from
-    ONE SNN pass (ccg_snn_multi) and the silhouettes over the bootstrap's
-    distinct cells (ccg_silhouette_cells, cell = the row-name match)."""
+    ONE SNN rows pass (ccg_snn_graphs -- the kernels of ccg_snn_rows_dev --
+    decoded per graph on the host by ccg_snn_graph_fetch, no device emit)
+    and the silhouettes over the bootstrap's distinct cells
+    (ccg_silhouette_cells, cell = the row-name match)."""
     code = open(RCODE).read()
     gca = code[code.index("getClustAssignments <- function("):code.index("#' kNN(jaccardDist, k)$id")]
     assert "C_ccg_r_snn_multi" in gca and "C_ccg_r_snn," not in gca
     assert "cell = match(rownames(pca), unique(rownames(pca)))" in gca
     sil = code[code.index("ccgSilhouetteMeans <- function("):code.index("#' Drop-in for getClustAssignments")]
     assert "C_ccg_r_silhouette_cells" in sil
-    assert re.search(r"ccg_silhouette_cells\(ctx,", _glue()) and re.search(r"ccg_snn_multi\(ctx,", _glue())
+    glue = _glue()
+    assert re.search(r"ccg_silhouette_cells\(ctx,", glue) and re.search(r"ccg_snn_graphs\(ctx,", glue)
+    assert "ccg_snn_graph_fetch(ctx, t," in glue and "ccg_snn_multi(" not in glue
+    # any number of k values: the glue chunks them 4 per device pass
+    multi = glue[glue.index("SEXP ccg_r_snn_multi("):]
+    assert "c0 += 4" in multi and "nk > 4" not in multi
 
 
 def test_r_level_batching_uses_the_segment_search():
@@ -121,6 +128,9 @@ def test_r_level_batching_uses_the_segment_search():
     code = open(RCODE).read()
     lvl = code[code.index("ccgLevelBootstrapKNN <- function("):code.index("ccgConsensusCore <- function(")]
     assert "C_ccg_r_knn_boot_segments" in lvl and ".ccg_draw_bootstraps(" in lvl
+    # subclusters with a bootstrap of <= kmax distinct cells stay out of the
+    # segment call, and segments x stacked cells stay below 2^31 per call
+    assert "length(unique(d$idx)) > kmax" in lvl and "2^31" in lvl and "pcas[grp]" in lvl
     core = code[code.index("ccgConsensusCore <- function("):code.index("ccgNullStatistics <- function(")]
     assert "prefetched$draws" in core and "prefetched$knns[bs]" in core
     assert "ccg_knn_boot_segments(ctx, cells, Ntot, d, idx, n, off, NULL" in _glue()
