@@ -138,9 +138,11 @@ getClustAssignments <- function(pca, clusterFun = "leiden", resRange, kNum, mode
     if (is.null(nu)) nu <<- nrow(unique(pca))
     nu
   }
-  # every graph of kNum from one SNN pass over the max(kNum) lists
+  # every graph of kNum from one SNN pass over the max(kNum) lists, at the
+  # level of the bootstrap's copies (rows sharing a row name share a class)
   ks <- sort(unique(as.integer(kNum)))
-  graphs <- .Call(C_ccg_r_snn_multi, eng, knn, ks, 0L)
+  cell <- match(rownames(pca), unique(rownames(pca)))
+  graphs <- .Call(C_ccg_r_snn_multi, eng, knn, ks, 0L, cell)
   labs <- list()
   for (k in kNum) {
     g <- .ccg_graph(graphs[[match(as.integer(k), ks)]], nrow(pca))
@@ -152,7 +154,7 @@ getClustAssignments <- function(pca, clusterFun = "leiden", resRange, kNum, mode
   mapback <- function(l) setNames(l, rownames(pca))[match(cellOrder, rownames(pca))]
   if (mode == "robust") {
     # copies of a cell share a row name: widths once per (cell, label)
-    s <- ccgSilhouetteMeans(pca, labs, eng, cell = match(rownames(pca), unique(rownames(pca))))
+    s <- ccgSilhouetteMeans(pca, labs, eng, cell = cell)
     score <- ifelse(s$nclust > 1 & s$minsize > minSize, s$mean, ifelse(s$minsize > minSize, 0, 0.15))
     r <- rank(score, ties.method = "first")
     return(mapback(labs[[which(r == max(r))]]))

@@ -292,13 +292,9 @@ def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, rob
     else:
         eng.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, knn)
     cut = eng.knn_last_fallback()
-    ro = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    rl = torch.zeros(n, dtype=torch.int32, device=dev)
-    cap = 700 * n
-    nbr = torch.empty(cap, dtype=torch.int32, device=dev)
-    wpk = torch.empty(cap, dtype=torch.int32, device=dev)
-    ne = torch.zeros(3, dtype=torch.int64, device=dev)
-    eng.snn_rows_t(knn, K_NUM, "number", ro, rl, nbr, wpk, ne)
+    sb = SnnBufs(torch, n, 400 * n, dev)
+    info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
+    sb.run(eng, knn, boot, info)
     L = labels0.shape[0]
     mean = torch.empty(L, dtype=torch.float64, device=dev)
     ncl = torch.empty(L, dtype=torch.int32, device=dev)
@@ -315,21 +311,15 @@ def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, rob
     oi, _ = O.knn_queries(X, 20, q, nthreads=threads)
     out["knn_rows_checked"] = int(q.size)
     out["knn_exact"] = bool(np.array_equal(kn[q], oi))
-    used = int(ro[-1].item()) if ne.min().item() >= 0 else 0
-    ok = used > 0
+    inf = info.cpu().numpy()
+    ok = int(inf[1]) == 0 and int(inf[3:].min()) >= 0
+    out["snn_classes"] = int(inf[0])
     if ok:
-        ln = rl.cpu().numpy().astype(np.int64)
-        off = ro.cpu().numpy()
-        i = np.repeat(np.arange(n, dtype=np.int64), ln)
-        pos = np.repeat(off[:-1], ln) + (np.arange(i.size) - np.repeat(np.cumsum(ln) - ln, ln))
-        j = nbr[:used].cpu().numpy()[pos]
-        w = wpk[:used].cpu().numpy().view(np.uint32)[pos]
+        got = sb.decode(n, int(inf[0]))
         for g, k in enumerate(K_NUM):
-            b = (w >> np.uint32(8 * g)) & np.uint32(0xFF)
-            m = b != 0
             ei, ej, ew = O.snn(kn, k, "number")
-            ok = ok and np.array_equal(i[m], ei) and np.array_equal(j[m], ej) and np.array_equal(
-                b[m].astype(np.float64), ew)
+            ok = ok and np.array_equal(got[g][0], ei) and np.array_equal(got[g][1], ej) and \
+                np.array_equal(got[g][2], ew)
     out["snn_graphs_exact"] = bool(ok)
     if robust:
         labs = labels0.cpu().numpy()
@@ -431,6 +421,92 @@ def decode_union_rows(off, ln, nbr, wpk, nk, r0=0, r1=None):
     return out
 
 
+def decode_class_rows(row_class, u, off, ln, nbr, wpk, ks, c0=0):
+    """Class-level rows (ccg_snn_classes_dev) -> per-graph row-level
+    (i, j, w) NUMBER edge lists sorted by (i, j) (numpy): rows x of class C
+    and y of class H get w(C, H); two rows of one class get k + 1.  c0: the
+    first class of a slice (row_class, off, ln relative to it; partners are
+    global ordinals)."""
+    row_class = np.asarray(row_class, np.int64)
+    n = row_class.size
+    m = np.bincount(row_class, minlength=u).astype(np.int64)
+    order = np.argsort(row_class, kind="stable")  # rows of each class, ascending
+    ms = np.concatenate([[0], np.cumsum(m)])
+    lens = ln[:u].astype(np.int64)
+    C = np.repeat(np.arange(u, dtype=np.int64), lens)
+    pos = np.repeat(off[:u], lens) + (np.arange(C.size, dtype=np.int64) - np.repeat(np.cumsum(lens) - lens, lens))
+    H = nbr[pos].astype(np.int64) - c0
+    W = wpk.view(np.uint32)[pos]
+    out = []
+    # pairs inside a class
+    mi = m[m > 1]
+    ci = np.flatnonzero(m > 1)
+    for g, k in enumerate(ks):
+        b = (W >> np.uint32(8 * g)) & np.uint32(0xFF)
+        sel = b != 0
+        Cg, Hg, wg = C[sel], H[sel], b[sel].astype(np.float64)
+        cnt = m[Cg] * m[Hg]
+        e = np.repeat(np.arange(Cg.size), cnt)
+        kk = np.arange(e.size, dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+        mh = m[Hg][e]
+        x = order[ms[Cg[e]] + kk // mh]
+        y = order[ms[Hg[e]] + kk % mh]
+        wv = wg[e]
+        # intra-class pairs x < y, weight k + 1
+        pc = mi * (mi - 1) // 2
+        ei = np.repeat(np.arange(ci.size), pc)
+        t = np.arange(ei.size, dtype=np.int64) - np.repeat(np.cumsum(pc) - pc, pc)
+        # t -> (a, b) with a < b inside the class (m <= 15: small tables)
+        a_ = np.zeros(ei.size, np.int64)
+        b_ = np.zeros(ei.size, np.int64)
+        for mm in np.unique(mi):
+            pa, pb = np.triu_indices(int(mm), 1)
+            s_ = mi[ei] == mm
+            a_[s_], b_[s_] = pa[t[s_]], pb[t[s_]]
+        xi = order[ms[ci[ei]] + a_]
+        yi = order[ms[ci[ei]] + b_]
+        I = np.concatenate([np.minimum(x, y), np.minimum(xi, yi)])
+        J = np.concatenate([np.maximum(x, y), np.maximum(xi, yi)])
+        Wt = np.concatenate([wv, np.full(xi.size, float(k + 1))])
+        o = np.lexsort((J, I))
+        out.append((I[o], J[o], Wt[o]))
+    return out
+
+
+class SnnBufs:
+    """Output buffers of one in-flight SNN pass at the level of row classes
+    (ccg_snn_classes_dev: the kernels both drop-ins run through
+    ccg_snn_graphs_cells): row -> class, class roots, the class rows
+    (capacity-based offsets, lengths, partner classes, packed per-graph
+    weights)."""
+
+    def __init__(self, torch, n, cap, dev):
+        self.n, self.cap = n, cap
+        self.row_class = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.class_root = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        self.ln = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.nbr = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.wpk = torch.empty(cap, dtype=torch.int32, device=dev)
+
+    def run(self, e, knn, cell, info, n=None):
+        """info: (3 + len(K_NUM),) int64 tensor row -- [u, status, required
+        capacity, class edges per graph (negative: capacity too small)]."""
+        n = self.n if n is None else n
+        e.snn_classes_t(knn, K_NUM, self.row_class[:n], self.class_root[:n], self.off[:n + 1], self.ln[:n], self.nbr,
+                        self.wpk, info, cell=cell)
+
+    def decode(self, n, u, r0=0, r1=None):
+        """Row-level graphs of rows [r0, r1) (a segment: its classes are a
+        contiguous ordinal range, rows and partners relative to r0)."""
+        r1 = n if r1 is None else r1
+        used = int(self.off[n].item())
+        rc = self.row_class[r0:r1].cpu().numpy().astype(np.int64)
+        c0, c1 = (int(rc[0]), int(rc.max()) + 1) if r0 > 0 or r1 < n else (0, u)
+        return decode_class_rows(rc - c0, c1 - c0, self.off[c0:c1 + 1].cpu().numpy(), self.ln[c0:c1].cpu().numpy(),
+                                 self.nbr[:used].cpu().numpy(), self.wpk[:used].cpu().numpy(), K_NUM, c0=c0)
+
+
 def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
     """cfg5's cpu_baseline check leg: the oracle as the checker of the first
     segmented launch set.  The batch runs again through the step's calls
@@ -450,13 +526,9 @@ def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
     knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
     eng.knn_boot_segments_t(inp["cells"], idx, off, su, 20, knn, local_ids=False)
     cut = eng.knn_last_fallback()
-    ro = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    rl = torch.zeros(n, dtype=torch.int32, device=dev)
-    cap = 700 * n
-    nbr = torch.empty(cap, dtype=torch.int32, device=dev)
-    wpk = torch.empty(cap, dtype=torch.int32, device=dev)
-    ne = torch.zeros(len(K_NUM), dtype=torch.int64, device=dev)
-    eng.snn_rows_t(knn, K_NUM, "number", ro, rl, nbr, wpk, ne)
+    sb = SnnBufs(torch, n, 300 * n, dev)
+    info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
+    sb.run(eng, knn, idx, info)
     rows = torch.empty((n, dpad), dtype=torch.float64, device=dev)
     eng.gather_rows_rm_t(inp["cells"], inp["cells"].shape[0], dpad, idx, rows)
     nsub = inp["nsub"]
@@ -475,10 +547,8 @@ def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     kn = knn.cpu().numpy()
     X_all = rows.cpu().numpy()
-    ok_snn = int(ne.min().item()) >= 0
-    offn, lnn = ro.cpu().numpy(), rl.cpu().numpy()
-    used = int(offn[-1]) if ok_snn else 0
-    nbn, wpn = nbr[:used].cpu().numpy(), wpk[:used].cpu().numpy()
+    inf = info.cpu().numpy()
+    ok_snn = int(inf[1]) == 0 and int(inf[3:].min()) >= 0
     rng = np.random.default_rng(11)
     out = {"segments_checked": [], "knn_rows_checked": 0}
     knn_ok, snn_ok, rel_max = True, ok_snn, 0.0
@@ -494,12 +564,11 @@ def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
         knn_ok = knn_ok and bool(np.array_equal(loc[qs], oi))
         out["knn_rows_checked"] += int(qs.size)
         if ok_snn:
-            got = decode_union_rows(offn, lnn, nbn, wpn, len(K_NUM), a, b)
+            graphs = sb.decode(n, int(inf[0]), a, b)  # the segment's classes (a contiguous range)
             for g, k in enumerate(K_NUM):
                 ei, ej, ew = O.snn(np.ascontiguousarray(loc), k, "number")
-                gi, gj, gw = got[g]
-                snn_ok = snn_ok and np.array_equal(gi - a, ei) and np.array_equal(gj - a, ej) and \
-                    np.array_equal(gw, ew)
+                gi, gj, gw = graphs[g]
+                snn_ok = snn_ok and np.array_equal(gi, ei) and np.array_equal(gj, ej) and np.array_equal(gw, ew)
         labs = labels[c][j].cpu().numpy()
         with cf.ThreadPoolExecutor(threads) as ex:
             ref = np.asarray(list(ex.map(lambda l_: O.silhouette(X, labs[l_])[1], range(L))))
@@ -549,11 +618,9 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     nmax = max(int(p[1][-1]) for p in plans)
     rows_s = [torch.empty((nmax, dpad), dtype=torch.float64, device=dev) for _ in range(S)]
     knn_s = [torch.empty((nmax, 20), dtype=torch.int32, device=dev) for _ in range(S)]
-    rcap = 700 * nmax
-    snn_s = [(torch.zeros(nmax + 1, dtype=torch.int64, device=dev), torch.zeros(nmax, dtype=torch.int32, device=dev),
-              torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
-             for _ in range(S)]
-    nedges = torch.zeros((len(batches), len(K_NUM)), dtype=torch.int64, device=dev)
+    rcap = 300 * nmax
+    snn_s = [SnnBufs(torch, nmax, rcap, dev) for _ in range(S)]
+    snn_info = torch.zeros((len(batches), 3 + len(K_NUM)), dtype=torch.int64, device=dev)
     means = [torch.empty((B, L), dtype=torch.float64, device=dev) for _ in range(nsub)]
     nclust = [torch.empty((B, L), dtype=torch.int32, device=dev) for _ in range(nsub)]
     minsize = [torch.empty((B, L), dtype=torch.int32, device=dev) for _ in range(nsub)]
@@ -569,8 +636,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         n = int(off[-1])
         rows, knn = rows_s[si][:n], knn_s[si][:n]
         e.knn_boot_segments_t(cells, idx, off, su, 20, knn, local_ids=False)
-        e.snn_rows_t(knn, K_NUM, "number", snn_s[si][0][:n + 1], snn_s[si][1][:n], snn_s[si][2], snn_s[si][3],
-                     nedges[t])
+        snn_s[si].run(e, knn, idx, snn_info[t], n=n)  # the classes of every segment in one pass
         e.gather_rows_rm_t(cells, N, dpad, idx, rows)
         for q, (c, j) in enumerate(segs):
             a, b = int(off[q]), int(off[q + 1])
@@ -599,8 +665,10 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    if int(nedges.min().item()) < 0:
+    if int(snn_info[:, 3:].min().item()) < 0:
         raise RuntimeError(f"SNN row capacity too small: {rcap}")
+    if int(snn_info[:, 1].max().item()) != 0:
+        raise RuntimeError("ccg_snn_classes_dev: the class contract failed")
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -847,19 +915,17 @@ def main():
     rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(RING)]
     knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(RING)]
     rows, knn = rows_s[0], knn_s[0]
-    rcap = 700 * n  # SNN row entries (items per node ~ 560 at cfg3); grown once after the warmup if short
+    rcap = 300 * n  # SNN class-row entries (items per class ~ 190 at cfg3); grown once after the warmup if short
 
     def alloc_snn(rcap):
-        # per stream: the union-graph rows of ccg_snn_rows_dev (row offsets, lengths, partners, packed weights)
-        return [(torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),
-                 torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
-                for _ in range(S)]
+        # per stream: the class-level rows of ccg_snn_classes_dev
+        return [SnnBufs(torch, n, rcap, dev) for _ in range(S)]
     snn_out = alloc_snn(rcap)
     if os.environ.get("CCG_BENCH_TORCH_STREAMS"):
         streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     else:
         streams = [e.torch_stream() for e in engs]  # each context's own non-blocking HIP stream
-    nedges = torch.zeros((B, len(K_NUM)), dtype=torch.int64, device=dev)
+    snn_info = torch.zeros((B, 3 + len(K_NUM)), dtype=torch.int64, device=dev)  # [u, status, cap, class edges]
     means = torch.empty((B, L), dtype=torch.float64, device=dev)
     nclust = torch.empty((B, L), dtype=torch.int32, device=dev)
     minsize = torch.empty((B, L), dtype=torch.int32, device=dev)
@@ -919,7 +985,7 @@ def main():
             with torch.cuda.stream(streams[si]):
                 e.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[si])
                 boot_knn(e, j, rows_s[si], knn_s[si])
-                e.snn_rows_t(knn_s[si], K_NUM, "number", *snn_out[si], nedges[j])
+                snn_out[si].run(e, knn_s[si], boots[j], snn_info[j])
                 if robust:  # granular mode scores no clustering (:688)
                     e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_t[0] += time.perf_counter() - th
@@ -935,15 +1001,17 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    short = int(nedges.min().item())
+    short = int(snn_info[:, 3:].min().item())
     if short < 0:  # rows did not fit: -short entries needed; grow once and redo the warmup
         rcap = int(-short * 1.25)
         snn_out = alloc_snn(rcap)
         step()
         torch.cuda.synchronize()
-        if int(nedges.min().item()) < 0:
+        if int(snn_info[:, 3:].min().item()) < 0:
             raise RuntimeError(f"SNN row capacity too small: {rcap}")
-    need = nedges.max(0).values.tolist()
+    if int(snn_info[:, 1].max().item()) != 0:  # (cannot happen for bootstrap copies under the kNN contract)
+        raise RuntimeError("ccg_snn_classes_dev: the class contract failed; the row-level pass would be needed")
+    need = snn_info[:, 3:].max(0).values.tolist()
     if emul:  # the other ranks' column blocks: this rank's columns with the cells rotated (same label counts)
         for k in range(1, emul):
             A_full[k * cpr:(k + 1) * cpr] = torch.roll(A_local, shifts=k * 7919, dims=1)
@@ -995,7 +1063,7 @@ def main():
         with torch.cuda.stream(streams[0]):
             eng.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[0])
             boot_knn(eng, j, rows_s[0], knn_s[0])
-            eng.snn_rows_t(knn_s[0], K_NUM, "number", *snn_out[0], nedges[j])
+            snn_out[0].run(eng, knn_s[0], boots[j], snn_info[j])
             if robust:
                 eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
         host_idle.append(time.perf_counter() - th)
@@ -1035,13 +1103,14 @@ def main():
     for j in range(nis):
         eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         boot_knn(eng, j, rows, knn)
-        eng.snn_rows_t(knn, K_NUM, "number", *snn_out[0], nedges[j])
+        snn_out[0].run(eng, knn, boots[j], snn_info[j])
         if robust:
             eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
     iso_snn = eng.timing_read("snn")
     iso_sil = eng.timing_read("silhouette")
     torch.cuda.synchronize()
-    iso_edges = nedges[:nis].sum(0).tolist()  # per graph, over the nis bootstraps
+    iso_edges = snn_info[:nis, 3:].sum(0).tolist()  # class edges per graph, over the nis bootstraps
+    iso_classes = float(snn_info[:nis, 0].double().mean().item())
     iso_npres = int(nclust[:nis].sum().item())  # sum over the bootstraps' labelings of present clusters
     eng.timing(False)
     if G > 1:
@@ -1143,9 +1212,9 @@ def main():
     snn_ms = iso_snn[0] / max(iso_snn[1], 1)
     sil_ms = iso_sil[0] / max(iso_sil[1], 1)
     nk_ = len(K_NUM)
-    e_union = iso_edges[-1] / max(nis, 1)  # the largest k's graph is the union graph
-    snn_bytes = n * max(K_NUM) * 4 + 8 * e_union + n * 4 + (n + 1) * 8 + nk_ * (n + 1) * 8
-    snn_bytes_survey = sum(n * k * 4 for k in K_NUM) + 16 * sum(iso_edges) / max(nis, 1)
+    e_union = iso_edges[-1] / max(nis, 1)  # class edges of the largest k's graph = the union
+    snn_bytes = (n * max(K_NUM) * 4 + 8 * e_union + 4 * n + 4 * iso_classes + 8 * (n + 1) + 4 * n +
+                 nk_ * (n + 1) * 8)
     snn_traffic = None
     if os.path.exists(args.traffic_json) and args.workload == "cfg3":
         with open(args.traffic_json) as f:
@@ -1154,17 +1223,18 @@ def main():
     if not robust:
         sil_ms = 0.0
     roof_snn = {
-        "kernel": "SNN union-graph rows pass (ccg_snn_rows_dev; the same kernels ccg_snn_graphs runs for the R and "
-                  "Python drop-ins: host lists, size-class build tiers, copy rows)",
+        "kernel": "SNN graphs at the level of row classes (ccg_snn_classes_dev; the same kernels "
+                  "ccg_snn_graphs_cells runs for the R and Python drop-ins before the host expands the rows)",
         "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
         "achieved": round(snn_bytes / (snn_ms * 1e-3) / 1e9, 1),
         "frac": round(snn_bytes / (snn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
         "traffic": snn_traffic,
-        "algorithmic_per_launch": f"n kmax 4 (kNN in) + 8 E_union + 12 n + 8 nk (n+1) (rows, offsets, per-graph "
-                                  f"offsets out) = {snn_bytes:.3e} B per bootstrap (E_union = {e_union:.0f})",
-        "survey_8d_bytes_per_boot": round(snn_bytes_survey),
-        "survey_8d_note": "SURVEY 8(d)'s sum_K (n K 4 + E_K 16) counts per-graph (i, j, w) lists, which neither "
-                          "the bench nor the drop-ins write on the device (host decode from the rows)",
+        "algorithmic_per_launch": f"n kmax 4 (kNN in) + 8 E_class + 4 n + 4 u + 8 (n+1) + 4 n + 8 nk (n+1) (class "
+                                  f"rows, row->class, roots, offsets, lengths, per-graph offsets out) = "
+                                  f"{snn_bytes:.3e} B per bootstrap (u = {iso_classes:.0f} classes, "
+                                  f"E_class = {e_union:.0f})",
+        "survey_8d_note": "SURVEY 8(d)'s sum_K (n K 4 + E_K 16) counts per-graph (i, j, w) row lists, which "
+                          "neither the bench nor the drop-ins write on the device (the host expands the classes)",
         "ms_per_boot": round(snn_ms, 4),
     }
     roof_sil = {
@@ -1227,7 +1297,7 @@ def main():
         "cocluster_avg_ms": round(coc_ms, 3),
         "knn_fallback_rows_last_boot": int(fb[1]),
         "knn_fallback_rows_last_boot_cold": int(fb_cold[1]),
-        "snn_edges_max_per_boot": [int(e) for e in need],
+        "snn_class_edges_max_per_boot": [int(e) for e in need],
     }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pcs.cpu().numpy(), B, n, N, d, args.cpu_sample_rows, robust=robust,

@@ -68,6 +68,8 @@ SIGNATURES = {
     "ccg_snn_multi": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p]),
     "ccg_snn_graphs": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p]),
     "ccg_snn_graph_fetch": (_i, [_p, _i, _p, _p, _p, _i64]),
+    "ccg_snn_graphs_cells": (_i, [_p, _p, _i64, _i, _p, _p, _i, _i, _p]),
+    "ccg_snn_classes_dev": (_i, [_p, _p, _i64, _i, _p, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _p, _p]),
     "ccg_silhouette_cells": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _i64, _p, _p, _p]),
     "ccg_knn_boot_segments_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
     "ccg_knn_boot_segments": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p, _i, _i, _p, _p, _p]),

@@ -124,7 +124,8 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
         raise ValueError(f"knn must be {n} x {kmax}, got {knn.shape}")
     fn = _cluster_fn(clusterFun)
     labels = []
-    graphs = eng.snn_multi(knn, [int(k) for k in kNum], "number")  # every k in one pass, :656-658
+    # every k in one pass (:656-658); copies of a cell share a row class
+    graphs = eng.snn_multi(knn, [int(k) for k in kNum], "number", cell=boot_idx)
     for g, k in enumerate(kNum):  # :653-654, k outer, resolution inner
         ei, ej, w = graphs[g]
         for res in resRange:

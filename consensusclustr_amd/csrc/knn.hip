@@ -1164,7 +1164,7 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                                                           int* __restrict__ bi, int* __restrict__ ovf_count) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     __shared__ __attribute__((aligned(16))) float sx[KNN_FX_QG][DMAX];
-    __shared__ double snx[KNN_FX_QG], stau[KNN_FX_QG];
+    __shared__ float sA[KNN_FX_QG];
     __shared__ int sq[KNN_FX_QG];
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
     const int nf = min(*fail_count, KNN_FX_ROWS);
@@ -1193,8 +1193,9 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                     nx = fma(y, y, nx);
                 }
             }
-            snx[i] = nx;
-            stau[i] = t;
+            // the row's part of the fp32 test below, rounded down
+            sA[i] = t < 0.0 ? INFINITY
+                            : __double2float_rd((1.0 - 0x1p-14) * nx - t - 0x1p-60 - 0x1p-21 * (nx + t));
             sq[i] = q;
         }
         __syncthreads();
@@ -1210,6 +1211,8 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
             ny = fma(y1, y1, ny);
             yf[k2] = f2{(float)y0, (float)y1};
         }
+        // the reference's part, rounded down
+        const float bj = __double2float_rd((1.0 - 0x1p-14 - 0x1p-21) * ny);
         for (int i = 0; i < nq; ++i) {  // block-uniform
             const float4* xp = reinterpret_cast<const float4*>(&sx[i][0]);
             f2 acc = {0.f, 0.f};
@@ -1219,12 +1222,18 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
                 acc = __builtin_elementwise_fma(f2{x.x, x.y}, yf[2 * k4], acc);
                 acc = __builtin_elementwise_fma(f2{x.z, x.w}, yf[2 * k4 + 1], acc);
             }
-            const double nx = snx[i], t = stau[i];
-            const double approx = nx + ny - 2.0 * ((double)acc.x + (double)acc.y);
+            // nx + ny - 2 x.y <= tau + 2^-14 (nx + ny) + 2^-60, with the fp32
+            // dot product (error <= 2^-17 (nx + ny)), rearranged as
+            // 2 x.y >= A_i + B_j in fp32 (A_i, B_j rounded down): the fp32
+            // sums here err by <= 2^-23 (nx + ny + tau), inside the 2^-21
+            // slack taken out of A_i and B_j, so the candidates stay a
+            // superset of the pairs within the radius.  An fp64 test here
+            // cost ~7 fp64 operations per pair.
+            const float lhs = 2.0f * (acc.x + acc.y);
             // a pair within radius + margin joins the row's candidates; its
             // exact distance is taken in knn_fx_select_kernel (no fp64 row
             // loads inside this loop: they stall the whole wave for one lane)
-            if (j < n && j != sq[i] && approx <= t + 0x1p-14 * (nx + ny) + 0x1p-60) {
+            if (j < n && j != sq[i] && lhs >= sA[i] + bj) {
                 const int slot = atomicAdd(&cnt[f0 + i], 1);
                 if (slot < KNN_FX_CAP) bi[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = j;
             }

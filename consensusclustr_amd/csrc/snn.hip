@@ -266,35 +266,39 @@ __device__ __forceinline__ void snn_row_counts(const SnnSpec& sp, int64_t (&c4)[
 // which the build tiers fill: one launch instead of two memsets)
 // Copy nodes (src[j] >= 0, snn_src_kernel) join class 3, whose fixed-grid
 // kernel skips them: the copy pass writes their rows.
+// (ucount: class-level build -- entries past the u classes are in no list)
 __global__ void snn_class_kernel(const int64_t* __restrict__ roff, int64_t n, int64_t* __restrict__ cls,
                                  int64_t* __restrict__ cnt, int nk, int* __restrict__ ov_count,
-                                 const int* __restrict__ src) {
+                                 const int* __restrict__ src, const int64_t* __restrict__ ucount) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < 64) ov_count[j] = 0;
     if (j <= n)
         for (int t = 0; t < nk; ++t) cnt[(int64_t)t * (n + 1) + j] = 0;
     if (j >= n) return;
     const int64_t M = roff[j + 1] - roff[j];
-    const int c = (src && src[j] >= 0) ? 3 : (M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3)));
+    int c = (src && src[j] >= 0) ? 3 : (M <= 512 ? 0 : (M <= 1024 ? 1 : (M <= 2048 ? 2 : 3)));
+    if (ucount && j >= *ucount) c = 3;  // not a class (the scatter lists class 3 only below u)
     cls[j] = c < 3 ? 1LL << (SNN_CLS_BITS * c) : 0;
 }
 
 // Lists of each class in node order; counts[c] = class size.
 __global__ void snn_class_scatter_kernel(const int64_t* __restrict__ cls_scan, int64_t n, int* __restrict__ lists,
-                                         int64_t* __restrict__ counts) {
+                                         int64_t* __restrict__ counts, const int64_t* __restrict__ ucount) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > n) return;
+    const int64_t jl = ucount ? min(j, *ucount) : j;  // entries past u are in no class
     const int64_t mask = (1LL << SNN_CLS_BITS) - 1;
     const int64_t v = cls_scan[j];
     int64_t r[4];
     r[0] = v & mask;
     r[1] = (v >> SNN_CLS_BITS) & mask;
     r[2] = (v >> (2 * SNN_CLS_BITS)) & mask;
-    r[3] = j - r[0] - r[1] - r[2];
+    r[3] = jl - r[0] - r[1] - r[2];
     if (j == n) {
         for (int c = 0; c < 4; ++c) counts[c] = r[c];
         return;
     }
+    if (j != jl) return;  // past u (class-level build): no list
     const int64_t d = cls_scan[j + 1] - v;  // this node's one-hot class (0 for class 3)
     const int c = d == 1 ? 0 : (d == (1LL << SNN_CLS_BITS) ? 1 : (d == (1LL << (2 * SNN_CLS_BITS)) ? 2 : 3));
     lists[c * n + r[c]] = (int)j;
@@ -389,8 +393,44 @@ struct SnnKeyT<unsigned long long> {
 
 // Packed per-graph contribution of one item from its key (snn_contrib's
 // value: byte t live iff m <= kk[t]).
+// Class-level items (row classes, below): key = H << PS | 4-bit fields,
+// field t = min(t_R(c), t_H(c)) for graph t -- the rows of the shared class c
+// that both N+ sets hold.  32-bit keys carry 3 graphs (partner < 2^20);
+// 64-bit keys 4 graphs.
 template <typename K>
+struct SnnClsKeyT;
+template <>
+struct SnnClsKeyT<uint32_t> {
+    static constexpr int PS = 12;
+};
+template <>
+struct SnnClsKeyT<unsigned long long> {
+    static constexpr int PS = 32;
+};
+template <typename K, bool CS>
+__host__ __device__ constexpr int snn_ps() {
+    return CS ? SnnClsKeyT<K>::PS : SnnKeyT<K>::PS;
+}
+__device__ __forceinline__ unsigned snn_min4(unsigned a, unsigned b) {
+    unsigned r = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const unsigned x = (a >> (4 * t)) & 15u, y = (b >> (4 * t)) & 15u;
+        r |= (x < y ? x : y) << (4 * t);
+    }
+    return r;
+}
+__host__ __device__ __forceinline__ unsigned snn_nib2byte(unsigned v) {  // 4-bit fields -> bytes
+    return (v & 0xFu) | ((v & 0xF0u) << 4) | ((v & 0xF00u) << 8) | ((v & 0xF000u) << 12);
+}
+
+template <typename K, bool CS = false>
 __device__ __forceinline__ unsigned snn_key_contrib(const SnnSpec& sp, K key) {
+    if constexpr (CS) {
+        constexpr int PS = SnnClsKeyT<K>::PS;
+        constexpr unsigned mask = PS >= 16 ? 0xFFFFu : ((1u << PS) - 1u);
+        return snn_nib2byte((unsigned)key & mask);
+    }
     const int m = SnnKeyT<K>::m(key);
     unsigned live = 0;
 #pragma unroll
@@ -484,9 +524,9 @@ __device__ __forceinline__ void snn_sort_regs(K (&y)[N]) {
 // exchange stages per key, most across lanes; this is one register network
 // of CAP keys per lane plus a few LDS passes.  Returns false (x untouched)
 // when a bucket holds more than CAP keys: the caller sorts bitonically.
-template <int E, int CAP, typename K>
+template <int E, int CAP, typename K, bool CS = false>
 __device__ __forceinline__ bool snn_bucket_sort(K (&x)[E], int M, int lane, int* hist, K* buf) {
-    constexpr int PS = SnnKeyT<K>::PS;
+    constexpr int PS = snn_ps<K, CS>();
     K kmin = ~(K)0, kmax = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e)
@@ -557,10 +597,10 @@ struct SnnBitonicLds {
 // equal partner are combined (sum / bytewise min of the per-graph values) and
 // the last key of each run writes (partner, packed values); per-graph counts.
 // W > 1 (the hub tier) joins the waves' runs through L's wave summaries.
-template <int E, int W, typename K, typename LDS>
+template <int E, int W, typename K, bool CS, typename LDS>
 __device__ __forceinline__ void snn_emit_sorted(LDS& L, const SnnSpec& sp, int64_t n, int64_t j, int wv, int lane,
                                                 K (&x)[E], const SnnRows& rows, int64_t* __restrict__ cnt) {
-    constexpr int PS = SnnKeyT<K>::PS;
+    constexpr int PS = snn_ps<K, CS>();
 #define SNN_SYNC()                            \
     do {                                      \
         if constexpr (W == 1) WAVE_LDS_SYNC(); \
@@ -572,7 +612,7 @@ __device__ __forceinline__ void snn_emit_sorted(LDS& L, const SnnSpec& sp, int64
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         p[e] = (int)(x[e] >> PS);
-        const unsigned c = snn_key_contrib<K>(sp, x[e]);
+        const unsigned c = snn_key_contrib<K, CS>(sp, x[e]);
         agg[e] = (e > 0 && p[e] == p[e - 1]) ? snn_combine(sp.type, agg[e - 1], c) : c;
     }
     // across lanes: the lane's last run continues into the next lane when
@@ -678,7 +718,7 @@ __device__ __forceinline__ void snn_emit_sorted(LDS& L, const SnnSpec& sp, int64
 
 // One node, W waves (W = 1: one wave; W = 4: a 256-thread block for the
 // hubs); wave w holds sorted elements 64*E*w .. 64*E*(w+1) - 1.
-template <int E, int W, typename K, bool BK = false>
+template <int E, int W, typename K, bool BK = false, bool CS = false>
 __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, const SnnSpec& sp, int64_t n, int64_t j,
                                                  const SnnMember& m, int wv, int lane,
                                                  const int2* __restrict__ hosts_s, const SnnRows& rows,
@@ -712,24 +752,33 @@ __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, cons
         mi[e] = v;
     }
     int2 hv[E];
+    int az[E];  // CS: the member's inclusion fields (mem.z)
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int t = base + 64 * e + lane;
         hv[e] = make_int2(0, 0);
+        az[e] = 0;
         if (t < M) {
             const int4 md = L.mem[mi[e]];
             const int q = md.x + (t - md.w);
             hv[e] = q < md.y ? hosts_s[q] : make_int2(md.z, 0);
+            az[e] = md.z;
         }
     }
     K x[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-        x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
+    for (int e = 0; e < E; ++e) {
+        if constexpr (CS)
+            x[e] = base + 64 * e + lane < M
+                       ? (((K)(unsigned)hv[e].x << snn_ps<K, true>()) | (K)snn_min4((unsigned)az[e], (unsigned)hv[e].y))
+                       : ~(K)0;
+        else
+            x[e] = base + 64 * e + lane < M ? SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y) : ~(K)0;
+    }
     SNN_SYNC();  // every mark is read
     if constexpr (BK && W == 1) {
-        if (snn_bucket_sort<E, (E >= 32 ? 64 : 32), K>(x, M, lane, reinterpret_cast<int*>(L.mem), L.u.buf)) {
-            snn_emit_sorted<E, W, K>(L, sp, n, j, wv, lane, x, rows, cnt);
+        if (snn_bucket_sort<E, (E >= 32 ? 64 : 32), K, CS>(x, M, lane, reinterpret_cast<int*>(L.mem), L.u.buf)) {
+            snn_emit_sorted<E, W, K, CS>(L, sp, n, j, wv, lane, x, rows, cnt);
             return;
         }
     }
@@ -776,147 +825,10 @@ __device__ __forceinline__ void snn_bitonic_node(SnnBitonicLds<E, W, K>& L, cons
             snn_bitonic_xor<E, K, S / 2>(x, lane);
         }
     }
-    snn_emit_sorted<E, W, K>(L, sp, n, j, wv, lane, x, rows, cnt);
+    snn_emit_sorted<E, W, K, CS>(L, sp, n, j, wv, lane, x, rows, cnt);
 #undef SNN_SYNC
 }
 
-
-// ---------------------------------------------------------- merge tier --
-// NUMBER graphs (32-bit keys p << 6 | m), one wave per node: a node's items
-// are <= kmax + 2 runs that are ALREADY sorted by partner -- each member's
-// hosts above j (ascending host lists), plus one run of the members
-// themselves (s > j, sorted across lanes) -- so instead of a full bitonic sort
-// of the padded 64 E slots the wave merges the runs pairwise, ceil(log2(kmax +
-// 2)) levels of merge path: each lane emits ceil(M / 64) consecutive outputs of
-// a level after a binary search for its start on the merge diagonal.  Work per
-// level is O(M), not O(64 E log^2).  The sorted keys then go through the same
-// combine / row write as the bitonic tier.  Measured slower than the bitonic
-// tier on MI355X (cfg3: classes 0/1/2 136/251/249 against 97/170/156 us per
-// bootstrap): each merge step is a dependent LDS read per lane, while the
-// register network is pure VALU issue.  Kept behind CCG_SNN_SORT=merge.
-template <int E>
-struct SnnMergeLds {
-    int4 mem[64];
-    int off[2][64];  // run offsets (ping-pong): nr + 1 entries
-    uint32_t a[64 * E];
-    union {
-        int mark[64 * E];  // gather: item t -> member whose run starts at t (-1 elsewhere)
-        uint32_t b[64 * E];
-    } u;
-};
-
-// One level: runs [off[r], off[r+1]) of src, pairs (2i, 2i+1) merged into dst
-// (ties: the left run first); lane emits outputs [lane VT, lane VT + VT).
-__device__ __forceinline__ void snn_merge_level(const uint32_t* src, uint32_t* dst, const int* off, int nr, int M,
-                                                int VT, int lane) {
-    int o = lane * VT;
-    const int oend = min(M, o + VT);
-    if (o >= oend) return;
-    const int np = (nr + 1) >> 1;
-    int P = 0;  // the last pair starting at or before o (it contains o)
-    while (P + 1 < np && off[2 * (P + 1)] <= o) ++P;
-    int a0 = off[2 * P], a1 = off[min(2 * P + 1, nr)], b1 = off[min(2 * P + 2, nr)];
-    const int dd = o - a0, la = a1 - a0, lb = b1 - a1;
-    int lo = max(0, dd - lb), hi = min(dd, la);
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (src[a0 + mid] <= src[a1 + dd - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    int ia = a0 + lo, ib = a1 + dd - lo;
-    for (; o < oend; ++o) {
-        while (ia == a1 && ib == b1) {  // this lane's outputs continue in the next pair
-            ++P;
-            a0 = off[2 * P];
-            a1 = off[min(2 * P + 1, nr)];
-            b1 = off[min(2 * P + 2, nr)];
-            ia = a0;
-            ib = a1;
-        }
-        const uint32_t va = ia < a1 ? src[ia] : 0xFFFFFFFFu;
-        const uint32_t vb = ib < b1 ? src[ib] : 0xFFFFFFFFu;
-        const bool ta = ia < a1 && (ib >= b1 || va <= vb);
-        dst[o] = ta ? va : vb;
-        ia += ta ? 1 : 0;
-        ib += ta ? 0 : 1;
-    }
-}
-
-template <int E>
-__device__ __forceinline__ void snn_merge_node(SnnMergeLds<E>& L, const SnnSpec& sp, int64_t n, int64_t j,
-                                               const SnnMember& m, int lane, const int2* __restrict__ hosts_s,
-                                               const SnnRows& rows, int64_t* __restrict__ cnt) {
-    using K = uint32_t;
-    const int kmax = sp.kk[sp.nk - 1];
-    // member lane's host items (ascending hosts above j) and its own item (s > j)
-    const bool selfi = lane >= 1 && lane <= kmax && m.len > 0 && m.cur > (int)j;
-    const int hl = m.len - (selfi ? 1 : 0);
-    const int incl = snn_scan_add(hl);
-    const int MH = __builtin_amdgcn_readlane(incl, 63);
-    const int pre = incl - hl;
-    K sk[1] = {selfi ? SnnKeyT<K>::make(m.cur, lane, 0) : ~(K)0};
-    snn_bitonic<1, K>(sk, lane);  // the self run, sorted across lanes
-    const int ns = __popcll(__ballot(selfi));
-    const int M = MH + ns;
-#pragma unroll
-    for (int e = 0; e < E; ++e) L.u.mark[64 * e + lane] = -1;
-    if (lane <= kmax) L.mem[lane] = make_int4((int)m.h0, (int)m.hend, m.cur, pre);
-    WAVE_LDS_SYNC();
-    if (lane <= kmax && hl > 0) L.u.mark[pre] = lane;
-    WAVE_LDS_SYNC();
-    int mi[E];
-    int carry = INT_MIN;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int v = snn_scan_max(max(L.u.mark[64 * e + lane], carry));
-        carry = __builtin_amdgcn_readlane(v, 63);
-        mi[e] = v;
-    }
-    int2 hv[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int t = 64 * e + lane;
-        hv[e] = make_int2(0, 0);
-        if (t < MH) {
-            const int4 md = L.mem[mi[e]];
-            hv[e] = hosts_s[md.x + (t - md.w)];
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int t = 64 * e + lane;
-        if (t < MH) L.a[t] = SnnKeyT<K>::make(hv[e].x, mi[e], hv[e].y);
-    }
-    if (lane < ns) L.a[MH + lane] = sk[0];
-    if (lane <= kmax) L.off[0][lane] = pre;
-    if (lane == kmax + 1) L.off[0][lane] = MH;
-    if (lane == kmax + 2) L.off[0][lane] = M;
-    int nr = kmax + 2;
-    WAVE_LDS_SYNC();
-    const int VT = (M + 63) >> 6;
-    uint32_t* src = L.a;
-    uint32_t* dst = L.u.b;
-    int cur = 0;
-    while (nr > 1) {
-        snn_merge_level(src, dst, L.off[cur], nr, M, VT, lane);
-        const int nr2 = (nr + 1) >> 1;
-        if (lane < nr2) L.off[cur ^ 1][lane] = L.off[cur][2 * lane];
-        if (lane == nr2) L.off[cur ^ 1][nr2] = M;
-        WAVE_LDS_SYNC();
-        uint32_t* t = src;
-        src = dst;
-        dst = t;
-        cur ^= 1;
-        nr = nr2;
-    }
-    K x[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int idx = E * lane + e;
-        x[e] = idx < M ? src[idx] : ~(K)0;
-    }
-    snn_emit_sorted<E, 1, K>(L, sp, n, j, 0, lane, x, rows, cnt);
-}
 
 // Size classes (items M of a node): 0: M <= 512 (E = 4 or 8 per node),
 // 1: <= 1024 (E = 16), 2: <= 2048 (E = 32), 3: <= 4096 (the hubs: 4 waves x
@@ -924,14 +836,43 @@ __device__ __forceinline__ void snn_merge_node(SnnMergeLds<E>& L, const SnnSpec&
 // wave (4 waves per block, 2 for class 2: its LDS stage is 8-16 KB per wave);
 // class 3 runs one node per 256-thread block over a fixed grid.
 __host__ __device__ constexpr int snn_bitonic_wpb(int cls) { return cls == 2 ? 2 : 4; }
-template <int CLS, typename K, bool MERGE = false, bool BUCKET = false>
+
+// Row classes (snn_cls_* below): the member slots of a class's root row.
+struct SnnClsIn {
+    const int* croot;      // [u] root row of each class
+    const int* mcls;       // [n (kmax + 1)] member class of root slot (row, lane), -1 = none
+    const unsigned* incl;  // [n (kmax + 1)] the member's packed inclusion counts (4 bits per graph)
+    const int64_t* ucount;  // device: u, the number of classes
+};
+
+// Member `lane` of class c: the class of a distinct member of its root's N+
+// set; its items are the hosts after the class in that member's host list.
+__device__ __forceinline__ SnnMember snn_cls_member(const SnnClsIn& ci, int kmax, int64_t c, int lane,
+                                                    const int64_t* __restrict__ hoff, const int* __restrict__ bp) {
+    SnnMember m{0, 0, 0, 0};
+    if (lane > kmax) return m;
+    const int64_t slot = (int64_t)ci.croot[c] * (kmax + 1) + lane;
+    const int cs = ci.mcls[slot];
+    if (cs < 0) return m;
+    m.cur = (int)ci.incl[slot];
+    m.h0 = hoff[cs] + bp[slot] + 1;
+    m.hend = hoff[cs + 1];
+    m.len = (int)(m.hend - m.h0);
+    return m;
+}
+
+template <int CLS, typename K, bool BUCKET = false, bool CS = false>
 __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_kernel(
     const int32_t* __restrict__ knn, int64_t n, int kstride, SnnSpec sp, const int64_t* __restrict__ hoff,
     const int2* __restrict__ hosts_s, const int* __restrict__ bp, const int* __restrict__ split,
     int64_t* __restrict__ cnt, SnnRows rows, const int* __restrict__ list, const int64_t* __restrict__ count,
-    int* __restrict__ ov_list, int* __restrict__ ov_count, const int* __restrict__ src) {
+    int* __restrict__ ov_list, int* __restrict__ ov_count, const int* __restrict__ src, SnnClsIn ci) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kmax = sp.kk[sp.nk - 1];
+    auto member = [&](int64_t j) {
+        if constexpr (CS) return snn_cls_member(ci, kmax, j, lane, hoff, bp);
+        else return snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+    };
     if constexpr (CLS == 3) {
         __shared__ SnnBitonicLds<16, 4, K> lds3;
         const int64_t nl = *count;
@@ -942,26 +883,10 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
                 if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1)] = (int)j;
                 continue;
             }
-            const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
-            snn_bitonic_node<16, 4, K>(lds3, sp, n, j, m, wv, lane, hosts_s, rows, cnt);
+            const SnnMember m = member(j);
+            snn_bitonic_node<16, 4, K, false, CS>(lds3, sp, n, j, m, wv, lane, hosts_s, rows, cnt);
             __syncthreads();
         }
-    } else if constexpr (MERGE) {
-        constexpr int EM = CLS == 0 ? 8 : (CLS == 1 ? 16 : 32);
-        constexpr int WPB = snn_bitonic_wpb(CLS);
-        __shared__ SnnMergeLds<EM> ldsm[WPB];
-        const int64_t f = (int64_t)blockIdx.x * WPB + wv;
-        if (f >= *count) return;
-        const int64_t j = list[f];
-        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
-        if constexpr (CLS == 0) {
-            if (__builtin_amdgcn_readlane(snn_scan_add(m.len), 63) <= 256) {
-                snn_merge_node<4>(*reinterpret_cast<SnnMergeLds<4>*>(&ldsm[wv]), sp, n, j, m, lane, hosts_s, rows,
-                                  cnt);
-                return;
-            }
-        }
-        snn_merge_node<EM>(ldsm[wv], sp, n, j, m, lane, hosts_s, rows, cnt);
     } else {
         constexpr int EM = CLS == 0 ? 8 : (CLS == 1 ? 16 : 32);
         constexpr int WPB = snn_bitonic_wpb(CLS);
@@ -969,15 +894,15 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
         const int64_t f = (int64_t)blockIdx.x * WPB + wv;
         if (f >= *count) return;
         const int64_t j = list[f];
-        const SnnMember m = snn_member(knn, n, kstride, kmax, j, lane, hoff, bp, split);
+        const SnnMember m = member(j);
         if constexpr (CLS == 0) {
             if (__builtin_amdgcn_readlane(snn_scan_add(m.len), 63) <= 256) {
-                snn_bitonic_node<4, 1, K>(*reinterpret_cast<SnnBitonicLds<4, 1, K>*>(&lds_all[wv]), sp, n, j, m, 0,
-                                          lane, hosts_s, rows, cnt);
+                snn_bitonic_node<4, 1, K, false, CS>(*reinterpret_cast<SnnBitonicLds<4, 1, K>*>(&lds_all[wv]), sp, n,
+                                                     j, m, 0, lane, hosts_s, rows, cnt);
                 return;
             }
         }
-        snn_bitonic_node<EM, 1, K, BUCKET && CLS >= 1>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
+        snn_bitonic_node<EM, 1, K, BUCKET && CLS >= 1, CS>(lds_all[wv], sp, n, j, m, 0, lane, hosts_s, rows, cnt);
     }
 }
 
@@ -997,7 +922,8 @@ __global__ __launch_bounds__(64 * snn_bitonic_wpb(CLS)) void snn_bitonic_build_k
 // ~23% of the copies (cfg3: ~7k of ~30k nodes skipped instead of ~30k).
 template <bool PACK>
 __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
-                                                      SnnSpec sp, int* __restrict__ src) {
+                                                      SnnSpec sp, int* __restrict__ src,
+                                                      const int32_t* __restrict__ cell) {
     constexpr int WL = PACK ? 32 : 64;  // lanes per node (PACK: kmax <= 31, two nodes per wave)
     constexpr int NPW = 64 / WL;
     const int lane = threadIdx.x & (WL - 1);
@@ -1018,6 +944,7 @@ __global__ __launch_bounds__(256) void snn_src_kernel(const int32_t* __restrict_
         // distance 0, ordered by row, so it is the cell's lowest other row)
         const int r = __shfl(a, 1, WL);
         bool ok = live && r >= 0 && r < (int)j && mine(__ballot(bad)) == 0ull;
+        if (cell && ok) ok = cell[r] == cell[j];  // row classes: copies of one cell only
         if (mine(__ballot(ok)) != 0ull) {  // (uniform in the node's lanes)
             int b = r;
             if (ok && lane >= 1 && lane <= kmax) b = knn[(int64_t)r * kstride + lane - 1];
@@ -1081,6 +1008,169 @@ __global__ __launch_bounds__(256) void snn_copy_rows_kernel(int64_t n, SnnSpec s
     }
 }
 
+// ------------------------------------------------------------ row classes --
+// Bootstrap rows repeat cells (:394): about a third of the rows at cfg3 are
+// extra copies.  A CLASS is a set of rows chained by src (equal N+_k sets for
+// every graph -- snn_src_kernel -- and, when the caller passes cell ids, the
+// same cell); its root, the lowest row, stands for it.  For NUMBER weights
+//   w_k(x, y) = |N+_k(x) n N+_k(y)| = sum over classes c of |S_x(c) n S_y(c)|,
+// S_x(c) = the rows of c in N+_k(x).  Copies of one point sit at equal
+// distance from every row, ordered by row index, so S_x(c) is a PREFIX of c's
+// rows in row order, and |S_x(c) n S_y(c)| = min(t_x(c), t_y(c)) with t the
+// prefix lengths.  So the graph of the classes -- items (partner class H,
+// per-graph min(t_R(c), t_H(c))) over the member classes c of each root R --
+// carries every row-level weight: rows x in R, y in H get w(R, H), and two
+// rows of one class get k + 1 (their common set).  snn_cls_members_kernel
+// checks the prefix property on every root's list (an input that breaks it
+// sets the status: the caller takes the row-level pass).  At cfg3 a root has
+// ~14 member classes instead of 21 member rows, and the class items are ~1/3
+// of the row items; the rows are expanded only on the host (ccg_snn_graphs).
+
+// root[x]: the end of x's src chain (src[r] < r); isroot[x] for the scan that
+// numbers the classes (ordinal = exclusive prefix at the root).
+// (also zeroes the contract status of snn_cls_members_kernel: no memset launch)
+__global__ void snn_cls_root_kernel(const int* __restrict__ src, int64_t n, int* __restrict__ root,
+                                    int64_t* __restrict__ isroot, int* __restrict__ status) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x == 0) *status = 0;
+    if (x >= n) return;
+    int r = (int)x;
+    while (src[r] >= 0) r = src[r];
+    root[x] = r;
+    isroot[x] = r == (int)x ? 1 : 0;
+}
+
+// Per row x: its class ordinal, its rank among its class's rows (row order:
+// every row of a class is in N+_kmin of each of them), and for a root the
+// class size and the ordinal -> root table.
+template <bool PACK>
+__global__ __launch_bounds__(256) void snn_cls_rank_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                           int kmax, const int* __restrict__ root,
+                                                           const int64_t* __restrict__ ord, int* __restrict__ row_class,
+                                                           int* __restrict__ crank, int* __restrict__ croot,
+                                                           int* __restrict__ csize) {
+    constexpr int WL = PACK ? 32 : 64;
+    constexpr int NPW = 64 / WL;
+    const int lane = threadIdx.x & (WL - 1);
+    const int half = PACK ? (int)((threadIdx.x >> 5) & 1) : 0;
+    auto mine = [&](unsigned long long b) -> unsigned long long {
+        return PACK ? ((half ? b >> 32 : b) & 0xffffffffull) : b;
+    };
+    for (int64_t xb = (int64_t)blockIdx.x * 4 * NPW; xb < n; xb += (int64_t)gridDim.x * 4 * NPW) {
+        const int64_t x = xb + (threadIdx.x / WL);
+        const bool live = x < n;
+        int a = (int)x;
+        if (live && lane >= 1 && lane <= kmax) a = knn[x * kstride + lane - 1];
+        const bool in = live && lane <= kmax && (unsigned)a < (unsigned)n;
+        const int ra = in ? root[a] : -1;
+        const int rx = live ? root[x] : -2;
+        const int cr = __popcll(mine(__ballot(in && ra == rx && a < (int)x)));
+        const int cs = __popcll(mine(__ballot(in && ra == (int)x)));
+        if (live && lane == 0) {
+            const int o = (int)ord[rx];
+            row_class[x] = o;
+            crank[x] = cr;
+            if (rx == (int)x) {
+                croot[o] = (int)x;
+                csize[o] = cs;
+            }
+        }
+    }
+}
+
+// Per root R (slots R (kmax + 1) + i, i = rank 0 .. kmax of N+(R)): the
+// distinct member classes with their prefix lengths t_k = the class's rows at
+// ranks <= k for every graph (4 bits each: a class has at most kmin + 1 <= 15
+// rows), as (member class, slot) pairs for the host-list sort (other slots:
+// key n, sorted past every class).  Checks the prefix property: a foreign
+// class's rows appear in R's list in the class's row order.
+template <bool PACK>
+__global__ __launch_bounds__(256) void snn_cls_members_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                                              SnnSpec sp, const int* __restrict__ root,
+                                                              const int* __restrict__ row_class,
+                                                              const int* __restrict__ crank, int* __restrict__ mcls,
+                                                              unsigned* __restrict__ incl, int32_t* __restrict__ keys,
+                                                              int32_t* __restrict__ vals, int* __restrict__ status) {
+    constexpr int WL = PACK ? 32 : 64;
+    constexpr int NPW = 64 / WL;
+    const int lane = threadIdx.x & (WL - 1);
+    const int kmax = sp.kk[sp.nk - 1];
+    for (int64_t xb = (int64_t)blockIdx.x * 4 * NPW; xb < n; xb += (int64_t)gridDim.x * 4 * NPW) {
+        const int64_t x = xb + (threadIdx.x / WL);
+        const bool live = x < n;
+        const bool isr = live && root[x] == (int)x;
+        int a = (int)x;
+        if (isr && lane >= 1 && lane <= kmax) a = knn[x * kstride + lane - 1];
+        const bool in = isr && lane <= kmax && (unsigned)a < (unsigned)n;
+        const int cs = in ? row_class[a] : -1 - lane;  // distinct dummies for idle lanes
+        const int own = __shfl(cs, 0, WL);
+        int before = 0;
+        unsigned t4 = 0;
+        for (int q = 0; q <= kmax; ++q) {
+            const int o = __shfl(cs, q, WL);
+            const bool same = o == cs;
+            before += (same && q < lane) ? 1 : 0;
+#pragma unroll
+            for (int t = 0; t < SNN_MAXK; ++t) t4 += (same && t < sp.nk && q <= sp.kk[t]) ? (1u << (4 * t)) : 0u;
+        }
+        const bool head = in && before == 0;
+        if (in && cs != own && crank[a] != before) atomicOr(status, 1);  // not a prefix in row order
+        if (live && lane <= kmax) {
+            const int64_t slot = x * (kmax + 1) + lane;
+            mcls[slot] = head ? cs : -1;
+            incl[slot] = t4;
+            keys[slot] = head ? cs : (int32_t)n;
+            vals[slot] = (int32_t)slot;
+        }
+    }
+}
+
+// hosts_s[p] = (host class ordinal, its inclusion fields); bp[slot] = the
+// host's position in the member class's list (hosts ascending).
+__global__ void snn_cls_hosts_kernel(const int32_t* __restrict__ skey, const int32_t* __restrict__ sval, int kmax,
+                                     const int64_t* __restrict__ hoff, const int64_t* __restrict__ ucount,
+                                     const int* __restrict__ row_class, const unsigned* __restrict__ incl,
+                                     int2* __restrict__ hosts_s, int* __restrict__ bp) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hoff[*ucount]) return;
+    const int c = skey[p], slot = sval[p];
+    const int rrow = slot / (kmax + 1);
+    hosts_s[p] = make_int2(row_class[rrow], (int)incl[slot]);
+    bp[slot] = (int)(p - hoff[c]);
+}
+
+// hoff[c] = first sorted position with key >= c (c = 0..u); entries past u
+// are unused.
+__global__ void snn_cls_hoff_kernel(const int32_t* __restrict__ skey, int64_t total, const int64_t* __restrict__ ucount,
+                                    int64_t* __restrict__ hoff) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > *ucount) return;
+    int64_t lo = 0, hi = total;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (skey[mid] < c) lo = mid + 1; else hi = mid;
+    }
+    hoff[c] = lo;
+}
+
+// Items of every class (its row capacity); 0 past u.
+template <bool PACK>
+__global__ __launch_bounds__(256) void snn_cls_items_kernel(int64_t n, int kmax, SnnClsIn ci,
+                                                            const int64_t* __restrict__ hoff,
+                                                            const int* __restrict__ bp, int64_t* __restrict__ cap) {
+    constexpr int WL = PACK ? 32 : 64;
+    constexpr int NPW = 64 / WL;
+    const int lane = threadIdx.x & (WL - 1);
+    const int64_t u = *ci.ucount;
+    for (int64_t cb = (int64_t)blockIdx.x * 4 * NPW; cb < n; cb += (int64_t)gridDim.x * 4 * NPW) {
+        const int64_t c = cb + (threadIdx.x / WL);
+        int v = 0;
+        if (c < u) v = snn_cls_member(ci, kmax, c, lane, hoff, bp).len;
+        for (int o = WL / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, WL);
+        if (lane == 0 && c < n) cap[c] = c < u ? v : 0;
+    }
+}
+
 // --------------------------------------------------------- block tier --
 // Nodes beyond the bitonic tier (more than SNN_BITONIC_MAX items): one
 // 256-thread block and a 16K-slot LDS hash table per node; the table is
@@ -1109,12 +1199,54 @@ __device__ __forceinline__ bool table_insert_blk(int* keys, unsigned* vals, int*
     return false;
 }
 
+// Every item (partner p > j, packed contribution c) of node j -- row-level
+// (members of N+(j), their host lists) or class-level (CS: member classes
+// of class j, the hosts after j) -- handed to f(p, c) by the block's threads.
+template <bool CS, typename F>
+__device__ __forceinline__ void snn_node_items(const int32_t* __restrict__ knn, int64_t n, int kstride,
+                                               const SnnSpec& sp, int64_t j, const int64_t* __restrict__ hoff,
+                                               const int2* __restrict__ hosts, const int* __restrict__ bp,
+                                               const SnnClsIn& ci, F&& f) {
+    const int kmax = sp.kk[sp.nk - 1];
+    for (int i = 0; i <= kmax; ++i) {
+        if constexpr (CS) {
+            const SnnMember m = snn_cls_member(ci, kmax, j, i, hoff, bp);
+            for (int o = threadIdx.x; o < m.len; o += blockDim.x) {
+                const int2 hr = hosts[m.h0 + o];
+                f(hr.x, snn_nib2byte(snn_min4((unsigned)m.cur, (unsigned)hr.y)));
+            }
+        } else {
+            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
+            if ((unsigned)cur >= (unsigned)n || (i > 0 && cur == j)) continue;  // invalid (CCG_DERR_SNN_INDEX)
+            const int64_t h0 = hoff[cur];
+            const int64_t len = hoff[cur + 1] - h0 + 1;
+            for (int64_t o = threadIdx.x; o < len; o += blockDim.x) {
+                int p, rp;
+                if (o == len - 1) {
+                    p = cur;
+                    rp = 0;
+                } else {
+                    const int2 hr = hosts[h0 + o];
+                    p = hr.x;
+                    rp = hr.y;
+                }
+                if (p > j) {
+                    const unsigned c = snn_contrib(sp, i, rp);
+                    if (c != sp.init) f(p, c);
+                }
+            }
+        }
+    }
+}
+
+template <bool CS>
 __global__ __launch_bounds__(256) void snn_block_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
                                                         SnnSpec sp, const int64_t* __restrict__ hoff,
                                                         const int2* __restrict__ hosts, int64_t* __restrict__ cnt,
                                                         SnnRows rows, const int* __restrict__ ov_list,
                                                         const int* __restrict__ ov_count, int* __restrict__ ov2_list,
-                                                        int* __restrict__ ov2_count) {
+                                                        int* __restrict__ ov2_count, const int* __restrict__ bp,
+                                                        SnnClsIn ci) {
     __shared__ int keys[SNN_BT];
     __shared__ unsigned vals[SNN_BT];
     __shared__ int count;
@@ -1123,7 +1255,6 @@ __global__ __launch_bounds__(256) void snn_block_kernel(const int32_t* __restric
     __shared__ int tcount[256];
     __shared__ int64_t wsum[4][SNN_MAXK];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int kmax = sp.kk[sp.nk - 1];
     constexpr int BITS = 14;
     constexpr int PER = SNN_BT / 256;  // slots owned per thread during compaction
     const int cap_entries = SNN_BT * 3 / 4;
@@ -1140,27 +1271,9 @@ __global__ __launch_bounds__(256) void snn_block_kernel(const int32_t* __restric
             full_s = 0;
         }
         __syncthreads();
-        for (int i = 0; i <= kmax; ++i) {
-            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
-            if ((unsigned)cur >= (unsigned)n || (i > 0 && cur == j)) continue;  // invalid (CCG_DERR_SNN_INDEX)
-            const int64_t h0 = hoff[cur];
-            const int64_t len = hoff[cur + 1] - h0 + 1;
-            for (int64_t o = tid; o < len; o += 256) {
-                int p, rp;
-                if (o == len - 1) {
-                    p = cur;
-                    rp = 0;
-                } else {
-                    const int2 hr = hosts[h0 + o];
-                    p = hr.x;
-                    rp = hr.y;
-                }
-                if (p > j) {
-                    const unsigned c = snn_contrib(sp, i, rp);
-                    if (c != sp.init && !table_insert_blk(keys, vals, &count, p, c, sp, BITS)) full_s = 1;
-                }
-            }
-        }
+        snn_node_items<CS>(knn, n, kstride, sp, j, hoff, hosts, bp, ci, [&](int p, unsigned c) {
+            if (!table_insert_blk(keys, vals, &count, p, c, sp, BITS)) full_s = 1;
+        });
         __syncthreads();
         if (full_s || count > cap_entries) {
             if (tid == 0) ov2_list[atomicAdd(ov2_count, 1)] = (int)j;
@@ -1251,17 +1364,17 @@ __global__ __launch_bounds__(256) void snn_block_kernel(const int32_t* __restric
 // --------------------------------------------------------- dense tier --
 // Exact O(n) per node with a dense word per partner.  Reads/writes go
 // through agent-scope atomics so the block never sees stale L1 lines.
+template <bool CS>
 __global__ __launch_bounds__(256) void snn_dense_kernel(const int32_t* __restrict__ knn, int64_t n, int kstride,
                                                         SnnSpec sp, const int64_t* __restrict__ hoff,
                                                         const int2* __restrict__ hosts,
                                                         const int* __restrict__ ov_list,
                                                         const int* __restrict__ ov_count,
                                                         unsigned* __restrict__ dense_all, int64_t* __restrict__ cnt,
-                                                        SnnRows rows) {
+                                                        SnnRows rows, const int* __restrict__ bp, SnnClsIn ci) {
     __shared__ int64_t wsum[4];
     unsigned* dense = dense_all + (int64_t)blockIdx.x * n;
     const int nov = *ov_count;
-    const int kmax = sp.kk[sp.nk - 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const bool write = rows.roff[n] <= rows.cap;
     for (int f = blockIdx.x; f < nov; f += gridDim.x) {
@@ -1269,27 +1382,8 @@ __global__ __launch_bounds__(256) void snn_dense_kernel(const int32_t* __restric
         for (int64_t p = j + 1 + threadIdx.x; p < n; p += 256)
             __hip_atomic_store(&dense[p], sp.init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        for (int i = 0; i <= kmax; ++i) {
-            const int32_t cur = (i == 0) ? (int32_t)j : knn[j * kstride + i - 1];
-            if ((unsigned)cur >= (unsigned)n || (i > 0 && cur == j)) continue;  // invalid (CCG_DERR_SNN_INDEX)
-            const int64_t h0 = hoff[cur];
-            const int64_t len = hoff[cur + 1] - h0 + 1;
-            for (int64_t o = threadIdx.x; o < len; o += 256) {
-                int p, rp;
-                if (o == len - 1) {
-                    p = cur;
-                    rp = 0;
-                } else {
-                    const int2 hr = hosts[h0 + o];
-                    p = hr.x;
-                    rp = hr.y;
-                }
-                if (p > j) {
-                    const unsigned c = snn_contrib(sp, i, rp);
-                    if (c != sp.init) snn_update(sp, &dense[p], c);
-                }
-            }
-        }
+        snn_node_items<CS>(knn, n, kstride, sp, j, hoff, hosts, bp, ci,
+                           [&](int p, unsigned c) { snn_update(sp, &dense[p], c); });
         __syncthreads();
         // the row: partners of the union graph (the largest k) in ascending p
         const int64_t ro = rows.roff[j];
@@ -1381,31 +1475,6 @@ __global__ void snn_copy_totals(const int64_t* __restrict__ cnt, int64_t n, int 
 }
 
 // --------------------------------------------------------------- driver --
-// CCG_SNN_NO_COPY=1 builds every node (tools / A-B checks of the copy pass)
-static bool snn_no_copy() {
-    static const bool v = [] {
-        const char* e = getenv("CCG_SNN_NO_COPY");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
-// Sort tier of size classes 1-2 (bit-identical rows in every mode):
-// CCG_SNN_SORT=bucket (default; 64 partner-range buckets, one register network
-// per lane: classes 1 / 2 172.5 -> 162.6 / 156.4 -> 154.7 us isolated at
-// cfg3), =bitonic (the wave-wide register bitonic sort), =merge (the merge
-// tier of the sorted host runs, NUMBER only: measured slower, SNN 1.01 against
-// 0.81 ms per bootstrap).  Returns 0 bitonic, 1 merge, 2 bucket.
-static int snn_sort_mode() {
-    static const int v = [] {
-        const char* e = getenv("CCG_SNN_SORT");
-        if (e && strcmp(e, "merge") == 0) return 1;
-        if (e && strcmp(e, "bitonic") == 0) return 0;
-        return 2;
-    }();
-    return v;
-}
-
 static int snn_spec(const int* ks, int nk, int type, int kstride, SnnSpec* sp) {
     CCG_REQUIRE(ks, "SNN: NULL ks");
     CCG_REQUIRE(nk >= 1 && nk <= SNN_MAXK, "SNN: 1 <= nk <= %d", SNN_MAXK);
@@ -1473,52 +1542,207 @@ static int snn_build(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, c
     int64_t* ccount = cls + (n + 1);
     int* lists = (int*)(ccount + 8);
     // copy nodes (NUMBER graphs only: RANK weights depend on the ranks)
-    int* src = sp.type == CCG_SNN_NUMBER && !snn_no_copy() ? ov : nullptr;
+    int* src = sp.type == CCG_SNN_NUMBER ? ov : nullptr;
     if (src) {
         if (kmax <= 31)
             snn_src_kernel<true><<<(unsigned)std::min<int64_t>(ccg_cdiv(n, 8), 16384), 256, 0, st>>>(knn, n, kstride,
-                                                                                                      sp, src);
+                                                                                                      sp, src, nullptr);
         else
-            snn_src_kernel<false><<<nblk, 256, 0, st>>>(knn, n, kstride, sp, src);
+            snn_src_kernel<false><<<nblk, 256, 0, st>>>(knn, n, kstride, sp, src, nullptr);
     }
     snn_class_kernel<<<(unsigned)ccg_cdiv(std::max<int64_t>(n + 1, 64), 256), 256, 0, st>>>(roff, n, cls, cnt, sp.nk,
-                                                                                           ov_count, src);
+                                                                                           ov_count, src, nullptr);
     rc = ccg_scan_i64(ctx, cls, cls, n, st);
     if (rc) return rc;
-    snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount);
+    snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount, nullptr);
     int* ov_list = ov + 3 * n;
-#define SNN_BITONIC(CLS_, K_, GRID_, MG_, BK_)                                                                 \
-    snn_bitonic_build_kernel<CLS_, K_, MG_, BK_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(             \
+#define SNN_BITONIC(CLS_, K_, GRID_, BK_)                                                                      \
+    snn_bitonic_build_kernel<CLS_, K_, BK_><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(                  \
         knn, n, kstride, sp, hoff, hosts_s, bp, split, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
-        ov_count + 1, src)
-#define SNN_BITONIC_ALL(K_, MG_, BK_)                                             \
-    do {                                                                          \
-        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), MG_, false); \
-        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), MG_, BK_);   \
-        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), MG_, BK_);   \
-        SNN_BITONIC(3, K_, 1024u, false, false);                                   \
+        ov_count + 1, src, SnnClsIn{})
+#define SNN_BITONIC_ALL(K_)                                                   \
+    do {                                                                      \
+        SNN_BITONIC(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), false); \
+        SNN_BITONIC(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), true);  \
+        SNN_BITONIC(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), true);  \
+        SNN_BITONIC(3, K_, 1024u, false);                                     \
     } while (0)
-    const int mode = snn_sort_mode();
-    if (sp.type == CCG_SNN_NUMBER) {
-        if (mode == 1) SNN_BITONIC_ALL(uint32_t, true, false);  // the merge tier (sorted host runs)
-        else if (mode == 2) SNN_BITONIC_ALL(uint32_t, false, true);
-        else SNN_BITONIC_ALL(uint32_t, false, false);
-    } else {
-        if (mode == 2) SNN_BITONIC_ALL(unsigned long long, false, true);
-        else SNN_BITONIC_ALL(unsigned long long, false, false);
-    }
+    // classes 1-2 sort through the bucket tier (64 partner-range buckets, one
+    // register network per lane; a bucket over its cap takes the wave-wide
+    // bitonic sort): classes 1 / 2 172.5 -> 162.6 / 156.4 -> 154.7 us at cfg3.
+    // (Round 4's merge-path tier of the sorted host runs measured slower --
+    // 136 / 251 / 249 against 97 / 170 / 156 us per class -- and is gone.)
+    if (sp.type == CCG_SNN_NUMBER) SNN_BITONIC_ALL(uint32_t);
+    else SNN_BITONIC_ALL(unsigned long long);
 #undef SNN_BITONIC_ALL
 #undef SNN_BITONIC
     // nodes with more than SNN_BITONIC_MAX items: the block tier, then dense
-    snn_block_kernel<<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list, ov_count + 1,
-                                          ov2_list, ov_count + 2);
-    snn_dense_kernel<<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list, ov_count + 2,
-                                                       dense, cnt, rows);
+    snn_block_kernel<false><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list,
+                                                 ov_count + 1, ov2_list, ov_count + 2, bp, SnnClsIn{});
+    snn_dense_kernel<false><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
+                                                              ov_count + 2, dense, cnt, rows, bp, SnnClsIn{});
     if (src) snn_copy_rows_kernel<<<nblk, 256, 0, st>>>(n, sp, src, cnt, rows, lists + 3 * n, ccount + 3);
     rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)sp.nk * (n + 1), st);  // every graph's offsets in one scan
     if (rc) return rc;
     *cnt_out = cnt;
     *roff_out = roff;
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+// Info of a class-level build (ccg_snn_classes_dev's d_info): u, status,
+// required row capacity, then per graph its class-edge count (or -(required
+// capacity) when the rows did not fit).
+__global__ void snn_cls_info_kernel(const int64_t* __restrict__ ucount, const int* __restrict__ status,
+                                    const int64_t* __restrict__ cnt, int64_t n, int nk,
+                                    const int64_t* __restrict__ roff, int64_t rcap, int64_t* __restrict__ info) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const bool fit = roff[n] <= rcap;
+    info[0] = *ucount;
+    info[1] = *status;
+    info[2] = roff[n];
+    for (int t = 0; t < nk; ++t) info[3 + t] = fit ? cnt[(int64_t)t * (n + 1) + n] - cnt[(int64_t)t * (n + 1)] : -roff[n];
+}
+
+// Whether the class-level build serves these graphs: NUMBER weights, and the
+// 4-bit prefix fields hold every class (a class has at most kmin + 1 rows).
+static bool snn_cls_ok(const SnnSpec& sp) { return sp.type == CCG_SNN_NUMBER && sp.kk[0] <= 14; }
+
+// The class-level graph (row classes above).  row_class[n] (class ordinal of
+// every row), croot[n] (root row of ordinal c < u); class rows over ordinals:
+// roff[n + 1] capacity-based (entries past u are empty), rlen, nbr (partner
+// classes > c, ascending), wpk (per-graph packed weights), written when
+// roff[n] <= cap.  *cnt_out: per-graph exclusive scans of the class rows'
+// edge counts; *u_out: device u; *status_out: device int, nonzero when the
+// input breaks the class contract (a prefix check failed: take the row pass).
+static int snn_build_cls(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                         const SnnSpec& sp, hipStream_t st, int32_t* row_class, int32_t* croot, int64_t* roff,
+                         int32_t* rlen, int32_t* nbr, uint32_t* wpk, int64_t cap, int64_t** cnt_out,
+                         const int64_t** u_out, const int** status_out) {
+    const int kmax = sp.kk[sp.nk - 1];
+    const int64_t S = n * (kmax + 1);  // member slots (root row, rank)
+    CCG_REQUIRE(S < (1LL << 31) - 64, "SNN: n*(kmax+1) too large");
+    CCG_REQUIRE(n < (1LL << SNN_CLS_BITS), "SNN: n must be below 2^%d", SNN_CLS_BITS);
+    int64_t* A = (int64_t*)ccg_ws(ctx, WS_SNN_A, sizeof(int64_t) * (2 * (n + 1) + 16));
+    int2* hosts_s = (int2*)ccg_ws(ctx, WS_SNN_B, sizeof(int2) * (S + 1));
+    int64_t* cnt = (int64_t*)ccg_ws(ctx, WS_SNN_C, sizeof(int64_t) * (sp.nk * (n + 1) + 1));
+    int* ov = (int*)ccg_ws(ctx, WS_SNN_E, sizeof(int) * (6 * n + 192));
+    unsigned* dense = (unsigned*)ccg_ws(ctx, WS_SNN_D, sizeof(unsigned) * n * SNN_DENSE_BLOCKS);
+    int32_t* pairs = (int32_t*)ccg_ws(ctx, WS_SNN_F, sizeof(int32_t) * 4 * (S + 16));
+    int* G = (int*)ccg_ws(ctx, WS_SNN_G, sizeof(int) * 3 * (S + 64));
+    int64_t* cls = (int64_t*)ccg_ws(ctx, WS_SNN_H, sizeof(int64_t) * (n + 1 + 8) + sizeof(int) * 4 * n);
+    if (!A || !hosts_s || !cnt || !ov || !dense || !pairs || !G || !cls) return CCG_ENOMEM;
+    int64_t* hoff = A;            // [n + 1] (u + 1 used)
+    int64_t* ord = A + (n + 1);   // [n + 1] isroot -> exclusive scan; ord[n] = u
+    const int64_t* ucount = ord + n;
+    int* src = ov;                // [n]
+    int* root = ov + n;           // [n]
+    int* crank = ov + 2 * n;      // [n]
+    int* csize = ov + 3 * n;      // [n]
+    int* ov_list = ov + 4 * n;    // [n]
+    int* ov2_list = ov + 5 * n;   // [n]
+    int* ov_count = ov + 6 * n;   // [64] (zeroed by the class kernel)
+    int* status = ov_count + 64;  // [1]
+    int32_t* keys = pairs;
+    int32_t* vals = pairs + (S + 16);
+    int32_t* skey = vals + (S + 16);
+    int32_t* sval = skey + (S + 16);
+    int* bp = G;
+    int* mcls = G + (S + 64);
+    unsigned* incl = (unsigned*)(G + 2 * (S + 64));
+    int64_t* ccount = cls + (n + 1);
+    int* lists = (int*)(ccount + 8);
+    const unsigned nw8 = (unsigned)std::min<int64_t>(ccg_cdiv(n, 8), 16384);  // two rows per wave (PACK)
+    const unsigned nw4 = (unsigned)std::min<int64_t>(ccg_cdiv(n, 4), 16384);
+    const bool pack = kmax <= 31;
+    // 1. classes: src chains (equal N+ sets, same cell), roots, ordinals, ranks
+    if (pack) snn_src_kernel<true><<<nw8, 256, 0, st>>>(knn, n, kstride, sp, src, cell);
+    else snn_src_kernel<false><<<nw4, 256, 0, st>>>(knn, n, kstride, sp, src, cell);
+    snn_cls_root_kernel<<<(unsigned)ccg_cdiv(n, 256), 256, 0, st>>>(src, n, root, ord, status);
+    int rc = ccg_scan_i64(ctx, ord, ord, n, st);
+    if (rc) return rc;
+    if (pack)
+        snn_cls_rank_kernel<true><<<nw8, 256, 0, st>>>(knn, n, kstride, kmax, root, ord, row_class, crank, croot, csize);
+    else
+        snn_cls_rank_kernel<false><<<nw4, 256, 0, st>>>(knn, n, kstride, kmax, root, ord, row_class, crank, croot,
+                                                         csize);
+    // 2. member classes of every root, the hosts of every class
+    if (pack)
+        snn_cls_members_kernel<true><<<nw8, 256, 0, st>>>(knn, n, kstride, sp, root, row_class, crank, mcls, incl,
+                                                           keys, vals, status);
+    else
+        snn_cls_members_kernel<false><<<nw4, 256, 0, st>>>(knn, n, kstride, sp, root, row_class, crank, mcls, incl,
+                                                            keys, vals, status);
+    int bits = 1;
+    while ((1LL << bits) <= n) ++bits;
+    rc = ccg_sort_pairs_i32(ctx, keys, skey, vals, sval, S, bits, st);
+    if (rc) return rc;
+    snn_cls_hoff_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(skey, S, ucount, hoff);
+    snn_cls_hosts_kernel<<<(unsigned)ccg_cdiv(S, 256), 256, 0, st>>>(skey, sval, kmax, hoff, ucount, row_class, incl,
+                                                                     hosts_s, bp);
+    // 3. capacities, size classes, build
+    const SnnClsIn ci{croot, mcls, incl, ucount};
+    if (pack) snn_cls_items_kernel<true><<<nw8, 256, 0, st>>>(n, kmax, ci, hoff, bp, roff);
+    else snn_cls_items_kernel<false><<<nw4, 256, 0, st>>>(n, kmax, ci, hoff, bp, roff);
+    rc = ccg_scan_i64(ctx, roff, roff, n, st);
+    if (rc) return rc;
+    SnnRows rows{roff, rlen, nbr, wpk, cap};
+    snn_class_kernel<<<(unsigned)ccg_cdiv(std::max<int64_t>(n + 1, 64), 256), 256, 0, st>>>(roff, n, cls, cnt, sp.nk,
+                                                                                           ov_count, nullptr, ucount);
+    rc = ccg_scan_i64(ctx, cls, cls, n, st);
+    if (rc) return rc;
+    snn_class_scatter_kernel<<<(unsigned)ccg_cdiv(n + 1, 256), 256, 0, st>>>(cls, n, lists, ccount, ucount);
+#define SNN_CBUILD(CLS_, K_, GRID_, BK_)                                                                         \
+    snn_bitonic_build_kernel<CLS_, K_, BK_, true><<<(GRID_), 64 * snn_bitonic_wpb(CLS_), 0, st>>>(              \
+        knn, n, kstride, sp, hoff, hosts_s, bp, nullptr, cnt, rows, lists + (CLS_) * n, ccount + (CLS_), ov_list, \
+        ov_count + 1, nullptr, ci)
+#define SNN_CBUILD_ALL(K_)                                                   \
+    do {                                                                     \
+        SNN_CBUILD(0, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(0)), false); \
+        SNN_CBUILD(1, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(1)), true);  \
+        SNN_CBUILD(2, K_, (unsigned)ccg_cdiv(n, snn_bitonic_wpb(2)), true);  \
+        SNN_CBUILD(3, K_, 1024u, false);                                     \
+    } while (0)
+    // 32-bit keys (partner << 12 | three 4-bit fields) when they fit
+    if (sp.nk <= 3 && n < (1LL << 20)) SNN_CBUILD_ALL(uint32_t);
+    else SNN_CBUILD_ALL(unsigned long long);
+#undef SNN_CBUILD_ALL
+#undef SNN_CBUILD
+    snn_block_kernel<true><<<256, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, cnt, rows, ov_list, ov_count + 1,
+                                                ov2_list, ov_count + 2, bp, ci);
+    snn_dense_kernel<true><<<SNN_DENSE_BLOCKS, 256, 0, st>>>(knn, n, kstride, sp, hoff, hosts_s, ov2_list,
+                                                             ov_count + 2, dense, cnt, rows, bp, ci);
+    rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)sp.nk * (n + 1), st);
+    if (rc) return rc;
+    *cnt_out = cnt;
+    *u_out = ucount;
+    *status_out = status;
+    CCG_HIP(hipGetLastError());
+    return CCG_OK;
+}
+
+extern "C" int ccg_snn_classes_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                                   const int* ks, int nk, int32_t* row_class, int32_t* class_root, int64_t* class_off,
+                                   int32_t* class_len, int32_t* nbr, uint32_t* wpk, int64_t cap, int64_t* d_info,
+                                   void* stream) {
+    CCG_REQUIRE(ctx && knn && ks && row_class && class_root && class_off && class_len && d_info,
+                "ccg_snn_classes_dev: NULL argument");
+    CCG_REQUIRE(cap == 0 || (nbr && wpk), "ccg_snn_classes_dev: NULL rows with cap > 0");
+    CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1, "ccg_snn_classes_dev: bad n");
+    SnnSpec sp;
+    int rc = snn_spec(ks, nk, CCG_SNN_NUMBER, kstride, &sp);
+    if (rc) return rc;
+    CCG_REQUIRE(snn_cls_ok(sp), "ccg_snn_classes_dev: the smallest k must be <= 14 (4-bit class prefix fields)");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int t_all = ccg_timer_start(ctx, CCG_KT_SNN, st);
+    int64_t* cnt = nullptr;
+    const int64_t* u = nullptr;
+    const int* status = nullptr;
+    rc = snn_build_cls(ctx, knn, n, kstride, cell, sp, st, row_class, class_root, class_off, class_len, nbr, wpk, cap,
+                       &cnt, &u, &status);
+    if (rc) return rc;
+    snn_cls_info_kernel<<<1, 64, 0, st>>>(u, status, cnt, n, nk, class_off, cap, d_info);
+    ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
@@ -1610,37 +1834,44 @@ extern "C" int ccg_snn_reserve(ccg_ctx* ctx, int64_t entries) {
 
 // ------------------------------------------------ host consumers (R, Python) --
 // What a host clustering call (igraph::make_graph + cluster_leiden, :656-658)
-// needs is every kNum graph as an edge list.  The device builds the union
-// graph's rows once (snn_build: the same kernels ccg_snn_rows_dev runs); the
-// rows -- 8 B per union edge, partner + packed per-graph values -- and the
-// per-graph row offsets go to pinned host memory the context owns, and each
-// graph's (i, j, w) list is decoded from them on the host.  The device work is
-// the rows pass alone (no per-graph emit), and PCIe carries 8 B per union edge
-// instead of 16 B per edge per graph.
+// needs is every kNum graph as an edge list.  The device builds the graph
+// ONCE -- for NUMBER graphs the class-level rows (snn_build_cls: the kernels
+// of ccg_snn_classes_dev, which bench.py times), otherwise (RANK, or an input
+// that breaks the class contract) the union graph's rows (snn_build: the
+// kernels of ccg_snn_rows_dev) -- and copies the rows (8 B per class / union
+// edge: partner + packed per-graph values), the per-graph row offsets and the
+// row -> class map to pinned host memory the context owns.  Each graph's
+// row-level (i, j, w) list is decoded from them on the host, sorted by (i, j).
+// No per-graph edge list is formed on the device.
 struct SnnStage {
     int64_t n = 0;
     SnnSpec sp{};
-    int64_t* roff = nullptr;   // n + 1 capacity-based row offsets
+    bool classes = false;      // class-level rows (u classes) or row-level union rows
+    int64_t u = 0;
+    int64_t* roff = nullptr;   // n + 1 capacity-based row offsets (rows or class ordinals)
     int32_t* rlen = nullptr;   // n used lengths
     int64_t* cnt = nullptr;    // nk (n + 1): per-graph exclusive scans of the row edge counts
     int32_t* nbr = nullptr;    // roff[n] partners
     uint32_t* wpk = nullptr;   // roff[n] packed per-graph values
-    size_t cap_n = 0, cap_l = 0, cap_e = 0, cap_w = 0, cap_c = 0;
+    int32_t* rcls = nullptr;   // n: class ordinal of every row (classes)
+    size_t cap_n = 0, cap_l = 0, cap_e = 0, cap_w = 0, cap_c = 0, cap_r = 0;
+    int64_t ne[SNN_MAXK] = {0, 0, 0, 0};  // row-level edges per graph
+    // classes: the rows of every class (ascending), built on the first fetch
+    std::vector<int64_t> mstart;
+    std::vector<int32_t> mrows;
     bool valid = false;
 };
 
 static void snn_stage_release(SnnStage* s) {
-    if (s->roff) (void)hipHostFree(s->roff);
-    if (s->rlen) (void)hipHostFree(s->rlen);
-    if (s->cnt) (void)hipHostFree(s->cnt);
-    if (s->nbr) (void)hipHostFree(s->nbr);
-    if (s->wpk) (void)hipHostFree(s->wpk);
+    for (void* p : {(void*)s->roff, (void*)s->rlen, (void*)s->cnt, (void*)s->nbr, (void*)s->wpk, (void*)s->rcls})
+        if (p) (void)hipHostFree(p);
     s->roff = nullptr;
     s->rlen = nullptr;
     s->cnt = nullptr;
     s->nbr = nullptr;
     s->wpk = nullptr;
-    s->cap_n = s->cap_l = s->cap_e = s->cap_w = s->cap_c = 0;
+    s->rcls = nullptr;
+    s->cap_n = s->cap_l = s->cap_e = s->cap_w = s->cap_c = s->cap_r = 0;
 }
 
 void ccg_snn_stage_free(ccg_ctx* ctx) {
@@ -1670,8 +1901,138 @@ static double snn_host_weight(const SnnSpec& sp, unsigned v, int t) {
     return w < 1e-6 ? 1e-6 : w;
 }
 
-extern "C" int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk,
-                              int type, int64_t* nedges) {
+static bool snn_host_has(const SnnSpec& sp, unsigned v, int t) {
+    const unsigned b = (v >> (8 * t)) & 0xFFu;
+    return sp.type == CCG_SNN_NUMBER ? b != 0u : b != 0xFFu;
+}
+
+// Host threads for the decode (the split does not change the output).
+static unsigned snn_host_threads(int64_t work) {
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    return work < (1 << 16) ? 1u : nt;
+}
+
+template <typename F>
+static void snn_host_parallel(int64_t n, unsigned nt, F&& f) {
+    if (nt <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned q = 0; q < nt; ++q) th.emplace_back(f, n * q / nt, n * (q + 1) / nt);
+    for (auto& x : th) x.join();
+}
+
+// One device pass + the copy to the host staging (rows or classes).
+static int snn_graphs_stage(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                            const SnnSpec& sp, SnnStage* S, bool try_classes) {
+    hipStream_t st = ctx->stream;
+    const int nk = sp.nk, kmax = sp.kk[nk - 1];
+    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
+    int32_t* dcell = cell ? (int32_t*)ccg_ws(ctx, WS_HOST_B, sizeof(int32_t) * n) : nullptr;
+    int32_t* dcls = (int32_t*)ccg_ws(ctx, WS_HOST_C, sizeof(int32_t) * 2 * n + 64);
+    int64_t* dinfo = (int64_t*)ccg_ws(ctx, WS_HOST_E, 256);
+    if (!dknn || (cell && !dcell) || !dcls || !dinfo) return CCG_ENOMEM;
+    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
+    if (cell) CCG_HIP(hipMemcpyAsync(dcell, cell, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    int rc = snn_host_grow(&S->roff, &S->cap_n, (size_t)n + 1);
+    if (!rc) rc = snn_host_grow(&S->rlen, &S->cap_l, (size_t)n);
+    if (!rc) rc = snn_host_grow(&S->cnt, &S->cap_c, (size_t)nk * (n + 1));
+    if (!rc) rc = snn_host_grow(&S->rcls, &S->cap_r, (size_t)n);
+    if (rc) return rc;
+    bool classes = try_classes && snn_cls_ok(sp);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        const int64_t rcap =
+            ctx->snn_row_reserve > 0 ? ctx->snn_row_reserve : (int64_t)SNN_ROW_RESERVE * n * (kmax + 1);
+        char* rbuf = (char*)ccg_ws(ctx, WS_SNN_ROWS,
+                                   (sizeof(int32_t) + sizeof(uint32_t)) * rcap + sizeof(int32_t) * (n + 64));
+        if (!rbuf) return CCG_ENOMEM;
+        int32_t* nbr = (int32_t*)rbuf;
+        uint32_t* wpk = (uint32_t*)(nbr + rcap);
+        int32_t* rlen = (int32_t*)(wpk + rcap);
+        int64_t* cnt = nullptr;
+        const int64_t* roff = nullptr;
+        int64_t info[3] = {0, 0, 0};
+        if (classes) {
+            int64_t* droff = (int64_t*)ccg_ws(ctx, WS_HOST_D, sizeof(int64_t) * (n + 1));
+            if (!droff) return CCG_ENOMEM;
+            const int64_t* u = nullptr;
+            const int* status = nullptr;
+            rc = snn_build_cls(ctx, dknn, n, kstride, dcell, sp, st, dcls, dcls + n, droff, rlen, nbr, wpk, rcap,
+                               &cnt, &u, &status);
+            if (rc) return rc;
+            snn_cls_info_kernel<<<1, 64, 0, st>>>(u, status, cnt, n, nk, droff, rcap, dinfo);
+            CCG_HIP(hipGetLastError());
+            CCG_HIP(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st));
+            roff = droff;
+        } else {
+            rc = snn_build(ctx, dknn, n, kstride, sp, st, nbr, wpk, rcap, nullptr, rlen, &cnt, &roff);
+            if (rc) return rc;
+        }
+        CCG_HIP(hipMemcpyAsync(S->roff, roff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
+        rc = ccg_take_device_error(ctx);  // synchronises; an invalid index raised on the device fails here
+        if (rc) return rc;
+        if (classes && info[1] != 0) {  // the input breaks the class contract: the row-level pass
+            classes = false;
+            continue;
+        }
+        const int64_t need = S->roff[n];
+        if (need > rcap) {  // the rows did not fit the reservation: grow it and rerun
+            ctx->snn_row_reserve = need + need / 8;
+            continue;
+        }
+        rc = snn_host_grow(&S->nbr, &S->cap_e, (size_t)std::max<int64_t>(need, 1));
+        if (!rc) rc = snn_host_grow(&S->wpk, &S->cap_w, (size_t)std::max<int64_t>(need, 1));
+        if (rc) return rc;
+        CCG_HIP(hipMemcpyAsync(S->rlen, rlen, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipMemcpyAsync(S->cnt, cnt, sizeof(int64_t) * nk * (n + 1), hipMemcpyDeviceToHost, st));
+        if (classes) CCG_HIP(hipMemcpyAsync(S->rcls, dcls, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        if (need > 0) {
+            CCG_HIP(hipMemcpyAsync(S->nbr, nbr, sizeof(int32_t) * need, hipMemcpyDeviceToHost, st));
+            CCG_HIP(hipMemcpyAsync(S->wpk, wpk, sizeof(uint32_t) * need, hipMemcpyDeviceToHost, st));
+        }
+        CCG_HIP(hipStreamSynchronize(st));
+        S->n = n;
+        S->sp = sp;
+        S->classes = classes;
+        S->u = classes ? info[0] : n;
+        S->mstart.clear();
+        S->mrows.clear();
+        if (!classes) {
+            for (int t = 0; t < nk; ++t) S->ne[t] = S->cnt[(int64_t)t * (n + 1) + n] - S->cnt[(int64_t)t * (n + 1)];
+        } else {
+            // row-level counts: m_C m_H per class edge of graph t, m_C (m_C - 1) / 2 inside a class
+            const int64_t u = S->u;
+            S->mstart.assign(u + 1, 0);
+            for (int64_t x = 0; x < n; ++x) S->mstart[S->rcls[x] + 1]++;
+            for (int64_t c = 0; c < u; ++c) S->mstart[c + 1] += S->mstart[c];
+            S->mrows.resize(n);
+            std::vector<int64_t> cur(S->mstart.begin(), S->mstart.end() - 1);
+            for (int64_t x = 0; x < n; ++x) S->mrows[cur[S->rcls[x]]++] = (int32_t)x;  // ascending within a class
+            for (int t = 0; t < nk; ++t) {
+                int64_t tot = 0;
+                for (int64_t c = 0; c < u; ++c) {
+                    const int64_t mc = S->mstart[c + 1] - S->mstart[c];
+                    tot += mc * (mc - 1) / 2;
+                    int64_t sm = 0;
+                    for (int q = 0; q < S->rlen[c]; ++q) {
+                        const int64_t e = S->roff[c] + q;
+                        if (snn_host_has(sp, S->wpk[e], t)) sm += S->mstart[S->nbr[e] + 1] - S->mstart[S->nbr[e]];
+                    }
+                    tot += mc * sm;
+                }
+                S->ne[t] = tot;
+            }
+        }
+        S->valid = true;
+        return CCG_OK;
+    }
+    ccg_set_error("ccg_snn_graphs: row reservation could not be satisfied");
+    return CCG_ENOMEM;
+}
+
+extern "C" int ccg_snn_graphs_cells(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                                    const int* ks, int nk, int type, int64_t* nedges) {
     CCG_REQUIRE(ctx && knn && ks && nedges, "ccg_snn_graphs: NULL argument");
     CCG_REQUIRE(n >= 1 && n < (1LL << 31) - 1 && kstride >= 1, "ccg_snn_graphs: bad sizes");
     SnnSpec sp;
@@ -1684,57 +2045,15 @@ extern "C" int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int k
     if (!ctx->snn_stage) ctx->snn_stage = new SnnStage();
     SnnStage* S = (SnnStage*)ctx->snn_stage;
     S->valid = false;
-    hipStream_t st = ctx->stream;
-    const int kmax = ks[nk - 1];
-    int32_t* dknn = (int32_t*)ccg_ws(ctx, WS_HOST_A, sizeof(int32_t) * n * kstride);
-    if (!dknn) return CCG_ENOMEM;
-    CCG_HIP(hipMemcpyAsync(dknn, knn, sizeof(int32_t) * n * kstride, hipMemcpyHostToDevice, st));
-    rc = snn_host_grow(&S->roff, &S->cap_n, (size_t)n + 1);
+    rc = snn_graphs_stage(ctx, knn, n, kstride, cell, sp, S, true);
     if (rc) return rc;
-    rc = snn_host_grow(&S->rlen, &S->cap_l, (size_t)n);
-    if (rc) return rc;
-    rc = snn_host_grow(&S->cnt, &S->cap_c, (size_t)nk * (n + 1));
-    if (rc) return rc;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const int64_t rcap =
-            ctx->snn_row_reserve > 0 ? ctx->snn_row_reserve : (int64_t)SNN_ROW_RESERVE * n * (kmax + 1);
-        char* rbuf = (char*)ccg_ws(ctx, WS_SNN_ROWS,
-                                   (sizeof(int32_t) + sizeof(uint32_t)) * rcap + sizeof(int32_t) * (n + 64));
-        if (!rbuf) return CCG_ENOMEM;
-        int32_t* nbr = (int32_t*)rbuf;
-        uint32_t* wpk = (uint32_t*)(nbr + rcap);
-        int32_t* rlen = (int32_t*)(wpk + rcap);
-        int64_t* cnt = nullptr;
-        const int64_t* roff = nullptr;
-        rc = snn_build(ctx, dknn, n, kstride, sp, st, nbr, wpk, rcap, nullptr, rlen, &cnt, &roff);
-        if (rc) return rc;
-        CCG_HIP(hipMemcpyAsync(S->roff, roff, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipStreamSynchronize(st));
-        const int64_t need = S->roff[n];
-        if (need > rcap) {  // the rows did not fit the reservation: grow it and rerun
-            ctx->snn_row_reserve = need + need / 8;
-            continue;
-        }
-        rc = snn_host_grow(&S->nbr, &S->cap_e, (size_t)std::max<int64_t>(need, 1));
-        if (rc) return rc;
-        rc = snn_host_grow(&S->wpk, &S->cap_w, (size_t)std::max<int64_t>(need, 1));
-        if (rc) return rc;
-        CCG_HIP(hipMemcpyAsync(S->rlen, rlen, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-        CCG_HIP(hipMemcpyAsync(S->cnt, cnt, sizeof(int64_t) * nk * (n + 1), hipMemcpyDeviceToHost, st));
-        if (need > 0) {
-            CCG_HIP(hipMemcpyAsync(S->nbr, nbr, sizeof(int32_t) * need, hipMemcpyDeviceToHost, st));
-            CCG_HIP(hipMemcpyAsync(S->wpk, wpk, sizeof(uint32_t) * need, hipMemcpyDeviceToHost, st));
-        }
-        rc = ccg_take_device_error(ctx);  // synchronises; an invalid index raised on the device fails here
-        if (rc) return rc;
-        S->n = n;
-        S->sp = sp;
-        S->valid = true;
-        for (int t = 0; t < nk; ++t) nedges[t] = S->cnt[(int64_t)t * (n + 1) + n] - S->cnt[(int64_t)t * (n + 1)];
-        return CCG_OK;
-    }
-    ccg_set_error("ccg_snn_graphs: row reservation could not be satisfied");
-    return CCG_ENOMEM;
+    for (int t = 0; t < nk; ++t) nedges[t] = S->ne[t];
+    return CCG_OK;
+}
+
+extern "C" int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk,
+                              int type, int64_t* nedges) {
+    return ccg_snn_graphs_cells(ctx, knn, n, kstride, nullptr, ks, nk, type, nedges);
 }
 
 extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t* out_j, double* out_w,
@@ -1744,47 +2063,114 @@ extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t*
     CCG_REQUIRE(S && S->valid, "ccg_snn_graph_fetch: no graphs staged (call ccg_snn_graphs first)");
     CCG_REQUIRE(t >= 0 && t < S->sp.nk, "ccg_snn_graph_fetch: graph %d of %d", t, S->sp.nk);
     const int64_t n = S->n;
-    const int64_t* c = S->cnt + (int64_t)t * (n + 1);
-    const int64_t ne = c[n] - c[0];
+    const int64_t ne = S->ne[t];
     if (cap < ne) {
         ccg_set_error("ccg_snn_graph_fetch: capacity %lld < %lld edges", (long long)cap, (long long)ne);
         return CCG_ECAP;
     }
     const SnnSpec sp = S->sp;
-    auto work = [&](int64_t j0, int64_t j1) {
-        for (int64_t j = j0; j < j1; ++j) {
-            int64_t e = c[j] - c[0];
-            const int64_t ro = S->roff[j];
-            const int u = S->rlen[j];
-            for (int q = 0; q < u; ++q) {
-                const unsigned v = S->wpk[ro + q];
-                const unsigned b = (v >> (8 * t)) & 0xFFu;
-                if (sp.type == CCG_SNN_NUMBER ? b == 0u : b == 0xFFu) continue;
-                if (out_i) out_i[e] = (int32_t)j;
-                if (out_j) out_j[e] = S->nbr[ro + q];
-                if (out_w) out_w[e] = snn_host_weight(sp, v, t);
+    const unsigned nt = snn_host_threads(ne);
+    if (!S->classes) {
+        // union rows: graph t's entries of row j, already ascending, at the
+        // row's per-graph offset
+        const int64_t* c = S->cnt + (int64_t)t * (n + 1);
+        auto work = [&](int64_t j0, int64_t j1) {
+            for (int64_t j = j0; j < j1; ++j) {
+                int64_t e = c[j] - c[0];
+                const int64_t ro = S->roff[j];
+                const int u = S->rlen[j];
+                for (int q = 0; q < u; ++q) {
+                    const unsigned v = S->wpk[ro + q];
+                    if (!snn_host_has(sp, v, t)) continue;
+                    if (out_i) out_i[e] = (int32_t)j;
+                    if (out_j) out_j[e] = S->nbr[ro + q];
+                    if (out_w) out_w[e] = snn_host_weight(sp, v, t);
+                    ++e;
+                }
+            }
+        };
+        snn_host_parallel(n, nt, work);
+        return CCG_OK;
+    }
+    // classes: the symmetric class adjacency of graph t, then per row x of
+    // class C every row y > x of C (weight k + 1: one common set) and of each
+    // neighbouring class, sorted by y
+    const int64_t u = S->u;
+    const int64_t* ms = S->mstart.data();
+    const int32_t* mr = S->mrows.data();
+    std::vector<int64_t> aoff(u + 1, 0);
+    for (int64_t c = 0; c < u; ++c)
+        for (int q = 0; q < S->rlen[c]; ++q) {
+            const int64_t e = S->roff[c] + q;
+            if (snn_host_has(sp, S->wpk[e], t)) {
+                aoff[c + 1]++;
+                aoff[S->nbr[e] + 1]++;
+            }
+        }
+    for (int64_t c = 0; c < u; ++c) aoff[c + 1] += aoff[c];
+    std::vector<int32_t> adj(aoff[u]);
+    std::vector<uint8_t> aw(aoff[u]);
+    {
+        std::vector<int64_t> cur(aoff.begin(), aoff.end() - 1);
+        for (int64_t c = 0; c < u; ++c)
+            for (int q = 0; q < S->rlen[c]; ++q) {
+                const int64_t e = S->roff[c] + q;
+                const unsigned v = S->wpk[e];
+                if (!snn_host_has(sp, v, t)) continue;
+                const int h = S->nbr[e];
+                const uint8_t w = (uint8_t)((v >> (8 * t)) & 0xFFu);
+                adj[cur[c]] = h;
+                aw[cur[c]++] = w;
+                adj[cur[h]] = (int32_t)c;
+                aw[cur[h]++] = w;
+            }
+    }
+    const uint8_t wself = (uint8_t)(sp.kk[t] + 1);
+    // rows of class h above x: [first, end) of its ascending member list
+    auto above = [&](int64_t h, int32_t x) {
+        const int32_t* b = mr + ms[h];
+        const int32_t* e = mr + ms[h + 1];
+        return std::make_pair(std::upper_bound(b, e, x), e);
+    };
+    std::vector<int64_t> roff(n + 1, 0);
+    snn_host_parallel(n, nt, [&](int64_t x0, int64_t x1) {
+        for (int64_t x = x0; x < x1; ++x) {
+            const int64_t c = S->rcls[x];
+            auto r = above(c, (int32_t)x);
+            int64_t k = r.second - r.first;
+            for (int64_t a = aoff[c]; a < aoff[c + 1]; ++a) {
+                auto q = above(adj[a], (int32_t)x);
+                k += q.second - q.first;
+            }
+            roff[x + 1] = k;
+        }
+    });
+    for (int64_t x = 0; x < n; ++x) roff[x + 1] += roff[x];
+    if (roff[n] != ne) {
+        ccg_set_error("ccg_snn_graph_fetch: internal count mismatch (%lld vs %lld)", (long long)roff[n], (long long)ne);
+        return CCG_EINVAL;
+    }
+    snn_host_parallel(n, nt, [&](int64_t x0, int64_t x1) {
+        std::vector<std::pair<int32_t, uint8_t>> buf;
+        for (int64_t x = x0; x < x1; ++x) {
+            buf.clear();
+            const int64_t c = S->rcls[x];
+            auto r = above(c, (int32_t)x);
+            for (auto p = r.first; p < r.second; ++p) buf.emplace_back(*p, wself);
+            for (int64_t a = aoff[c]; a < aoff[c + 1]; ++a) {
+                auto q = above(adj[a], (int32_t)x);
+                for (auto p = q.first; p < q.second; ++p) buf.emplace_back(*p, aw[a]);
+            }
+            std::sort(buf.begin(), buf.end());
+            int64_t e = roff[x];
+            for (const auto& pw : buf) {
+                if (out_i) out_i[e] = (int32_t)x;
+                if (out_j) out_j[e] = pw.first;
+                if (out_w) out_w[e] = (double)pw.second;
                 ++e;
             }
         }
-    };
-    // rows split by edge count over the host's threads (each row's slots are
-    // fixed by the per-graph offsets, so the output is independent of the split)
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (ne < (1 << 16)) nt = 1;
-    if (nt == 1) {
-        work(0, n);
-        return CCG_OK;
-    }
-    std::vector<std::thread> th;
-    int64_t j0 = 0;
-    for (unsigned q = 0; q < nt; ++q) {
-        const int64_t target = c[0] + (ne * (int64_t)(q + 1)) / nt;
-        int64_t j1 = q + 1 == nt ? n : (int64_t)(std::lower_bound(c, c + n, target) - c);
-        j1 = std::max(j1, j0);
-        th.emplace_back(work, j0, j1);
-        j0 = j1;
-    }
-    for (auto& x : th) x.join();
+    });
     return CCG_OK;
 }
 

@@ -56,7 +56,7 @@ __device__ __forceinline__ unsigned long long rs_lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-template <int RS_IPT, bool STAGE>
+template <int RS_IPT>
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restrict__ kin,
                                                          const int32_t* __restrict__ vin, int64_t n, int shift,
                                                          int bits, int ntiles, const int64_t* __restrict__ off,
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
     __shared__ int goff[1 << RS_MAXBITS];
     __shared__ int dstart[1 << RS_MAXBITS];  // tile-local first position of each digit
     __shared__ int wsum[RS_WAVES];
-    __shared__ int2 stage[STAGE ? RS_THREADS * RS_IPT : 1];
+    __shared__ int2 stage[RS_THREADS * RS_IPT];
     const int nb = 1 << bits;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int t = threadIdx.x; t < RS_WAVES * nb; t += RS_THREADS) wcnt[t / nb][t % nb] = 0;
@@ -112,17 +112,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
         dstart[t] = s;
     }
     __syncthreads();
-    if (!STAGE) {  // direct writes (CCG_SORT_STAGE=0)
-#pragma unroll
-        for (int i = 0; i < RS_IPT; ++i) {
-            if (base + 64 * i + lane >= n) continue;
-            const unsigned dg = ((unsigned)kk[i] >> shift) & (unsigned)(nb - 1);
-            const int pos = goff[dg] + wcnt[w][dg] + rk[i];
-            kout[pos] = kk[i];
-            vout[pos] = vv[i];
-        }
-        return;
-    }
     {  // dstart -> exclusive prefix over the digits (two digits per thread)
         const int d0 = 2 * threadIdx.x;
         const int c0 = d0 < nb ? dstart[d0] : 0, c1 = d0 + 1 < nb ? dstart[d0 + 1] : 0;
@@ -159,15 +148,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
     }
 }
 
-// CCG_SORT_STAGE=0: the scatter writes straight from registers (A/B of the LDS staging)
-static bool rs_stage() {
-    static const bool v = [] {
-        const char* e = getenv("CCG_SORT_STAGE");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
                        int32_t* vals_out, int64_t n, int key_bits, hipStream_t st) {
     CCG_REQUIRE(n >= 0 && n < (1LL << 31), "ccg_sort_pairs_i32: n out of range");
@@ -182,7 +162,6 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
         return CCG_OK;
     }
     const int npass = (key_bits + RS_MAXBITS - 1) / RS_MAXBITS;
-    const bool stage = rs_stage();
     const size_t cnt_ints = (size_t)(1 << RS_MAXBITS) * ntiles;
     char* ws = (char*)ccg_ws(ctx, WS_SORT, sizeof(int64_t) * (cnt_ints + 1) + sizeof(int32_t) * 2 * (size_t)n + 256);
     if (!ws) return CCG_ENOMEM;
@@ -202,8 +181,7 @@ int ccg_sort_pairs_i32(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
         rs_hist<IPT_><<<ntiles, RS_THREADS, 0, st>>>(ck, n, shift, bits, ntiles, cnt);             \
         const int rc = ccg_scan_i64(ctx, cnt, cnt, (int64_t)(1 << bits) * ntiles, st);            \
         if (rc) return rc;                                                                         \
-        if (stage) rs_scatter<IPT_, true><<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov); \
-        else rs_scatter<IPT_, false><<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov); \
+        rs_scatter<IPT_><<<ntiles, RS_THREADS, 0, st>>>(ck, cv, n, shift, bits, ntiles, cnt, ok, ov);       \
     } while (0)
         if (ipt == 16) RS_PASS(16);
         else if (ipt == 8) RS_PASS(8);

@@ -203,21 +203,25 @@ class Engine:
         check(self.lib.ccg_snn_graph_fetch(self.ctx, t, _ptr(ei), _ptr(ej), _ptr(w), m))
         return ei, ej, w
 
-    def snn_multi(self, knn_idx, ks, type="number"):
+    def snn_multi(self, knn_idx, ks, type="number", cell=None):
         """The graph of every k in ks (any order, repeats allowed) from one
-        device pass per 4 distinct values (ccg_snn_graphs: the union-graph
-        rows, staged on the host; ccg_snn_graph_fetch decodes each graph).
-        Returns a list of (i, j, w) edge lists aligned with ks."""
+        device pass per 4 distinct values (ccg_snn_graphs_cells: class-level
+        rows for NUMBER graphs, union rows otherwise, staged on the host;
+        ccg_snn_graph_fetch decodes each graph).  cell: the cell of every
+        bootstrap row (copies share one; None = unknown).  Returns a list of
+        (i, j, w) edge lists aligned with ks."""
         knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
         n, kst = knn_idx.shape
         t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
+        cl = None if cell is None else np.ascontiguousarray(cell, dtype=np.int32)
         uk = sorted({int(k) for k in ks})
         got = {}
         for c0 in range(0, len(uk), 4):  # the library builds at most 4 graphs per pass
             chunk = uk[c0:c0 + 4]
             nk = len(chunk)
             ne = (ctypes.c_int64 * nk)()
-            check(self.lib.ccg_snn_graphs(self.ctx, _ptr(knn_idx), n, kst, (ctypes.c_int * nk)(*chunk), nk, t, ne))
+            check(self.lib.ccg_snn_graphs_cells(self.ctx, _ptr(knn_idx), n, kst, _ptr(cl),
+                                                (ctypes.c_int * nk)(*chunk), nk, t, ne))
             for g, k in enumerate(chunk):
                 got[k] = self._snn_fetch(g, ne[g])
         return [got[int(k)] for k in ks]
@@ -496,6 +500,19 @@ class Engine:
         karr = (ctypes.c_int * nk)(*ks)
         check(self.lib.ccg_snn_rows_dev(self.ctx, _ptr(knn_idx), n, kst, karr, nk, t, _ptr(row_off), _ptr(row_len),
                                         _ptr(nbr), _ptr(wpk), nbr.numel(), _ptr(d_nedges), _stream()))
+
+    def snn_classes_t(self, knn_idx, ks, row_class, class_root, class_off, class_len, nbr, wpk, d_info, cell=None):
+        """The NUMBER graphs of ks at the level of row classes
+        (ccg_snn_classes_dev): row_class / class_root (n,) int32, class_off
+        (n+1,) int64, class_len (n,) int32, nbr / wpk (cap,) int32 tensors,
+        d_info (3 + len(ks),) int64 = [u, status, required cap, class edges per
+        graph]; cell (n,) int32 tensor or None."""
+        n, kst = knn_idx.shape
+        nk = len(ks)
+        karr = (ctypes.c_int * nk)(*ks)
+        check(self.lib.ccg_snn_classes_dev(self.ctx, _ptr(knn_idx), n, kst, _ptr(cell), karr, nk, _ptr(row_class),
+                                           _ptr(class_root), _ptr(class_off), _ptr(class_len), _ptr(nbr), _ptr(wpk),
+                                           nbr.numel(), _ptr(d_info), _stream()))
 
     def snn_reserve(self, entries):
         check(self.lib.ccg_snn_reserve(self.ctx, entries))

@@ -299,15 +299,23 @@ int ccg_snn_multi(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                   int64_t* nedges);
 
 /* The kNum graphs for a HOST consumer (igraph::make_graph + cluster_leiden,
- * R/consensusClust.R:656-658): ONE device pass -- exactly the kernels of
- * ccg_snn_rows_dev below -- builds the union graph's rows; the rows (8 B per
- * union edge: partner + packed per-graph values) and each graph's per-row
- * edge offsets are copied to pinned host memory owned by the context, and
- * nedges[t] (host, nk entries) receives graph ks[t]'s edge count.  No edge
+ * R/consensusClust.R:656-658): ONE device pass -- for NUMBER graphs the
+ * kernels of ccg_snn_classes_dev below (class-level rows), for RANK graphs or
+ * an input that breaks the class contract those of ccg_snn_rows_dev (union
+ * rows) -- then the rows (8 B per class / union edge: partner + packed
+ * per-graph values), each graph's per-row offsets and the row -> class map
+ * are copied to pinned host memory owned by the context, and nedges[t]
+ * (host, nk entries) receives graph ks[t]'s row-level edge count.  No edge
  * list is formed on the device.  ks ascending, nk <= 4, ks <= 32.
  * Synchronises. */
 int ccg_snn_graphs(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int* ks, int nk, int type,
                    int64_t* nedges);
+/* ccg_snn_graphs for bootstrap rows whose copies are known: cell (host, n
+ * entries, may be NULL) names each row's cell (R: match(rownames(pca),
+ * unique(rownames(pca))) - 1); only rows of one cell join a row class (see
+ * ccg_snn_classes_dev).  ccg_snn_graphs is this with cell = NULL. */
+int ccg_snn_graphs_cells(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                         const int* ks, int nk, int type, int64_t* nedges);
 /* Graph t (0 <= t < nk) of the last ccg_snn_graphs call on this context,
  * decoded on the host from the staged rows (no device work): edges i < j
  * sorted by (i, j), weights as ccg_snn.  Any output may be NULL; cap < the
@@ -331,6 +339,37 @@ int ccg_snn_rows_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride,
                      const int* ks, int nk, int type, int64_t* row_off,
                      int32_t* row_len, int32_t* nbr, uint32_t* wpk, int64_t cap,
                      int64_t* d_nedges, void* stream);
+/* The NUMBER graphs of a bootstrap at the level of ROW CLASSES: the rows
+ * chained by equal N+ sets (every k of ks; the copies of a cell, whose kNN
+ * lists list each other first and then the same rows) form a class, and
+ *   w_k(x, y) = sum over classes c of min(t_x(c), t_y(c)),
+ * t_x(c) = the rows of c in N+_k(x) -- a prefix of c's rows in row order,
+ * because copies of one point sit at equal distance from every row, ordered
+ * by row index (the kNN contract).  So the graph of the classes carries every
+ * row-level weight: rows x of class C and y of class H get w(C, H), two rows of
+ * one class get k + 1.  One pass builds it; nothing row-level is written.
+ *   cell      : device, n entries or NULL: only rows of one cell share a class
+ *   row_class : device int32 n: class ordinal of every row (classes are
+ *               numbered in the order of their lowest row)
+ *   class_root: device int32 n (u used): lowest row of every class
+ *   class_off : device int64 n + 1: capacity-based row offsets over class
+ *               ordinals (entries from u on are empty); class_len: used lengths;
+ *               nbr / wpk: partners H > C in ascending order with per-graph
+ *               packed weights (byte t = w of graph ks[t], 0 = no edge),
+ *               written when class_off[n] <= cap
+ *   d_info    : device int64, 3 + nk: u, status (0: valid; 1: the input breaks
+ *               the class contract -- a class's rows out of row order in some
+ *               list -- use ccg_snn_rows_dev), required row capacity, then per
+ *               graph its class-edge count (or -(required capacity) when it
+ *               exceeds cap: rows not written).
+ * Requires ks ascending, nk <= 4, ks[0] <= 14.  No host synchronisation.
+ * ccg_snn_graphs(_cells) runs these kernels for a host consumer and expands
+ * the rows on the host. */
+int ccg_snn_classes_dev(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kstride, const int32_t* cell,
+                        const int* ks, int nk, int32_t* row_class, int32_t* class_root, int64_t* class_off,
+                        int32_t* class_len, int32_t* nbr, uint32_t* wpk, int64_t cap, int64_t* d_info,
+                        void* stream);
+
 /* Row entries the per-graph functions reserve in the context workspace
  * (0 = the default 40 n (kmax+1)); ccg_snn grows it on demand, the _dev
  * functions report -(required) in d_nedges instead. */

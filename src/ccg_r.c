@@ -322,10 +322,11 @@ SEXP ccg_r_snn(SEXP e, SEXP knn, SEXP k, SEXP type) {
     return fetch_edge_list(ctx, 0, ne);
 }
 
-/* Every graph of kNum (ccg_snn_graphs: one device pass per 4 values): knn
- * n x kst 1-based, ks the distinct k values in ascending order; returns a
- * list (one per k) of list(from, to, weight), 1-based, from < to. */
-SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type) {
+/* Every graph of kNum (ccg_snn_graphs_cells: one device pass per 4 values):
+ * knn n x kst 1-based, ks the distinct k values in ascending order, cell the
+ * 1-based cell of every bootstrap row (copies share one; NULL = unknown);
+ * returns a list (one per k) of list(from, to, weight), 1-based, from < to. */
+SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type, SEXP cell) {
     ccg_ctx* ctx;
     ccg_group* grp;
     engine_of(e, &ctx, &grp);
@@ -334,16 +335,22 @@ SEXP ccg_r_snn_multi(SEXP e, SEXP knn, SEXP ks, SEXP type) {
     int32_t* kn = knn_from_r(knn, &n, &kst);
     const int nk = Rf_length(ks);
     if (nk < 1) Rf_error("ccg_r_snn_multi: no values of k");
+    int32_t* cl = NULL;
+    if (cell != R_NilValue) {
+        if (Rf_length(cell) != n) Rf_error("ccg_r_snn_multi: cell must have one entry per row");
+        cl = (int32_t*)R_alloc((size_t)n, sizeof(int32_t));
+        for (int64_t r = 0; r < n; ++r) cl[r] = INTEGER(cell)[r] - 1;
+    }
     SEXP out = PROTECT(Rf_allocVector(VECSXP, nk));
     for (int c0 = 0; c0 < nk; c0 += 4) {  /* the library builds up to 4 graphs per pass */
         const int m = nk - c0 < 4 ? nk - c0 : 4;
         int kv[4];
         int64_t ne[4] = {0, 0, 0, 0};
         for (int t = 0; t < m; ++t) kv[t] = INTEGER(ks)[c0 + t];
-        int rc = ccg_snn_graphs(ctx, kn, n, kst, kv, m, Rf_asInteger(type), ne);
+        int rc = ccg_snn_graphs_cells(ctx, kn, n, kst, cl, kv, m, Rf_asInteger(type), ne);
         if (rc != CCG_OK) {
             UNPROTECT(1);
-            fail("ccg_snn_graphs", rc);
+            fail("ccg_snn_graphs_cells", rc);
         }
         for (int t = 0; t < m; ++t) SET_VECTOR_ELT(out, c0 + t, fetch_edge_list(ctx, t, ne[t]));
     }
@@ -621,7 +628,7 @@ static const R_CallMethodDef call_methods[] = {
     {"ccg_r_knn_segments", (DL_FUNC)&ccg_r_knn_segments, 3},
     {"ccg_r_knn_boot_segments", (DL_FUNC)&ccg_r_knn_boot_segments, 4},
     {"ccg_r_snn", (DL_FUNC)&ccg_r_snn, 4},
-    {"ccg_r_snn_multi", (DL_FUNC)&ccg_r_snn_multi, 4},
+    {"ccg_r_snn_multi", (DL_FUNC)&ccg_r_snn_multi, 5},
     {"ccg_r_silhouette", (DL_FUNC)&ccg_r_silhouette, 3},
     {"ccg_r_silhouette_cells", (DL_FUNC)&ccg_r_silhouette_cells, 4},
     {"ccg_r_cocluster_dist", (DL_FUNC)&ccg_r_cocluster_dist, 2},

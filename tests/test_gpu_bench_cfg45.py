@@ -118,6 +118,10 @@ def cfg5(engine):
     wpk = torch.empty(cap, dtype=torch.int32, device=dev)
     ne = torch.zeros(3, dtype=torch.int64, device=dev)
     engine.snn_rows_t(knn, K_NUM, "number", ro, rl, nbr, wpk, ne)
+    # the bench's pass: the row classes of all 160 segments in one call (cells: global ids)
+    sb = bench.SnnBufs(torch, n, 300 * n, dev)
+    info = torch.zeros(6, dtype=torch.int64, device=dev)
+    sb.run(engine, knn, idx, info)
     rows = torch.empty((n, inp["dpad"]), dtype=torch.float64, device=dev)
     engine.gather_rows_rm_t(inp["cells"], inp["cells"].shape[0], inp["dpad"], idx, rows)
     torch.cuda.synchronize()
@@ -125,7 +129,8 @@ def cfg5(engine):
     used = int(ro[-1].item())
     return dict(inp=inp, segs=segs, off=off, idx=idx, knn=knn.cpu().numpy(), stats=st, cut=cut,
                 ro=ro.cpu().numpy(), rl=rl.cpu().numpy(), nbr=nbr[:used].cpu().numpy(),
-                wpk=wpk[:used].cpu().numpy(), ne=ne.cpu().numpy(), rows=rows, rows_np=rows.cpu().numpy())
+                wpk=wpk[:used].cpu().numpy(), ne=ne.cpu().numpy(), rows=rows, rows_np=rows.cpu().numpy(),
+                sb=sb, info=info.cpu().numpy())
 
 
 def test_cfg5_launch_set_knn_rows_per_segment_vs_oracle(cfg5):
@@ -172,6 +177,23 @@ def test_cfg5_launch_set_snn_graphs_per_segment_vs_oracle(cfg5):
             assert np.array_equal(gi - a, ei) and np.array_equal(gj - a, ej) and np.array_equal(gw, ew), (q, k)
             tot[g] += ei.size
     assert np.array_equal(tot, c["ne"])
+
+
+def test_cfg5_launch_set_snn_classes_per_segment_vs_oracle(cfg5):
+    """The bench's cfg5 SNN pass: ONE ccg_snn_classes_dev over the disjoint
+    union (classes never span segments); every segment's three graphs,
+    expanded from its classes, equal the oracle's."""
+    c = cfg5
+    off, kn, inf = c["off"], c["knn"], c["info"]
+    n = int(off[-1])
+    assert inf[1] == 0 and inf[3:].min() > 0
+    for q in range(len(c["segs"])):
+        a, b = int(off[q]), int(off[q + 1])
+        got = c["sb"].decode(n, int(inf[0]), a, b)
+        loc = np.ascontiguousarray(kn[a:b] - a)
+        for g, k in enumerate(K_NUM):
+            ref = O.snn(loc, k, "number")
+            assert all(np.array_equal(x, y) for x, y in zip(got[g], ref)), (q, k)
 
 
 def test_cfg5_first_bootstrap_silhouettes_per_subcluster_vs_oracle(engine, cfg5):

@@ -147,6 +147,29 @@ def test_snn_rows_cfg3_all_graphs_vs_oracle(engine, cfg3):
             assert np.array_equal(a, b)
 
 
+def test_snn_classes_cfg3_all_graphs_vs_oracle(engine, cfg3):
+    """The bench's SNN pass (ccg_snn_classes_dev with the bootstrap's cells):
+    the class-level rows expand to exactly the oracle's three graphs over
+    the whole n = 90k bootstrap."""
+    import torch
+    import bench
+    c = cfg3
+    dev = c["knn"].device
+    sb = bench.SnnBufs(torch, NB, 300 * NB, dev)  # bench.py's reservation
+    info = torch.zeros(6, dtype=torch.int64, device=dev)
+    sb.run(engine, c["knn"], c["boot"], info)
+    torch.cuda.synchronize()
+    inf = info.cpu().numpy()
+    u = int(inf[0])
+    assert inf[1] == 0 and inf[3:].min() > 0
+    assert u == np.unique(c["boot_np"]).size  # one class per distinct cell (copies of a cell, <= 11 of them)
+    got = sb.decode(NB, u)
+    for g, k in enumerate(K_NUM):
+        ref = O.snn(c["knn_np"], k, "number")
+        for a, b in zip(got[g], ref):
+            assert np.array_equal(a, b)
+
+
 def test_silhouette_cells_cfg3_60_bench_labelings_vs_oracle(engine, cfg3):
     import concurrent.futures as cf
     import torch

@@ -511,3 +511,76 @@ def test_snn_copy_node_chains_of_distinct_points(engine):
     for g, k in enumerate(ks):
         for a, b in zip(got[g], O.snn(idx[0], k, "number")):
             assert np.array_equal(a, b)
+
+
+def _classes(engine, knn_np, cell, ks=(10, 15, 20), cap=None):
+    import torch
+    import bench
+    n = knn_np.shape[0]
+    knn_t = torch.from_numpy(np.ascontiguousarray(knn_np)).cuda()
+    sb = bench.SnnBufs(torch, n, cap if cap is not None else 300 * n, "cuda")
+    info = torch.zeros(3 + len(ks), dtype=torch.int64, device="cuda")
+    cl = None if cell is None else torch.from_numpy(np.ascontiguousarray(cell, dtype=np.int32)).cuda()
+    engine.snn_classes_t(knn_t, ks, sb.row_class, sb.class_root, sb.off, sb.ln, sb.nbr, sb.wpk, info, cell=cl)
+    torch.cuda.synchronize()
+    return sb, info.cpu().numpy()
+
+
+@pytest.mark.parametrize("with_cell", [True, False])
+def test_snn_classes_bootstrap_copies_vs_oracle(engine, with_cell):
+    """ccg_snn_classes_dev on a bootstrap with copies in twos and threes, a
+    cell drawn 14 times (more than kmin + 1: its rows are singletons) and 9
+    distinct cells at one point: the class rows expand to the oracle's
+    graphs, with and without the cell ids; the roots are each class's lowest
+    row; too small a capacity reports -(required) and writes nothing."""
+    rng = np.random.default_rng(35)
+    N = 5000
+    X = _mixture(rng, N, 10)
+    X[100:108] = X[7]
+    boot = rng.integers(0, N, 4500).astype(np.int32)
+    boot[rng.choice(4500, 14, replace=False)] = 3
+    boot[rng.choice(4500, 5, replace=False)] = 104
+    idx, _ = engine.knn_boot(X, boot, kmax=20)
+    sb, inf = _classes(engine, idx[0], boot if with_cell else None)
+    n = idx.shape[1]
+    u = int(inf[0])
+    assert inf[1] == 0 and u < n
+    rc = sb.row_class.cpu().numpy()
+    roots = sb.class_root[:u].cpu().numpy()
+    assert np.array_equal(roots, np.array([np.flatnonzero(rc == c)[0] for c in range(u)]))
+    if with_cell:  # a class never mixes cells
+        assert all(np.unique(boot[rc == c]).size == 1 for c in range(u))
+    got = sb.decode(n, u)
+    for g, k in enumerate((10, 15, 20)):
+        ref = O.snn(idx[0], k, "number")
+        assert int(inf[3 + g]) > 0
+        for a, b in zip(got[g], ref):
+            assert np.array_equal(a, b)
+    _, inf2 = _classes(engine, idx[0], boot if with_cell else None, cap=100)
+    assert inf2[3:].max() < 0 and -inf2[3] == inf2[2] == inf[2]
+
+
+def test_snn_classes_contract_check_and_host_fallback(engine):
+    """Distinct points with identical N+ sets (a tight ball of 11 cells far
+    from the rest) may share a class only if every list holds them in row
+    order; the check reports a violation in d_info[1], and the host flavour
+    then takes the row-level pass -- both flavours stay exact."""
+    rng = np.random.default_rng(43)
+    N, d = 3000, 8
+    X = _mixture(rng, N, d)
+    X[200:211] = X[50] + 1e-7 * rng.normal(size=(11, d)) + 500.0
+    boot = np.concatenate([np.arange(N), rng.integers(0, N, 600)]).astype(np.int32)
+    idx, _ = engine.knn_boot(X, boot, kmax=20)
+    n = idx.shape[1]
+    for cell in (None, boot):
+        sb, inf = _classes(engine, idx[0], cell)
+        if cell is not None:
+            assert inf[1] == 0  # the cells keep the ball's points in classes of their own
+        if inf[1] == 0:
+            got = sb.decode(n, int(inf[0]))
+            for g, k in enumerate((10, 15, 20)):
+                for a, b in zip(got[g], O.snn(idx[0], k, "number")):
+                    assert np.array_equal(a, b)
+        for k, got in zip((10, 15, 20), engine.snn_multi(idx[0], [10, 15, 20], "number", cell=cell)):
+            for a, b in zip(got, O.snn(idx[0], k, "number")):
+                assert np.array_equal(a, b)

@@ -109,11 +109,12 @@ def test_r_getclustassignments_runs_the_bench_kernels():
     code = open(RCODE).read()
     gca = code[code.index("getClustAssignments <- function("):code.index("#' kNN(jaccardDist, k)$id")]
     assert "C_ccg_r_snn_multi" in gca and "C_ccg_r_snn," not in gca
-    assert "cell = match(rownames(pca), unique(rownames(pca)))" in gca
+    assert "cell <- match(rownames(pca), unique(rownames(pca)))" in gca and "cell = cell" in gca
+    assert "C_ccg_r_snn_multi, eng, knn, ks, 0L, cell)" in gca
     sil = code[code.index("ccgSilhouetteMeans <- function("):code.index("#' Drop-in for getClustAssignments")]
     assert "C_ccg_r_silhouette_cells" in sil
     glue = _glue()
-    assert re.search(r"ccg_silhouette_cells\(ctx,", glue) and re.search(r"ccg_snn_graphs\(ctx,", glue)
+    assert re.search(r"ccg_silhouette_cells\(ctx,", glue) and re.search(r"ccg_snn_graphs_cells\(ctx,", glue)
     assert "ccg_snn_graph_fetch(ctx, t," in glue and "ccg_snn_multi(" not in glue
     # any number of k values: the glue chunks them 4 per device pass
     multi = glue[glue.index("SEXP ccg_r_snn_multi("):]

@@ -43,14 +43,21 @@ def main():
     snn = (torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),
            torch.empty(rcap, dtype=torch.int32, device=dev), torch.empty(rcap, dtype=torch.int32, device=dev))
     ned = torch.zeros(3, dtype=torch.int64, device=dev)
+    sb = bench.SnnBufs(torch, n, 300 * n, dev)  # the class-level pass (bench.py's)
+    info = torch.zeros(6, dtype=torch.int64, device=dev)
     mean = torch.empty(60, dtype=torch.float64, device=dev)
     ncl = torch.empty(60, dtype=torch.int32, device=dev)
     mns = torch.empty(60, dtype=torch.int32, device=dev)
 
+    mode = os.environ.get("BM_SNN", "classes")
+
     def one(b):
         eng.gather_rows_rm_t(pcs, N, d, boots[b], rows)
         eng.knn_boot_table_t(pcs_cm, N, d, boots[b], uniq[b], rows, 20, tab_idx, tab_d2, knn)
-        eng.snn_rows_t(knn, bench.K_NUM, "number", *snn, ned)
+        if mode == "rows":
+            eng.snn_rows_t(knn, bench.K_NUM, "number", *snn, ned)
+        else:
+            sb.run(eng, knn, boots[b], info)
         eng.silhouette_cells_t(rows, labels[b], cmax, boots[b], N, mean, ncl, mns)
 
     eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
@@ -73,7 +80,8 @@ def main():
         out[w + "_ms_per_boot"] = ms / max(cnt, 1)
     eng.timing(False)
     out["means0"] = float(mean[0].item())
-    out["edges"] = [int(e) for e in ned.tolist()]
+    out["snn_mode"] = mode
+    out["edges"] = [int(e) for e in ned.tolist()] if mode == "rows" else [int(e) for e in info.tolist()]
     print(json.dumps(out))
 
 
