@@ -26,7 +26,8 @@ Workloads (--workload; the default cfg3 line is the metric line):
   cfg5    : iterate=TRUE on 100k cells: every subcluster (5k-20k cells, d_c
             5-15 PCs) of one level through the batched segment kNN
             (ccg_knn_boot_segments_dev), one SNN pass over the disjoint union,
-            per-segment silhouettes, map-back and per-subcluster co-clusters.
+            one segmented silhouette launch set (ccg_silhouette_segments_dev),
+            map-back and per-subcluster co-clusters.
 
 Usage: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1
 and no WORLD_SIZE in the environment, this process (which never touches the
@@ -89,6 +90,10 @@ def parse():
                          "screen: a screen per bootstrap (warm-started)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues for this process (0: the runtime's default)")
+    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
+                    help="graph: the step's bootstrap phase (table, every bootstrap's gather, kNN, SNN, silhouette "
+                         "on the S streams) is captured once after the warmup as one HIP graph and replayed per step; "
+                         "eager: launched from the host every step")
     ap.add_argument("--table-k", type=int, default=48,
                     help="cell-table length K (<= 48): cells with fewer than 20 of their K nearest cells in a "
                          "bootstrap take the exact search")
@@ -403,6 +408,15 @@ def cfg5_seg_plan(torch, inp, b0, b1):
     return segs, off, su, idx
 
 
+def cfg5_sil_keys(torch, inp, plan, b0):
+    """Cell keys of a batch's rows for ccg_silhouette_segments_dev: distinct
+    between segments -- global cell id + (bootstrap slot) x N (segments of one
+    subcluster's bootstraps share global ids); ncell = slots x N."""
+    segs, off, _, idx = plan
+    slot = torch.from_numpy(np.repeat(np.array([j - b0 for _, j in segs], np.int32), np.diff(off))).to(idx.device)
+    return (idx + slot * int(inp["cells"].shape[0])).to(torch.int32)
+
+
 def decode_union_rows(off, ln, nbr, wpk, nk, r0=0, r1=None):
     """Union-graph rows (ccg_snn_rows_dev) of rows [r0, r1) -> per-graph
     (i, j, w) NUMBER edge lists in (i, j) order (numpy, vectorised)."""
@@ -507,11 +521,11 @@ class SnnBufs:
                                  self.nbr[:used].cpu().numpy(), self.wpk[:used].cpu().numpy(), K_NUM, c0=c0)
 
 
-def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
+def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512, b0=0):
     """cfg5's cpu_baseline check leg: the oracle as the checker of the first
     segmented launch set.  The batch runs again through the step's calls
-    (ccg_knn_boot_segments_dev with global ids, ONE ccg_snn_rows_dev over
-    the disjoint union, the per-segment cell silhouettes); for three
+    (ccg_knn_boot_segments_dev with global ids, ONE row-class SNN pass over
+    the disjoint union, ONE ccg_silhouette_segments_dev); for three
     segments (the smallest and the largest subcluster's first bootstrap and
     the batch's last segment) sampled kNN rows plus every exact-search row
     must equal orc_knn_queries on the segment's rows (segment-local ids), the
@@ -534,15 +548,10 @@ def cfg5_check(eng, torch, inp, labels, cmax, plan, sample=512):
     nsub = inp["nsub"]
     pick = sorted({0, max(range(nsub), key=lambda c: inp["sizes"][c]), len(segs) - 1})
     L = labels[0].shape[1]
-    sil = {}
-    for q in pick:
-        c, j = segs[q]
-        a, b = int(off[q]), int(off[q + 1])
-        m_ = torch.empty(L, dtype=torch.float64, device=dev)
-        nc_ = torch.empty(L, dtype=torch.int32, device=dev)
-        ms_ = torch.empty(L, dtype=torch.int32, device=dev)
-        eng.silhouette_cells_t(rows[a:b], labels[c][j], cmax, inp["boots_t"][c][j], inp["sizes"][c], m_, nc_, ms_)
-        sil[q] = m_
+    sil = [torch.empty(L, dtype=torch.float64, device=dev) for _ in segs]
+    slots = 1 + max(j for _, j in segs) - b0
+    eng.silhouette_segments_t(rows, off, [labels[c][j] for c, j in segs], cmax, cfg5_sil_keys(torch, inp, plan, b0),
+                              slots * inp["cells"].shape[0], sil)
     torch.cuda.synchronize()
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     kn = knn.cpu().numpy()
@@ -591,8 +600,9 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
     bootstraps of EVERY subcluster per launch set: the segmented distinct-cell
     kNN (ccg_knn_boot_segments_dev, one segment per (subcluster, bootstrap),
     neighbour ids of the concatenation), ONE SNN rows pass over the disjoint
-    union of all the batch's graphs, then per segment the silhouettes of its
-    60 clusterings; per subcluster the selection + map-back and its co-cluster
+    union of all the batch's graphs, ONE ccg_silhouette_segments_dev for the
+    60 clusterings of every segment; per subcluster the selection + map-back
+    and its co-cluster
     triangle.  The subclusters' PC matrices are slices of synthetic PCs (the
     per-subset PCA, f4, is timed on its own)."""
     eng = engs[0]
@@ -615,6 +625,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         return cfg5_seg_plan(torch, inp, b0, b1)
 
     plans = [seg_plan(b0, b1) for b0, b1 in batches]
+    skeys = [cfg5_sil_keys(torch, inp, p, b0) for p, (b0, _) in zip(plans, batches)]
     nmax = max(int(p[1][-1]) for p in plans)
     rows_s = [torch.empty((nmax, dpad), dtype=torch.float64, device=dev) for _ in range(S)]
     knn_s = [torch.empty((nmax, 20), dtype=torch.int32, device=dev) for _ in range(S)]
@@ -638,10 +649,10 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         e.knn_boot_segments_t(cells, idx, off, su, 20, knn, local_ids=False)
         snn_s[si].run(e, knn, idx, snn_info[t], n=n)  # the classes of every segment in one pass
         e.gather_rows_rm_t(cells, N, dpad, idx, rows)
-        for q, (c, j) in enumerate(segs):
-            a, b = int(off[q]), int(off[q + 1])
-            e.silhouette_cells_t(rows[a:b], labels[c][j], cmax, boots_t[c][j], sizes[c], means[c][j], nclust[c][j],
-                                 minsize[c][j])
+        # every segment's 60 silhouettes in one launch set
+        e.silhouette_segments_t(rows, off, [labels[c][j] for c, j in segs], cmax, skeys[t], SB * N,
+                                [means[c][j] for c, j in segs], [nclust[c][j] for c, j in segs],
+                                [minsize[c][j] for c, j in segs])
 
     def step():
         cur = torch.cuda.current_stream()
@@ -968,9 +979,7 @@ def main():
 
     host_t = [0.0]  # host time spent enqueueing the bootstrap loop (the launches are asynchronous)
 
-    def step(evs=None):
-        mark(evs, "start")
-        th = time.perf_counter()
+    def boot_phase():
         # S bootstraps in flight: bootstrap j runs on stream j % S with its own
         # engine context (workspaces), so one bootstrap's latency-bound SNN
         # build overlaps another's MFMA-bound kNN screen
@@ -988,9 +997,19 @@ def main():
                 snn_out[si].run(e, knn_s[si], boots[j], snn_info[j])
                 if robust:  # granular mode scores no clustering (:688)
                     e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
-        host_t[0] += time.perf_counter() - th
         for st_ in streams:
             cur.wait_stream(st_)
+
+    graph = [None]  # the captured bootstrap phase (--launch graph)
+
+    def step(evs=None):
+        mark(evs, "start")
+        th = time.perf_counter()
+        if graph[0] is not None:
+            graph[0].replay()  # every kernel of the phase runs again; only the host launch work is gone
+        else:
+            boot_phase()
+        host_t[0] += time.perf_counter() - th
         step_tail(evs)
 
     def barrier():
@@ -1012,6 +1031,31 @@ def main():
     if int(snn_info[:, 1].max().item()) != 0:  # (cannot happen for bootstrap copies under the kNN contract)
         raise RuntimeError("ccg_snn_classes_dev: the class contract failed; the row-level pass would be needed")
     need = snn_info[:, 3:].max(0).values.tolist()
+    # --launch graph: capture the bootstrap phase once (the warmup sized every
+    # workspace, so the capture allocates nothing); the replay is checked
+    # against an eager step's outputs before timing
+    launch_note = "eager"
+    if args.launch == "graph" and not W.get("no_graph"):
+        try:
+            torch.cuda.synchronize()
+            ref_means = means.clone()
+            g = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(device=dev)
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.graph(g, stream=cs):
+                boot_phase()
+            torch.cuda.synchronize()
+            means.fill_(-9.0)
+            g.replay()
+            torch.cuda.synchronize()
+            if robust and not torch.equal(means, ref_means):
+                raise RuntimeError("graph replay differs from the eager step")
+            graph[0] = g
+            launch_note = "hipgraph"
+        except Exception as ex:  # (capture unsupported here: stay eager and say why)
+            graph[0] = None
+            launch_note = f"eager (graph capture failed: {type(ex).__name__}: {str(ex)[:160]})"
+            torch.cuda.synchronize()
     if emul:  # the other ranks' column blocks: this rank's columns with the cells rotated (same label counts)
         for k in range(1, emul):
             A_full[k * cpr:(k + 1) * cpr] = torch.roll(A_local, shifts=k * 7919, dims=1)
@@ -1292,6 +1336,7 @@ def main():
                          "phases come from torch-stream events in the extra timer step: the bootstrap loop, "
                          "selection + map-back, the RCCL all-gather of the assignment columns, this rank's "
                          "co/both row slab",
+        "launch": launch_note,
         "host_enqueue_ms_per_step": round(host_ms, 3),
         "host_launch_ms_per_boot_idle_gpu": round(host_idle_ms, 3),
         "cocluster_avg_ms": round(coc_ms, 3),

@@ -84,6 +84,7 @@ SIGNATURES = {
     "ccg_silhouette": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p]),
     "ccg_silhouette_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p, _p]),
     "ccg_silhouette_cells_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _i64, _p, _p, _p, _p]),
+    "ccg_silhouette_segments_dev": (_i, [_p, _p, _i, _i, _p, _p, _i, _i, _p, _i64, _p, _p, _p, _p]),
     "ccg_select_mapback_dev": (_i, [_p, _i, _p, _p, _i64, _i, _i, _i64, _p, _p, _p, _i, _p, _i, _i64, _p, _p]),
     "ccg_cocluster": (_i, [_p, _p, _i, _i64, _i64, _p, _p, _p]),
     "ccg_cocluster_dev": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),

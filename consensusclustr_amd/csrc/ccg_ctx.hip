@@ -77,10 +77,34 @@ extern "C" int ccg_close(ccg_ctx* ctx) {
         (void)hipEventDestroy(ctx->timers[t].stop);
     }
     free(ctx->timers);
+    for (int s = 0; s < CCG_PIN_RING; ++s) {
+        if (ctx->pin_buf[s]) (void)hipHostFree(ctx->pin_buf[s]);
+        if (ctx->pin_ev[s]) (void)hipEventDestroy(ctx->pin_ev[s]);
+    }
     ccg_snn_stage_free(ctx);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+    return CCG_OK;
+}
+
+int ccg_h2d_staged(ccg_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return CCG_OK;
+    const int s = ctx->pin_next;
+    ctx->pin_next = (s + 1) % CCG_PIN_RING;
+    if (!ctx->pin_ev[s]) CCG_HIP(hipEventCreateWithFlags(&ctx->pin_ev[s], hipEventDisableTiming));
+    else CCG_HIP(hipEventSynchronize(ctx->pin_ev[s]));  // the slot's previous copy has run
+    if (ctx->pin_bytes[s] < bytes) {
+        if (ctx->pin_buf[s]) CCG_HIP(hipHostFree(ctx->pin_buf[s]));
+        ctx->pin_buf[s] = nullptr;
+        ctx->pin_bytes[s] = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        CCG_HIP(hipHostMalloc(&ctx->pin_buf[s], want, hipHostMallocDefault));
+        ctx->pin_bytes[s] = want;
+    }
+    memcpy(ctx->pin_buf[s], src, bytes);
+    CCG_HIP(hipMemcpyAsync(dst, ctx->pin_buf[s], bytes, hipMemcpyHostToDevice, st));
+    CCG_HIP(hipEventRecord(ctx->pin_ev[s], st));
     return CCG_OK;
 }
 

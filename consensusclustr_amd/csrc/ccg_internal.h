@@ -60,6 +60,9 @@ enum ccg_ws_slot {
     WS_SEG_ROWS,     // batched bootstrap segments: the gathered rows of every segment
     WS_SEG_TAB,      // batched bootstrap segments: row and distinct-cell segment offsets
     WS_KB_C,         // distinct-cell kNN: per-cell counts / offsets / cursors / cell -> distinct id (counting grouping)
+    WS_SIL_IMG,      // silhouette: per-labeling LDS images of the fp16-screen width kernel
+    WS_SIL_SEG,      // silhouette segments: offsets, tile starts, label and output pointers
+    WS_FX_Q,         // kNN exact search of failed rows (fp16 path): their row images, tests and ids
     WS_NSLOTS
 };
 
@@ -76,6 +79,8 @@ struct ccg_timer_rec {
 #define CCG_DERR_CLUSTER_INDEX 4  // block sums / contingency: cluster position outside [0, K)
 #define CCG_DERR_KNN_UNIQUE 8     // ccg_knn_boot_dev: n_unique differs from the distinct cells of idx
 
+#define CCG_PIN_RING 8
+
 struct ccg_ctx {
     int device;
     hipStream_t stream;
@@ -91,6 +96,13 @@ struct ccg_ctx {
     // kNN: the exact-search row list of the last call and its count (device; ccg_knn_last_fallback)
     const int* last_fail_list;
     const int* last_fail_count;
+    // pinned staging ring for host tables copied inside asynchronous entry
+    // points (ccg_h2d_staged): the caller's host memory may be gone before
+    // the copy runs
+    void* pin_buf[CCG_PIN_RING];
+    size_t pin_bytes[CCG_PIN_RING];
+    hipEvent_t pin_ev[CCG_PIN_RING];
+    int pin_next;
     // kernel timing (ccg_timing_*)
     int timing;
     ccg_timer_rec* timers;   // pool, grows
@@ -101,6 +113,12 @@ struct ccg_ctx {
 // timing is disabled).  Returns a handle for ccg_timer_stop or -1.
 int ccg_timer_start(ccg_ctx* ctx, int which, hipStream_t st);
 void ccg_timer_stop(ccg_ctx* ctx, int handle, hipStream_t st);
+
+// Copy bytes of host memory to device dst on stream st through a pinned
+// staging slot of the context (the source may be freed when this returns;
+// a pageable source would be read by the DMA after that).  Waits only when
+// the slot's previous copy, CCG_PIN_RING uses ago, has not run yet.
+int ccg_h2d_staged(ccg_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t st);
 
 void ccg_set_error(const char* fmt, ...);
 int ccg_hip_fail(hipError_t e, const char* what, const char* file, int line);

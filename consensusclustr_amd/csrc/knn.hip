@@ -1075,10 +1075,12 @@ static int knn_seg_plan(ccg_ctx* ctx, const int64_t* seg_off, int nseg, int d, i
     int64_t* d_po = (int64_t*)(tab + offb);
     int4* d_blk = (int4*)(tab + 2 * offb);
     int* d_perm = (int*)(d_blk + nblk);
-    CCG_HIP(hipMemcpyAsync(d_off, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(d_po, po.data(), sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(d_blk, hblk.data(), sizeof(int4) * nblk, hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(d_perm, hperm.data(), sizeof(int) * npos, hipMemcpyHostToDevice, st));
+    // (host tables through the context's pinned ring: they are freed when the call returns)
+    int rc = ccg_h2d_staged(ctx, d_off, seg_off, sizeof(int64_t) * (nseg + 1), st);
+    if (!rc) rc = ccg_h2d_staged(ctx, d_po, po.data(), sizeof(int64_t) * (nseg + 1), st);
+    if (!rc) rc = ccg_h2d_staged(ctx, d_blk, hblk.data(), sizeof(int4) * nblk, st);
+    if (!rc) rc = ccg_h2d_staged(ctx, d_perm, hperm.data(), sizeof(int) * npos, st);
+    if (rc) return rc;
     *out = KnnSegs{nseg, d_off, npos, d_perm, d_blk, d_po};
     return CCG_OK;
 }
@@ -1241,6 +1243,153 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
     }
 }
 
+// The same candidate lists on the fp16 matrix core (round 5; the table
+// path, where max|x| of the rows is known).  Rows scaled by 2^e (max|x|
+// 2^e < 2^12) and split into fp16 hi + lo (knn_split16); x.y ~ hi.hi +
+// hi.lo + lo.hi on v_mfma_f32_32x32x16_f16 with A = 32 failed rows (LDS)
+// and B = 32 references (registers), so a lane (h, j) gets 16 failed rows
+// against reference j.  The error of the product is below
+//   E = 2^-17.2 |x'||y'| + 2^-13.9 sqrt(d) (|x'| + |y'|)
+// at KSTEPS <= 2 (split residuals 2^-22 relative + 2^-14 absolute per
+// factor, fp32 accumulation of 48 KSTEPS exact products; 2^-16.3 |x'||y'| at
+// KSTEPS = 4), and |x'||y'| <= (nx' + ny') / 2; the test takes the kNN
+// screen's certification budget (1024 fp32 ulps of (|x'| + |y'|)^2 <=
+// 2^-13 (nx' + ny')) with a factor 2 to spare, so a pair within the radius
+// (nx' + ny' - 2 x'.y' <= tau') passes
+//   2 x'.y'(mfma) >= A_x + B_y,
+//   A_x = (1 - 2^-12) nx' - (1 + 2^-20) tau' - 2^-11 sqrt(d) |x'| - 8,
+//   B_y = (1 - 2^-12) ny' - 2^-11 sqrt(d) |y'|
+// (both rounded down to fp32; the slack past 2E covers the fp32 sum and
+// the fp64 exact test's own rounding): the
+// candidates are a superset of the exact ones, and knn_fx_select_kernel
+// keeps exactly the pairs whose fp64 d2 is within the radius.  Per pair:
+// 3 MACs of 16 x KSTEPS dims on the matrix core and one fp32 compare,
+// against the fp32 scan's 16 KSTEPS packed FMAs on the vector unit.
+#define KNN_FXQ 128  // failed rows per staged group
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __restrict__ rows, int d,
+                                                            const int* __restrict__ fail_list,
+                                                            const int* __restrict__ fail_count,
+                                                            const double* __restrict__ fail_tau,
+                                                            const unsigned* __restrict__ maxabs_bits,
+                                                            uint4* __restrict__ qimg, float* __restrict__ qa,
+                                                            int* __restrict__ qid) {
+    constexpr int NCH = 4 * KSTEPS;  // 16-byte chunks (s, hi/lo, h) per row image, swizzled by row & (NCH - 1)
+    const int nf = min(*fail_count, KNN_FX_ROWS);
+    const int nfp = (nf + KNN_FXQ - 1) / KNN_FXQ * KNN_FXQ;
+    const int e = knn_scale_exp(maxabs_bits);
+    const double sqd = sqrt((double)d);
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfp; f += gridDim.x * blockDim.x) {
+        const bool valid = f < nf;
+        const int q = valid ? fail_list[f] : -1;
+        double t = valid ? fail_tau[f] : -1.0;
+        if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
+        _Float16 hv[NCH * 8];
+        double nx = 0.0;
+#pragma unroll
+        for (int k = 0; k < KSTEPS * 16; ++k) {
+            const double xs = (valid && k < d) ? ldexp(rows[(int64_t)q * d + k], e) : 0.0;
+            nx = fma(xs, xs, nx);
+            _Float16 hi, lo;
+            knn_split16(xs, hi, lo);
+            const int s = k >> 4, h = (k >> 3) & 1, i = k & 7;
+            hv[(s * 4 + h) * 8 + i] = hi;
+            hv[(s * 4 + 2 + h) * 8 + i] = lo;
+        }
+        const int c = f % KNN_FXQ;  // the row's place in its staged group (the swizzle's row)
+        uint4* out = qimg + (int64_t)f * NCH;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) out[ch ^ (c & (NCH - 1))] = *reinterpret_cast<const uint4*>(&hv[ch * 8]);
+        const double ts = ldexp(t, 2 * e);
+        qa[f] = (t < 0.0) ? INFINITY
+                          : __double2float_rd((1.0 - 0x1p-12) * nx - (1.0 + 0x1p-20) * ts - 0x1p-11 * sqd * sqrt(nx) - 8.0);
+        qid[f] = q;
+    }
+}
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __restrict__ rows, int n, int d,
+                                                            const int* __restrict__ fail_count,
+                                                            const unsigned* __restrict__ maxabs_bits,
+                                                            const uint4* __restrict__ qimg,
+                                                            const float* __restrict__ qa, const int* __restrict__ qid,
+                                                            int* __restrict__ cnt, int* __restrict__ bi,
+                                                            int* __restrict__ ovf_count) {
+    constexpr int NCH = 4 * KSTEPS;
+    __shared__ uint4 sq[KNN_FXQ * NCH];
+    __shared__ __attribute__((aligned(16))) float sa[KNN_FXQ];
+    __shared__ int sid[KNN_FXQ];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
+    const int nf = min(*fail_count, KNN_FX_ROWS);
+    if (nf == 0) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    // the wave's 32 references: B fragments (dims 16 s + 8 h ..) and the reference's part of the test
+    const int jr = blockIdx.x * 128 + wave * 32 + j;
+    const bool inr = jr < n;
+    const int e = knn_scale_exp(maxabs_bits);
+    h8 bh[KSTEPS], bl[KSTEPS];
+    double ny = 0.0;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = 16 * s + 8 * h + i;
+            const double ys = (inr && k < d) ? ldexp(rows[(int64_t)jr * d + k], e) : 0.0;
+            ny = fma(ys, ys, ny);
+            _Float16 hi, lo;
+            knn_split16(ys, hi, lo);
+            bh[s][i] = hi;
+            bl[s][i] = lo;
+        }
+    ny += __shfl_xor(ny, 32, 64);
+    const float bj = inr ? __double2float_rd((1.0 - 0x1p-12) * ny - 0x1p-11 * sqrt((double)d) * sqrt(ny)) : INFINITY;
+    for (int g0 = 0; g0 < nf; g0 += KNN_FXQ) {
+        const int nq = min(KNN_FXQ, nf - g0);
+        __syncthreads();  // the previous group's reads of the stage are done
+        for (int t = threadIdx.x; t < KNN_FXQ * NCH; t += 256) sq[t] = qimg[(int64_t)g0 * NCH + t];
+        if (threadIdx.x < KNN_FXQ) {
+            sa[threadIdx.x] = qa[g0 + threadIdx.x];  // (the prep writes whole groups: INFINITY past nf)
+            sid[threadIdx.x] = qid[g0 + threadIdx.x];
+        }
+        __syncthreads();
+        for (int t = 0; t < (nq + 31) >> 5; ++t) {  // block-uniform
+            typedef float f16x __attribute__((ext_vector_type(16)));
+            f16x acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            const int c = t * 32 + j;
+            const uint4* ar = sq + c * NCH;
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                const uint4 ahv = ar[(s * 4 + h) ^ (c & (NCH - 1))];
+                const uint4 alv = ar[(s * 4 + 2 + h) ^ (c & (NCH - 1))];
+                const h8 ah = *reinterpret_cast<const h8*>(&ahv);
+                const h8 al = *reinterpret_cast<const h8*>(&alv);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+            }
+            // register r holds failed row t*32 + (r & 3) + 8 (r >> 2) + 4h against reference jr
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 a4 = *reinterpret_cast<const float4*>(&sa[t * 32 + 8 * g + 4 * h]);
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (2.0f * acc[4 * g + q] >= av[q] + bj) {  // rare: the candidates
+                        const int i = t * 32 + 8 * g + 4 * h + q;
+                        if (jr != sid[i]) {
+                            const int slot = atomicAdd(&cnt[g0 + i], 1);
+                            if (slot < KNN_FX_CAP) bi[(int64_t)(g0 + i) * KNN_FX_CAP + slot] = jr;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 #ifndef WAVE_LDS_SYNC
 // a wave's LDS writes are visible to its other lanes' later LDS reads (the
 // LDS pipeline is in order per wave); the clobber stops compiler reordering
@@ -1379,12 +1528,15 @@ static int* knn_fail_ws(ccg_ctx* ctx, int64_t n, double** tau) {
 // Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
 static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
                                const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
-                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr) {
+                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr,
+                               const unsigned* maxabs = nullptr) {
     if (!seg_off && fail_tau) {
         // the radius search; its leftovers (overflow) continue below
         int* cnt = (int*)ccg_ws(ctx, WS_FX_A, sizeof(int) * (KNN_FX_ROWS + 64 + n));
         int* bi = (int*)ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-        if (!cnt || !bi) return CCG_ENOMEM;
+        // the fp16 path's failed-row images, tests and ids (max|x| known: the table path)
+        char* qw = maxabs ? (char*)ccg_ws(ctx, WS_FX_Q, (size_t)KNN_FX_ROWS * (64 * 4 + 8) + 64) : nullptr;
+        if (!cnt || !bi || (maxabs && !qw)) return CCG_ENOMEM;
         if (ctx->fx_zeroed != (void*)cnt) {  // fresh buffer: the select kernel keeps the counters zero afterwards
             CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * KNN_FX_ROWS, st));
             ctx->fx_zeroed = (void*)cnt;
@@ -1393,8 +1545,20 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         int* ovf_list = ovf_count + 64;
 #define CCG_FX(DM_)                                                                                              \
     do {                                                                                                         \
-        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, \
-                                                             bi, ovf_count);                                      \
+        if (maxabs) {                                                                                            \
+            constexpr int KS_ = DM_ / 16;                                                                        \
+            uint4* qimg = (uint4*)qw;                                                                            \
+            float* qa = (float*)(qimg + (size_t)KNN_FX_ROWS * 4 * KS_);                                          \
+            int* qid = (int*)(qa + KNN_FX_ROWS);                                                                 \
+            knn_fx_prep16_kernel<KS_><<<64, 256, 0, st>>>(rows, d, fail_list, fail_count, fail_tau, maxabs, qimg, \
+                                                          qa, qid);                                              \
+            knn_fx_scan16_kernel<KS_><<<(unsigned)ccg_cdiv(n, 128), 256, 0, st>>>(rows, (int)n, d, fail_count,    \
+                                                                                 maxabs, qimg, qa, qid, cnt, bi,  \
+                                                                                 ovf_count);                      \
+        } else {                                                                                                 \
+            knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, \
+                                                                 cnt, bi, ovf_count);                             \
+        }                                                                                                        \
         knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, fail_list, fail_count, fail_tau, cnt, bi,     \
                                                        out_idx, out_dist, dist_sq, ovf_list, ovf_count);          \
     } while (0)
@@ -1787,17 +1951,29 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
 // the distinct cells' rows, copied from the gathered (row-major) bootstrap
 // rows of each cell's first copy: coalesced, unlike a gather from the
 // column-major PCs
-__global__ void kb_urows_kernel(const double* __restrict__ rows, int d, int u, const int* __restrict__ ustart,
-                                const int* __restrict__ srow, double* __restrict__ urows,
-                                const int32_t* __restrict__ idx, const float* __restrict__ cell_hint,
-                                float* __restrict__ urow_hint) {
+__global__ __launch_bounds__(256) void kb_urows_kernel(const double* __restrict__ rows, int d, int u,
+                                                       const int* __restrict__ ustart, const int* __restrict__ srow,
+                                                       double* __restrict__ urows, const int32_t* __restrict__ idx,
+                                                       const float* __restrict__ cell_hint,
+                                                       float* __restrict__ urow_hint, unsigned* __restrict__ maxabs) {
+    __shared__ unsigned red[4];
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)u * d) return;
-    const int64_t uid = t / d;
-    const int k = (int)(t - uid * d);
-    const int r0 = srow[ustart[uid]];
-    urows[t] = rows[(int64_t)r0 * d + k];
-    if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
+    unsigned mb = 0u;
+    if (t < (int64_t)u * d) {
+        const int64_t uid = t / d;
+        const int k = (int)(t - uid * d);
+        const int r0 = srow[ustart[uid]];
+        const double v = rows[(int64_t)r0 * d + k];
+        urows[t] = v;
+        if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
+        mb = __float_as_uint(nextafterf((float)fabs(v), INFINITY));  // a float at or above |v|
+    }
+    if (maxabs) {  // max|x| of the distinct rows (the fp16 radius search's scale): one atomic per block
+        for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mb;
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(maxabs, max(max(red[0], red[1]), max(red[2], red[3])));
+    }
 }
 
 // The hint for the next bootstrap: each distinct cell's certified squared
@@ -2059,110 +2235,115 @@ __global__ void kt_transpose_kernel(const double* __restrict__ pcs, int64_t N, i
     rows[i * d + k] = pcs[t];
 }
 
-// one wave per distinct cell: the first kq present entries of its table row
-__global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, const int* __restrict__ ustart,
+// Radius for a cell short of kq present table entries (one wave per cell):
+// the kq-th smallest exact d2 over distinct present cells near it -- its
+// present table entries, and for every table entry the first present cell of
+// that entry's own row outside the cell's row.  Any kq distinct present
+// cells bound the kq-th neighbour distance from above; +inf (the
+// per-thread-list search) when fewer than kq are found.  Lane t holds the
+// cell's table entry v (-1 past K), present as distinct cell u1 (-1: absent).
+#define KT_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
+struct KtTauLds {
+    int hset[128];  // the cell's own table row as an open-addressing set (K <= 48 of 128 slots)
+    int pick[64];
+    double val[128];
+};
+__device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int K, int d, int uid, int64_t c, int v,
+                                              int u1, double val1, const int* __restrict__ cell2u,
+                                              const int32_t* __restrict__ tab_idx, const double* __restrict__ urows) {
+    auto hslot = [](int x) { return (int)(((unsigned)x * 2654435761u) >> 25); };
+    S.hset[lane] = -1;
+    S.hset[64 + lane] = -1;
+    KT_SYNC();
+    if (v >= 0)
+        for (int h = hslot(v);; h = (h + 1) & 127) {
+            const int prev = atomicCAS(&S.hset[h], -1, v);
+            if (prev == -1 || prev == v) break;
+        }
+    KT_SYNC();
+    int w = -1;
+    if (v >= 0) {
+        for (int s = 0; s < K && w < 0; ++s) {
+            const int x = tab_idx[(int64_t)v * K + s];
+            if (x < 0 || x == (int)c || cell2u[x] < 0) continue;
+            bool in_row = false;
+            for (int h = hslot(x);; h = (h + 1) & 127) {
+                const int y = S.hset[h];
+                if (y == x) {
+                    in_row = true;
+                    break;
+                }
+                if (y == -1) break;
+            }
+            if (!in_row) w = x;
+        }
+    }
+    S.pick[lane] = w;
+    KT_SYNC();
+    bool dup = false;
+    for (int t = 0; t < lane; ++t) dup |= w >= 0 && S.pick[t] == w;
+    double val2 = INFINITY;
+    if (w >= 0 && !dup) {
+        const double* xr = urows + (int64_t)uid * d;
+        const double* yr = urows + (int64_t)cell2u[w] * d;
+        double s2 = 0.0;
+        for (int k = 0; k < d; ++k) {
+            const double t = __dsub_rn(xr[k], yr[k]);
+            s2 = __dadd_rn(s2, __dmul_rn(t, t));
+        }
+        val2 = s2;
+    }
+    if (u1 < 0) val1 = INFINITY;
+    S.val[lane] = val1;
+    S.val[64 + lane] = val2;
+    KT_SYNC();
+    int c1 = 0, c2 = 0;
+    for (int t = 0; t < 128; ++t) {
+        const double b = S.val[t];
+        c1 += b <= val1 ? 1 : 0;
+        c2 += b <= val2 ? 1 : 0;
+    }
+    double best = INFINITY;
+    if (val1 < INFINITY && c1 >= kq) best = val1;
+    if (val2 < INFINITY && c2 >= kq) best = fmin(best, val2);
+    for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+    KT_SYNC();
+    return best;
+}
+
+// one wave per distinct cell: the first kq present entries of its table row;
+// a cell short of kq of them joins the exact search with its radius (round
+// 5: taken here, in the same wave, instead of a separate kt_tau pass over the
+// failed list)
+__global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, int d, const int* __restrict__ ustart,
                                                         const int32_t* __restrict__ scell,
                                                         const int* __restrict__ cell2u,
                                                         const int32_t* __restrict__ tab_idx,
-                                                        const double* __restrict__ tab_d2, int32_t* __restrict__ uidx,
+                                                        const double* __restrict__ tab_d2,
+                                                        const double* __restrict__ urows, int32_t* __restrict__ uidx,
                                                         double* __restrict__ ud2, int* __restrict__ fail_list,
-                                                        int* __restrict__ fail_count) {
+                                                        int* __restrict__ fail_count, double* __restrict__ tau) {
+    __shared__ KtTauLds tl[4];
     const int uid = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (uid >= u) return;
     const int lane = threadIdx.x & 63;
     const int64_t c = scell[ustart[uid]];
     const int v = lane < K ? tab_idx[c * K + lane] : -1;
     const int w = v >= 0 ? cell2u[v] : -1;
+    const double dv = w >= 0 ? tab_d2[c * K + lane] : INFINITY;
     const unsigned long long m = __ballot(w >= 0);
     const int rank = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
     if (w >= 0 && rank < kq) {
         uidx[(int64_t)uid * kq + rank] = w;
-        ud2[(int64_t)uid * kq + rank] = tab_d2[c * K + lane];
+        ud2[(int64_t)uid * kq + rank] = dv;
     }
-    if (lane == 0 && __popcll(m) < kq) fail_list[atomicAdd(fail_count, 1)] = uid;
-}
-
-// Radius for a cell short of kq present table entries (one wave per cell):
-// the kq-th smallest exact d2 over distinct present cells near it -- its
-// present table entries, and for every table entry the first present cell of
-// that entry's own row outside the cell's row.  Any kq distinct present
-// cells bound the kq-th neighbour distance from above; +inf (the
-// per-thread-list search) when fewer than kq are found.
-#define KT_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
-__global__ __launch_bounds__(256) void kt_tau_kernel(int kq, int K, int d, const int* __restrict__ ustart,
-                                                     const int32_t* __restrict__ scell, const int* __restrict__ cell2u,
-                                                     const int32_t* __restrict__ tab_idx,
-                                                     const double* __restrict__ tab_d2, const double* __restrict__ urows,
-                                                     const int* __restrict__ fail_list,
-                                                     const int* __restrict__ fail_count, double* __restrict__ tau) {
-    __shared__ int hset_[4][128];  // the cell's own table row as an open-addressing set (K <= 48 of 128 slots)
-    __shared__ int pick_[4][64];
-    __shared__ double val_[4][128];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int nf = *fail_count;
-    auto hslot = [](int x) { return (int)(((unsigned)x * 2654435761u) >> 25); };
-    for (int f = blockIdx.x * 4 + wv; f < nf; f += gridDim.x * 4) {
-        const int uid = fail_list[f];
-        const int64_t c = scell[ustart[uid]];
-        const int v = lane < K ? tab_idx[c * K + lane] : -1;
-        hset_[wv][lane] = -1;
-        hset_[wv][64 + lane] = -1;
-        const int u1 = v >= 0 ? cell2u[v] : -1;
-        const double val1 = u1 >= 0 ? tab_d2[c * K + lane] : INFINITY;
-        KT_SYNC();
-        if (v >= 0)
-            for (int h = hslot(v);; h = (h + 1) & 127) {
-                const int prev = atomicCAS(&hset_[wv][h], -1, v);
-                if (prev == -1 || prev == v) break;
-            }
-        KT_SYNC();
-        int w = -1;
-        if (v >= 0) {
-            for (int s = 0; s < K && w < 0; ++s) {
-                const int x = tab_idx[(int64_t)v * K + s];
-                if (x < 0 || x == (int)c || cell2u[x] < 0) continue;
-                bool in_row = false;
-                for (int h = hslot(x);; h = (h + 1) & 127) {
-                    const int y = hset_[wv][h];
-                    if (y == x) {
-                        in_row = true;
-                        break;
-                    }
-                    if (y == -1) break;
-                }
-                if (!in_row) w = x;
-            }
+    if (__popcll(m) < kq) {  // (wave-uniform)
+        const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c, v, w, dv, cell2u, tab_idx, urows);
+        if (lane == 0) {
+            const int f = atomicAdd(fail_count, 1);
+            fail_list[f] = uid;
+            tau[f] = best;
         }
-        pick_[wv][lane] = w;
-        KT_SYNC();
-        bool dup = false;
-        for (int t = 0; t < lane; ++t) dup |= w >= 0 && pick_[wv][t] == w;
-        double val2 = INFINITY;
-        if (w >= 0 && !dup) {
-            const double* xr = urows + (int64_t)uid * d;
-            const double* yr = urows + (int64_t)cell2u[w] * d;
-            double s2 = 0.0;
-            for (int k = 0; k < d; ++k) {
-                const double t = __dsub_rn(xr[k], yr[k]);
-                s2 = __dadd_rn(s2, __dmul_rn(t, t));
-            }
-            val2 = s2;
-        }
-        val_[wv][lane] = val1;
-        val_[wv][64 + lane] = val2;
-        KT_SYNC();
-        int c1 = 0, c2 = 0;
-        for (int t = 0; t < 128; ++t) {
-            const double b = val_[wv][t];
-            c1 += b <= val1 ? 1 : 0;
-            c2 += b <= val2 ? 1 : 0;
-        }
-        double best = INFINITY;
-        if (val1 < INFINITY && c1 >= kq) best = val1;
-        if (val2 < INFINITY && c2 >= kq) best = fmin(best, val2);
-        for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
-        if (lane == 0) tau[f] = best;
-        KT_SYNC();
     }
 }
 
@@ -2275,18 +2456,18 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     kb_fixup_big_kernel<<<16, 256, 0, st>>>(n, ustart, srow, row2u, big, nbig, rid);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
+    // the table path: fail counts, expansion tie count and max|x| (misc[4..7]) zeroed first
+    unsigned* umax = (kq >= 1 && tab_idx) ? misc + 7 : nullptr;
+    if (umax) CCG_HIP(hipMemsetAsync(misc + 4, 0, 4 * sizeof(unsigned), st));
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
-                                                                            cell_hint, urow_hint);
+                                                                            cell_hint, urow_hint, umax);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
         int* ufail = (int*)(misc + 5);
-        CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));  // fail counts, expansion tie count
-        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, ustart, scell, cell2u, tab_idx, tab_d2,
-                                                                   uidx, ud2, fail_list, ufail);
-        kt_tau_kernel<<<256, 256, 0, st>>>(kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, fail_list, ufail,
-                                           ftau);
-        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau);
+        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2,
+                                                                   urows, uidx, ud2, fail_list, ufail, ftau);
+        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau, umax);
         if (rc) return rc;
         if (stats) {
             int nf = 0;
@@ -2318,8 +2499,9 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
                                              fail_list, fail_count, ftau);
     }
+    // (the rows are copies of the distinct rows: the same max|x|)
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st, false,
-                             KNN_EXPAND_RADIUS ? ftau : nullptr);
+                             KNN_EXPAND_RADIUS ? ftau : nullptr, umax);
     if (rc) return rc;
     ctx->last_fail_list = fail_list;
     ctx->last_fail_count = fail_count;
@@ -2418,8 +2600,11 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     double* ud2 = urows + (size_t)u * d;
     int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kmax);
     int* fail_count = (int*)(misc + 4);
-    CCG_HIP(hipMemcpyAsync(dso, seg_off, sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
-    CCG_HIP(hipMemcpyAsync(duo, uoff.data(), sizeof(int64_t) * (nseg + 1), hipMemcpyHostToDevice, st));
+    {
+        int rs = ccg_h2d_staged(ctx, dso, seg_off, sizeof(int64_t) * (nseg + 1), st);
+        if (!rs) rs = ccg_h2d_staged(ctx, duo, uoff.data(), sizeof(int64_t) * (nseg + 1), st);
+        if (rs) return rs;
+    }
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     const unsigned ng = (unsigned)ccg_cdiv(n, 256);
     // 1. the rows, and (segment, cell) keys sorted stably: each segment's cells, each cell's rows ascending
@@ -2436,7 +2621,7 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     if (rc) return rc;
     kb_tables_kernel<<<ng, 256, 0, st>>>(skeys, srow, n, head, (int)u, ustart, row2u, ctx->d_err);
     kb_urows_kernel<<<(unsigned)ccg_cdiv(u * d, 256), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
-                                                                      nullptr);
+                                                                      nullptr, nullptr);
     // 3. every segment's distinct cells among themselves (kq = kmax: each has >= kmax + 1)
     std::vector<int64_t> po;
     std::vector<int> hperm;

@@ -9,10 +9,12 @@
 // and the mean over non-NaN widths.
 //
 // Every cross-row reduction (cluster sums, variances, the mean) is done in
-// 64-bit fixed point with integer atomics, so the result is bitwise
-// reproducible regardless of scheduling; the scale is chosen on the device
-// from max|x| so no partial sum can overflow.  Quantisation error is below
-// 2^-36 relative for the sizes we support, far inside the 1e-5 tolerance.
+// fixed point with integer atomics, so the result is bitwise reproducible
+// regardless of scheduling; the scales are chosen on the device from max|x|
+// so no partial sum can overflow.  The cluster sums take int32 rows (2^-30 of
+// max|x|, round 5: the tiled sums stage them in LDS) and int64 sums; the
+// squared norms and the widths' sum 64-bit values.  The quantisation error
+// of a centroid is below 2^-30 max|x|, far inside the 1e-5 tolerance.
 // The widths' squared distances are |x|^2 + |mu|^2 + v - 2 x.mu with x.mu on
 // the fp64 matrix core (a fixed-order MFMA chain, so also reproducible).
 // Grid: (row tiles) x (groups of SIL_LG labelings); x rows are held in
@@ -22,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "ccg_internal.h"
 
@@ -34,11 +37,66 @@
 #define SIL_LG 5
 #endif
 
-__device__ __forceinline__ int scale_exp(double bound) {
+__host__ __device__ __forceinline__ int scale_exp(double bound) {
     // largest e with bound * 2^e <= 2^61
     if (!(bound > 0.0)) return 52;
     int e = 61 - (ilogb(bound) + 1);
     return e > 52 ? 52 : e;
+}
+
+// the int32 fixed-point rows of the cluster sums (round 5): largest e with
+// maxabs * 2^e <= 2^30 (sums of up to 2^31 weighted rows stay inside int64)
+__host__ __device__ inline int scale_exp32(double maxabs) {
+    if (!(maxabs > 0.0)) return 30;
+    const int e = 29 - ilogb(maxabs);
+    return e > 52 ? 52 : e;
+}
+
+// A batch of segments (ccg_silhouette_segments_dev): segment q holds rows
+// [off[q], off[q+1]) of the concatenation and labels lab[q] ([L][m_q]); its
+// tiles of the sums / width grids start at ts[q] / tw[q]; the means,
+// cluster counts and smallest sizes of its L labelings go to mean[q],
+// ncl[q], mns[q] (each may be NULL).  Labeling l of segment q is the
+// "virtual labeling" q L + l of every per-labeling table.  nseg = 0: one
+// matrix (the single-call entry points).
+struct SilSegs {
+    int nseg;
+    const int64_t* off;
+    const int32_t* const* lab;
+    const int* ts;
+    const int* tw;
+    double* const* mean;
+    int32_t* const* ncl;
+    int32_t* const* mns;
+};
+// the segment of tile b: the largest q with pre[q] <= b
+__device__ __forceinline__ int sil_seg_tile(const int* __restrict__ pre, int nseg, int b) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// the segment of row r
+__device__ __forceinline__ int sil_seg_row(const int64_t* __restrict__ off, int nseg, int64_t r) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// label of row r in labeling l (segments: of r's segment q)
+__device__ __forceinline__ int sil_label(const int32_t* __restrict__ labels, int64_t m, const SilSegs& sg, int q,
+                                         int l, int64_t r) {
+    if (sg.nseg) {
+        const int64_t o = sg.off[q];
+        return sg.lab[q][(int64_t)l * (sg.off[q + 1] - o) + (r - o)];
+    }
+    return labels[(int64_t)l * m + r];
 }
 
 // one atomic per block on one word: a small grid (a 1024-block grid spent
@@ -156,15 +214,15 @@ __host__ __device__ inline double sil_s2_bound(double maxabs, int d, int64_t m) 
 }
 template <int DMAX>
 __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const unsigned* __restrict__ maxabs_bits,
-                          long long* __restrict__ q1, long long* __restrict__ q2) {
+                          int* __restrict__ q1, long long* __restrict__ q2) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t / DMAX;  // m * DMAX is a multiple of DMAX: a row's threads are all in or all out
     if (r >= m) return;
     const int k = (int)(t - r * DMAX);
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
+    const double sc = ldexp(1.0, scale_exp32(maxabs));
     const double v = k < d ? x[r * d + k] : 0.0;
-    q1[t] = __double2ll_rn(v * sc);
+    q1[t] = __double2int_rn(v * sc);
     // |x|^2 of the row: its DMAX threads are DMAX-aligned lanes of one wave
     // (fixed xor tree: deterministic)
     double s2 = v * v;
@@ -173,186 +231,161 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
     if (k == 0) q2[r] = __double2ll_rn(s2 * ldexp(1.0, scale_exp(sil_s2_bound(maxabs, d, m))));
 }
 
-// K1 (sorted segments): cluster sums S1 = sum x, S2 = sum |x|^2 and counts of
-// a SIL_SORT_ROWS-row tile for one labeling (grid y), without a per-row
-// atomic.  The tile's rows are counting-sorted by label in LDS; each wave
-// then walks a quarter of the sorted rows with lanes along the dimensions
-// (64 / DMAX rows per step) and keeps running sums in registers while the
-// label repeats, so a lane issues one LDS atomic per label segment instead of
-// one per row.  Large tiles keep the flush of the LDS sums to the global sums
-// (atomics from every block on the same words) rare.  Integer sums: any
-// order gives the same bits.  LDS: acc1 [cmax+1][DMAX] and acc2 [cmax+1]
-// int64, counts/offsets [cmax+1], sorted rows, labels and weights
-// [SIL_SORT_ROWS].
-#ifndef SIL_SORT_ROWS
-#define SIL_SORT_ROWS 1024
-#endif
-#ifndef SIL_SUMS_UNROLL
-#define SIL_SUMS_UNROLL 8  // walk steps whose loads are in flight together per wave
-#endif
-#ifndef SIL_SUMS_ROWS
-#define SIL_SUMS_ROWS 0  // tools only: 1 = cluster sums over every row, not the representatives (A/B)
-#endif
-template <int DMAX>
-__host__ __device__ constexpr size_t sil_sorted_lds(int cmax) {
-    return (size_t)(cmax + 1) * DMAX * 8 + (size_t)(cmax + 1) * 16 + 3 * SIL_SORT_ROWS * 4;
+// K1 (round 5, tiles staged once for a group of labelings): cluster sums
+// S1 = sum x, S2 = sum |x|^2 and counts.  A block of 1024 threads takes a
+// tile of T positions (rows, or representatives weighted by their copies)
+// and stages their fixed-point rows in LDS ONCE (int32 q1 at stride d, scale
+// 2^e with max|x| 2^e <= 2^30, and int64 q2 = |x|^2): round 4 re-read the
+// rows from L2 for every labeling (60 x 59k x 256 B = 0.9 GB per bootstrap at
+// cfg3).  Then per labeling of its group (grid y, sg labelings): lanes along
+// the dimensions, 64 / DMAX positions per wave instruction, one int64 LDS
+// atomic per (position, dimension) into the block's [cmax+1][d] sums (the
+// positions of one instruction share an address only when their labels
+// match); after a barrier each thread adds the sums it owns to the global
+// sums (one atomic per present (cluster, dimension), contiguous) and zeroes
+// them.  The next labeling's labels and weights are loaded a phase ahead and
+// written to LDS during the flush: two barriers per labeling.  Integer
+// sums: any order gives the same bits.  LDS (dynamic): q1 [T][d] int32,
+// q2 [T] int64, labels and weights [T] int, acc1 [cmax+1][d], acc2 and
+// counts [cmax+1] int64.  T is the largest of 1024 / 512 / 256 that fits.
+#define SIL_ST 1024  // threads of the tiled sums kernel (16 waves, one block per CU)
+#define SIL_LDS_CU 163840
+__host__ __device__ inline size_t sil_tile_lds(int T, int d, int cmax) {
+    return (size_t)T * d * 4 + (size_t)T * 16 + (size_t)(cmax + 1) * (d + 2) * 8;
 }
 
 // Distinct-cell form (rep != nullptr): tile position p is the representative
 // row rep[p] of a cell, weighted by the cnt[p] rows of the cell less the
 // mult[l][p] of them labelled apart in labeling l (those rows are added by
-// sil_sums_exc); the integer sums are those of the rows.  (Grid order: tiles
-// fastest.  Dealing a tile's labelings to one XCD instead, so its rows are
-// read into one L2, measured slower: 335 against 223 us at cfg3.)
-
-template <int DMAX>
-__global__ __launch_bounds__(SIL_T) void sil_sums_sorted(int64_t m, int d, const int32_t* __restrict__ labels,
-                                                         int cmax, const long long* __restrict__ q1,
-                                                         const long long* __restrict__ q2,
-                                                         unsigned long long* __restrict__ gsum,
-                                                         unsigned long long* __restrict__ gsum2,
-                                                         unsigned long long* __restrict__ gcnt,
-                                                         const int* __restrict__ rep, const int* __restrict__ mult,
-                                                         const int* __restrict__ cnt, int64_t mw,
-                                                         const int64_t* __restrict__ nrep) {
+// sil_sums_exc); the integer sums are those of the rows.
+template <int DMAX, bool SEG>
+__global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T, int sg,
+                                                        const int32_t* __restrict__ labels, int L, int cmax,
+                                                        const int* __restrict__ q1, const long long* __restrict__ q2,
+                                                        unsigned long long* __restrict__ gsum,
+                                                        unsigned long long* __restrict__ gsum2,
+                                                        unsigned long long* __restrict__ gcnt,
+                                                        const int* __restrict__ rep, const int* __restrict__ mult,
+                                                        const int* __restrict__ cnt, int64_t mw,
+                                                        const int64_t* __restrict__ nrep,
+                                                        const int64_t* __restrict__ scan, SilSegs sgs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int RPT = SIL_SORT_ROWS / SIL_T;  // rows per thread in the sort
-    constexpr int RPW = 64 / DMAX;              // rows per wave step
-    constexpr int STEPS = SIL_SORT_ROWS / 4 / RPW;
-    unsigned long long* acc1 = (unsigned long long*)smem;                 // [cmax+1][DMAX]
-    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * DMAX;         // [cmax+1]
-    int* hcnt = (int*)(acc2 + (cmax + 1));                                // [cmax+1]
-    int* hoff = hcnt + (cmax + 1);                                        // [cmax+1]
-    int* srow = hoff + (cmax + 1);                                        // [SIL_SORT_ROWS]
-    int* slab = srow + SIL_SORT_ROWS;                                     // [SIL_SORT_ROWS]
-    int* swgt = slab + SIL_SORT_ROWS;                                     // [SIL_SORT_ROWS]
-    __shared__ int sh[SIL_T / 64];
+    int* q1s = (int*)smem;                                    // [T][d]
+    long long* q2s = (long long*)(q1s + (int64_t)T * d);      // [T] (T * d * 4 is a multiple of 8: T even)
+    int* slab = (int*)(q2s + T);                              // [T]
+    int* swgt = slab + T;                                     // [T]
+    unsigned long long* acc1 = (unsigned long long*)(swgt + T);  // [cmax+1][d]
+    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * d;   // [cmax+1]
+    unsigned long long* accn = acc2 + (cmax + 1);                // [cmax+1] weighted counts
+    constexpr int NW = SIL_ST / 64;
+    constexpr int RPW = 64 / DMAX;  // positions per wave instruction
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k = lane % DMAX, sub = lane / DMAX;
-    const int l = blockIdx.y;
-    const int64_t rb = (int64_t)blockIdx.x * SIL_SORT_ROWS;
-    const int64_t npos = rep ? *nrep : m;  // positions: rows, or the representatives (counted on the device)
+    int64_t rb, npos;  // the tile's first position, the end of its positions
+    int q = 0;
+    if constexpr (SEG) {  // a tile of segment q: its representatives are positions [scan[off_q], scan[off_q+1])
+        q = sil_seg_tile(sgs.ts, sgs.nseg, blockIdx.x);
+        rb = scan[sgs.off[q]] + (int64_t)(blockIdx.x - sgs.ts[q]) * T;
+        npos = scan[sgs.off[q + 1]];
+    } else {
+        rb = (int64_t)blockIdx.x * T;
+        npos = rep ? *nrep : m;  // positions: rows, or the representatives (counted on the device)
+    }
     if (rb >= npos) return;
-    const int nacc = (cmax + 1) * DMAX;
-    for (int t = tid; t < nacc + cmax + 1; t += SIL_T) acc1[t] = 0ull;
-    for (int t = tid; t <= cmax; t += SIL_T) hcnt[t] = 0;
+    const int l0 = blockIdx.y * sg, l1 = min(L, l0 + sg);
+    // one position per thread (T <= SIL_ST)
+    const bool own = tid < T && rb + tid < npos;
+    const int rowv = own ? (rep ? rep[rb + tid] : (int)(rb + tid)) : -1;
+    if (tid < T) slab[tid] = rowv;
     __syncthreads();
-    // label 0 collects rows past m and codes outside [1, cmax]
-    int lab[RPT], rank[RPT], wgt[RPT], row[RPT];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-        const int64_t p = rb + i * SIL_T + tid;
-        int lb = 0, w = 0, r = 0;
-        if (p < npos) {
-            r = rep ? rep[p] : (int)p;
-            lb = labels[(int64_t)l * m + r];
-            w = rep ? cnt[p] - mult[(int64_t)l * mw + p] : 1;
-            if (lb < 1 || lb > cmax || w <= 0) lb = 0;
-        }
-        lab[i] = lb;
-        wgt[i] = w;
-        row[i] = r;
-        rank[i] = atomicAdd(&hcnt[lb], 1);
+    for (int e = tid; e < T * d; e += SIL_ST) {
+        const int i = e / d, kk = e - i * d;
+        const int r = slab[i];
+        q1s[e] = r >= 0 ? q1[(int64_t)r * DMAX + kk] : 0;
     }
-    __syncthreads();
-    int carry = 0;
-    for (int c0 = 0; c0 <= cmax; c0 += SIL_T) {
-        const int c = c0 + tid;
-        const int v = c <= cmax ? hcnt[c] : 0;
-        int tot;
-        const int ex = carry + sil_block_excl_scan(v, sh, &tot);
-        if (c <= cmax) hoff[c] = ex;
-        carry += tot;
-    }
-    __syncthreads();
-    // the sorted positions carry (position in the tile, weight); hcnt becomes
-    // the weighted row count of each label
-    __syncthreads();
-    for (int t = tid; t <= cmax; t += SIL_T) hcnt[t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-        srow[hoff[lab[i]] + rank[i]] = row[i];  // the row itself: no dependent load in the walk
-        slab[hoff[lab[i]] + rank[i]] = lab[i];
-        swgt[hoff[lab[i]] + rank[i]] = wgt[i];
-        if (lab[i]) atomicAdd(&hcnt[lab[i]], wgt[i]);
-    }
-    __syncthreads();
-    long long a1 = 0, a2 = 0;
-    int cur = 0;
-    const int p0 = wave * (SIL_SORT_ROWS / 4) + sub;
-    // batches of U steps: the batch's LDS reads, then its gathered global
-    // loads (all in flight together), then the segment logic and its LDS
-    // atomics (an atomic between them would keep the compiler from hoisting
-    // the next step's reads: the walk waited on one load at a time)
-    constexpr int U = SIL_SUMS_UNROLL;
-    static_assert(STEPS % U == 0, "walk batches");
-    for (int st0 = 0; st0 < STEPS; st0 += U) {
-        int lbv[U];
-        int64_t rv[U];
-        long long wv[U], v1[U], v2[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int pos = p0 + (st0 + u) * RPW;
-            lbv[u] = slab[pos];
-            rv[u] = srow[pos];
-            wv[u] = swgt[pos];
+    if (tid < T) q2s[tid] = rowv >= 0 ? q2[rowv] : 0ll;
+    for (int t = tid; t < (cmax + 1) * (d + 2); t += SIL_ST) acc1[t] = 0ull;
+    // label 0: positions past npos, codes outside [1, cmax] and weight 0
+    int lbn = 0, wgn = 0;
+    auto fetch = [&](int l) {
+        lbn = 0;
+        wgn = 0;
+        if (l < l1 && own) {
+            lbn = sil_label(labels, m, sgs, q, l, rowv);
+            wgn = rep ? cnt[rb + tid] - mult[(int64_t)l * mw + rb + tid] : 1;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v1[u] = lbv[u] ? q1[rv[u] * DMAX + k] : 0ll;
-            v2[u] = (lbv[u] && k == 0) ? q2[rv[u]] : 0ll;
+    };
+    auto put = [&]() {
+        if (tid < T) {
+            const bool ok = lbn >= 1 && lbn <= cmax && wgn > 0;
+            slab[tid] = ok ? lbn : 0;
+            swgt[tid] = ok ? wgn : 0;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int lb = lbv[u];
-            if (lb != cur) {
-                if (cur && k < d) {
-                    atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
-                    if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
+    };
+    fetch(l0);
+    __syncthreads();  // the rows' ids in slab are read
+    put();
+    fetch(l0 + 1);
+    __syncthreads();
+    const int ppw = T / NW;  // positions per wave
+    for (int l = l0; l < l1; ++l) {
+        for (int p0 = wave * ppw; p0 < (wave + 1) * ppw; p0 += RPW) {
+            const int pl = p0 + sub;
+            const int lb = slab[pl];
+            if (lb) {
+                const long long w = swgt[pl];
+                if (k < d) atomicAdd(&acc1[lb * d + k], (unsigned long long)(w * (long long)q1s[pl * d + k]));
+                if (k == 0) {
+                    atomicAdd(&acc2[lb], (unsigned long long)(w * q2s[pl]));
+                    atomicAdd(&accn[lb], (unsigned long long)w);
                 }
-                cur = lb;
-                a1 = 0;
-                a2 = 0;
             }
-            a1 += wv[u] * v1[u];
-            a2 += wv[u] * v2[u];
         }
-    }
-    if (cur && k < d) {
-        atomicAdd(&acc1[cur * DMAX + k], (unsigned long long)a1);
-        if (k == 0) atomicAdd(&acc2[cur], (unsigned long long)a2);
-    }
-    __syncthreads();
-    unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
-    for (int t = tid; t < nacc; t += SIL_T) {
-        const int c = t / DMAX, kk = t - c * DMAX;
-        if (kk < d && c >= 1 && acc1[t]) atomicAdd(&gs[(int64_t)c * d + kk], acc1[t]);
-    }
-    for (int c = 1 + tid; c <= cmax; c += SIL_T) {
-        if (hcnt[c]) atomicAdd(&gcnt[(int64_t)l * (cmax + 1) + c], (unsigned long long)hcnt[c]);
-        if (acc2[c]) atomicAdd(&gsum2[(int64_t)l * (cmax + 1) + c], acc2[c]);
+        __syncthreads();
+        // flush-and-zero (each entry read and cleared by one thread), the next labels
+        const int lv = q * L + l;  // (the virtual labeling)
+        unsigned long long* gs = gsum + (int64_t)lv * (cmax + 1) * d;
+        for (int t = tid; t < (cmax + 1) * d; t += SIL_ST) {
+            const unsigned long long v = acc1[t];
+            if (v) {
+                atomicAdd(&gs[t], v);
+                acc1[t] = 0ull;
+            }
+        }
+        for (int c = tid; c <= cmax; c += SIL_ST) {
+            if (accn[c]) {
+                atomicAdd(&gcnt[(int64_t)lv * (cmax + 1) + c], accn[c]);
+                atomicAdd(&gsum2[(int64_t)lv * (cmax + 1) + c], acc2[c]);
+                accn[c] = 0ull;
+                acc2[c] = 0ull;
+            }
+        }
+        put();
+        fetch(l + 2);
+        __syncthreads();
     }
 }
 
 // Rows labelled apart from their cell's representative (the exception list
 // of sil_mult_kernel, l << 32 | row): their fixed-point rows added alone.
 template <int DMAX>
-__global__ void sil_sums_exc(int64_t m, int d, const int32_t* __restrict__ labels, int cmax,
-                             const long long* __restrict__ q1, const long long* __restrict__ q2,
+__global__ void sil_sums_exc(int64_t m, int d, const int32_t* __restrict__ labels, int L, int cmax,
+                             const int* __restrict__ q1, const long long* __restrict__ q2,
                              const unsigned long long* __restrict__ exc, const int* __restrict__ nexc,
                              unsigned long long* __restrict__ gsum, unsigned long long* __restrict__ gsum2,
-                             unsigned long long* __restrict__ gcnt) {
+                             unsigned long long* __restrict__ gcnt, SilSegs sgs) {
     const int ne = *nexc;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
         const int l = (int)(exc[e] >> 32);
         const int64_t r = (int64_t)(exc[e] & 0xffffffffull);
-        const int lab = labels[(int64_t)l * m + r];
+        const int q = sgs.nseg ? sil_seg_row(sgs.off, sgs.nseg, r) : 0;
+        const int lab = sil_label(labels, m, sgs, q, l, r);
         if (lab < 1 || lab > cmax) continue;
-        unsigned long long* gs = gsum + ((int64_t)l * (cmax + 1) + lab) * d;
-        for (int k = 0; k < d; ++k) atomicAdd(&gs[k], (unsigned long long)q1[r * DMAX + k]);
-        atomicAdd(&gsum2[(int64_t)l * (cmax + 1) + lab], (unsigned long long)q2[r]);
-        atomicAdd(&gcnt[(int64_t)l * (cmax + 1) + lab], 1ull);
+        const int64_t lv = (int64_t)q * L + l;
+        unsigned long long* gs = gsum + (lv * (cmax + 1) + lab) * d;
+        for (int k = 0; k < d; ++k) atomicAdd(&gs[k], (unsigned long long)(long long)q1[r * DMAX + k]);
+        atomicAdd(&gsum2[lv * (cmax + 1) + lab], (unsigned long long)q2[r]);
+        atomicAdd(&gcnt[lv * (cmax + 1) + lab], 1ull);
     }
 }
 
@@ -371,7 +404,7 @@ __host__ __device__ __forceinline__ int sil_mfma_pos(int k) {
 // With the sums of squares (gsum2, the sorted-segment path) also
 // v_c = mean |x - mu_c|^2 = sum_k (S2 / n - mu_k^2).  One block per labeling.
 template <int DMAX>
-__global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
+__global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax, int q32,
                                                 const unsigned* __restrict__ maxabs_bits,
                                                 const unsigned long long* __restrict__ gsum,
                                                 const unsigned long long* __restrict__ gsum2,
@@ -382,7 +415,8 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
     __shared__ int sh[SIL_T / 64];
     const int l = blockIdx.x;
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
+    // the sums' scale: the int32 rows of the tiled sums, or sil_centroid's
+    const double inv_sc = ldexp(1.0, q32 ? -scale_exp32(maxabs) : -scale_exp(maxabs * (double)m));
     const unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
     const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
     int* pl = pos + (int64_t)l * (cmax + 1);
@@ -737,6 +771,327 @@ __global__ __launch_bounds__(SIL_T) void sil_width(const double* __restrict__ x,
     }
 }
 
+// K5' (round 5, d <= 32): the nearest other cluster screened on the fp16
+// matrix core, the two distances a width needs taken exactly in fp64.
+//
+// Screen: rows and centroids scaled by 2^e (max|x| 2^e < 2^12) and split
+// into fp16 hi + lo (flushed below 2^-14); x.mu ~ hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_32x32x16_f16 with A = 32 centroids (LDS) and B = 32
+// representatives (registers, built once per block), so lane (h, j) gets 16
+// centroids of the tile against representative j.  Per value
+// a = (|mu|^2 + v) 2^2e - 2 x.mu (= D^2 - |x|^2, scaled) with the value's
+// register and tile packed into its 7 low mantissa bits, the own cluster
+// masked, and the two smallest kept (two med3): 6 VALU per value.  The
+// error of a is taken as
+//   E = 2^-14 (|x'| + max|mu'|)^2 + 2^-11 sqrt(d) (|x'| + max|mu'|)
+//       + 2^-14 max A' + 8
+// (the kNN screen's certification budget, 1024 fp32 ulps of s^2, for the
+// split residuals and the fp32 accumulation of 3 DMAX products; the flushed
+// parts below 2^-14; the fp32 A' and the 7-bit packing), so
+// when the second smallest exceeds the smallest by more than 2E the
+// smallest is the true nearest other cluster; otherwise (rare) every
+// centroid is taken exactly.  Exact: D^2 = sum_k (x_k - mu_k)^2 + v_c in
+// fp64 (fixed order: reproducible), lane h = 0 for the own cluster, h = 1
+// for the nearest other one.  The matrix work per (representative,
+// centroid) is 3 x 16 DMAX/16 fp16 MACs against round 4's DMAX fp64 MACs
+// on the fp64 matrix core (78.6 vs 2500 dense TFLOP/s).
+//
+// Each labeling's LDS image (fp16 fragments, fp64 centroids, v, A', the
+// screen's bounds, code -> ordinal) is built once by sil_w16_prep; the
+// width kernel double-buffers the images and copies the next one with
+// global_load_lds while it screens the current one (one barrier per
+// labeling, no dependent loads in the stage).
+// Grid: 128 representatives per block (4 waves x 32) x groups of SIL_WLG
+// labelings.
+typedef _Float16 sil_h8 __attribute__((ext_vector_type(8)));
+typedef float sil_f16x __attribute__((ext_vector_type(16)));
+#define SIL_WT 256      // threads of sil_width16 (4 waves x 32 representatives)
+#define SIL_WLG 15      // labelings per sil_width16 block
+#define SIL_WCMAX 256   // 8 tiles of 32: the tile fits the packed minimum's 3 bits
+#define SIL_BIG 1.0e38f
+#define SIL_W16_LDS 81920  // two image buffers (40 KB each) per block: cmax <= 96 at d <= 32
+
+// image of a labeling with cpl = 32 x tiles centroid slots: fragments
+// [cpl][64] f16 (8 chunks (s, hi/lo, h) of 8, chunk q at q ^ (c & 7)),
+// centroids [cpl][DMAX] f64 (16-byte chunk q at q ^ (c & (DMAX/2 - 1))),
+// v [cpl] f64, A' [cpl] f32 (SIL_BIG: padding), bounds 2 f64, code ->
+// ordinal [cmax+1] int
+__host__ __device__ inline size_t sil_img_bytes(int cpl, int dmax, int cmax) {
+    return (size_t)cpl * (128 + 8 * (size_t)dmax + 12) + 16 + 4 * (size_t)(cmax + 1);
+}
+__host__ __device__ inline size_t sil_img_stride(int cmax, int dmax) {
+    return (sil_img_bytes((cmax + 31) & ~31, dmax, cmax) + 1023) & ~(size_t)1023;
+}
+__host__ __device__ inline int sil_e16(double maxabs) {
+    return maxabs > 0.0 ? 11 - ilogb(maxabs) : 0;
+}
+
+__device__ __forceinline__ void sil_split16(double v, _Float16& hi, _Float16& lo) {
+    const float f = (float)v;
+    hi = fabsf(f) < 0x1p-14f ? (_Float16)0.0f : (_Float16)f;
+    const float r = (float)(v - (double)(float)hi);
+    lo = fabsf(r) < 0x1p-14f ? (_Float16)0.0f : (_Float16)r;
+}
+
+// One block per labeling: its image (layout above).
+template <int DMAX>
+__global__ __launch_bounds__(256) void sil_w16_prep(int cmax, const unsigned* __restrict__ maxabs_bits,
+                                                    const int* __restrict__ npres, const int* __restrict__ codes,
+                                                    const int* __restrict__ pos, const double* __restrict__ mu,
+                                                    const double* __restrict__ auxc, unsigned char* __restrict__ img,
+                                                    size_t imgs) {
+    __shared__ double red[2][4];
+    const int l = blockIdx.x, tid = threadIdx.x;
+    const int C = npres[l], cpl = ((C + 31) >> 5) << 5;
+    unsigned char* base = img + (size_t)l * imgs;
+    _Float16* fr = (_Float16*)base;
+    double* m64 = (double*)(base + (size_t)cpl * 128);
+    double* sv = m64 + (size_t)cpl * DMAX;
+    float* sa = (float*)(sv + cpl);
+    double* bnd = (double*)(sa + cpl);
+    int* sp = (int*)(bnd + 2);
+    const int e16 = sil_e16((double)__uint_as_float(*maxabs_bits));
+    const double* ml = mu + (int64_t)l * (cmax + 1) * DMAX;
+    const int* cl = codes + (int64_t)l * cmax;
+    for (int t = tid; t < cpl * DMAX; t += 256) {
+        const int c = t / DMAX, k = t - c * DMAX;
+        const double v = c < C ? ml[(int64_t)cl[c] * DMAX + k] : 0.0;
+        m64[c * DMAX + ((((k >> 1) ^ (c & (DMAX / 2 - 1)))) << 1) + (k & 1)] = v;
+        _Float16 hi, lo;
+        sil_split16(ldexp(v, e16), hi, lo);
+        const int s = k >> 4, hh = (k >> 3) & 1, i = k & 7;
+        fr[c * 64 + (((s * 4 + hh) ^ (c & 7)) << 3) + i] = hi;
+        fr[c * 64 + (((s * 4 + 2 + hh) ^ (c & 7)) << 3) + i] = lo;
+    }
+    const double* al = auxc + (int64_t)l * cmax * 2;
+    double mb = 0.0, ab = 0.0;
+    for (int c = tid; c < cpl; c += 256) {
+        const bool pr = c < C;
+        const double a0 = pr ? al[2 * c] : 0.0, a1 = pr ? al[2 * c + 1] : 0.0;
+        sv[c] = a1;
+        sa[c] = pr ? (float)ldexp(a0 + a1, 2 * e16) : SIL_BIG;
+        mb = fmax(mb, a0);
+        ab = fmax(ab, a0 + a1);
+    }
+    for (int c = tid; c <= cmax; c += 256) sp[c] = pos[(int64_t)l * (cmax + 1) + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        ab = fmax(ab, __shfl_xor(ab, o, 64));
+    }
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = mb;
+        red[1][tid >> 6] = ab;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bnd[0] = sqrt(fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3])));
+        bnd[1] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+    }
+}
+
+template <int DMAX, int IMGB, bool SEG>
+__global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
+    const double* __restrict__ x, int64_t m, int d, const int32_t* __restrict__ labels, int L, int cmax,
+    const unsigned* __restrict__ maxabs_bits, const int* __restrict__ npres, const unsigned char* __restrict__ img,
+    size_t imgs, unsigned long long* __restrict__ wsum, unsigned long long* __restrict__ wcnt,
+    double* __restrict__ out_width, const int* __restrict__ rep, const int* __restrict__ mult,
+    const int* __restrict__ cnt, int64_t mw, int nbw, const int64_t* __restrict__ nrep, double wsc, double sqd,
+    const int64_t* __restrict__ scan, SilSegs sgs) {
+    constexpr int KS = DMAX / 16;  // K steps of 16 dimensions
+    constexpr int QM = DMAX / 2 - 1;  // fp64 chunk swizzle mask
+    // two image buffers as two objects, and the labeling loop unrolled by two,
+    // so the compiler sees that the copy into one does not alias the reads of
+    // the other (with one array it waits for the copy before every LDS read)
+    __shared__ __attribute__((aligned(1024))) unsigned char buf0[IMGB];
+    __shared__ __attribute__((aligned(1024))) unsigned char buf1[IMGB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    // 32 representatives per wave; tile tb of the (segment's) positions
+    int64_t pb, npos;
+    int q = 0, tb = blockIdx.x;
+    if constexpr (SEG) {  // segment q's representatives are positions [scan[off_q], scan[off_q+1])
+        q = sil_seg_tile(sgs.tw, sgs.nseg, blockIdx.x);
+        tb = blockIdx.x - sgs.tw[q];
+        pb = scan[sgs.off[q]] + (int64_t)tb * (SIL_WT / 2);
+        npos = scan[sgs.off[q + 1]];
+    } else {
+        pb = (int64_t)blockIdx.x * (SIL_WT / 2);
+        npos = rep ? *nrep : m;  // representatives: counted on the device
+    }
+    if (pb >= npos) return;  // the partials of idle blocks stay 0
+    const int l0 = blockIdx.y * SIL_WLG, l1 = min(L, l0 + SIL_WLG);
+    const int lq = q * L;  // virtual labeling of (q, 0)
+    // copy labeling l's image into buffer b: 1 KB per wave instruction
+    auto stage = [&](int l, unsigned char* dst) {
+        const int cpl = ((npres[lq + l] + 31) >> 5) << 5;
+        const int nch = (int)((sil_img_bytes(cpl, DMAX, cmax) + 1023) >> 10);
+        const unsigned char* src = img + (size_t)(lq + l) * imgs;
+        for (int ch = wave; ch < nch; ch += SIL_WT / 64)
+            __builtin_amdgcn_global_load_lds(
+                (const void __attribute__((address_space(1)))*)(src + (size_t)ch * 1024 + lane * 16),
+                (void __attribute__((address_space(3)))*)(dst + (size_t)ch * 1024), 16, 0, 0);
+    };
+    stage(l0, buf0);
+    // representative j of the wave (both lane halves hold it)
+    const int64_t p = pb + wave * 32 + j;
+    const bool in = p < npos;
+    const int64_t row = in ? (rep ? (int64_t)rep[p] : p) : 0;
+    const int e16 = sil_e16((double)__uint_as_float(*maxabs_bits));
+    double xr[DMAX];
+    double xx = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) {
+        xr[k] = (in && k < d) ? x[row * d + k] : 0.0;
+        xx = fma(xr[k], xr[k], xx);
+    }
+    const double xn = ldexp(sqrt(xx), e16);
+    sil_h8 bh[KS], bl[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            _Float16 hi, lo;
+            // a bit select, not a lane-dependent register index (which spills to scratch)
+            const long long hm = -(long long)h;
+            const double v = __longlong_as_double((__double_as_longlong(xr[16 * s + i]) & ~hm) |
+                                                  (__double_as_longlong(xr[16 * s + 8 + i]) & hm));
+            sil_split16(ldexp(v, e16), hi, lo);
+            bh[s][i] = hi;
+            bl[s][i] = lo;
+        }
+    const int cw = rep && in ? cnt[p] : 1;
+    // 32-bit offsets from wave-uniform bases (no 64-bit address pairs held across the loop)
+    const int pi = (int)p;
+    const int32_t* lbase = labels;  // labels of row rowl in labeling l: lbase[l * lstride + rowl]
+    int64_t lstride = m;
+    int rowl = (int)row;
+    if constexpr (SEG) {
+        lbase = sgs.lab[q];
+        lstride = sgs.off[q + 1] - sgs.off[q];
+        rowl = (int)(row - sgs.off[q]);
+    }
+    int lab = in ? (lbase + (int64_t)l0 * lstride)[rowl] : 0;
+    int mlt = (rep && in) ? (mult + (int64_t)l0 * mw)[pi] : 0;
+    // (wsc = 2^scale_exp(m) and sqd = sqrt(d) come as kernel arguments: SGPRs)
+    auto labeling = [&](int l, const unsigned char* __restrict__ bs, unsigned char* __restrict__ nxt) {
+        const int C = npres[lq + l];
+        const int nt = (C + 31) >> 5, cpl = nt << 5;
+        __syncthreads();  // image l has landed; the other buffer is free
+        const _Float16* sA = (const _Float16*)bs;
+        const double* smu = (const double*)(bs + (size_t)cpl * 128);
+        const double* sv = smu + (size_t)cpl * DMAX;
+        const float* sAf = (const float*)(sv + cpl);
+        const double* sbnd = (const double*)(sAf + cpl);
+        const int* spos = (const int*)(sbnd + 2);
+        // lab and mlt are consumed before the next image's copy is issued: a
+        // use of an ordinary load after it would wait for the copy too
+        const int po = (lab >= 1 && lab <= cmax) ? spos[lab] : -1;  // own ordinal
+        const int wt = cw - mlt;
+        int labn = 0, mltn = 0;
+        if (l + 1 < l1) {
+            labn = in ? (lbase + (int64_t)(l + 1) * lstride)[rowl] : 0;
+            mltn = (rep && in) ? (mult + (int64_t)(l + 1) * mw)[pi] : 0;
+            stage(l + 1, nxt);
+        }
+        // the own cluster's (register, tile) in this lane's values, or -1
+        int ownkey = -1;
+        if (po >= 0) {
+            const int i = po & 31;
+            if (((i >> 2) & 1) == h) ownkey = (i & 3) + 4 * (i >> 3) + 16 * (po >> 5);
+        }
+        float m1 = SIL_BIG, m2 = SIL_BIG;
+        // the packing mask in a VGPR (one v_and_or per value: VOP3 takes no literal here)
+        unsigned msk = ~127u;
+        asm volatile("" : "+v"(msk));
+        for (int t = 0; t < nt; ++t) {
+            sil_f16x acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            const int c = t * 32 + j;
+            const _Float16* ar = sA + c * 64;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const sil_h8 ah = *reinterpret_cast<const sil_h8*>(ar + (((s * 4 + h) ^ (c & 7)) << 3));
+                const sil_h8 alo = *reinterpret_cast<const sil_h8*>(ar + (((s * 4 + 2 + h) ^ (c & 7)) << 3));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh[s], acc, 0, 0, 0);
+            }
+            // register r holds centroid t*32 + (r & 3) + 8 (r >> 2) + 4h
+            const float4* af = reinterpret_cast<const float4*>(sAf + t * 32 + 4 * h);
+            const int key0 = 16 * t;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 a4 = af[2 * g];
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = 4 * g + q;
+                    const float a = fmaf(-2.0f, acc[r], av[q]);
+                    float pk = __uint_as_float((__float_as_uint(a) & msk) | (unsigned)(key0 + r));
+                    pk = key0 + r == ownkey ? SIL_BIG : pk;
+                    // med3 for both (fminf would add a canonicalising max per value)
+                    m2 = __builtin_amdgcn_fmed3f(m1, pk, m2);
+                    m1 = __builtin_amdgcn_fmed3f(-SIL_BIG, m1, pk);
+                }
+            }
+        }
+        // merge the lane halves: the smallest, its centroid, the second smallest
+        const unsigned kb = __float_as_uint(m1) & 127u;
+        const int myarg = (int)((kb & 3) + 8 * ((kb >> 2) & 3) + 4 * h + 32 * (kb >> 4));
+        const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
+        const int oarg = __shfl_xor(myarg, 32, 64);
+        const int arg1 = (m1 < o1 || (m1 == o1 && h == 0)) ? myarg : oarg;
+        const float n1 = fminf(m1, o1), n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
+        const bool none = !(n1 < 1.0e37f);  // no other cluster
+        const double mbs = ldexp(sbnd[0], e16), abs2 = ldexp(sbnd[1], 2 * e16);
+        const double E = 0x1p-14 * (xn + mbs) * (xn + mbs) + 0x1p-11 * sqd * (xn + mbs) + 0x1p-14 * abs2 + 8.0;
+        const bool amb = !none && (double)n2 - (double)n1 <= 2.0 * E;
+        auto dsq = [&](int c) {
+            const double* mr = smu + c * DMAX;
+            const int cm = c & QM;
+            double s = sv[c];
+#pragma unroll
+            for (int q = 0; q < DMAX / 2; ++q) {
+                const double2 v = *reinterpret_cast<const double2*>(mr + ((q ^ cm) << 1));
+                const double t0 = xr[2 * q] - v.x, t1 = xr[2 * q + 1] - v.y;
+                s = fma(t0, t0, s);
+                s = fma(t1, t1, s);
+            }
+            return s;
+        };
+        // one exact distance per lane: h = 0 the own cluster, h = 1 the nearest other
+        const int cx = h == 0 ? (po >= 0 ? po : 0) : ((none || amb) ? 0 : arg1);
+        const double dx = dsq(cx);
+        const double S = po >= 0 ? dx : INFINITY;  // (read on h = 0)
+        double O = (h == 1 && !none && !amb) ? dx : INFINITY;
+        if (amb)  // a near tie in the screen: every other centroid exactly, split over the lane pair
+            for (int c = h; c < C; c += 2)
+                if (c != po) O = fmin(O, dsq(c));
+        O = fmin(O, __shfl_xor(O, 32, 64));
+        long long wq = 0;
+        unsigned wn = 0;
+        sil_row_width(S, O, in && h == 0, C, wsc,
+                      (out_width && !rep && in && h == 0) ? out_width + (int64_t)l * m + p : nullptr, wq, wn, wt);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            wq += __shfl_xor(wq, o, 64);
+            wn += __shfl_xor(wn, o, 64);
+        }
+        if (lane == 0) {
+            wsum[(int64_t)(lq + l) * nbw + 4 * tb + wave] = (unsigned long long)wq;
+            wcnt[(int64_t)(lq + l) * nbw + 4 * tb + wave] = (unsigned long long)wn;
+        }
+        lab = labn;
+        mlt = mltn;
+    };
+    for (int l = l0; l < l1; l += 2) {
+        labeling(l, buf0, buf1);
+        if (l + 1 < l1) labeling(l + 1, buf1, buf0);
+    }
+}
+
 // One block per labeling: the cluster count and smallest size from the
 // counts, and the mean width from the per-block fixed-point partials.
 __global__ __launch_bounds__(256) void sil_final(int64_t m, int L, int cmax, int nbw,
@@ -744,7 +1099,7 @@ __global__ __launch_bounds__(256) void sil_final(int64_t m, int L, int cmax, int
                                                  const unsigned long long* __restrict__ wsum,
                                                  const unsigned long long* __restrict__ wcnt,
                                                  double* __restrict__ out_mean, int32_t* __restrict__ out_nclust,
-                                                 int32_t* __restrict__ out_minsize) {
+                                                 int32_t* __restrict__ out_minsize, SilSegs sgs) {
     __shared__ unsigned long long rq[4], rn[4];
     __shared__ int rc[4];
     __shared__ long long rmin[4];
@@ -781,9 +1136,17 @@ __global__ __launch_bounds__(256) void sil_final(int64_t m, int L, int cmax, int
         np = rc[0] + rc[1] + rc[2] + rc[3];
         mn = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
         const double inv_wsc = ldexp(1.0, -scale_exp((double)m));
-        if (out_mean) out_mean[l] = n ? ((double)(long long)q * inv_wsc) / (double)n : NAN;
-        if (out_nclust) out_nclust[l] = np;
-        if (out_minsize) out_minsize[l] = (int32_t)(mn == LLONG_MAX ? 0 : mn);
+        int lo = l;  // (blockIdx.x: the virtual labeling q L + lo of segment q)
+        if (sgs.nseg) {
+            const int qs = l / L;
+            lo = l - qs * L;
+            out_mean = sgs.mean[qs];
+            out_nclust = sgs.ncl[qs];
+            out_minsize = sgs.mns[qs];
+        }
+        if (out_mean) out_mean[lo] = n ? ((double)(long long)q * inv_wsc) / (double)n : NAN;
+        if (out_nclust) out_nclust[lo] = np;
+        if (out_minsize) out_minsize[lo] = (int32_t)(mn == LLONG_MAX ? 0 : mn);
     }
 }
 
@@ -793,9 +1156,12 @@ template <int DMAX>
 constexpr int sil_width_rows() {
     return 4 * sil_rt<DMAX>() * 16;
 }
+// (d <= 32: sil_width16's 4 waves x 32 representatives per block; the round-4
+// kernel, kept for d > 32 and cmax past sil_width16's stage, takes 256 rows
+// per block, so it uses the first half of the partials)
 static int sil_width_blocks(int64_t m, int d) {
-    const int rb = d <= 16 ? sil_width_rows<16>() : (d <= 32 ? sil_width_rows<32>() : sil_width_rows<64>());
-    return 4 * (int)ccg_cdiv(m, rb);
+    if (d <= 32) return 4 * (int)ccg_cdiv(m, SIL_WT / 2);
+    return 4 * (int)ccg_cdiv(m, sil_width_rows<64>());
 }
 
 // ---------------------------------------------- distinct-cell widths --
@@ -846,14 +1212,16 @@ __global__ void sil_rep_kernel(const int32_t* __restrict__ cell, int64_t m, cons
 // cnt - dis) and the row joins the exception list (l << 32 | row).
 __global__ void sil_mult_kernel(int64_t m, int L, const int32_t* __restrict__ labels,
                                 const int64_t* __restrict__ scan, const int3* __restrict__ nonrep, int64_t mw,
-                                int* __restrict__ dis, unsigned long long* __restrict__ exc, int* __restrict__ nexc) {
+                                int* __restrict__ dis, unsigned long long* __restrict__ exc, int* __restrict__ nexc,
+                                SilSegs sgs) {
     const int64_t nn = m - scan[m];
     for (int l = blockIdx.y; l < L; l += gridDim.y) {
-        const int32_t* lab = labels + (int64_t)l * m;
         for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nn; j += (int64_t)gridDim.x * blockDim.x) {
             const int3 e = nonrep[j];
             const int r = e.x, rp = e.y;
-            if (lab[r] != lab[rp]) {
+            // (a row and its representative are in one segment: the cell ids are per segment)
+            const int q = sgs.nseg ? sil_seg_row(sgs.off, sgs.nseg, r) : 0;
+            if (sil_label(labels, m, sgs, q, l, r) != sil_label(labels, m, sgs, q, l, rp)) {
                 atomicAdd(&dis[(int64_t)l * mw + e.z], 1);
                 const int e = atomicAdd(nexc, 1);
                 exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
@@ -863,66 +1231,95 @@ __global__ void sil_mult_kernel(int64_t m, int L, const int32_t* __restrict__ la
 }
 
 // One thread per exception row: its width against labeling l's centroids
-// (fp64, the same D^2 = |x|^2 + (|mu|^2 + v) - 2 x.mu), added to the
-// labeling's first width partial (integer atomics: order-independent).
+// (fp64, D^2 = sum_k (x_k - mu_k)^2 + v_c as sil_width16 takes it), added
+// to the labeling's first width partial (integer atomics: order-independent).
 template <int DMAX>
 __global__ void sil_width_exc(const double* __restrict__ x, int64_t m, int d, const int32_t* __restrict__ labels,
-                              int cmax, const int* __restrict__ npres, const int* __restrict__ codes,
+                              int L, int cmax, const int* __restrict__ npres, const int* __restrict__ codes,
                               const double* __restrict__ muc, const double* __restrict__ auxc,
                               const unsigned long long* __restrict__ exc, const int* __restrict__ nexc, int nbw,
-                              unsigned long long* __restrict__ wsum, unsigned long long* __restrict__ wcnt) {
+                              unsigned long long* __restrict__ wsum, unsigned long long* __restrict__ wcnt,
+                              SilSegs sgs) {
     const int ne = *nexc;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
     const int l = (int)(exc[e] >> 32);
     const int64_t r = (int64_t)(exc[e] & 0xffffffffull);
-    const int lab = labels[(int64_t)l * m + r];
+    const int q = sgs.nseg ? sil_seg_row(sgs.off, sgs.nseg, r) : 0;
+    const int lab = sil_label(labels, m, sgs, q, l, r);
+    const int64_t lv = (int64_t)q * L + l;
     double xr[DMAX];
-    double xx = 0.0;
 #pragma unroll
-    for (int k = 0; k < DMAX; ++k) {
-        xr[k] = k < d ? x[r * d + k] : 0.0;
-        xx = fma(xr[k], xr[k], xx);
-    }
-    const int np = npres[l];
+    for (int k = 0; k < DMAX; ++k) xr[k] = k < d ? x[r * d + k] : 0.0;
+    const int np = npres[lv];
     double self = INFINITY, oth = INFINITY;
     for (int p = 0; p < np; ++p) {
-        const double* mp = muc + ((int64_t)l * cmax + p) * DMAX;
-        double dot = 0.0;
+        const double* mp = muc + (lv * cmax + p) * DMAX;
+        double s2 = fmax(auxc[2 * (lv * cmax + p) + 1], 0.0);
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) dot = fma(xr[k], mp[sil_mfma_pos<DMAX>(k)], dot);
-        const double tv = fma(-2.0, dot, auxc[2 * ((int64_t)l * cmax + p)] + auxc[2 * ((int64_t)l * cmax + p) + 1]);
-        if (codes[(int64_t)l * cmax + p] == lab) self = tv;
-        else oth = fmin(oth, tv);
+        for (int k = 0; k < DMAX; ++k) {
+            const double t = xr[k] - mp[sil_mfma_pos<DMAX>(k)];
+            s2 = fma(t, t, s2);
+        }
+        if (codes[lv * cmax + p] == lab) self = s2;
+        else oth = fmin(oth, s2);
     }
     long long wq = 0;
     unsigned wn = 0;
-    sil_row_width(fmax(xx + self, 0.0), fmax(xx + oth, 0.0), true, np, ldexp(1.0, scale_exp((double)m)), nullptr,
-                  wq, wn);
+    sil_row_width(self, oth, true, np, ldexp(1.0, scale_exp((double)m)), nullptr, wq, wn);
     if (wn) {
-        atomicAdd(&wsum[(int64_t)l * nbw], (unsigned long long)wq);  // the first partial of the labeling
-        atomicAdd(&wcnt[(int64_t)l * nbw], 1ull);
+        atomicAdd(&wsum[lv * nbw], (unsigned long long)wq);  // the first partial of the labeling
+        atomicAdd(&wcnt[lv * nbw], 1ull);
     }
     }
 }
 
+// Positions per tiled-sums block (the largest whose LDS fits the CU), or
+// 0: the unsorted sil_centroid path.
+static int sil_tile_T(int d, int cmax) {
+    for (int T = SIL_ST; T >= 256; T >>= 1)
+        if (sil_tile_lds(T, d, cmax) <= SIL_LDS_CU) return T;
+    return 0;
+}
+
+// The launch set after max|x| (and, for the distinct-cell forms, the
+// representative tables).  Segments (sgs.nseg > 0, cells form only) run the
+// tiled sums and sil_width16 over every segment at once: the sums' tiles and
+// the width tiles are laid out per segment (ts_tiles, tw_tiles blocks), the
+// per-labeling tables over Lv = nseg L virtual labelings.
 template <int DMAX>
 static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels, int L, int cmax,
                        unsigned* maxabs, unsigned long long* gsum, unsigned long long* gsum2, unsigned long long* gcnt,
                        unsigned long long* gvar, unsigned long long* wsum, unsigned long long* wcnt,
-                       int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc, long long* q,
-                       double* out_width, hipStream_t st, const int* rep = nullptr, const int* mult = nullptr,
-                       const int* cnt = nullptr, int64_t mw = 0, const unsigned long long* exc = nullptr,
-                       const int* nexc = nullptr, const int64_t* nrep = nullptr) {
-    if (q) {
-        // sorted segments: S1, S2 and counts in one pass, v_c in sil_mu
-        sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q, q + m * DMAX);
-        dim3 grid((unsigned)ccg_cdiv(m, SIL_SORT_ROWS), (unsigned)L);
-        const bool reps = rep && !SIL_SUMS_ROWS;
-        sil_sums_sorted<DMAX><<<grid, SIL_T, sil_sorted_lds<DMAX>(cmax), st>>>(
-            m, d, labels, cmax, q, q + m * DMAX, gsum, gsum2, gcnt, reps ? rep : nullptr, mult, cnt, mw, nrep);
-        if (reps)
-            sil_sums_exc<DMAX><<<64, 256, 0, st>>>(m, d, labels, cmax, q, q + m * DMAX, exc, nexc, gsum, gsum2, gcnt);
-        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
+                       int* npres, int* codes, int* pos, double* mu, double* muc, double* auxc, void* q,
+                       unsigned char* img, double* out_width, int nbw, hipStream_t st, const int* rep = nullptr,
+                       const int* mult = nullptr, const int* cnt = nullptr, int64_t mw = 0,
+                       const unsigned long long* exc = nullptr, const int* nexc = nullptr,
+                       const int64_t* nrep = nullptr, const int64_t* scan = nullptr, SilSegs sgs = SilSegs{},
+                       int ts_tiles = 0, int tw_tiles = 0) {
+    const bool seg = sgs.nseg > 0;
+    const int Lv = seg ? sgs.nseg * L : L;  // virtual labelings
+    const int T = q ? sil_tile_T(d, cmax) : 0;
+    if (T) {
+        // tiled sums: S1, S2 and counts in one pass, v_c in sil_mu
+        int* q1 = (int*)q;
+        long long* q2 = (long long*)(q1 + m * DMAX);
+        sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q1, q2);
+        // about one block per CU: the representatives are ~0.64 of the rows of a bootstrap
+        const int64_t gx = seg ? ts_tiles : ccg_cdiv(m, T);
+        const int64_t tiles = seg ? (gx * 16 + 24) / 25 : ccg_cdiv(rep ? (m * 16 + 24) / 25 : m, T);
+        const int groups = (int)std::max<int64_t>(1, std::min<int64_t>(L, 256 / std::max<int64_t>(tiles, 1)));
+        const int sg = (int)ccg_cdiv(L, groups);
+        dim3 grid((unsigned)gx, (unsigned)ccg_cdiv(L, sg));
+        const size_t lds = sil_tile_lds(T, d, cmax);
+        if (seg)
+            sil_sums_tile<DMAX, true><<<grid, SIL_ST, lds, st>>>(m, d, T, sg, labels, L, cmax, q1, q2, gsum, gsum2,
+                                                                 gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
+        else
+            sil_sums_tile<DMAX, false><<<grid, SIL_ST, lds, st>>>(m, d, T, sg, labels, L, cmax, q1, q2, gsum, gsum2,
+                                                                  gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
+        if (rep)
+            sil_sums_exc<DMAX><<<64, 256, 0, st>>>(m, d, labels, L, cmax, q1, q2, exc, nexc, gsum, gsum2, gcnt, sgs);
+        sil_mu<DMAX><<<Lv, SIL_T, 0, st>>>(m, d, cmax, 1, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
     } else {
         dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
         const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
@@ -931,7 +1328,8 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
             sil_centroid<DMAX, true><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
         else
             sil_centroid<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
-        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, nullptr, gcnt, npres, codes, pos, mu, muc, auxc);
+        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, 0, maxabs, gsum, nullptr, gcnt, npres, codes, pos, mu, muc,
+                                          auxc);
         if (lds2 <= SIL_LDS_CAP)
             sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
         else
@@ -942,17 +1340,44 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
     // the width partials are laid out for m rows (nbw blocks per labeling);
     // the representative grid uses its first blocks
     const int64_t nrows = rep ? mw : m;
+    bool w16 = false;
+    if constexpr (DMAX <= 32) w16 = cmax <= SIL_WCMAX && 2 * sil_img_stride(cmax, DMAX) <= SIL_W16_LDS && img;
+    if (w16) {
+        if constexpr (DMAX <= 32) {
+        const size_t imgs = sil_img_stride(cmax, DMAX);
+        sil_w16_prep<DMAX><<<Lv, 256, 0, st>>>(cmax, maxabs, npres, codes, pos, mu, auxc, img, imgs);
+        dim3 g16((unsigned)(seg ? tw_tiles : ccg_cdiv(nrows, SIL_WT / 2)), (unsigned)ccg_cdiv(L, SIL_WLG));
+        const double wsc = ldexp(1.0, scale_exp((double)m)), sqd = sqrt((double)d);
+        double* ow = rep ? nullptr : out_width;
+#define SIL_W16(B_)                                                                                                  \
+        if (seg)                                                                                                     \
+            sil_width16<DMAX, B_, true><<<g16, SIL_WT, 0, st>>>(x, m, d, labels, L, cmax, maxabs, npres, img, imgs,  \
+                                                                wsum, wcnt, ow, rep, mult, cnt, mw, nbw, nrep, wsc,  \
+                                                                sqd, scan, sgs);                                     \
+        else                                                                                                         \
+            sil_width16<DMAX, B_, false><<<g16, SIL_WT, 0, st>>>(x, m, d, labels, L, cmax, maxabs, npres, img, imgs, \
+                                                                 wsum, wcnt, ow, rep, mult, cnt, mw, nbw, nrep, wsc, \
+                                                                 sqd, scan, sgs)
+        if (imgs <= 14336) { SIL_W16(14336); }
+        else if (imgs <= 26624) { SIL_W16(26624); }
+        else { SIL_W16(40960); }
+#undef SIL_W16
+        if (rep)
+            sil_width_exc<DMAX><<<64, 256, 0, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, exc, nexc, nbw,
+                                                    wsum, wcnt, sgs);
+        }
+        return;
+    }
     dim3 grid2((unsigned)ccg_cdiv(nrows, sil_width_rows<DMAX>()), (unsigned)ccg_cdiv(L, SIL_LG));
     // the stage holds a whole group of SIL_LG labelings when it can
     const int CH = (int)std::min<int64_t>(sil_chunk<DMAX>(), (int64_t)SIL_LG * (((int64_t)cmax + 15) / 16 * 16));
     const size_t lds5 = (size_t)CH * sil_sp<DMAX>() * 8 + (size_t)CH * 8 + (size_t)CH * 4;
-    const int nbw = 4 * (int)ccg_cdiv(m, sil_width_rows<DMAX>());
     if (rep) {
         // partials of blocks past the representative grid stay 0 (zeroed with the buffer)
         sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
                                                 nullptr, CH, rep, mult, cnt, mw, nbw, nrep);
-        sil_width_exc<DMAX><<<64, 256, 0, st>>>(
-            x, m, d, labels, cmax, npres, codes, muc, auxc, exc, nexc, nbw, wsum, wcnt);
+        sil_width_exc<DMAX><<<64, 256, 0, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, exc, nexc, nbw,
+                                                wsum, wcnt, sgs);
     } else {
         sil_width<DMAX><<<grid2, SIL_T, lds5, st>>>(x, m, d, labels, L, cmax, npres, codes, muc, auxc, wsum, wcnt,
                                                 out_width, CH, nullptr, nullptr, nullptr, 0, nbw, nullptr);
@@ -990,69 +1415,71 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     int* npres = (int*)(auxc + 2 * (size_t)L * cmax);
     int* codes = npres + L;
     int* pos = codes + (size_t)L * cmax;
-    const size_t lds_sorted = dmax == 16 ? sil_sorted_lds<16>(cmax)
-                                         : (dmax == 32 ? sil_sorted_lds<32>(cmax) : sil_sorted_lds<64>(cmax));
-    long long* q = nullptr;  // fixed-point rows of the sorted-segment path (cmax small enough for its LDS)
-    if (lds_sorted <= SIL_LDS_CAP) {
-        q = (long long*)ccg_ws(ctx, WS_SIL_Q, 2 * sizeof(long long) * (size_t)m * dmax);
+    void* q = nullptr;  // fixed-point rows of the tiled sorted-segment path (cmax small enough for its LDS)
+    if (sil_tile_T(d, cmax)) {
+        q = ccg_ws(ctx, WS_SIL_Q, sizeof(int) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
         if (!q) return CCG_ENOMEM;
+    }
+    unsigned char* img = nullptr;  // LDS images of the fp16-screen widths (d <= 32, cmax small enough)
+    if (dmax <= 32 && cmax <= SIL_WCMAX && 2 * sil_img_stride(cmax, dmax) <= SIL_W16_LDS) {
+        img = (unsigned char*)ccg_ws(ctx, WS_SIL_IMG, (size_t)L * sil_img_stride(cmax, dmax));
+        if (!img) return CCG_ENOMEM;
     }
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
     sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
     if (d <= 16)
         sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
-                        out_width, st);
+                        img, out_width, nbw, st);
     else if (d <= 32)
         sil_launch<32>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
-                        out_width, st);
+                        img, out_width, nbw, st);
     else
         sil_launch<64>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
-                        out_width, st);
-    sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean,
-                                                       out_nclust, out_minsize);
+                        img, out_width, nbw, st);
+    sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean, out_nclust, out_minsize, SilSegs{});
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
 
-extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels,
-                                        int L, int cmax, const int32_t* cell, int64_t ncell, double* out_mean,
-                                        int32_t* out_nclust, int32_t* out_minsize, void* stream) {
-    CCG_REQUIRE(ctx && x && labels && cell, "ccg_silhouette_cells_dev: NULL argument");
-    CCG_REQUIRE(m >= 1 && m < (1LL << 31) && d >= 1 && d <= 64 && L >= 1 && (int64_t)L * m < (1LL << 31),
-                "ccg_silhouette_cells_dev: bad sizes m=%lld d=%d L=%d", (long long)m, d, L);
-    CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_cells_dev: cmax=%d must be in [1, 2^24]", cmax);
-    CCG_REQUIRE(ncell >= 1 && ncell < (1LL << 31), "ccg_silhouette_cells_dev: bad ncell");
-    hipStream_t st = ccg_pick_stream(ctx, stream);
+// The distinct-cell launch set over m rows (one matrix, or a batch of
+// segments: sgs.nseg > 0, per-labeling tables over nseg L virtual
+// labelings, nbw width partials per virtual labeling).
+static int sil_cells_run(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels, int L, int cmax,
+                         const int32_t* cell, int64_t ncell, double* out_mean, int32_t* out_nclust,
+                         int32_t* out_minsize, hipStream_t st, SilSegs sgs, int ts_tiles, int tw_tiles, int nbw) {
+    const int64_t Lv = sgs.nseg ? (int64_t)sgs.nseg * L : L;
     const int64_t nacc = (int64_t)(cmax + 1) * d;
-    const int nbw = sil_width_blocks(m, d);
-    const int64_t words = 2 * (int64_t)L * nacc + 2 * (int64_t)L * (cmax + 1) + 2 * (int64_t)L * nbw + 8;
+    const int64_t words = 2 * Lv * nacc + 2 * Lv * (cmax + 1) + 2 * Lv * nbw + 8;
     unsigned long long* buf = (unsigned long long*)ccg_ws(ctx, WS_SIL_A, sizeof(unsigned long long) * words);
     if (!buf) return CCG_ENOMEM;
     unsigned long long* gsum = buf;
-    unsigned long long* gsum2 = gsum + (int64_t)L * nacc;
-    unsigned long long* gcnt = gsum2 + (int64_t)L * nacc;
-    unsigned long long* gvar = gcnt + (int64_t)L * (cmax + 1);
-    unsigned long long* wsum = gvar + (int64_t)L * (cmax + 1);
-    unsigned long long* wcnt = wsum + (int64_t)L * nbw;
-    unsigned* maxabs = (unsigned*)(wcnt + (int64_t)L * nbw);
+    unsigned long long* gsum2 = gsum + Lv * nacc;
+    unsigned long long* gcnt = gsum2 + Lv * nacc;
+    unsigned long long* gvar = gcnt + Lv * (cmax + 1);
+    unsigned long long* wsum = gvar + Lv * (cmax + 1);
+    unsigned long long* wcnt = wsum + Lv * nbw;
+    unsigned* maxabs = (unsigned*)(wcnt + Lv * nbw);
     const int dmax = d <= 16 ? 16 : (d <= 32 ? 32 : 64);
-    const size_t mu_words = (size_t)L * (cmax + 1) * dmax + (size_t)L * cmax * dmax + 2 * (size_t)L * cmax;
-    const size_t tab_ints = (size_t)L * cmax + (size_t)L * (cmax + 1) + L + 8;
+    const size_t mu_words = (size_t)Lv * (cmax + 1) * dmax + (size_t)Lv * cmax * dmax + 2 * (size_t)Lv * cmax;
+    const size_t tab_ints = (size_t)Lv * cmax + (size_t)Lv * (cmax + 1) + Lv + 8;
     double* mu = (double*)ccg_ws(ctx, WS_SIL_B, sizeof(double) * mu_words + sizeof(int) * tab_ints);
     if (!mu) return CCG_ENOMEM;
-    double* muc = mu + (size_t)L * (cmax + 1) * dmax;
-    double* auxc = muc + (size_t)L * cmax * dmax;
-    int* npres = (int*)(auxc + 2 * (size_t)L * cmax);
-    int* codes = npres + L;
-    int* pos = codes + (size_t)L * cmax;
-    const size_t lds_sorted = dmax == 16 ? sil_sorted_lds<16>(cmax)
-                                         : (dmax == 32 ? sil_sorted_lds<32>(cmax) : sil_sorted_lds<64>(cmax));
-    long long* q = nullptr;
-    if (lds_sorted <= SIL_LDS_CAP) {
-        q = (long long*)ccg_ws(ctx, WS_SIL_Q, 2 * sizeof(long long) * (size_t)m * dmax);
+    double* muc = mu + (size_t)Lv * (cmax + 1) * dmax;
+    double* auxc = muc + (size_t)Lv * cmax * dmax;
+    int* npres = (int*)(auxc + 2 * (size_t)Lv * cmax);
+    int* codes = npres + Lv;
+    int* pos = codes + (size_t)Lv * cmax;
+    void* q = nullptr;  // fixed-point rows of the tiled sums (cmax small enough for its LDS)
+    if (sil_tile_T(d, cmax)) {
+        q = ccg_ws(ctx, WS_SIL_Q, sizeof(int) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
         if (!q) return CCG_ENOMEM;
+    }
+    unsigned char* img = nullptr;  // LDS images of the fp16-screen widths (d <= 32, cmax small enough)
+    if (dmax <= 32 && cmax <= SIL_WCMAX && 2 * sil_img_stride(cmax, dmax) <= SIL_W16_LDS) {
+        img = (unsigned char*)ccg_ws(ctx, WS_SIL_IMG, (size_t)Lv * sil_img_stride(cmax, dmax));
+        if (!img) return CCG_ENOMEM;
     }
     // distinct-cell tables: first row per cell, representative list, rows per
     // cell, the other rows, per-labeling disagreements, exceptions
@@ -1083,19 +1510,122 @@ extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m
     // mw = the number of representatives (the distinct cells): device-side
     // only, so the width grid covers m positions and the weights' stride is m
     dim3 gx((unsigned)std::min<int64_t>(ccg_cdiv(m, 256), 32), (unsigned)std::min(L, 65535));
-    sil_mult_kernel<<<gx, 256, 0, st>>>(m, L, labels, scan, nonrep, m, mult, exc, nexc);
+    sil_mult_kernel<<<gx, 256, 0, st>>>(m, L, labels, scan, nonrep, m, mult, exc, nexc, sgs);
     sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
 #define SIL_CELLS(DM_)                                                                                              \
     sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
-                    auxc, q, nullptr, st, rep, mult, cnt, m, exc, nexc, scan + m)
+                    auxc, q, img, nullptr, nbw, st, rep, mult, cnt, m, exc, nexc, scan + m, scan, sgs, ts_tiles,     \
+                    tw_tiles)
     if (d <= 16) SIL_CELLS(16);
     else if (d <= 32) SIL_CELLS(32);
     else SIL_CELLS(64);
 #undef SIL_CELLS
-    sil_final<<<L, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean, out_nclust, out_minsize);
+    sil_final<<<(unsigned)Lv, 256, 0, st>>>(m, L, cmax, nbw, gcnt, wsum, wcnt, out_mean, out_nclust, out_minsize, sgs);
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
+}
+
+extern "C" int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels,
+                                        int L, int cmax, const int32_t* cell, int64_t ncell, double* out_mean,
+                                        int32_t* out_nclust, int32_t* out_minsize, void* stream) {
+    CCG_REQUIRE(ctx && x && labels && cell, "ccg_silhouette_cells_dev: NULL argument");
+    CCG_REQUIRE(m >= 1 && m < (1LL << 31) && d >= 1 && d <= 64 && L >= 1 && (int64_t)L * m < (1LL << 31),
+                "ccg_silhouette_cells_dev: bad sizes m=%lld d=%d L=%d", (long long)m, d, L);
+    CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_cells_dev: cmax=%d must be in [1, 2^24]", cmax);
+    CCG_REQUIRE(ncell >= 1 && ncell < (1LL << 31), "ccg_silhouette_cells_dev: bad ncell");
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    return sil_cells_run(ctx, x, m, d, labels, L, cmax, cell, ncell, out_mean, out_nclust, out_minsize, st, SilSegs{},
+                         0, 0, sil_width_blocks(m, d));
+}
+
+// Segments (R/consensusClust.R:562-566, :664: every subcluster of an
+// iterate=TRUE level scores its bootstraps' clusterings): one launch set for
+// a batch of segments whose rows are concatenated in x.  The sums and width
+// kernels tile each segment's representatives separately; the per-labeling
+// tables hold nseg x L virtual labelings.  Outside the tiled sums /
+// sil_width16 envelope (d > 32 or a large cmax) the segments run one call
+// each.
+extern "C" int ccg_silhouette_segments_dev(ccg_ctx* ctx, const double* x, int d, int nseg, const int64_t* seg_off,
+                                           const int32_t* const* labels, int L, int cmax, const int32_t* cell,
+                                           int64_t ncell, double* const* out_mean, int32_t* const* out_nclust,
+                                           int32_t* const* out_minsize, void* stream) {
+    CCG_REQUIRE(ctx && x && seg_off && labels && cell, "ccg_silhouette_segments_dev: NULL argument");
+    CCG_REQUIRE(nseg >= 1 && d >= 1 && d <= 64 && L >= 1, "ccg_silhouette_segments_dev: bad sizes nseg=%d d=%d L=%d",
+                nseg, d, L);
+    CCG_REQUIRE(cmax >= 1 && cmax <= (1 << 24), "ccg_silhouette_segments_dev: cmax=%d must be in [1, 2^24]", cmax);
+    CCG_REQUIRE(ncell >= 1 && ncell < (1LL << 31), "ccg_silhouette_segments_dev: bad ncell");
+    CCG_REQUIRE(seg_off[0] == 0, "ccg_silhouette_segments_dev: seg_off[0] must be 0");
+    int64_t mq_max = 0;
+    for (int s = 0; s < nseg; ++s) {
+        CCG_REQUIRE(seg_off[s + 1] > seg_off[s], "ccg_silhouette_segments_dev: segment %d is empty", s);
+        CCG_REQUIRE(labels[s], "ccg_silhouette_segments_dev: labels of segment %d are NULL", s);
+        mq_max = std::max(mq_max, seg_off[s + 1] - seg_off[s]);
+    }
+    const int64_t m = seg_off[nseg];
+    CCG_REQUIRE(m < (1LL << 31) && (int64_t)L * m < (1LL << 31) && (int64_t)nseg * L < (1LL << 31),
+                "ccg_silhouette_segments_dev: %lld rows x %d labelings too many", (long long)m, L);
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    const int dmax = d <= 16 ? 16 : (d <= 32 ? 32 : 64);
+    const int T = sil_tile_T(d, cmax);
+    const bool one_set = dmax <= 32 && T && cmax <= SIL_WCMAX && 2 * sil_img_stride(cmax, dmax) <= SIL_W16_LDS;
+    if (!one_set) {
+        for (int s = 0; s < nseg; ++s) {
+            const int64_t o = seg_off[s];
+            const int rc = ccg_silhouette_cells_dev(ctx, x + o * d, seg_off[s + 1] - o, d, labels[s], L, cmax, cell + o,
+                                                    ncell, out_mean ? out_mean[s] : nullptr,
+                                                    out_nclust ? out_nclust[s] : nullptr,
+                                                    out_minsize ? out_minsize[s] : nullptr, st);
+            if (rc) return rc;
+        }
+        return CCG_OK;
+    }
+    // the segment table: offsets, tile starts, label and output pointers
+    const size_t n1 = (size_t)nseg + 1;
+    const size_t bytes = 8 * n1 + 8 * n1 + 8 * (size_t)nseg * 4;
+    std::vector<unsigned char> hb(bytes);
+    int64_t* hoff = (int64_t*)hb.data();
+    int* hts = (int*)(hoff + n1);
+    int* htw = hts + n1;
+    const void** hptr = (const void**)(hts + 2 * n1 + ((2 * n1) & 1));
+    int64_t ts = 0, tw = 0;
+    for (size_t s = 0; s < n1; ++s) {
+        hoff[s] = seg_off[s];
+        hts[s] = (int)ts;
+        htw[s] = (int)tw;
+        if (s < (size_t)nseg) {
+            const int64_t mq = seg_off[s + 1] - seg_off[s];
+            ts += ccg_cdiv(mq, T);
+            tw += ccg_cdiv(mq, SIL_WT / 2);
+        }
+    }
+    CCG_REQUIRE(ts < (1LL << 31) && tw < (1LL << 31), "ccg_silhouette_segments_dev: too many tiles");
+    for (int s = 0; s < nseg; ++s) {
+        hptr[s] = labels[s];
+        hptr[nseg + s] = out_mean ? out_mean[s] : nullptr;
+        hptr[2 * nseg + s] = out_nclust ? out_nclust[s] : nullptr;
+        hptr[3 * nseg + s] = out_minsize ? out_minsize[s] : nullptr;
+    }
+    unsigned char* db = (unsigned char*)ccg_ws(ctx, WS_SIL_SEG, bytes);
+    if (!db) return CCG_ENOMEM;
+    {
+        const int rs = ccg_h2d_staged(ctx, db, hb.data(), bytes, st);  // (hb is freed when this call returns)
+        if (rs) return rs;
+    }
+    const size_t po = (const unsigned char*)hptr - hb.data();
+    SilSegs sgs;
+    sgs.nseg = nseg;
+    sgs.off = (const int64_t*)db;
+    sgs.ts = (const int*)(db + 8 * n1);
+    sgs.tw = sgs.ts + n1;
+    sgs.lab = (const int32_t* const*)(db + po);
+    sgs.mean = (double* const*)(db + po + 8 * (size_t)nseg);
+    sgs.ncl = (int32_t* const*)(db + po + 16 * (size_t)nseg);
+    sgs.mns = (int32_t* const*)(db + po + 24 * (size_t)nseg);
+    // width partials per virtual labeling: 4 per 128-position tile of the largest segment
+    const int nbw = 4 * (int)ccg_cdiv(mq_max, SIL_WT / 2);
+    return sil_cells_run(ctx, x, m, d, nullptr, L, cmax, cell, ncell, nullptr, nullptr, nullptr, st, sgs, (int)ts,
+                         (int)tw, nbw);
 }
 
 extern "C" int ccg_silhouette(ccg_ctx* ctx, const double* x, int64_t m, int d, const int32_t* labels,

@@ -532,6 +532,29 @@ class Engine:
         check(self.lib.ccg_silhouette_cells_dev(self.ctx, _ptr(x), m, d, _ptr(labels), L, cmax, _ptr(cell), ncell,
                                                 _ptr(out_mean), _ptr(out_nclust), _ptr(out_minsize), _stream()))
 
+    def silhouette_segments_t(self, x, seg_off, labels, cmax, cell, ncell, means=None, nclust=None, minsize=None):
+        """ccg_silhouette_segments_dev: one launch set for a batch of segments.
+        x (n, d) device rows of every segment concatenated, seg_off (nseg+1,)
+        host int64 row offsets, labels: nseg device (L, m_s) int32 tensors,
+        cell (n,) int32 cell ids distinct between segments, in [0, ncell);
+        means / nclust / minsize: None or nseg device tensors of L values."""
+        import ctypes
+        n, d = x.shape
+        off = np.ascontiguousarray(seg_off, dtype=np.int64)
+        nseg = off.size - 1
+        L = labels[0].shape[0]
+
+        def arr(ts):
+            if ts is None:
+                return None
+            a = (ctypes.c_void_p * nseg)(*[t.data_ptr() if t is not None else None for t in ts])
+            return a
+        lab = arr(labels)
+        om, onc, oms = arr(means), arr(nclust), arr(minsize)
+        check(self.lib.ccg_silhouette_segments_dev(
+            self.ctx, _ptr(x), d, nseg, off.ctypes.data, lab, L, cmax, _ptr(cell), int(ncell),
+            om, onc, oms, _stream()))
+
     def select_mapback_t(self, mode, labels, boot_idx, N, A, col0, means=None, nclust=None, minsize=None,
                          min_size=0, out_choice=None):
         """A: (B, N) uint8 or uint16 tensor (label width from its dtype)."""

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 5
+#define CCG_ABI_VERSION 6
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -401,6 +401,25 @@ int ccg_silhouette_cells_dev(ccg_ctx* ctx, const double* x, int64_t m, int d,
                              const int32_t* labels, int L, int cmax,
                              const int32_t* cell, int64_t ncell, double* out_mean,
                              int32_t* out_nclust, int32_t* out_minsize, void* stream);
+
+/* A batch of segments in one launch set (an iterate=TRUE level scores every
+ * subcluster's bootstraps, R/consensusClust.R:562-566 and :664): segment s
+ * is rows [seg_off[s], seg_off[s+1]) of x (device, seg_off[nseg] x d,
+ * row-major), labelled by labels[s] (device, L x m_s int32 codes in
+ * [1, cmax]); cell (device, seg_off[nseg] entries in [0, ncell)) names each
+ * row's cell and must differ between rows of different segments (e.g. slot
+ * x ncell_per_slot + cell).  seg_off and the pointer arrays labels,
+ * out_mean, out_nclust, out_minsize (nseg entries each, each entry a device
+ * pointer to L values or NULL; the arrays themselves may be NULL) are host
+ * memory.  Results equal nseg calls of ccg_silhouette_cells_dev (the
+ * fixed-point scales are taken over the whole batch).  Segments must be
+ * non-empty.  Replaces: bluster::approxSilhouette at R/consensusClust.R:664
+ * per (subcluster, bootstrap). */
+int ccg_silhouette_segments_dev(ccg_ctx* ctx, const double* x, int d, int nseg,
+                                const int64_t* seg_off, const int32_t* const* labels,
+                                int L, int cmax, const int32_t* cell, int64_t ncell,
+                                double* const* out_mean, int32_t* const* out_nclust,
+                                int32_t* const* out_minsize, void* stream);
 
 /* Host flavour of ccg_silhouette_cells_dev (all pointers host): what an R
  * getClustAssignments calls with the bootstrap matrix pca[sample(...), ] and

@@ -1,6 +1,6 @@
 /*
  * ccg_r.c -- the .Call glue a consensusClustR maintainer adds to reach
- * libccg.so (include/ccg.h, ABI version 5) from R.  Build with the package:
+ * libccg.so (include/ccg.h, ABI version 6) from R.  Build with the package:
  *   src/Makevars:  PKG_CPPFLAGS = -I$(CCG_HOME)/include
  *                  PKG_LIBS     = -L$(CCG_HOME)/consensusclustr_amd -lccg -Wl,-rpath,$(CCG_HOME)/consensusclustr_amd
  * (R is not installed in the image this repository is built in, so this file

@@ -226,3 +226,43 @@ def test_cfg5_first_bootstrap_silhouettes_per_subcluster_vs_oracle(engine, cfg5)
         for l_, (_, m, C) in enumerate(ref):
             np.testing.assert_allclose(got[l_], m, rtol=1e-5)
             assert nc_[l_].item() == C
+
+
+def test_cfg5_segmented_silhouettes_match_per_segment_calls(engine, cfg5):
+    """The bench's ONE ccg_silhouette_segments_dev over the first batch's 160
+    segments equals 160 ccg_silhouette_cells_dev calls (cluster counts and
+    smallest sizes exactly, means within 1e-8: the batch's fixed-point scale
+    is taken over every segment), and the per-segment calls are the ones the
+    oracle test above pins."""
+    import torch
+    import bench
+    c = cfg5
+    inp = c["inp"]
+    dev = c["rows"].device
+    L = 60
+    segs, off = c["segs"], c["off"]
+    Nof = inp["Nof"]
+    labels = [bench.synth_labels(torch, inp["popc"][Nof[cc]:Nof[cc + 1]], inp["boots_t"][cc][j], L, dev, 1000 + j,
+                                 chi=20) for cc, j in segs]
+    cmax = max(int(lb.max().item()) for lb in labels)
+    plan = (segs, off, None, c["idx"])
+    keys = bench.cfg5_sil_keys(torch, inp, plan, 0)
+    nseg = len(segs)
+    means = [torch.empty(L, dtype=torch.float64, device=dev) for _ in range(nseg)]
+    ncl = [torch.empty(L, dtype=torch.int32, device=dev) for _ in range(nseg)]
+    mns = [torch.empty(L, dtype=torch.int32, device=dev) for _ in range(nseg)]
+    slots = 1 + max(j for _, j in segs)
+    engine.silhouette_segments_t(c["rows"], off, labels, cmax, keys, slots * inp["cells"].shape[0], means, ncl, mns)
+    bad = []
+    for q, (cc, j) in enumerate(segs):
+        a, b = int(off[q]), int(off[q + 1])
+        m_ = torch.empty(L, dtype=torch.float64, device=dev)
+        nc_ = torch.empty(L, dtype=torch.int32, device=dev)
+        ms_ = torch.empty(L, dtype=torch.int32, device=dev)
+        engine.silhouette_cells_t(c["rows"][a:b], labels[q], cmax, inp["boots_t"][cc][j], inp["sizes"][cc], m_, nc_,
+                                  ms_)
+        if not (torch.equal(nc_, ncl[q]) and torch.equal(ms_, mns[q])
+                and torch.allclose(means[q], m_, rtol=1e-8, atol=1e-12, equal_nan=True)):
+            bad.append(q)
+    torch.cuda.synchronize()
+    assert not bad, bad[:10]
