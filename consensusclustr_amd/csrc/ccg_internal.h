@@ -62,7 +62,6 @@ enum ccg_ws_slot {
     WS_KB_C,         // distinct-cell kNN: per-cell counts / offsets / cursors / cell -> distinct id (counting grouping)
     WS_SIL_IMG,      // silhouette: per-labeling LDS images of the fp16-screen width kernel
     WS_SIL_SEG,      // silhouette segments: offsets, tile starts, label and output pointers
-    WS_FX_Q,         // kNN exact search of failed rows (fp16 path): their row images, tests and ids
     WS_NSLOTS
 };
 

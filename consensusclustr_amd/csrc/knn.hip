@@ -1243,153 +1243,6 @@ __global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restri
     }
 }
 
-// The same candidate lists on the fp16 matrix core (round 5; the table
-// path, where max|x| of the rows is known).  Rows scaled by 2^e (max|x|
-// 2^e < 2^12) and split into fp16 hi + lo (knn_split16); x.y ~ hi.hi +
-// hi.lo + lo.hi on v_mfma_f32_32x32x16_f16 with A = 32 failed rows (LDS)
-// and B = 32 references (registers), so a lane (h, j) gets 16 failed rows
-// against reference j.  The error of the product is below
-//   E = 2^-17.2 |x'||y'| + 2^-13.9 sqrt(d) (|x'| + |y'|)
-// at KSTEPS <= 2 (split residuals 2^-22 relative + 2^-14 absolute per
-// factor, fp32 accumulation of 48 KSTEPS exact products; 2^-16.3 |x'||y'| at
-// KSTEPS = 4), and |x'||y'| <= (nx' + ny') / 2; the test takes the kNN
-// screen's certification budget (1024 fp32 ulps of (|x'| + |y'|)^2 <=
-// 2^-13 (nx' + ny')) with a factor 2 to spare, so a pair within the radius
-// (nx' + ny' - 2 x'.y' <= tau') passes
-//   2 x'.y'(mfma) >= A_x + B_y,
-//   A_x = (1 - 2^-12) nx' - (1 + 2^-20) tau' - 2^-11 sqrt(d) |x'| - 8,
-//   B_y = (1 - 2^-12) ny' - 2^-11 sqrt(d) |y'|
-// (both rounded down to fp32; the slack past 2E covers the fp32 sum and
-// the fp64 exact test's own rounding): the
-// candidates are a superset of the exact ones, and knn_fx_select_kernel
-// keeps exactly the pairs whose fp64 d2 is within the radius.  Per pair:
-// 3 MACs of 16 x KSTEPS dims on the matrix core and one fp32 compare,
-// against the fp32 scan's 16 KSTEPS packed FMAs on the vector unit.
-#define KNN_FXQ 128  // failed rows per staged group
-template <int KSTEPS>
-__global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __restrict__ rows, int d,
-                                                            const int* __restrict__ fail_list,
-                                                            const int* __restrict__ fail_count,
-                                                            const double* __restrict__ fail_tau,
-                                                            const unsigned* __restrict__ maxabs_bits,
-                                                            uint4* __restrict__ qimg, float* __restrict__ qa,
-                                                            int* __restrict__ qid) {
-    constexpr int NCH = 4 * KSTEPS;  // 16-byte chunks (s, hi/lo, h) per row image, swizzled by row & (NCH - 1)
-    const int nf = min(*fail_count, KNN_FX_ROWS);
-    const int nfp = (nf + KNN_FXQ - 1) / KNN_FXQ * KNN_FXQ;
-    const int e = knn_scale_exp(maxabs_bits);
-    const double sqd = sqrt((double)d);
-    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfp; f += gridDim.x * blockDim.x) {
-        const bool valid = f < nf;
-        const int q = valid ? fail_list[f] : -1;
-        double t = valid ? fail_tau[f] : -1.0;
-        if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
-        _Float16 hv[NCH * 8];
-        double nx = 0.0;
-#pragma unroll
-        for (int k = 0; k < KSTEPS * 16; ++k) {
-            const double xs = (valid && k < d) ? ldexp(rows[(int64_t)q * d + k], e) : 0.0;
-            nx = fma(xs, xs, nx);
-            _Float16 hi, lo;
-            knn_split16(xs, hi, lo);
-            const int s = k >> 4, h = (k >> 3) & 1, i = k & 7;
-            hv[(s * 4 + h) * 8 + i] = hi;
-            hv[(s * 4 + 2 + h) * 8 + i] = lo;
-        }
-        const int c = f % KNN_FXQ;  // the row's place in its staged group (the swizzle's row)
-        uint4* out = qimg + (int64_t)f * NCH;
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) out[ch ^ (c & (NCH - 1))] = *reinterpret_cast<const uint4*>(&hv[ch * 8]);
-        const double ts = ldexp(t, 2 * e);
-        qa[f] = (t < 0.0) ? INFINITY
-                          : __double2float_rd((1.0 - 0x1p-12) * nx - (1.0 + 0x1p-20) * ts - 0x1p-11 * sqd * sqrt(nx) - 8.0);
-        qid[f] = q;
-    }
-}
-
-template <int KSTEPS>
-__global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __restrict__ rows, int n, int d,
-                                                            const int* __restrict__ fail_count,
-                                                            const unsigned* __restrict__ maxabs_bits,
-                                                            const uint4* __restrict__ qimg,
-                                                            const float* __restrict__ qa, const int* __restrict__ qid,
-                                                            int* __restrict__ cnt, int* __restrict__ bi,
-                                                            int* __restrict__ ovf_count) {
-    constexpr int NCH = 4 * KSTEPS;
-    __shared__ uint4 sq[KNN_FXQ * NCH];
-    __shared__ __attribute__((aligned(16))) float sa[KNN_FXQ];
-    __shared__ int sid[KNN_FXQ];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
-    const int nf = min(*fail_count, KNN_FX_ROWS);
-    if (nf == 0) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, j = lane & 31;
-    // the wave's 32 references: B fragments (dims 16 s + 8 h ..) and the reference's part of the test
-    const int jr = blockIdx.x * 128 + wave * 32 + j;
-    const bool inr = jr < n;
-    const int e = knn_scale_exp(maxabs_bits);
-    h8 bh[KSTEPS], bl[KSTEPS];
-    double ny = 0.0;
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int k = 16 * s + 8 * h + i;
-            const double ys = (inr && k < d) ? ldexp(rows[(int64_t)jr * d + k], e) : 0.0;
-            ny = fma(ys, ys, ny);
-            _Float16 hi, lo;
-            knn_split16(ys, hi, lo);
-            bh[s][i] = hi;
-            bl[s][i] = lo;
-        }
-    ny += __shfl_xor(ny, 32, 64);
-    const float bj = inr ? __double2float_rd((1.0 - 0x1p-12) * ny - 0x1p-11 * sqrt((double)d) * sqrt(ny)) : INFINITY;
-    for (int g0 = 0; g0 < nf; g0 += KNN_FXQ) {
-        const int nq = min(KNN_FXQ, nf - g0);
-        __syncthreads();  // the previous group's reads of the stage are done
-        for (int t = threadIdx.x; t < KNN_FXQ * NCH; t += 256) sq[t] = qimg[(int64_t)g0 * NCH + t];
-        if (threadIdx.x < KNN_FXQ) {
-            sa[threadIdx.x] = qa[g0 + threadIdx.x];  // (the prep writes whole groups: INFINITY past nf)
-            sid[threadIdx.x] = qid[g0 + threadIdx.x];
-        }
-        __syncthreads();
-        for (int t = 0; t < (nq + 31) >> 5; ++t) {  // block-uniform
-            typedef float f16x __attribute__((ext_vector_type(16)));
-            f16x acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-            const int c = t * 32 + j;
-            const uint4* ar = sq + c * NCH;
-#pragma unroll
-            for (int s = 0; s < KSTEPS; ++s) {
-                const uint4 ahv = ar[(s * 4 + h) ^ (c & (NCH - 1))];
-                const uint4 alv = ar[(s * 4 + 2 + h) ^ (c & (NCH - 1))];
-                const h8 ah = *reinterpret_cast<const h8*>(&ahv);
-                const h8 al = *reinterpret_cast<const h8*>(&alv);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
-            }
-            // register r holds failed row t*32 + (r & 3) + 8 (r >> 2) + 4h against reference jr
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 a4 = *reinterpret_cast<const float4*>(&sa[t * 32 + 8 * g + 4 * h]);
-                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (2.0f * acc[4 * g + q] >= av[q] + bj) {  // rare: the candidates
-                        const int i = t * 32 + 8 * g + 4 * h + q;
-                        if (jr != sid[i]) {
-                            const int slot = atomicAdd(&cnt[g0 + i], 1);
-                            if (slot < KNN_FX_CAP) bi[(int64_t)(g0 + i) * KNN_FX_CAP + slot] = jr;
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
 #ifndef WAVE_LDS_SYNC
 // a wave's LDS writes are visible to its other lanes' later LDS reads (the
 // LDS pipeline is in order per wave); the clobber stops compiler reordering
@@ -1528,15 +1381,12 @@ static int* knn_fail_ws(ccg_ctx* ctx, int64_t n, double** tau) {
 // Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
 static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
                                const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
-                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr,
-                               const unsigned* maxabs = nullptr) {
+                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr) {
     if (!seg_off && fail_tau) {
         // the radius search; its leftovers (overflow) continue below
         int* cnt = (int*)ccg_ws(ctx, WS_FX_A, sizeof(int) * (KNN_FX_ROWS + 64 + n));
         int* bi = (int*)ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-        // the fp16 path's failed-row images, tests and ids (max|x| known: the table path)
-        char* qw = maxabs ? (char*)ccg_ws(ctx, WS_FX_Q, (size_t)KNN_FX_ROWS * (64 * 4 + 8) + 64) : nullptr;
-        if (!cnt || !bi || (maxabs && !qw)) return CCG_ENOMEM;
+        if (!cnt || !bi) return CCG_ENOMEM;
         if (ctx->fx_zeroed != (void*)cnt) {  // fresh buffer: the select kernel keeps the counters zero afterwards
             CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * KNN_FX_ROWS, st));
             ctx->fx_zeroed = (void*)cnt;
@@ -1545,20 +1395,8 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         int* ovf_list = ovf_count + 64;
 #define CCG_FX(DM_)                                                                                              \
     do {                                                                                                         \
-        if (maxabs) {                                                                                            \
-            constexpr int KS_ = DM_ / 16;                                                                        \
-            uint4* qimg = (uint4*)qw;                                                                            \
-            float* qa = (float*)(qimg + (size_t)KNN_FX_ROWS * 4 * KS_);                                          \
-            int* qid = (int*)(qa + KNN_FX_ROWS);                                                                 \
-            knn_fx_prep16_kernel<KS_><<<64, 256, 0, st>>>(rows, d, fail_list, fail_count, fail_tau, maxabs, qimg, \
-                                                          qa, qid);                                              \
-            knn_fx_scan16_kernel<KS_><<<(unsigned)ccg_cdiv(n, 128), 256, 0, st>>>(rows, (int)n, d, fail_count,    \
-                                                                                 maxabs, qimg, qa, qid, cnt, bi,  \
-                                                                                 ovf_count);                      \
-        } else {                                                                                                 \
-            knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, \
-                                                                 cnt, bi, ovf_count);                             \
-        }                                                                                                        \
+        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, \
+                                                             bi, ovf_count);                                      \
         knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, fail_list, fail_count, fail_tau, cnt, bi,     \
                                                        out_idx, out_dist, dist_sq, ovf_list, ovf_count);          \
     } while (0)
@@ -1951,29 +1789,17 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
 // the distinct cells' rows, copied from the gathered (row-major) bootstrap
 // rows of each cell's first copy: coalesced, unlike a gather from the
 // column-major PCs
-__global__ __launch_bounds__(256) void kb_urows_kernel(const double* __restrict__ rows, int d, int u,
-                                                       const int* __restrict__ ustart, const int* __restrict__ srow,
-                                                       double* __restrict__ urows, const int32_t* __restrict__ idx,
-                                                       const float* __restrict__ cell_hint,
-                                                       float* __restrict__ urow_hint, unsigned* __restrict__ maxabs) {
-    __shared__ unsigned red[4];
+__global__ void kb_urows_kernel(const double* __restrict__ rows, int d, int u, const int* __restrict__ ustart,
+                                const int* __restrict__ srow, double* __restrict__ urows,
+                                const int32_t* __restrict__ idx, const float* __restrict__ cell_hint,
+                                float* __restrict__ urow_hint) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned mb = 0u;
-    if (t < (int64_t)u * d) {
-        const int64_t uid = t / d;
-        const int k = (int)(t - uid * d);
-        const int r0 = srow[ustart[uid]];
-        const double v = rows[(int64_t)r0 * d + k];
-        urows[t] = v;
-        if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
-        mb = __float_as_uint(nextafterf((float)fabs(v), INFINITY));  // a float at or above |v|
-    }
-    if (maxabs) {  // max|x| of the distinct rows (the fp16 radius search's scale): one atomic per block
-        for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mb;
-        __syncthreads();
-        if (threadIdx.x == 0) atomicMax(maxabs, max(max(red[0], red[1]), max(red[2], red[3])));
-    }
+    if (t >= (int64_t)u * d) return;
+    const int64_t uid = t / d;
+    const int k = (int)(t - uid * d);
+    const int r0 = srow[ustart[uid]];
+    urows[t] = rows[(int64_t)r0 * d + k];
+    if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
 }
 
 // The hint for the next bootstrap: each distinct cell's certified squared
@@ -2456,18 +2282,17 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     kb_fixup_big_kernel<<<16, 256, 0, st>>>(n, ustart, srow, row2u, big, nbig, rid);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
-    // the table path: fail counts, expansion tie count and max|x| (misc[4..7]) zeroed first
-    unsigned* umax = (kq >= 1 && tab_idx) ? misc + 7 : nullptr;
-    if (umax) CCG_HIP(hipMemsetAsync(misc + 4, 0, 4 * sizeof(unsigned), st));
+    // the table path: fail counts and the expansion tie count (misc[4..6]) zeroed first
+    if (kq >= 1 && tab_idx) CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));
     kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
-                                                                            cell_hint, urow_hint, umax);
+                                                                            cell_hint, urow_hint);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
         int* ufail = (int*)(misc + 5);
         kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2,
                                                                    urows, uidx, ud2, fail_list, ufail, ftau);
-        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau, umax);
+        rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau);
         if (rc) return rc;
         if (stats) {
             int nf = 0;
@@ -2499,9 +2324,8 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         kb_expand_kernel<<<ng, 256, 0, st>>>(n, u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
                                              fail_list, fail_count, ftau);
     }
-    // (the rows are copies of the distinct rows: the same max|x|)
     rc = knn_fallback_launch(ctx, rows, n, d, kmax, fail_list, fail_count, out_idx, out_dist, nullptr, 1, st, false,
-                             KNN_EXPAND_RADIUS ? ftau : nullptr, umax);
+                             KNN_EXPAND_RADIUS ? ftau : nullptr);
     if (rc) return rc;
     ctx->last_fail_list = fail_list;
     ctx->last_fail_count = fail_count;
@@ -2621,7 +2445,7 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     if (rc) return rc;
     kb_tables_kernel<<<ng, 256, 0, st>>>(skeys, srow, n, head, (int)u, ustart, row2u, ctx->d_err);
     kb_urows_kernel<<<(unsigned)ccg_cdiv(u * d, 256), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
-                                                                      nullptr, nullptr);
+                                                                      nullptr);
     // 3. every segment's distinct cells among themselves (kq = kmax: each has >= kmax + 1)
     std::vector<int64_t> po;
     std::vector<int> hperm;

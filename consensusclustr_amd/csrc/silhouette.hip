@@ -11,10 +11,13 @@
 // Every cross-row reduction (cluster sums, variances, the mean) is done in
 // fixed point with integer atomics, so the result is bitwise reproducible
 // regardless of scheduling; the scales are chosen on the device from max|x|
-// so no partial sum can overflow.  The cluster sums take int32 rows (2^-30 of
-// max|x|, round 5: the tiled sums stage them in LDS) and int64 sums; the
-// squared norms and the widths' sum 64-bit values.  The quantisation error
-// of a centroid is below 2^-30 max|x|, far inside the 1e-5 tolerance.
+// so no partial sum can overflow.  The cluster sums take int64 rows at scale
+// 2^e with m max|x| 2^e <= 2^61 (the round-5 tiled sums stage them in LDS);
+// the squared norms and the widths' sum 64-bit values.  (An int32 row scale,
+// 2^-30 max|x|, was tried in round 5: v_c = S2/n - |mu_c|^2 then mixes the
+// unquantised S2 with quantised centroids, and a singleton cluster's v_c came
+// out ~1e-8 instead of 0 -- its rows' own distance ~1e-4, widths off by
+// ~1e-4, means by up to 1.6e-4 relative on the pipeline tests.)
 // The widths' squared distances are |x|^2 + |mu|^2 + v - 2 x.mu with x.mu on
 // the fp64 matrix core (a fixed-order MFMA chain, so also reproducible).
 // Grid: (row tiles) x (groups of SIL_LG labelings); x rows are held in
@@ -41,14 +44,6 @@ __host__ __device__ __forceinline__ int scale_exp(double bound) {
     // largest e with bound * 2^e <= 2^61
     if (!(bound > 0.0)) return 52;
     int e = 61 - (ilogb(bound) + 1);
-    return e > 52 ? 52 : e;
-}
-
-// the int32 fixed-point rows of the cluster sums (round 5): largest e with
-// maxabs * 2^e <= 2^30 (sums of up to 2^31 weighted rows stay inside int64)
-__host__ __device__ inline int scale_exp32(double maxabs) {
-    if (!(maxabs > 0.0)) return 30;
-    const int e = 29 - ilogb(maxabs);
     return e > 52 ? 52 : e;
 }
 
@@ -207,25 +202,31 @@ __device__ __forceinline__ int sil_block_excl_scan(int v, int* sh, int* total) {
 }
 
 // K1': fixed-point rows, once per call: q1 = round(x * sc) [m][DMAX] int64
-// (zero past d) and q2 = round(|x|^2 * sc2) [m] (v_c needs only the
-// cluster's total sum of squares: v_c = S2 / n - |mu_c|^2).
+// (zero past d; sc = 2^scale_exp(m max|x|)) and q2 = round(|x|^2 * sc2) [m]
+// (v_c needs only the cluster's total sum of squares: v_c = S2 / n - |mu_c|^2).
 __host__ __device__ inline double sil_s2_bound(double maxabs, int d, int64_t m) {
     return maxabs * maxabs * (double)d * (double)m;
 }
 template <int DMAX>
 __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const unsigned* __restrict__ maxabs_bits,
-                          int* __restrict__ q1, long long* __restrict__ q2) {
+                          long long* __restrict__ q1, long long* __restrict__ q2) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t / DMAX;  // m * DMAX is a multiple of DMAX: a row's threads are all in or all out
     if (r >= m) return;
     const int k = (int)(t - r * DMAX);
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    const double sc = ldexp(1.0, scale_exp32(maxabs));
+    const double sc = ldexp(1.0, scale_exp(maxabs * (double)m));
     const double v = k < d ? x[r * d + k] : 0.0;
-    q1[t] = __double2int_rn(v * sc);
-    // |x|^2 of the row: its DMAX threads are DMAX-aligned lanes of one wave
-    // (fixed xor tree: deterministic)
-    double s2 = v * v;
+    const long long qv = __double2ll_rn(v * sc);
+    q1[t] = qv;
+    // |x_q|^2 of the QUANTISED row (exact in fp64: qv is an integer-valued
+    // double), so that v_c = S2/n - |mu_c|^2 is the spread of the same points
+    // the centroid averages: copies of one point give v_c = 0 up to fp64
+    // rounding (with |x|^2 of the raw row, a singleton's v_c was the
+    // quantisation residue 2 |x| 2^-e).  Its DMAX threads are DMAX-aligned
+    // lanes of one wave (fixed xor tree: deterministic).
+    const double vq = (double)qv / sc;
+    double s2 = vq * vq;
 #pragma unroll
     for (int o = DMAX / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
     if (k == 0) q2[r] = __double2ll_rn(s2 * ldexp(1.0, scale_exp(sil_s2_bound(maxabs, d, m))));
@@ -234,8 +235,8 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
 // K1 (round 5, tiles staged once for a group of labelings): cluster sums
 // S1 = sum x, S2 = sum |x|^2 and counts.  A block of 1024 threads takes a
 // tile of T positions (rows, or representatives weighted by their copies)
-// and stages their fixed-point rows in LDS ONCE (int32 q1 at stride d, scale
-// 2^e with max|x| 2^e <= 2^30, and int64 q2 = |x|^2): round 4 re-read the
+// and stages their fixed-point rows in LDS ONCE (int64 q1 at stride d, scale
+// 2^e with m max|x| 2^e <= 2^61, and int64 q2 = |x|^2): round 4 re-read the
 // rows from L2 for every labeling (60 x 59k x 256 B = 0.9 GB per bootstrap at
 // cfg3).  Then per labeling of its group (grid y, sg labelings): lanes along
 // the dimensions, 64 / DMAX positions per wave instruction, one int64 LDS
@@ -245,13 +246,23 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
 // sums (one atomic per present (cluster, dimension), contiguous) and zeroes
 // them.  The next labeling's labels and weights are loaded a phase ahead and
 // written to LDS during the flush: two barriers per labeling.  Integer
-// sums: any order gives the same bits.  LDS (dynamic): q1 [T][d] int32,
-// q2 [T] int64, labels and weights [T] int, acc1 [cmax+1][d], acc2 and
-// counts [cmax+1] int64.  T is the largest of 1024 / 512 / 256 that fits.
+// sums: any order gives the same bits.  LDS (dynamic): q1 [T][d] and q2 [T]
+// int64, labels and weights [T] int, acc1 [cmax+1][d], acc2 and counts
+// [cmax+1] int64.  T is the largest of 1024 / 512 / 256 that fits.
 #define SIL_ST 1024  // threads of the tiled sums kernel (16 waves, one block per CU)
+#define SIL_SUMS_PF 4  // labelings whose labels / weights are in flight ahead of the walk
 #define SIL_LDS_CU 163840
 __host__ __device__ inline size_t sil_tile_lds(int T, int d, int cmax) {
-    return (size_t)T * d * 4 + (size_t)T * 16 + (size_t)(cmax + 1) * (d + 2) * 8;
+    return (size_t)T * d * 8 + (size_t)T * 16 + (size_t)(cmax + 1) * (d + 2) * 8;
+}
+
+// A workgroup barrier that waits for the wave's LDS operations only: the
+// flush's global atomics (fire and forget) and the label prefetches stay in
+// flight across it.  __syncthreads() waits vmcnt(0) as well, which made
+// every labeling wait for its 1 230 global atomics to return (~5 us each).
+__device__ __forceinline__ void sil_lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt and expcnt left at their maxima
+    __builtin_amdgcn_s_barrier();
 }
 
 // Distinct-cell form (rep != nullptr): tile position p is the representative
@@ -261,7 +272,8 @@ __host__ __device__ inline size_t sil_tile_lds(int T, int d, int cmax) {
 template <int DMAX, bool SEG>
 __global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T, int sg,
                                                         const int32_t* __restrict__ labels, int L, int cmax,
-                                                        const int* __restrict__ q1, const long long* __restrict__ q2,
+                                                        const long long* __restrict__ q1,
+                                                        const long long* __restrict__ q2,
                                                         unsigned long long* __restrict__ gsum,
                                                         unsigned long long* __restrict__ gsum2,
                                                         unsigned long long* __restrict__ gcnt,
@@ -270,8 +282,8 @@ __global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T,
                                                         const int64_t* __restrict__ nrep,
                                                         const int64_t* __restrict__ scan, SilSegs sgs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int* q1s = (int*)smem;                                    // [T][d]
-    long long* q2s = (long long*)(q1s + (int64_t)T * d);      // [T] (T * d * 4 is a multiple of 8: T even)
+    long long* q1s = (long long*)smem;                        // [T][d]
+    long long* q2s = q1s + (int64_t)T * d;                    // [T]
     int* slab = (int*)(q2s + T);                              // [T]
     int* swgt = slab + T;                                     // [T]
     unsigned long long* acc1 = (unsigned long long*)(swgt + T);  // [cmax+1][d]
@@ -305,64 +317,83 @@ __global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T,
     }
     if (tid < T) q2s[tid] = rowv >= 0 ? q2[rowv] : 0ll;
     for (int t = tid; t < (cmax + 1) * (d + 2); t += SIL_ST) acc1[t] = 0ull;
-    // label 0: positions past npos, codes outside [1, cmax] and weight 0
-    int lbn = 0, wgn = 0;
-    auto fetch = [&](int l) {
-        lbn = 0;
-        wgn = 0;
+    // label 0: positions past npos, codes outside [1, cmax] and weight 0.
+    // The labels and weights of the next SIL_SUMS_PF labelings are in flight
+    // in a register ring (the loop is unrolled by SIL_SUMS_PF so the ring's
+    // slots are static): with one phase of prefetch each labeling waited on a
+    // global load (187 us per bootstrap at cfg3).
+    // (the loads only fill the ring; the weight cnt - mult is formed at put
+    // time, so no wait is forced at the fetch)
+    const int cw = (own && rep) ? cnt[rb + tid] : 1;
+    auto fetch = [&](int l, int& lb, int& mt) {
+        lb = 0;
+        mt = 0;
         if (l < l1 && own) {
-            lbn = sil_label(labels, m, sgs, q, l, rowv);
-            wgn = rep ? cnt[rb + tid] - mult[(int64_t)l * mw + rb + tid] : 1;
+            lb = sil_label(labels, m, sgs, q, l, rowv);
+            if (rep) mt = mult[(int64_t)l * mw + rb + tid];
         }
     };
-    auto put = [&]() {
+    auto put = [&](int lb, int mt) {
         if (tid < T) {
-            const bool ok = lbn >= 1 && lbn <= cmax && wgn > 0;
-            slab[tid] = ok ? lbn : 0;
-            swgt[tid] = ok ? wgn : 0;
+            const int wg = cw - mt;
+            const bool ok = own && lb >= 1 && lb <= cmax && wg > 0;
+            slab[tid] = ok ? lb : 0;
+            swgt[tid] = ok ? wg : 0;
         }
     };
-    fetch(l0);
+    int rl[SIL_SUMS_PF], rm[SIL_SUMS_PF];
+#pragma unroll
+    for (int i = 0; i < SIL_SUMS_PF; ++i) fetch(l0 + i, rl[i], rm[i]);
     __syncthreads();  // the rows' ids in slab are read
-    put();
-    fetch(l0 + 1);
+    put(rl[0], rm[0]);
+    fetch(l0 + SIL_SUMS_PF, rl[0], rm[0]);
     __syncthreads();
     const int ppw = T / NW;  // positions per wave
-    for (int l = l0; l < l1; ++l) {
-        for (int p0 = wave * ppw; p0 < (wave + 1) * ppw; p0 += RPW) {
-            const int pl = p0 + sub;
-            const int lb = slab[pl];
-            if (lb) {
-                const long long w = swgt[pl];
-                if (k < d) atomicAdd(&acc1[lb * d + k], (unsigned long long)(w * (long long)q1s[pl * d + k]));
-                if (k == 0) {
-                    atomicAdd(&acc2[lb], (unsigned long long)(w * q2s[pl]));
-                    atomicAdd(&accn[lb], (unsigned long long)w);
+    for (int lg = l0; lg < l1; lg += SIL_SUMS_PF) {
+#pragma unroll
+        for (int i = 0; i < SIL_SUMS_PF; ++i) {
+            const int l = lg + i;
+            if (l >= l1) break;  // (block-uniform)
+            for (int p0 = wave * ppw; p0 < (wave + 1) * ppw; p0 += RPW) {
+                const int pl = p0 + sub;
+                const int lb = slab[pl];
+                if (lb) {
+                    const long long w = swgt[pl];
+                    if (k < d) atomicAdd(&acc1[lb * d + k], (unsigned long long)(w * q1s[pl * d + k]));
+                    if (k == 0) {
+                        atomicAdd(&acc2[lb], (unsigned long long)(w * q2s[pl]));
+                        atomicAdd(&accn[lb], (unsigned long long)w);
+                    }
                 }
             }
-        }
-        __syncthreads();
-        // flush-and-zero (each entry read and cleared by one thread), the next labels
-        const int lv = q * L + l;  // (the virtual labeling)
-        unsigned long long* gs = gsum + (int64_t)lv * (cmax + 1) * d;
-        for (int t = tid; t < (cmax + 1) * d; t += SIL_ST) {
-            const unsigned long long v = acc1[t];
-            if (v) {
-                atomicAdd(&gs[t], v);
-                acc1[t] = 0ull;
+            sil_lds_barrier();
+            // the next labeling's labels into LDS first (its loads, issued
+            // SIL_SUMS_PF labelings ago, and the previous flush's atomics are
+            // what the wait here covers: vmcnt counts them in order), then this
+            // labeling's flush-and-zero (each entry read and cleared by one
+            // thread) and the next prefetch
+            const int s1 = (i + 1) % SIL_SUMS_PF;  // the ring slot of labeling l + 1
+            put(rl[s1], rm[s1]);
+            const int lv = q * L + l;  // (the virtual labeling)
+            unsigned long long* gs = gsum + (int64_t)lv * (cmax + 1) * d;
+            for (int t = tid; t < (cmax + 1) * d; t += SIL_ST) {
+                const unsigned long long v = acc1[t];
+                if (v) {
+                    atomicAdd(&gs[t], v);
+                    acc1[t] = 0ull;
+                }
             }
-        }
-        for (int c = tid; c <= cmax; c += SIL_ST) {
-            if (accn[c]) {
-                atomicAdd(&gcnt[(int64_t)lv * (cmax + 1) + c], accn[c]);
-                atomicAdd(&gsum2[(int64_t)lv * (cmax + 1) + c], acc2[c]);
-                accn[c] = 0ull;
-                acc2[c] = 0ull;
+            for (int c = tid; c <= cmax; c += SIL_ST) {
+                if (accn[c]) {
+                    atomicAdd(&gcnt[(int64_t)lv * (cmax + 1) + c], accn[c]);
+                    atomicAdd(&gsum2[(int64_t)lv * (cmax + 1) + c], acc2[c]);
+                    accn[c] = 0ull;
+                    acc2[c] = 0ull;
+                }
             }
+            fetch(l + 1 + SIL_SUMS_PF, rl[s1], rm[s1]);
+            sil_lds_barrier();
         }
-        put();
-        fetch(l + 2);
-        __syncthreads();
     }
 }
 
@@ -370,7 +401,7 @@ __global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T,
 // of sil_mult_kernel, l << 32 | row): their fixed-point rows added alone.
 template <int DMAX>
 __global__ void sil_sums_exc(int64_t m, int d, const int32_t* __restrict__ labels, int L, int cmax,
-                             const int* __restrict__ q1, const long long* __restrict__ q2,
+                             const long long* __restrict__ q1, const long long* __restrict__ q2,
                              const unsigned long long* __restrict__ exc, const int* __restrict__ nexc,
                              unsigned long long* __restrict__ gsum, unsigned long long* __restrict__ gsum2,
                              unsigned long long* __restrict__ gcnt, SilSegs sgs) {
@@ -383,7 +414,7 @@ __global__ void sil_sums_exc(int64_t m, int d, const int32_t* __restrict__ label
         if (lab < 1 || lab > cmax) continue;
         const int64_t lv = (int64_t)q * L + l;
         unsigned long long* gs = gsum + (lv * (cmax + 1) + lab) * d;
-        for (int k = 0; k < d; ++k) atomicAdd(&gs[k], (unsigned long long)(long long)q1[r * DMAX + k]);
+        for (int k = 0; k < d; ++k) atomicAdd(&gs[k], (unsigned long long)q1[r * DMAX + k]);
         atomicAdd(&gsum2[lv * (cmax + 1) + lab], (unsigned long long)q2[r]);
         atomicAdd(&gcnt[lv * (cmax + 1) + lab], 1ull);
     }
@@ -404,7 +435,7 @@ __host__ __device__ __forceinline__ int sil_mfma_pos(int k) {
 // With the sums of squares (gsum2, the sorted-segment path) also
 // v_c = mean |x - mu_c|^2 = sum_k (S2 / n - mu_k^2).  One block per labeling.
 template <int DMAX>
-__global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax, int q32,
+__global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax,
                                                 const unsigned* __restrict__ maxabs_bits,
                                                 const unsigned long long* __restrict__ gsum,
                                                 const unsigned long long* __restrict__ gsum2,
@@ -415,8 +446,8 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax, int 
     __shared__ int sh[SIL_T / 64];
     const int l = blockIdx.x;
     const double maxabs = (double)__uint_as_float(*maxabs_bits);
-    // the sums' scale: the int32 rows of the tiled sums, or sil_centroid's
-    const double inv_sc = ldexp(1.0, q32 ? -scale_exp32(maxabs) : -scale_exp(maxabs * (double)m));
+    // the sums' scale (the tiled sums' rows and sil_centroid's alike)
+    const double inv_sc = ldexp(1.0, -scale_exp(maxabs * (double)m));
     const unsigned long long* gs = gsum + (int64_t)l * (cmax + 1) * d;
     const unsigned long long* gc = gcnt + (int64_t)l * (cmax + 1);
     int* pl = pos + (int64_t)l * (cmax + 1);
@@ -453,7 +484,12 @@ __global__ __launch_bounds__(SIL_T) void sil_mu(int64_t m, int d, int cmax, int 
             const double inv_sc2 = ldexp(1.0, -scale_exp(sil_s2_bound(maxabs, d, m)));
             const double n = (double)gc[c];
             const double v = ((double)(long long)gsum2[(int64_t)l * (cmax + 1) + c] * inv_sc2) / n - s;
-            auxc[((int64_t)l * cmax + pc) * 2 + 1] = fmax(v, 0.0);  // clamp the cancellation noise of equal points
+            // equal points (a singleton, a cell's copies) have v_c = 0; the
+            // formula leaves the rounding of the rows' |x|^2 (<= 2^-s2 / 2
+            // each) and of |mu|^2: below that floor v_c is taken as 0, so the
+            // result does not depend on the batch's scale (m)
+            const double floor_v = inv_sc2 + 0x1p-50 * s;
+            auxc[((int64_t)l * cmax + pc) * 2 + 1] = v > floor_v ? v : 0.0;
         }
     }
 }
@@ -809,6 +845,7 @@ typedef float sil_f16x __attribute__((ext_vector_type(16)));
 #define SIL_WLG 15      // labelings per sil_width16 block
 #define SIL_WCMAX 256   // 8 tiles of 32: the tile fits the packed minimum's 3 bits
 #define SIL_BIG 1.0e38f
+#define SIL_NCAND 4  // exact candidates listed per lane for a near tie
 #define SIL_W16_LDS 81920  // two image buffers (40 KB each) per block: cmax <= 96 at d <= 32
 
 // image of a labeling with cpl = 32 x tiles centroid slots: fragments
@@ -1046,7 +1083,7 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
         const float n1 = fminf(m1, o1), n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
         const bool none = !(n1 < 1.0e37f);  // no other cluster
         const double mbs = ldexp(sbnd[0], e16), abs2 = ldexp(sbnd[1], 2 * e16);
-        const double E = 0x1p-14 * (xn + mbs) * (xn + mbs) + 0x1p-11 * sqd * (xn + mbs) + 0x1p-14 * abs2 + 8.0;
+        const double E = 0x1p-13 * xn * mbs + 0x1p-11 * sqd * (xn + mbs) + 0x1p-14 * abs2 + 8.0;
         const bool amb = !none && (double)n2 - (double)n1 <= 2.0 * E;
         auto dsq = [&](int c) {
             const double* mr = smu + c * DMAX;
@@ -1066,9 +1103,61 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
         const double dx = dsq(cx);
         const double S = po >= 0 ? dx : INFINITY;  // (read on h = 0)
         double O = (h == 1 && !none && !amb) ? dx : INFINITY;
-        if (amb)  // a near tie in the screen: every other centroid exactly, split over the lane pair
-            for (int c = h; c < C; c += 2)
-                if (c != po) O = fmin(O, dsq(c));
+        if (__any(amb)) {
+            // a near tie in the screen: the tiles again, listing (per lane) the
+            // other centroids whose screen value is within 2E of the smallest --
+            // every centroid that can be the nearest -- and each taken exactly.
+            // (Round 5 first took every centroid of an ambiguous lane: 60% of
+            // the waves paid C exact distances.)
+            const float thr = amb ? (float)((double)n1 + 2.0 * E) * (1.0f + 0x1p-20f) : -SIL_BIG;
+            int cand[SIL_NCAND];
+            int nc = 0;
+#pragma unroll
+            for (int u = 0; u < SIL_NCAND; ++u) cand[u] = 0;
+            for (int t = 0; t < nt; ++t) {
+                sil_f16x acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+                const int c = t * 32 + j;
+                const _Float16* ar = sA + c * 64;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const sil_h8 ah = *reinterpret_cast<const sil_h8*>(ar + (((s * 4 + h) ^ (c & 7)) << 3));
+                    const sil_h8 alo = *reinterpret_cast<const sil_h8*>(ar + (((s * 4 + 2 + h) ^ (c & 7)) << 3));
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh[s], acc, 0, 0, 0);
+                }
+                const float4* af = reinterpret_cast<const float4*>(sAf + t * 32 + 4 * h);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 a4 = af[2 * g];
+                    const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = 4 * g + q;
+                        const int ci = t * 32 + q + 8 * g + 4 * h;
+                        const float a = fmaf(-2.0f, acc[r], av[q]);
+                        if (a <= thr && ci != po && ci < C) {
+#pragma unroll
+                            for (int u = 0; u < SIL_NCAND; ++u) cand[u] = nc == u ? ci : cand[u];
+                            ++nc;
+                        }
+                    }
+                }
+            }
+            // a lane with more candidates than its list takes every centroid of its half
+            const bool full = nc > SIL_NCAND;
+            int ncw = full ? 0 : nc;
+            for (int o = 32; o > 0; o >>= 1) ncw = max(ncw, __shfl_xor(ncw, o, 64));
+            for (int u = 0; u < SIL_NCAND; ++u) {
+                if (u >= ncw) break;  // (wave-uniform)
+                if (!full && u < nc) O = fmin(O, dsq(cand[u]));
+            }
+            if (__any(full))
+                for (int c = h; c < C; c += 2)
+                    if (full && c != po) O = fmin(O, dsq(c));
+        }
         O = fmin(O, __shfl_xor(O, 32, 64));
         long long wq = 0;
         unsigned wn = 0;
@@ -1301,8 +1390,8 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
     const int T = q ? sil_tile_T(d, cmax) : 0;
     if (T) {
         // tiled sums: S1, S2 and counts in one pass, v_c in sil_mu
-        int* q1 = (int*)q;
-        long long* q2 = (long long*)(q1 + m * DMAX);
+        long long* q1 = (long long*)q;
+        long long* q2 = q1 + m * DMAX;
         sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q1, q2);
         // about one block per CU: the representatives are ~0.64 of the rows of a bootstrap
         const int64_t gx = seg ? ts_tiles : ccg_cdiv(m, T);
@@ -1319,7 +1408,7 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
                                                                   gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
         if (rep)
             sil_sums_exc<DMAX><<<64, 256, 0, st>>>(m, d, labels, L, cmax, q1, q2, exc, nexc, gsum, gsum2, gcnt, sgs);
-        sil_mu<DMAX><<<Lv, SIL_T, 0, st>>>(m, d, cmax, 1, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
+        sil_mu<DMAX><<<Lv, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
     } else {
         dim3 grid((unsigned)ccg_cdiv(m, SIL_T), (unsigned)ccg_cdiv(L, SIL_LG));
         const size_t lds1 = (size_t)(cmax + 1) * d * 8 + (size_t)(cmax + 1) * 4;
@@ -1328,8 +1417,7 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
             sil_centroid<DMAX, true><<<grid, SIL_T, lds1, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
         else
             sil_centroid<DMAX, false><<<grid, SIL_T, 0, st>>>(x, m, d, labels, L, cmax, maxabs, gsum, gcnt);
-        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, 0, maxabs, gsum, nullptr, gcnt, npres, codes, pos, mu, muc,
-                                          auxc);
+        sil_mu<DMAX><<<L, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, nullptr, gcnt, npres, codes, pos, mu, muc, auxc);
         if (lds2 <= SIL_LDS_CAP)
             sil_var<DMAX, true><<<grid, SIL_T, lds2, st>>>(x, m, d, labels, L, cmax, maxabs, mu, gvar);
         else
@@ -1417,7 +1505,7 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     int* pos = codes + (size_t)L * cmax;
     void* q = nullptr;  // fixed-point rows of the tiled sorted-segment path (cmax small enough for its LDS)
     if (sil_tile_T(d, cmax)) {
-        q = ccg_ws(ctx, WS_SIL_Q, sizeof(int) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
+        q = ccg_ws(ctx, WS_SIL_Q, sizeof(long long) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
         if (!q) return CCG_ENOMEM;
     }
     unsigned char* img = nullptr;  // LDS images of the fp16-screen widths (d <= 32, cmax small enough)
@@ -1473,7 +1561,7 @@ static int sil_cells_run(ccg_ctx* ctx, const double* x, int64_t m, int d, const 
     int* pos = codes + (size_t)Lv * cmax;
     void* q = nullptr;  // fixed-point rows of the tiled sums (cmax small enough for its LDS)
     if (sil_tile_T(d, cmax)) {
-        q = ccg_ws(ctx, WS_SIL_Q, sizeof(int) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
+        q = ccg_ws(ctx, WS_SIL_Q, sizeof(long long) * (size_t)m * dmax + sizeof(long long) * (size_t)m + 64);
         if (!q) return CCG_ENOMEM;
     }
     unsigned char* img = nullptr;  // LDS images of the fp16-screen widths (d <= 32, cmax small enough)

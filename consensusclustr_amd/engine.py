@@ -24,9 +24,20 @@ def _ptr(a):
     return _vp(a.data_ptr())  # torch tensor
 
 
+_HIP_STREAM_LEGACY = 1  # hipStreamLegacy
+
+
 def _stream():
+    """torch's current stream for the library's launches.  torch's default
+    stream is HIP's legacy null stream (handle 0), which the C API reads as
+    "the context's own stream" (a non-blocking stream, unordered with
+    torch's work); hipStreamLegacy is passed instead, so a tensor torch
+    computed just before a call is complete when the library reads it, and a
+    temporary freed just after a call is not reused while the library still
+    reads it."""
     import torch
-    return _vp(torch.cuda.current_stream().cuda_stream)
+    h = torch.cuda.current_stream().cuda_stream
+    return _vp(h if h else _HIP_STREAM_LEGACY)
 
 
 class Engine:

@@ -12,8 +12,10 @@
  *     glue binds.  They copy in, run, copy out and
  *     synchronise.
  *   - device-pointer functions (*_dev): inputs/outputs already in HBM,
- *     enqueued on `stream` (a hipStream_t; NULL = the context's stream).
- *     No host synchronisation unless stated.
+ *     enqueued on `stream` (a hipStream_t; NULL = the context's stream, a
+ *     non-blocking stream: a caller whose inputs come from the legacy null
+ *     stream -- torch's default stream -- passes hipStreamLegacy, or orders
+ *     the streams itself).  No host synchronisation unless stated.
  *
  * Reference interfaces replaced (paths relative to the reference repo):
  *   ccg_knn_boot / ccg_knn_rows_dev : BiocNeighbors::findKNN as reached by
