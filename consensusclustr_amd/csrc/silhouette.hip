@@ -12,7 +12,7 @@
 // fixed point with integer atomics, so the result is bitwise reproducible
 // regardless of scheduling; the scales are chosen on the device from max|x|
 // so no partial sum can overflow.  The cluster sums take int64 rows at scale
-// 2^e with m max|x| 2^e <= 2^61 (the round-5 tiled sums stage them in LDS);
+// 2^e with m max|x| 2^e <= 2^61;
 // the squared norms and the widths' sum 64-bit values.  (An int32 row scale,
 // 2^-30 max|x|, was tried in round 5: v_c = S2/n - |mu_c|^2 then mixes the
 // unquantised S2 with quantised centroids, and a singleton cluster's v_c came
@@ -232,167 +232,159 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
     if (k == 0) q2[r] = __double2ll_rn(s2 * ldexp(1.0, scale_exp(sil_s2_bound(maxabs, d, m))));
 }
 
-// K1 (round 5, tiles staged once for a group of labelings): cluster sums
-// S1 = sum x, S2 = sum |x|^2 and counts.  A block of 1024 threads takes a
-// tile of T positions (rows, or representatives weighted by their copies)
-// and stages their fixed-point rows in LDS ONCE (int64 q1 at stride d, scale
-// 2^e with m max|x| 2^e <= 2^61, and int64 q2 = |x|^2): round 4 re-read the
-// rows from L2 for every labeling (60 x 59k x 256 B = 0.9 GB per bootstrap at
-// cfg3).  Then per labeling of its group (grid y, sg labelings): lanes along
-// the dimensions, 64 / DMAX positions per wave instruction, one int64 LDS
-// atomic per (position, dimension) into the block's [cmax+1][d] sums (the
-// positions of one instruction share an address only when their labels
-// match); after a barrier each thread adds the sums it owns to the global
-// sums (one atomic per present (cluster, dimension), contiguous) and zeroes
-// them.  The next labeling's labels and weights are loaded a phase ahead and
-// written to LDS during the flush: two barriers per labeling.  Integer
-// sums: any order gives the same bits.  LDS (dynamic): q1 [T][d] and q2 [T]
-// int64, labels and weights [T] int, acc1 [cmax+1][d], acc2 and counts
-// [cmax+1] int64.  T is the largest of 1024 / 512 / 256 that fits.
-#define SIL_ST 1024  // threads of the tiled sums kernel (16 waves, one block per CU)
-#define SIL_SUMS_PF 4  // labelings whose labels / weights are in flight ahead of the walk
+// K1 (round 5): cluster sums S1 = sum x, S2 = sum |x|^2 and counts, one
+// block of 1024 threads per (tile of SIL_SP positions, group of G <=
+// SIL_SGMAX labelings).  A position is a row, or a representative row
+// weighted by its cell's copies.  The block first writes its positions'
+// rows, and their labels and weights in each labeling of the group, to LDS
+// (coalesced), then walks them: lanes along the dimensions, 64 / DMAX
+// positions per wave instruction, the fixed-point row read from the L2 ONCE
+// for the group and one int64 LDS atomic per (position, dimension,
+// labeling) into the block's [G][cmax+1][d] sums; a barrier; one global
+// atomic per present (labeling, cluster, dimension).  The rows are re-read
+// per group (60 / G x 59k x 256 B at cfg3), and the grid is XCD-aware: the
+// blocks of a tile, over all groups, run on one XCD (block b on XCD b mod
+// 8), whose 4 MB L2 then holds its eighth of the rows (23 MB of int64 rows
+// at cfg3 would not fit one L2).  Measured at cfg3: one labeling per block
+// 137 us per bootstrap; an earlier round-5 form that staged a tile's rows in
+// LDS once for many labelings paid two barriers per labeling, each waiting
+// on the previous flush's global atomics (170 us).  Integer sums: any order
+// gives the same bits.  LDS (dynamic): rows [SIL_SP], labels and weights
+// [G][SIL_SP] int, acc [G]{[cmax+1][d] sums, [cmax+1] S2, [cmax+1] counts}
+// int64.
+#define SIL_SB 1024   // threads of the sums kernel
+#define SIL_SP 1024   // positions per sums block
+#define SIL_SGMAX 4   // labelings per sums block
 #define SIL_LDS_CU 163840
-__host__ __device__ inline size_t sil_tile_lds(int T, int d, int cmax) {
-    return (size_t)T * d * 8 + (size_t)T * 16 + (size_t)(cmax + 1) * (d + 2) * 8;
+#define SIL_LDS_SUMS 81920  // two blocks per CU
+__host__ __device__ inline size_t sil_tile_lds(int d, int cmax, int G) {
+    return (size_t)SIL_SP * 4 + (size_t)G * SIL_SP * 8 + (size_t)G * (cmax + 1) * (d + 2) * 8;
+}
+// labelings per sums block: the most whose LDS keeps two blocks per CU (one
+// if even G = 1 needs more), 0 if G = 1 does not fit the CU
+static inline int sil_sums_G(int d, int cmax) {
+    for (int G = SIL_SGMAX; G >= 1; G >>= 1)
+        if (sil_tile_lds(d, cmax, G) <= SIL_LDS_SUMS) return G;
+    return sil_tile_lds(d, cmax, 1) <= SIL_LDS_CU ? 1 : 0;
 }
 
-// A workgroup barrier that waits for the wave's LDS operations only: the
-// flush's global atomics (fire and forget) and the label prefetches stay in
-// flight across it.  __syncthreads() waits vmcnt(0) as well, which made
-// every labeling wait for its 1 230 global atomics to return (~5 us each).
-__device__ __forceinline__ void sil_lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt and expcnt left at their maxima
-    __builtin_amdgcn_s_barrier();
-}
-
-// Distinct-cell form (rep != nullptr): tile position p is the representative
+// Distinct-cell form (rep != nullptr): position p is the representative
 // row rep[p] of a cell, weighted by the cnt[p] rows of the cell less the
 // mult[l][p] of them labelled apart in labeling l (those rows are added by
-// sil_sums_exc); the integer sums are those of the rows.
+// sil_sums_exc); the integer sums are those of the rows.  Grid: 8 tpx
+// cdiv(L, G) blocks; block b takes group (b / 8) / tpx and tile ((b / 8)
+// mod tpx) 8 + b mod 8 of the ntile tiles.
 template <int DMAX, bool SEG>
-__global__ __launch_bounds__(SIL_ST) void sil_sums_tile(int64_t m, int d, int T, int sg,
-                                                        const int32_t* __restrict__ labels, int L, int cmax,
-                                                        const long long* __restrict__ q1,
-                                                        const long long* __restrict__ q2,
-                                                        unsigned long long* __restrict__ gsum,
-                                                        unsigned long long* __restrict__ gsum2,
-                                                        unsigned long long* __restrict__ gcnt,
-                                                        const int* __restrict__ rep, const int* __restrict__ mult,
-                                                        const int* __restrict__ cnt, int64_t mw,
-                                                        const int64_t* __restrict__ nrep,
-                                                        const int64_t* __restrict__ scan, SilSegs sgs) {
+__global__ __launch_bounds__(SIL_SB) void sil_sums_blk(int64_t m, int d, int ntile, int tpx, int G,
+                                                       const int32_t* __restrict__ labels, int L, int cmax,
+                                                       const long long* __restrict__ q1,
+                                                       const long long* __restrict__ q2,
+                                                       unsigned long long* __restrict__ gsum,
+                                                       unsigned long long* __restrict__ gsum2,
+                                                       unsigned long long* __restrict__ gcnt,
+                                                       const int* __restrict__ rep, const int* __restrict__ mult,
+                                                       const int* __restrict__ cnt, int64_t mw,
+                                                       const int64_t* __restrict__ nrep,
+                                                       const int64_t* __restrict__ scan, SilSegs sgs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    long long* q1s = (long long*)smem;                        // [T][d]
-    long long* q2s = q1s + (int64_t)T * d;                    // [T]
-    int* slab = (int*)(q2s + T);                              // [T]
-    int* swgt = slab + T;                                     // [T]
-    unsigned long long* acc1 = (unsigned long long*)(swgt + T);  // [cmax+1][d]
-    unsigned long long* acc2 = acc1 + (int64_t)(cmax + 1) * d;   // [cmax+1]
-    unsigned long long* accn = acc2 + (cmax + 1);                // [cmax+1] weighted counts
-    constexpr int NW = SIL_ST / 64;
-    constexpr int RPW = 64 / DMAX;  // positions per wave instruction
+    int* srow = (int*)smem;                                      // [SIL_SP]
+    int* slab = srow + SIL_SP;                                   // [G][SIL_SP]
+    int* swgt = slab + G * SIL_SP;                               // [G][SIL_SP]
+    unsigned long long* acc = (unsigned long long*)(swgt + G * SIL_SP);  // [G][(cmax+1)(d+2)]
+    const int na = (cmax + 1) * (d + 2);                         // per labeling: sums, then S2, then counts
+    constexpr int NW = SIL_SB / 64;
+    constexpr int RPW = 64 / DMAX;      // positions per wave instruction
+    constexpr int PPW = SIL_SP / NW;    // positions per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k = lane % DMAX, sub = lane / DMAX;
+    const int loc = blockIdx.x >> 3;
+    const int grp = loc / tpx;
+    const int tile = (loc - grp * tpx) * 8 + (blockIdx.x & 7);
+    const int l0 = grp * G;
+    if (l0 >= L || tile >= ntile) return;
+    const int ng = min(G, L - l0);
     int64_t rb, npos;  // the tile's first position, the end of its positions
     int q = 0;
     if constexpr (SEG) {  // a tile of segment q: its representatives are positions [scan[off_q], scan[off_q+1])
-        q = sil_seg_tile(sgs.ts, sgs.nseg, blockIdx.x);
-        rb = scan[sgs.off[q]] + (int64_t)(blockIdx.x - sgs.ts[q]) * T;
+        q = sil_seg_tile(sgs.ts, sgs.nseg, tile);
+        rb = scan[sgs.off[q]] + (int64_t)(tile - sgs.ts[q]) * SIL_SP;
         npos = scan[sgs.off[q + 1]];
     } else {
-        rb = (int64_t)blockIdx.x * T;
+        rb = (int64_t)tile * SIL_SP;
         npos = rep ? *nrep : m;  // positions: rows, or the representatives (counted on the device)
     }
     if (rb >= npos) return;
-    const int l0 = blockIdx.y * sg, l1 = min(L, l0 + sg);
-    // one position per thread (T <= SIL_ST)
-    const bool own = tid < T && rb + tid < npos;
-    const int rowv = own ? (rep ? rep[rb + tid] : (int)(rb + tid)) : -1;
-    if (tid < T) slab[tid] = rowv;
-    __syncthreads();
-    for (int e = tid; e < T * d; e += SIL_ST) {
-        const int i = e / d, kk = e - i * d;
-        const int r = slab[i];
-        q1s[e] = r >= 0 ? q1[(int64_t)r * DMAX + kk] : 0;
+    for (int t = tid; t < ng * na; t += SIL_SB) acc[t] = 0ull;
+    // label 0: positions past npos, codes outside [1, cmax] and weight 0
+    for (int p = tid; p < SIL_SP; p += SIL_SB) {
+        const int64_t ps = rb + p;
+        const bool in = ps < npos;
+        const int row = in ? (rep ? rep[ps] : (int)ps) : 0;
+        srow[p] = row;
+        const int c0 = (in && rep) ? cnt[ps] : 1;
+        for (int g = 0; g < G; ++g) {
+            int lb = 0, wg = 0;
+            if (in && g < ng) {
+                const int l = l0 + g;
+                if constexpr (SEG) lb = sil_label(labels, m, sgs, q, l, row);
+                else lb = labels[(int64_t)l * m + row];
+                wg = rep ? c0 - mult[(int64_t)l * mw + ps] : 1;
+            }
+            const bool ok = lb >= 1 && lb <= cmax && wg > 0;
+            slab[g * SIL_SP + p] = ok ? lb : 0;
+            swgt[g * SIL_SP + p] = ok ? wg : 0;
+        }
     }
-    if (tid < T) q2s[tid] = rowv >= 0 ? q2[rowv] : 0ll;
-    for (int t = tid; t < (cmax + 1) * (d + 2); t += SIL_ST) acc1[t] = 0ull;
-    // label 0: positions past npos, codes outside [1, cmax] and weight 0.
-    // The labels and weights of the next SIL_SUMS_PF labelings are in flight
-    // in a register ring (the loop is unrolled by SIL_SUMS_PF so the ring's
-    // slots are static): with one phase of prefetch each labeling waited on a
-    // global load (187 us per bootstrap at cfg3).
-    // (the loads only fill the ring; the weight cnt - mult is formed at put
-    // time, so no wait is forced at the fetch)
-    const int cw = (own && rep) ? cnt[rb + tid] : 1;
-    auto fetch = [&](int l, int& lb, int& mt) {
-        lb = 0;
-        mt = 0;
-        if (l < l1 && own) {
-            lb = sil_label(labels, m, sgs, q, l, rowv);
-            if (rep) mt = mult[(int64_t)l * mw + rb + tid];
-        }
-    };
-    auto put = [&](int lb, int mt) {
-        if (tid < T) {
-            const int wg = cw - mt;
-            const bool ok = own && lb >= 1 && lb <= cmax && wg > 0;
-            slab[tid] = ok ? lb : 0;
-            swgt[tid] = ok ? wg : 0;
-        }
-    };
-    int rl[SIL_SUMS_PF], rm[SIL_SUMS_PF];
-#pragma unroll
-    for (int i = 0; i < SIL_SUMS_PF; ++i) fetch(l0 + i, rl[i], rm[i]);
-    __syncthreads();  // the rows' ids in slab are read
-    put(rl[0], rm[0]);
-    fetch(l0 + SIL_SUMS_PF, rl[0], rm[0]);
     __syncthreads();
-    const int ppw = T / NW;  // positions per wave
-    for (int lg = l0; lg < l1; lg += SIL_SUMS_PF) {
+    // SU positions per lane in flight: rows from LDS, then the row loads
+    // (unconditional: q1 is zero past d, row 0 stands in for an empty
+    // position), then per labeling of the group the atomics
+    constexpr int SU = 8;
+    static_assert((PPW / RPW) % SU == 0, "walk unroll");
+    for (int i0 = 0; i0 < PPW / RPW; i0 += SU) {
+        int rr[SU];
+        long long v[SU], v2[SU];
 #pragma unroll
-        for (int i = 0; i < SIL_SUMS_PF; ++i) {
-            const int l = lg + i;
-            if (l >= l1) break;  // (block-uniform)
-            for (int p0 = wave * ppw; p0 < (wave + 1) * ppw; p0 += RPW) {
-                const int pl = p0 + sub;
+        for (int u = 0; u < SU; ++u) rr[u] = srow[wave * PPW + (i0 + u) * RPW + sub];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            v[u] = q1[(int64_t)rr[u] * DMAX + k];
+            v2[u] = q2[rr[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) asm volatile("" : "+v"(v[u]), "+v"(v2[u]));  // (keeps every load ahead of the atomics)
+        for (int g = 0; g < ng; ++g) {
+            unsigned long long* ag = acc + g * na;
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const int pl = g * SIL_SP + wave * PPW + (i0 + u) * RPW + sub;
                 const int lb = slab[pl];
                 if (lb) {
                     const long long w = swgt[pl];
-                    if (k < d) atomicAdd(&acc1[lb * d + k], (unsigned long long)(w * q1s[pl * d + k]));
+                    if (k < d) atomicAdd(&ag[lb * d + k], (unsigned long long)(w * v[u]));
                     if (k == 0) {
-                        atomicAdd(&acc2[lb], (unsigned long long)(w * q2s[pl]));
-                        atomicAdd(&accn[lb], (unsigned long long)w);
+                        atomicAdd(&ag[(cmax + 1) * d + lb], (unsigned long long)(w * v2[u]));
+                        atomicAdd(&ag[(cmax + 1) * (d + 1) + lb], (unsigned long long)w);
                     }
                 }
             }
-            sil_lds_barrier();
-            // the next labeling's labels into LDS first (its loads, issued
-            // SIL_SUMS_PF labelings ago, and the previous flush's atomics are
-            // what the wait here covers: vmcnt counts them in order), then this
-            // labeling's flush-and-zero (each entry read and cleared by one
-            // thread) and the next prefetch
-            const int s1 = (i + 1) % SIL_SUMS_PF;  // the ring slot of labeling l + 1
-            put(rl[s1], rm[s1]);
-            const int lv = q * L + l;  // (the virtual labeling)
-            unsigned long long* gs = gsum + (int64_t)lv * (cmax + 1) * d;
-            for (int t = tid; t < (cmax + 1) * d; t += SIL_ST) {
-                const unsigned long long v = acc1[t];
-                if (v) {
-                    atomicAdd(&gs[t], v);
-                    acc1[t] = 0ull;
-                }
+        }
+    }
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+        const int lv = q * L + l0 + g;  // (the virtual labeling)
+        const unsigned long long* ag = acc + g * na;
+        unsigned long long* gs = gsum + (int64_t)lv * (cmax + 1) * d;
+        for (int t = tid; t < (cmax + 1) * d; t += SIL_SB) {
+            const unsigned long long v = ag[t];
+            if (v) atomicAdd(&gs[t], v);
+        }
+        for (int c = tid; c <= cmax; c += SIL_SB) {
+            const unsigned long long n = ag[(cmax + 1) * (d + 1) + c];
+            if (n) {
+                atomicAdd(&gcnt[(int64_t)lv * (cmax + 1) + c], n);
+                atomicAdd(&gsum2[(int64_t)lv * (cmax + 1) + c], ag[(cmax + 1) * d + c]);
             }
-            for (int c = tid; c <= cmax; c += SIL_ST) {
-                if (accn[c]) {
-                    atomicAdd(&gcnt[(int64_t)lv * (cmax + 1) + c], accn[c]);
-                    atomicAdd(&gsum2[(int64_t)lv * (cmax + 1) + c], acc2[c]);
-                    accn[c] = 0ull;
-                    acc2[c] = 0ull;
-                }
-            }
-            fetch(l + 1 + SIL_SUMS_PF, rl[s1], rm[s1]);
-            sil_lds_barrier();
         }
     }
 }
@@ -1362,12 +1354,10 @@ __global__ void sil_width_exc(const double* __restrict__ x, int64_t m, int d, co
     }
 }
 
-// Positions per tiled-sums block (the largest whose LDS fits the CU), or
-// 0: the unsorted sil_centroid path.
+// Positions per sums block (SIL_SP when the block's sums fit the CU's
+// LDS), or 0: the unsorted sil_centroid path.
 static int sil_tile_T(int d, int cmax) {
-    for (int T = SIL_ST; T >= 256; T >>= 1)
-        if (sil_tile_lds(T, d, cmax) <= SIL_LDS_CU) return T;
-    return 0;
+    return sil_sums_G(d, cmax) ? SIL_SP : 0;
 }
 
 // The launch set after max|x| (and, for the distinct-cell forms, the
@@ -1393,19 +1383,17 @@ static void sil_launch(const double* x, int64_t m, int d, const int32_t* labels,
         long long* q1 = (long long*)q;
         long long* q2 = q1 + m * DMAX;
         sil_quant<DMAX><<<(unsigned)ccg_cdiv(m * DMAX, 256), 256, 0, st>>>(x, m, d, maxabs, q1, q2);
-        // about one block per CU: the representatives are ~0.64 of the rows of a bootstrap
-        const int64_t gx = seg ? ts_tiles : ccg_cdiv(m, T);
-        const int64_t tiles = seg ? (gx * 16 + 24) / 25 : ccg_cdiv(rep ? (m * 16 + 24) / 25 : m, T);
-        const int groups = (int)std::max<int64_t>(1, std::min<int64_t>(L, 256 / std::max<int64_t>(tiles, 1)));
-        const int sg = (int)ccg_cdiv(L, groups);
-        dim3 grid((unsigned)gx, (unsigned)ccg_cdiv(L, sg));
-        const size_t lds = sil_tile_lds(T, d, cmax);
+        const int ntile = (int)(seg ? ts_tiles : ccg_cdiv(m, T));
+        const int tpx = (int)ccg_cdiv(ntile, 8);
+        const int G = sil_sums_G(d, cmax);
+        const unsigned gb = (unsigned)(8 * (int64_t)tpx * ccg_cdiv(L, G));
+        const size_t lds = sil_tile_lds(d, cmax, G);
         if (seg)
-            sil_sums_tile<DMAX, true><<<grid, SIL_ST, lds, st>>>(m, d, T, sg, labels, L, cmax, q1, q2, gsum, gsum2,
-                                                                 gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
+            sil_sums_blk<DMAX, true><<<gb, SIL_SB, lds, st>>>(m, d, ntile, tpx, G, labels, L, cmax, q1, q2, gsum, gsum2,
+                                                              gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
         else
-            sil_sums_tile<DMAX, false><<<grid, SIL_ST, lds, st>>>(m, d, T, sg, labels, L, cmax, q1, q2, gsum, gsum2,
-                                                                  gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
+            sil_sums_blk<DMAX, false><<<gb, SIL_SB, lds, st>>>(m, d, ntile, tpx, G, labels, L, cmax, q1, q2, gsum, gsum2,
+                                                               gcnt, rep, mult, cnt, mw, nrep, scan, sgs);
         if (rep)
             sil_sums_exc<DMAX><<<64, 256, 0, st>>>(m, d, labels, L, cmax, q1, q2, exc, nexc, gsum, gsum2, gcnt, sgs);
         sil_mu<DMAX><<<Lv, SIL_T, 0, st>>>(m, d, cmax, maxabs, gsum, gsum2, gcnt, npres, codes, pos, mu, muc, auxc);
