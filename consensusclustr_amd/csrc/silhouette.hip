@@ -919,6 +919,42 @@ __global__ __launch_bounds__(256) void sil_w16_prep(int cmax, const unsigned* __
     }
 }
 
+typedef float sil_f2 __attribute__((ext_vector_type(2)));
+// the value of lane (lane mod 32) + 32 hb of the wave (v_permlane32_swap:
+// no LDS permute); hb = 0 the low half, 1 the high half
+__device__ __forceinline__ unsigned sil_half(unsigned v, int hb) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // {low half twice, high half twice}
+    return hb ? r[1] : r[0];
+}
+__device__ __forceinline__ int sil_half(int v, int hb) { return (int)sil_half((unsigned)v, hb); }
+__device__ __forceinline__ float sil_half(float v, int hb) { return __uint_as_float(sil_half(__float_as_uint(v), hb)); }
+__device__ __forceinline__ double sil_half(double v, int hb) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = sil_half((unsigned)b, hb), hi = sil_half((unsigned)(b >> 32), hb);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// the sum over the wave of a 64-bit integer (uniform result): DPP within
+// each row of 16 (quad xor 1, xor 2, row rotate 4, 8), then the four rows'
+// sums read from lanes 15, 31, 47, 63 -- no LDS permutes
+template <int CTRL>
+__device__ __forceinline__ unsigned long long sil_dpp64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xf, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long sil_wave_sum_u64(unsigned long long v) {
+    v += sil_dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += sil_dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += sil_dpp64<0x124>(v);  // row_ror:4
+    v += sil_dpp64<0x128>(v);  // row_ror:8
+    unsigned long long t = 0;
+#pragma unroll
+    for (int r = 15; r < 64; r += 16)
+        t += ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), r) << 32) |
+             (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, r);
+    return t;
+}
+
 template <int DMAX, int IMGB, bool SEG>
 __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
     const double* __restrict__ x, int64_t m, int d, const int32_t* __restrict__ labels, int L, int cmax,
@@ -1029,7 +1065,10 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
             const int i = po & 31;
             if (((i >> 2) & 1) == h) ownkey = (i & 3) + 4 * (i >> 3) + 16 * (po >> 5);
         }
-        float m1 = SIL_BIG, m2 = SIL_BIG;
+        // the three smallest packed values (the own cluster is dropped after
+        // the loop: three med3 per value instead of a compare, a select and
+        // two med3)
+        float m1 = SIL_BIG, m2 = SIL_BIG, m3 = SIL_BIG;
         // the packing mask in a VGPR (one v_and_or per value: VOP3 takes no literal here)
         unsigned msk = ~127u;
         asm volatile("" : "+v"(msk));
@@ -1053,29 +1092,51 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 a4 = af[2 * g];
-                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                // a = A' - 2 x.mu, two values per packed fma
+                const sil_f2 lo2 = __builtin_elementwise_fma((sil_f2){acc[4 * g], acc[4 * g + 1]}, (sil_f2){-2.0f, -2.0f},
+                                                             (sil_f2){a4.x, a4.y});
+                const sil_f2 hi2 = __builtin_elementwise_fma((sil_f2){acc[4 * g + 2], acc[4 * g + 3]},
+                                                             (sil_f2){-2.0f, -2.0f}, (sil_f2){a4.z, a4.w});
+                const float av[4] = {lo2.x, lo2.y, hi2.x, hi2.y};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int r = 4 * g + q;
-                    const float a = fmaf(-2.0f, acc[r], av[q]);
-                    float pk = __uint_as_float((__float_as_uint(a) & msk) | (unsigned)(key0 + r));
-                    pk = key0 + r == ownkey ? SIL_BIG : pk;
-                    // med3 for both (fminf would add a canonicalising max per value)
+                    unsigned kr = (unsigned)(key0 + r);
+                    asm volatile("" : "+s"(kr));  // (the key in an SGPR: one v_and_or, not and + or3)
+                    const float pk = __uint_as_float((__float_as_uint(av[q]) & msk) | kr);
+                    // (med3 throughout: fminf would add a canonicalising max per value)
+                    m3 = __builtin_amdgcn_fmed3f(m2, pk, m3);
                     m2 = __builtin_amdgcn_fmed3f(m1, pk, m2);
                     m1 = __builtin_amdgcn_fmed3f(-SIL_BIG, m1, pk);
                 }
             }
         }
-        // merge the lane halves: the smallest, its centroid, the second smallest
+        if (ownkey >= 0) {  // (keys are distinct: at most one of the three is the own cluster)
+            if ((int)(__float_as_uint(m1) & 127u) == ownkey) {
+                m1 = m2;
+                m2 = m3;
+            } else if ((int)(__float_as_uint(m2) & 127u) == ownkey) {
+                m2 = m3;
+            }
+        }
+        // merge the lane halves (v_permlane32_swap: each half gets the other's
+        // value): the smallest, its centroid, the second smallest
         const unsigned kb = __float_as_uint(m1) & 127u;
         const int myarg = (int)((kb & 3) + 8 * ((kb >> 2) & 3) + 4 * h + 32 * (kb >> 4));
-        const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
-        const int oarg = __shfl_xor(myarg, 32, 64);
-        const int arg1 = (m1 < o1 || (m1 == o1 && h == 0)) ? myarg : oarg;
-        const float n1 = fminf(m1, o1), n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
+        const float m1l = sil_half(m1, 0), m1h = sil_half(m1, 1);
+        const float m2l = sil_half(m2, 0), m2h = sil_half(m2, 1);
+        const int al = sil_half(myarg, 0), ahh = sil_half(myarg, 1);
+        const int arg1 = m1l <= m1h ? al : ahh;
+        const float n1 = fminf(m1l, m1h), n2 = fminf(fmaxf(m1l, m1h), fminf(m2l, m2h));
         const bool none = !(n1 < 1.0e37f);  // no other cluster
+        // E bounds the error of one screened value a (scaled units; see the
+        // header): 2 x (3 2^-22 + 95 2^-24) xn mbs for the split and the fp32
+        // accumulation of 3 DMAX products, 2^-13 sqrt(d) (xn + mbs) for the
+        // parts flushed below 2^-14, (2^-16 + 2^-23) |a| for the 7-bit
+        // packing and the fma, |a| <= abs2 + 2 xn mbs: within 2^-14 xn mbs +
+        // 2^-13 sqrt(d) (xn + mbs) + 2^-15 abs2 (+8 for what is left)
         const double mbs = ldexp(sbnd[0], e16), abs2 = ldexp(sbnd[1], 2 * e16);
-        const double E = 0x1p-13 * xn * mbs + 0x1p-11 * sqd * (xn + mbs) + 0x1p-14 * abs2 + 8.0;
+        const double E = 0x1p-14 * xn * mbs + 0x1p-13 * sqd * (xn + mbs) + 0x1p-15 * abs2 + 8.0;
         const bool amb = !none && (double)n2 - (double)n1 <= 2.0 * E;
         auto dsq = [&](int c) {
             const double* mr = smu + c * DMAX;
@@ -1150,19 +1211,33 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
                 for (int c = h; c < C; c += 2)
                     if (full && c != po) O = fmin(O, dsq(c));
         }
-        O = fmin(O, __shfl_xor(O, 32, 64));
+        O = fmin(O, sil_half(O, 0));
+        O = fmin(O, sil_half(O, 1));  // (both halves: the minimum over the wave's pair of lanes)
+        // one square root per lane (h = 0 the own distance, h = 1 the other),
+        // exchanged between the halves
+        const double rt = sqrt(h == 0 ? S : O);
+        const double rt1 = sil_half(rt, 1);  // (every lane takes part in the swap)
+        const double ort = h == 0 ? rt1 : rt;
         long long wq = 0;
         unsigned wn = 0;
-        sil_row_width(S, O, in && h == 0, C, wsc,
-                      (out_width && !rep && in && h == 0) ? out_width + (int64_t)l * m + p : nullptr, wq, wn, wt);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            wq += __shfl_xor(wq, o, 64);
-            wn += __shfl_xor(wn, o, 64);
+        if (in && h == 0) {
+            double w = 0.0;
+            if (C > 1) {
+                double mx = fmax(ort, rt);
+                if (isnan(ort) || isnan(rt)) mx = NAN;
+                w = (ort - rt) / mx;
+            }
+            if (out_width && !rep) out_width[(int64_t)l * m + p] = w;
+            if (!isnan(w)) {
+                wq = (long long)wt * __double2ll_rn(w * wsc);
+                wn = (unsigned)wt;
+            }
         }
+        const unsigned long long tq = sil_wave_sum_u64((unsigned long long)wq);
+        const unsigned long long tn = sil_wave_sum_u64((unsigned long long)wn);
         if (lane == 0) {
-            wsum[(int64_t)(lq + l) * nbw + 4 * tb + wave] = (unsigned long long)wq;
-            wcnt[(int64_t)(lq + l) * nbw + 4 * tb + wave] = (unsigned long long)wn;
+            wsum[(int64_t)(lq + l) * nbw + 4 * tb + wave] = tq;
+            wcnt[(int64_t)(lq + l) * nbw + 4 * tb + wave] = tn;
         }
         lab = labn;
         mlt = mltn;
