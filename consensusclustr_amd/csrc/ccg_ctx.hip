@@ -57,10 +57,14 @@ extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
     }
     e = hipMalloc(&c->d_err, 64);
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, 64);
+    if (e == hipSuccess) e = hipMalloc(&c->d_scan, SCAN_LB_BYTES);
+    if (e == hipSuccess) e = hipMemset(c->d_scan, 0, SCAN_LB_BYTES);
     if (e != hipSuccess) {
+        if (c->d_err) (void)hipFree(c->d_err);
+        if (c->d_scan) (void)hipFree(c->d_scan);
         (void)hipStreamDestroy(c->stream);
         delete c;
-        return ccg_hip_fail(e, "hipMalloc(d_err)", __FILE__, __LINE__);
+        return ccg_hip_fail(e, "hipMalloc(d_err, d_scan)", __FILE__, __LINE__);
     }
     *out = c;
     return CCG_OK;
@@ -83,6 +87,7 @@ extern "C" int ccg_close(ccg_ctx* ctx) {
     }
     ccg_snn_stage_free(ctx);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->d_scan) (void)hipFree(ctx->d_scan);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return CCG_OK;
@@ -323,19 +328,33 @@ __global__ __launch_bounds__(SCAN_T) void scan_tiles(const int64_t* in, int64_t*
     if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = bsum[nb];
 }
 
-// Second pass for up to SCAN_DIRECT_MAX tiles: each block adds up the raw
-// sums of the tiles before it itself (<= 1024 loads), so the single-block
-// pass over the tile sums -- a launch on the critical path -- is skipped.
-#define SCAN_DIRECT_MAX 1024
-__global__ __launch_bounds__(SCAN_T) void scan_tiles_direct(const int64_t* in, int64_t* out, int64_t n,
-                                                            const int64_t* __restrict__ bsum, int64_t nb) {
+// Single pass for up to SCAN_LB_MAX tiles (decoupled look-back): block b
+// scans its tile and publishes a status word, (1 << 62) | aggregate, then
+// walks back over the words of the tiles before it -- adding aggregates
+// until it meets an inclusive prefix, (2 << 62) | prefix -- and publishes
+// its own inclusive prefix; wave 0 reads 64 predecessors' words per round
+// (one per lane: one word per round took ~1 us per predecessor, the words
+// being read past the L2).  One launch instead of the tile-sums pass plus
+// the tile pass (two launches on the critical path of each of a bootstrap's
+// ~8 scans).  Status and value share one 64-bit word, so relaxed
+// device-scope atomics suffice: no release / acquire fences (their L2
+// write-back and invalidate cost a first version of this kernel 21 us per
+// call under three streams).  A block waits only on lower-numbered blocks,
+// which the dispatcher starts first.  The last block to finish (the
+// finished count) clears the words for the next call, so the kernel needs no
+// per-call epoch and replays from a HIP graph.  Tile sums and prefixes must
+// lie in [0, 2^62): the library scans counts.
+#define SCAN_ST_AGG (1ull << 62)
+#define SCAN_ST_INC (2ull << 62)
+#define SCAN_VAL_MASK ((1ull << 62) - 1)
+__global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_t* out, int64_t n, int nb,
+                                                       unsigned long long* __restrict__ stat,
+                                                       unsigned* __restrict__ done) {
     __shared__ int64_t sh[SCAN_T / 64];
+    __shared__ int64_t pref;
     constexpr int E = SCAN_TILE / SCAN_T;
-    int64_t pre = 0;
-    for (int64_t b = threadIdx.x; b < blockIdx.x; b += SCAN_T) pre += bsum[b];
-    int64_t prefix;
-    block_excl_scan(pre, sh, &prefix);
-    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * E;
+    const int b = blockIdx.x;
+    const int64_t base = (int64_t)b * SCAN_TILE + threadIdx.x * E;
     int64_t v[E];
     int64_t s = 0;
 #pragma unroll
@@ -344,13 +363,59 @@ __global__ __launch_bounds__(SCAN_T) void scan_tiles_direct(const int64_t* in, i
         s += v[e];
     }
     int64_t tot;
-    int64_t ex = block_excl_scan(s, sh, &tot) + prefix;
+    int64_t ex = block_excl_scan(s, sh, &tot);
+    if (threadIdx.x < 64) {  // wave 0: the look-back, 64 predecessors per round (one per lane)
+        const int lane = threadIdx.x;
+        unsigned long long run = 0;
+        if (b == 0) {
+            if (lane == 0)
+                __hip_atomic_store(&stat[0], SCAN_ST_INC | ((unsigned long long)tot & SCAN_VAL_MASK),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&stat[b], SCAN_ST_AGG | ((unsigned long long)tot & SCAN_VAL_MASK),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int j0 = b - 1;;) {
+                const int j = j0 - lane;  // (j < 0 reads as a prefix past tile 0's, which is never reached)
+                const unsigned long long w =
+                    j >= 0 ? __hip_atomic_load(&stat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SCAN_ST_INC;
+                const unsigned long long st2 = w >> 62;
+                const unsigned long long inc = __ballot(st2 == 2);
+                const int lim = inc ? __ffsll((long long)inc) - 1 : 64;  // the nearest inclusive prefix
+                const unsigned long long need = lim == 64 ? ~0ull : ((2ull << lim) - 1);
+                if (__ballot(st2 == 0) & need) {  // a tile before it has not published yet (wave-uniform)
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long v = lane <= lim ? (w & SCAN_VAL_MASK) : 0ull;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                run += v;
+                if (lim < 64) break;
+                j0 -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&stat[b], SCAN_ST_INC | ((run + (unsigned long long)tot) & SCAN_VAL_MASK),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) pref = (int64_t)run;
+    }
+    __syncthreads();
+    ex += pref;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         if (base + e < n) out[base + e] = ex;
         ex += v[e];
     }
-    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = prefix + tot;
+    if (b == nb - 1 && threadIdx.x == 0) out[n] = pref + tot;
+    if (threadIdx.x == 0) {
+        // every block counted here has finished its look-back
+        const unsigned t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == (unsigned)nb - 1) {
+            for (int j = 0; j < nb; ++j) __hip_atomic_store(&stat[j], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
@@ -359,14 +424,15 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipSt
         return CCG_OK;
     }
     int64_t nb = ccg_cdiv(n, SCAN_TILE);
-    int64_t* bsum = (int64_t*)ccg_ws(ctx, WS_SCAN, sizeof(int64_t) * (nb + 1));
-    if (!bsum) return CCG_ENOMEM;
-    scan_tile_sums<<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
-    if (nb <= SCAN_DIRECT_MAX) {
-        scan_tiles_direct<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
+    if (nb <= SCAN_LB_MAX) {
+        unsigned long long* stat = (unsigned long long*)ctx->d_scan;
+        scan_onepass<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, (int)nb, stat, (unsigned*)(stat + SCAN_LB_MAX));
         CCG_HIP(hipGetLastError());
         return CCG_OK;
     }
+    int64_t* bsum = (int64_t*)ccg_ws(ctx, WS_SCAN, sizeof(int64_t) * (nb + 1));
+    if (!bsum) return CCG_ENOMEM;
+    scan_tile_sums<<<(unsigned)nb, SCAN_T, 0, st>>>(in, n, bsum);
     scan_block_sums<<<1, SCAN_T, 0, st>>>(bsum, nb);
     scan_tiles<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, bsum, nb);
     CCG_HIP(hipGetLastError());

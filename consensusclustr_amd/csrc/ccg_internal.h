@@ -102,6 +102,10 @@ struct ccg_ctx {
     size_t pin_bytes[CCG_PIN_RING];
     hipEvent_t pin_ev[CCG_PIN_RING];
     int pin_next;
+    // single-pass scan state (ccg_scan_i64): per-tile status words and the
+    // finished-tile count, zero between calls (the kernel's last tile clears
+    // them)
+    void* d_scan;
     // kernel timing (ccg_timing_*)
     int timing;
     ccg_timer_rec* timers;   // pool, grows
@@ -154,6 +158,10 @@ static inline hipStream_t ccg_pick_stream(ccg_ctx* ctx, void* s) {
 
 // Exclusive scan of int64 values on device: out[i] = sum_{t<i} in[i]; the
 // total goes to out[n].  in may alias out.  Uses WS_SCAN.
+// ccg_scan_i64's single pass: up to SCAN_LB_MAX tiles; its state (status
+// words, finished count) in ctx->d_scan
+#define SCAN_LB_MAX 1024
+#define SCAN_LB_BYTES (SCAN_LB_MAX * 8 + 64)
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n,
                  hipStream_t st);
 

@@ -281,6 +281,47 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
     if (__any(nan) && lane == 0) cc.flags[0] = 1;
 }
 
+// Tile order (round 5).  Tiles (row tile I of 128 rows from I0, column
+// tile J of 256) are grouped into supertiles of COF_ST x COF_ST: row tiles
+// 8g..8g+7 of the slab and column tiles Jlo_g + 8s.. (Jlo_g = the first
+// column tile of the group's first row: (I0 + 8g) / 2 in the triangle, 0 for
+// full rows).  Supertile S runs on XCD S mod 8 (block b runs on XCD b mod 8),
+// its 64 tiles as XCD-consecutive blocks, so the ~64 blocks an XCD holds at
+// once share 8 A panels and 8 B panels of the entry matrix in that XCD's L2
+// (~1 MB at cfg3).  Row-major tile order re-read every B panel from beyond
+// the L2 for each row tile: 1.9e10 B per launch at N = 100k, B = 125
+// (profiles/r04_pmc_cocluster_traffic.md).  Slots outside the slab, the
+// column range or the triangle (J < I / 2) exit.
+#define COF_ST 8
+__host__ __device__ inline int64_t cof_supertiles_row(int64_t g, int64_t TC, int64_t I0, bool tri) {
+    const int64_t jlo = tri ? (I0 + COF_ST * g) / 2 : 0;
+    return (TC - jlo + COF_ST - 1) / COF_ST;
+}
+// blocks of the launch: 8 XCDs x 64 slots x the supertiles per XCD
+static inline int64_t cof_tile_blocks(int64_t TR, int64_t TC, int64_t I0, bool tri) {
+    int64_t ns = 0;
+    for (int64_t g = 0; g < (TR + COF_ST - 1) / COF_ST; ++g) ns += cof_supertiles_row(g, TC, I0, tri);
+    return 8 * (int64_t)COF_ST * COF_ST * ((ns + 7) / 8);
+}
+__device__ __forceinline__ bool cof_tile_of(int64_t b, int64_t TR, int64_t TC, int64_t I0, bool tri, int64_t& I,
+                                            int64_t& J) {
+    const int64_t k = b >> 3;
+    const int64_t S = (k / (COF_ST * COF_ST)) * 8 + (b & 7);  // supertile
+    const int slot = (int)(k % (COF_ST * COF_ST));
+    const int64_t G = (TR + COF_ST - 1) / COF_ST;
+    int64_t g = 0, cum = 0;
+    for (; g < G; ++g) {  // (block-uniform scalar loop: G ~ 100 at N = 100k)
+        const int64_t n = cof_supertiles_row(g, TC, I0, tri);
+        if (S < cum + n) break;
+        cum += n;
+    }
+    if (g == G) return false;
+    const int64_t Ir = COF_ST * g + slot / COF_ST;
+    I = I0 + Ir;
+    J = (tri ? (I0 + COF_ST * g) / 2 : 0) + COF_ST * (S - cum) + slot % COF_ST;
+    return Ir < TR && J < TC && (!tri || J >= I / 2);
+}
+
 // E: the chunk's entry matrix (cof_entries_kernel), Npad bytes per slot.
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
@@ -292,25 +333,9 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
     constexpr int LOADS = COF_SLOTS * ROWD / 256;       // dwords per thread per stage
     __shared__ __attribute__((aligned(16))) uint8_t panel[2][COF_SLOTS][COF_ROWS];
     __shared__ __attribute__((aligned(16))) v4i ftab[COF_TAB];
-    const int64_t t = blockIdx.x;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     int64_t I, J;
-    if (MODE != COF_RECT) {
-        // tile t -> (I, J): row tiles of 128 from I0, col tiles of 256 from J = I/2
-        // cum(Ir) = sum_{s<Ir} (TC - (I0+s)/2)
-        auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };  // sum_{s<x} s/2
-        auto cum = [&](int64_t Ir) { return Ir * TC - (fl(I0 + Ir) - fl(I0)); };
-        int64_t lo = 0, hi = TR;
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (cum(mid) <= t) lo = mid; else hi = mid;
-        }
-        I = I0 + lo;
-        J = I / 2 + (t - cum(lo));
-    } else {
-        I = I0 + t / TC;
-        J = t - (t / TC) * TC;
-    }
+    if (!cof_tile_of(blockIdx.x, TR, TC, I0, MODE != COF_RECT, I, J)) return;
     const int64_t rowA0 = I * COF_BM, rowB0 = J * COF_BN;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -593,7 +618,8 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
     else
         cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                          pl.nslot, pl.E);
-    cof_tile_kernel<MODE><<<(unsigned)ntiles, 256, 0, st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
+    cof_tile_kernel<MODE><<<(unsigned)cof_tile_blocks(ccg_cdiv(r1 - r0, COF_BM), TC, I0, MODE != COF_RECT), 256, 0,
+                            st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
                                                             both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
 }
 
@@ -617,7 +643,7 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
-    CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_dev: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, true) < (1LL << 31), "ccg_cocluster_dev: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     uint16_t *pco = co, *pboth = both;  // partial counts between chunks
     if (nch > 1 && (!co || !both)) {
@@ -653,7 +679,7 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
     const int64_t I0 = r0 / COF_BM;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     const int64_t ntiles = TR * TC;
-    CCG_REQUIRE(ntiles < (1LL << 31), "ccg_cocluster_rows: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, false) < (1LL << 31), "ccg_cocluster_rows: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t cb0 = pl.cuts[c], Bc = pl.cuts[c + 1] - cb0;
@@ -973,7 +999,7 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     const int64_t TC = ccg_cdiv(N, COF_BN), TR = ccg_cdiv(N, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - fl(TR);
-    CCG_REQUIRE(ntiles < (1LL << 31), "consensus kNN: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, 0, true) < (1LL << 31), "consensus kNN: too many tiles");
     CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, ~0ull / (uint64_t)N, flags};
     cof_launch<COF_CAND>(label_bits, Ap, 0, B, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
                          nullptr, nullptr, st, N, cc);

@@ -166,9 +166,16 @@ __device__ __forceinline__ int knn_scale_exp(const unsigned* maxabs_bits) {
 __device__ __forceinline__ void knn_split16(double xs, _Float16& hi, _Float16& lo) {
     // parts below the smallest normal fp16 are flushed here, explicitly,
     // so the certification floor (KNN_F16_FLOOR) holds in any denorm mode
-    hi = (_Float16)(float)xs;
+    // (the fp32 values are pinned in registers: without that the compiler
+    // folds double -> float -> half into a ~40-instruction software
+    // conversion; with it, v_cvt_f32_f64 + v_cvt_f16_f32, the same rounding)
+    float f = (float)xs;
+    asm volatile("" : "+v"(f));
+    hi = (_Float16)f;
     if (fabs((double)(float)hi) < KNN_F16_FLOOR) hi = (_Float16)0.0f;
-    lo = (_Float16)(float)(xs - (double)(float)hi);
+    float r = (float)(xs - (double)(float)hi);
+    asm volatile("" : "+v"(r));
+    lo = (_Float16)r;
     if (fabs((double)(float)lo) < KNN_F16_FLOOR) lo = (_Float16)0.0f;
 }
 
@@ -1106,7 +1113,7 @@ static int knn_seg_plan(ccg_ctx* ctx, const int64_t* seg_off, int nseg, int d, i
 #define KNN_FX_CAP 1024
 #define KNN_FX_ROWS 16384
 #define KNN_FX_CHUNK 64
-#define KNN_FX_GRID 1024
+#define KNN_FX_GRID 512   // (grid-stride; a failed group of 64 rows spans n / 256 units)
 
 template <int DMAX>
 __device__ __forceinline__ double knn_exact_d2(const double (&xq)[DMAX], const double* y, int d) {
@@ -2069,6 +2076,7 @@ __global__ void kt_transpose_kernel(const double* __restrict__ pcs, int64_t N, i
 // per-thread-list search) when fewer than kq are found.  Lane t holds the
 // cell's table entry v (-1 past K), present as distinct cell u1 (-1: absent).
 #define KT_SYNC() do { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); } while (0)
+#define KT_TB 8  // table entries tested per round in kt_tau_wave
 struct KtTauLds {
     int hset[128];  // the cell's own table row as an open-addressing set (K <= 48 of 128 slots)
     int pick[64];
@@ -2087,21 +2095,32 @@ __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int
             if (prev == -1 || prev == v) break;
         }
     KT_SYNC();
+    // the first entry of v's row that is present and outside the cell's row:
+    // KT_TB entries per round (independent loads; one entry per round was a
+    // chain of dependent loads tens of entries long, and this wave the
+    // filter kernel's critical path)
     int w = -1;
     if (v >= 0) {
-        for (int s = 0; s < K && w < 0; ++s) {
-            const int x = tab_idx[(int64_t)v * K + s];
-            if (x < 0 || x == (int)c || cell2u[x] < 0) continue;
-            bool in_row = false;
-            for (int h = hslot(x);; h = (h + 1) & 127) {
-                const int y = S.hset[h];
-                if (y == x) {
-                    in_row = true;
-                    break;
+        for (int s0 = 0; s0 < K && w < 0; s0 += KT_TB) {
+            int x[KT_TB], pr[KT_TB];
+#pragma unroll
+            for (int j = 0; j < KT_TB; ++j) x[j] = s0 + j < K ? tab_idx[(int64_t)v * K + s0 + j] : -1;
+#pragma unroll
+            for (int j = 0; j < KT_TB; ++j) pr[j] = (x[j] >= 0 && x[j] != (int)c) ? cell2u[x[j]] : -1;
+#pragma unroll
+            for (int j = 0; j < KT_TB; ++j) {
+                if (w >= 0 || pr[j] < 0) continue;
+                bool in_row = false;
+                for (int h = hslot(x[j]);; h = (h + 1) & 127) {
+                    const int y = S.hset[h];
+                    if (y == x[j]) {
+                        in_row = true;
+                        break;
+                    }
+                    if (y == -1) break;
                 }
-                if (y == -1) break;
+                if (!in_row) w = x[j];
             }
-            if (!in_row) w = x;
         }
     }
     S.pick[lane] = w;
@@ -2112,10 +2131,23 @@ __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int
     if (w >= 0 && !dup) {
         const double* xr = urows + (int64_t)uid * d;
         const double* yr = urows + (int64_t)cell2u[w] * d;
+        // (the dimension-order sum; loads issued 8 dimensions at a time --
+        // one dependent load pair per dimension made this the filter
+        // kernel's critical path)
         double s2 = 0.0;
-        for (int k = 0; k < d; ++k) {
-            const double t = __dsub_rn(xr[k], yr[k]);
-            s2 = __dadd_rn(s2, __dmul_rn(t, t));
+        for (int k0 = 0; k0 < d; k0 += 8) {
+            double a[8], b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[j] = k0 + j < d ? xr[k0 + j] : 0.0;
+                b[j] = k0 + j < d ? yr[k0 + j] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k0 + j < d) {
+                    const double t = __dsub_rn(a[j], b[j]);
+                    s2 = __dadd_rn(s2, __dmul_rn(t, t));
+                }
         }
         val2 = s2;
     }
@@ -2137,10 +2169,13 @@ __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int
     return best;
 }
 
-// one wave per distinct cell: the first kq present entries of its table row;
-// a cell short of kq of them joins the exact search with its radius (round
-// 5: taken here, in the same wave, instead of a separate kt_tau pass over the
-// failed list)
+// KT_CPW distinct cells per wave: the first kq present entries of each one's
+// table row; a cell short of kq of them joins the exact search with its
+// radius (round 5: taken here, in the same wave, instead of a separate
+// kt_tau pass over the failed list).  The kernel is a chain of dependent
+// gathers (distinct id -> cell -> table row -> presence); the cells of a wave
+// issue each level's loads together.
+#define KT_CPW 2
 __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, int d, const int* __restrict__ ustart,
                                                         const int32_t* __restrict__ scell,
                                                         const int* __restrict__ cell2u,
@@ -2150,25 +2185,42 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, in
                                                         double* __restrict__ ud2, int* __restrict__ fail_list,
                                                         int* __restrict__ fail_count, double* __restrict__ tau) {
     __shared__ KtTauLds tl[4];
-    const int uid = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (uid >= u) return;
+    const int u0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * KT_CPW;
+    if (u0 >= u) return;
     const int lane = threadIdx.x & 63;
-    const int64_t c = scell[ustart[uid]];
-    const int v = lane < K ? tab_idx[c * K + lane] : -1;
-    const int w = v >= 0 ? cell2u[v] : -1;
-    const double dv = w >= 0 ? tab_d2[c * K + lane] : INFINITY;
-    const unsigned long long m = __ballot(w >= 0);
-    const int rank = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
-    if (w >= 0 && rank < kq) {
-        uidx[(int64_t)uid * kq + rank] = w;
-        ud2[(int64_t)uid * kq + rank] = dv;
+    int64_t c[KT_CPW];
+    int v[KT_CPW], w[KT_CPW];
+    double dv[KT_CPW];
+#pragma unroll
+    for (int i = 0; i < KT_CPW; ++i) c[i] = u0 + i < u ? ustart[u0 + i] : -1;
+#pragma unroll
+    for (int i = 0; i < KT_CPW; ++i) c[i] = c[i] >= 0 ? scell[c[i]] : -1;
+#pragma unroll
+    for (int i = 0; i < KT_CPW; ++i) {
+        const bool e = c[i] >= 0 && lane < K;
+        v[i] = e ? tab_idx[c[i] * K + lane] : -1;
+        dv[i] = e ? tab_d2[c[i] * K + lane] : INFINITY;
     }
-    if (__popcll(m) < kq) {  // (wave-uniform)
-        const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c, v, w, dv, cell2u, tab_idx, urows);
-        if (lane == 0) {
-            const int f = atomicAdd(fail_count, 1);
-            fail_list[f] = uid;
-            tau[f] = best;
+#pragma unroll
+    for (int i = 0; i < KT_CPW; ++i) w[i] = v[i] >= 0 ? cell2u[v[i]] : -1;
+    for (int i = 0; i < KT_CPW; ++i) {
+        const int uid = u0 + i;
+        if (uid >= u) break;  // (wave-uniform)
+        const double di = w[i] >= 0 ? dv[i] : INFINITY;
+        const unsigned long long m = __ballot(w[i] >= 0);
+        const int rank = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        if (w[i] >= 0 && rank < kq) {
+            uidx[(int64_t)uid * kq + rank] = w[i];
+            ud2[(int64_t)uid * kq + rank] = di;
+        }
+        if (__popcll(m) < kq) {  // (wave-uniform)
+            const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c[i], v[i], w[i], di, cell2u,
+                                            tab_idx, urows);
+            if (lane == 0) {
+                const int f = atomicAdd(fail_count, 1);
+                fail_list[f] = uid;
+                tau[f] = best;
+            }
         }
     }
 }
@@ -2290,7 +2342,7 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
         int* ufail = (int*)(misc + 5);
-        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2,
+        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4 * KT_CPW), 256, 0, st>>>(u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2,
                                                                    urows, uidx, ud2, fail_list, ufail, ftau);
         rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau);
         if (rc) return rc;

@@ -856,9 +856,12 @@ __host__ __device__ inline int sil_e16(double maxabs) {
 }
 
 __device__ __forceinline__ void sil_split16(double v, _Float16& hi, _Float16& lo) {
-    const float f = (float)v;
+    // (fp32 pinned in registers: see knn_split16)
+    float f = (float)v;
+    asm volatile("" : "+v"(f));
     hi = fabsf(f) < 0x1p-14f ? (_Float16)0.0f : (_Float16)f;
-    const float r = (float)(v - (double)(float)hi);
+    float r = (float)(v - (double)(float)hi);
+    asm volatile("" : "+v"(r));
     lo = fabsf(r) < 0x1p-14f ? (_Float16)0.0f : (_Float16)r;
 }
 
