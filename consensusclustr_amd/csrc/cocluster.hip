@@ -860,62 +860,73 @@ __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B
     }
 }
 
-// tstar[row] for rows [a, b): from cb[(row - a) * NS + q], the k-th largest
-// fp32 similarity over q != row with both > 0, minus half an ulp (as a
-// double, exact); -inf when fewer than k sampled columns are usable.
+// tstar[row] for rows [a, b): a lower bound of the k-th largest fp32
+// similarity over the sampled columns q != row with both > 0 (-inf when fewer
+// than k are usable).  One wave per row counts its sampled similarities into
+// CKC_NBK buckets of width 1 / CKC_NBK in LDS (bucket of the approximate
+// quotient c * rcp(u), within one bucket of the exact one), finds the bucket
+// bk holding the k-th largest by a suffix count, and takes (bk - 1) /
+// CKC_NBK: the k values at or above bucket bk are all >= that.  Round 4 kept
+// a sorted 32-entry register list per lane (a 32-step insertion chain per
+// value: 5.5 ms per call at N = 100k); the bound is now looser by at most
+// 2 / CKC_NBK, a few more candidates per row.
+#define CKC_NBK 4096
 __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict__ cb, int64_t a, int64_t b,
                                                       int64_t NS, int k, double* __restrict__ tstar) {
-    const int lane = threadIdx.x & 63;
-    const int64_t row = a + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= b) return;
-    const uint32_t* r = cb + (row - a) * NS;
-    float lv[CKNN_K];
-    int li[CKNN_K];
+    __shared__ unsigned hist[4][CKC_NBK];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t row = a + (int64_t)blockIdx.x * 4 + wv;
+    if (row >= b) return;  // (whole waves: the wave's LDS slice is its own)
+    unsigned* h = hist[wv];
+    constexpr int PB = CKC_NBK / 64;  // buckets per lane, lane l owning [l PB, (l + 1) PB)
 #pragma unroll
-    for (int t = 0; t < CKNN_K; ++t) {
-        lv[t] = -INFINITY;
-        li[t] = 0x7fffffff;
-    }
+    for (int i = 0; i < PB; i += 4) *reinterpret_cast<uint4*>(&h[lane * PB + i]) = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const uint32_t* r = cb + (row - a) * NS;
+    int usable = 0;
     for (int64_t q = lane; q < NS; q += 64) {
         const uint32_t v = r[q];
         const unsigned c = v & 0xFFFFu, u = v >> 16;
         if (q == row || u == 0) continue;
-        const float s = (float)((double)c / (double)u);
-        if (!(s > lv[CKNN_K - 1])) continue;
-        cknn_insert(lv, li, s, (int)q);
+        ++usable;
+        const float s = (float)c * __builtin_amdgcn_rcpf((float)u);
+        const int bk = min(CKC_NBK - 1, max(0, (int)(s * (float)CKC_NBK)));
+        atomicAdd(&h[bk], 1u);
     }
-    // k rounds of wave arg-max: the k-th extracted value
-    float kth = -INFINITY;
-    for (int rr = 0; rr < k; ++rr) {
-        float bk = lv[0];
-        int bi = li[0];
+    for (int o = 32; o > 0; o >>= 1) usable += __shfl_xor(usable, o, 64);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // the lane holding the k-th largest: suffix sums of the lanes' bucket counts
+    int mine = 0;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ok = __shfl_xor(bk, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (ok > bk || (ok == bk && oi < bi)) {
-                bk = ok;
-                bi = oi;
+    for (int i = 0; i < PB; ++i) mine += (int)h[lane * PB + i];
+    int suf = mine;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += y;
+    }
+    // the highest lane whose suffix reaches k (suffix sums fall with the lane)
+    const unsigned long long reach = __ballot(suf >= k);
+    double t = -INFINITY;
+    if (usable >= k && reach) {
+        const int L = 63 - __clzll(reach);
+        int bk = 0;
+        if (lane == L) {
+            int acc = suf - mine;  // values above this lane's buckets
+            for (int i = PB - 1; i >= 0; --i) {
+                acc += (int)h[lane * PB + i];
+                if (acc >= k) {
+                    bk = lane * PB + i;
+                    break;
+                }
             }
         }
-        kth = bk;
-        if (li[0] == bi) {
-#pragma unroll
-            for (int t = 0; t < CKNN_K - 1; ++t) {
-                lv[t] = lv[t + 1];
-                li[t] = li[t + 1];
-            }
-            lv[CKNN_K - 1] = -INFINITY;
-            li[CKNN_K - 1] = 0x7fffffff;
-        }
+        bk = __shfl(bk, L, 64);
+        t = bk >= 2 ? (double)(bk - 1) / (double)CKC_NBK : -1.0;  // (<= 0: every co-sampled pair qualifies)
     }
-    if (lane == 0) {
-        double t;
-        if (!(kth > -INFINITY)) t = -INFINITY;
-        else if (kth <= 0.0f) t = -1.0;  // every co-sampled pair qualifies
-        else t = (double)kth - ldexp(1.0, ilogbf(kth) - 24);
-        tstar[row] = t;
-    }
+    if (lane == 0) tstar[row] = t;
 }
 
 // Per permuted row (one wave): the row's candidates, exact fp32 similarity,
