@@ -842,11 +842,13 @@ typedef float sil_f16x __attribute__((ext_vector_type(16)));
 
 // image of a labeling with cpl = 32 x tiles centroid slots: fragments
 // [cpl][64] f16 (8 chunks (s, hi/lo, h) of 8, chunk q at q ^ (c & 7)),
-// centroids [cpl][DMAX] f64 (16-byte chunk q at q ^ (c & (DMAX/2 - 1))),
-// v [cpl] f64, A' [cpl] f32 (SIL_BIG: padding), bounds 2 f64, code ->
-// ordinal [cmax+1] int
+// centroid rows [cpl][DMAX + 2] f64 (mu, then v_c, then a pad: the odd
+// 16-byte stride puts the lanes' reads of different centroids in different
+// bank groups, and a lane's 16 reads of one row take immediate offsets --
+// round 5 first XOR-swizzled the chunks, two VALU per read), A' [cpl] f32
+// (SIL_BIG: padding), bounds 2 f64, code -> ordinal [cmax+1] int
 __host__ __device__ inline size_t sil_img_bytes(int cpl, int dmax, int cmax) {
-    return (size_t)cpl * (128 + 8 * (size_t)dmax + 12) + 16 + 4 * (size_t)(cmax + 1);
+    return (size_t)cpl * (128 + 8 * ((size_t)dmax + 2) + 4) + 16 + 4 * (size_t)(cmax + 1);
 }
 __host__ __device__ inline size_t sil_img_stride(int cmax, int dmax) {
     return (sil_img_bytes((cmax + 31) & ~31, dmax, cmax) + 1023) & ~(size_t)1023;
@@ -878,8 +880,7 @@ __global__ __launch_bounds__(256) void sil_w16_prep(int cmax, const unsigned* __
     unsigned char* base = img + (size_t)l * imgs;
     _Float16* fr = (_Float16*)base;
     double* m64 = (double*)(base + (size_t)cpl * 128);
-    double* sv = m64 + (size_t)cpl * DMAX;
-    float* sa = (float*)(sv + cpl);
+    float* sa = (float*)(m64 + (size_t)cpl * (DMAX + 2));
     double* bnd = (double*)(sa + cpl);
     int* sp = (int*)(bnd + 2);
     const int e16 = sil_e16((double)__uint_as_float(*maxabs_bits));
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(256) void sil_w16_prep(int cmax, const unsigned* __
     for (int t = tid; t < cpl * DMAX; t += 256) {
         const int c = t / DMAX, k = t - c * DMAX;
         const double v = c < C ? ml[(int64_t)cl[c] * DMAX + k] : 0.0;
-        m64[c * DMAX + ((((k >> 1) ^ (c & (DMAX / 2 - 1)))) << 1) + (k & 1)] = v;
+        m64[c * (DMAX + 2) + k] = v;
         _Float16 hi, lo;
         sil_split16(ldexp(v, e16), hi, lo);
         const int s = k >> 4, hh = (k >> 3) & 1, i = k & 7;
@@ -900,7 +901,8 @@ __global__ __launch_bounds__(256) void sil_w16_prep(int cmax, const unsigned* __
     for (int c = tid; c < cpl; c += 256) {
         const bool pr = c < C;
         const double a0 = pr ? al[2 * c] : 0.0, a1 = pr ? al[2 * c + 1] : 0.0;
-        sv[c] = a1;
+        m64[c * (DMAX + 2) + DMAX] = a1;
+        m64[c * (DMAX + 2) + DMAX + 1] = 0.0;
         sa[c] = pr ? (float)ldexp(a0 + a1, 2 * e16) : SIL_BIG;
         mb = fmax(mb, a0);
         ab = fmax(ab, a0 + a1);
@@ -945,6 +947,14 @@ __device__ __forceinline__ unsigned long long sil_dpp64(unsigned long long v) {
     const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xf, 0xf, false);
     return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ unsigned sil_wave_sum_u32(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 15) + (unsigned)__builtin_amdgcn_readlane((int)v, 31) +
+           (unsigned)__builtin_amdgcn_readlane((int)v, 47) + (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ unsigned long long sil_wave_sum_u64(unsigned long long v) {
     v += sil_dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
     v += sil_dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -967,7 +977,6 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
     const int* __restrict__ cnt, int64_t mw, int nbw, const int64_t* __restrict__ nrep, double wsc, double sqd,
     const int64_t* __restrict__ scan, SilSegs sgs) {
     constexpr int KS = DMAX / 16;  // K steps of 16 dimensions
-    constexpr int QM = DMAX / 2 - 1;  // fp64 chunk swizzle mask
     // two image buffers as two objects, and the labeling loop unrolled by two,
     // so the compiler sees that the copy into one does not alias the reads of
     // the other (with one array it waits for the copy before every LDS read)
@@ -1048,8 +1057,7 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
         __syncthreads();  // image l has landed; the other buffer is free
         const _Float16* sA = (const _Float16*)bs;
         const double* smu = (const double*)(bs + (size_t)cpl * 128);
-        const double* sv = smu + (size_t)cpl * DMAX;
-        const float* sAf = (const float*)(sv + cpl);
+        const float* sAf = (const float*)(smu + (size_t)cpl * (DMAX + 2));
         const double* sbnd = (const double*)(sAf + cpl);
         const int* spos = (const int*)(sbnd + 2);
         // lab and mlt are consumed before the next image's copy is issued: a
@@ -1142,12 +1150,11 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
         const double E = 0x1p-14 * xn * mbs + 0x1p-13 * sqd * (xn + mbs) + 0x1p-15 * abs2 + 8.0;
         const bool amb = !none && (double)n2 - (double)n1 <= 2.0 * E;
         auto dsq = [&](int c) {
-            const double* mr = smu + c * DMAX;
-            const int cm = c & QM;
-            double s = sv[c];
+            const double* mr = smu + c * (DMAX + 2);
+            double s = mr[DMAX];  // v_c
 #pragma unroll
             for (int q = 0; q < DMAX / 2; ++q) {
-                const double2 v = *reinterpret_cast<const double2*>(mr + ((q ^ cm) << 1));
+                const double2 v = *reinterpret_cast<const double2*>(mr + 2 * q);
                 const double t0 = xr[2 * q] - v.x, t1 = xr[2 * q + 1] - v.y;
                 s = fma(t0, t0, s);
                 s = fma(t1, t1, s);
@@ -1237,7 +1244,7 @@ __global__ __launch_bounds__(SIL_WT, 3) void sil_width16(
             }
         }
         const unsigned long long tq = sil_wave_sum_u64((unsigned long long)wq);
-        const unsigned long long tn = sil_wave_sum_u64((unsigned long long)wn);
+        const unsigned long long tn = sil_wave_sum_u32(wn);  // (a wave's weights: < 2^32)
         if (lane == 0) {
             wsum[(int64_t)(lq + l) * nbw + 4 * tb + wave] = tq;
             wcnt[(int64_t)(lq + l) * nbw + 4 * tb + wave] = tn;
