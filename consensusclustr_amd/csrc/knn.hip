@@ -1098,22 +1098,22 @@ static int knn_seg_plan(ccg_ctx* ctx, const int64_t* seg_off, int nseg, int d, i
 // kmax references lie within (certify: the kmax-th exact candidate distance;
 // a candidate set is a subset of the references, so its kmax-th distance
 // bounds the true kmax-th from above):
-//   scan   : (64-row group, reference range) blocks, one failed row per lane,
-//            the range staged through LDS in 64-reference chunks that every
-//            lane reads by broadcast; the exact d2 (the contract's unfused
-//            dimension-order arithmetic) of each (row, reference) pair, and
-//            every reference within tau is appended to the row's candidate
-//            buffer (rare: tau is tight);
-//   select : one block per row bitonic-sorts its candidates by (d2, row) in
-//            LDS and writes the first kmax.
-// The failed rows' references are read once per 64 rows instead of once per
-// row.  Rows with tau = +inf, past KNN_FX_ROWS, or with more than KNN_FX_CAP
+//   prep   : each failed row's fp16 hi/lo image at its own power-of-two
+//            scale, its part of the test and its id;
+//   scan   : 128 references per block on the fp16 matrix core against the
+//            failed rows staged in groups of 128 (below); every reference
+//            that passes the pre-test (a superset of those within tau) is
+//            appended to the row's candidate buffer (rare: tau is tight);
+//   select : one wave per row takes the candidates' exact fp64 d2 (the
+//            contract's unfused dimension-order arithmetic), keeps those
+//            within tau, sorts them by (d2, row) and writes the first kmax.
+// Rows with tau = +inf, past KNN_FX_ROWS, or with more than KNN_FX_CAP
 // candidates (massive ties at the radius) go to the per-thread-list kernels
 // below.
 #define KNN_FX_CAP 1024
 #define KNN_FX_ROWS 16384
 #define KNN_FX_CHUNK 64
-#define KNN_FX_GRID 512   // (grid-stride; a failed group of 64 rows spans n / 256 units)
+#define KNN_FX_PREP_GRID 16  // failed-row prep: grid-stride over <= KNN_FX_ROWS rows
 
 template <int DMAX>
 __device__ __forceinline__ double knn_exact_d2(const double (&xq)[DMAX], const double* y, int d) {
@@ -1150,101 +1150,175 @@ __device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
     __syncthreads();
 }
 
-// Each (row, reference) pair is first tested by an fp32 dot product,
-// approx = |x|^2 + |y|^2 - 2 (float) x.y, against radius + margin, the margin
-// covering the fp32 rounding of x, y and the 30-term accumulation
-// (<= 2^-17 (|x|^2 + |y|^2) with room to spare, plus an absolute 2^-60); only
-// pairs within it take the exact fp64 sum.  So the candidates are exactly the
-// plain scan's.  (The exact form costs three fp64 operations per dimension;
-// the filter one packed fp32 FMA per two.)
-//
-// A block takes 64 failed rows (a group) and 256 references, one per lane
-// of its 4 waves, held in registers as fp32 pairs with their fp64 norms
-// (converted on the fly from the fp64 rows).  The group's rows are staged once
-// in LDS as fp32 with their norms and radii; every wave then walks them at
-// wave-uniform LDS addresses (broadcast reads): per (row, reference) pair one
-// packed fp32 FMA per two dimensions.  An empty failed list exits at once.
-#define KNN_FX_QG 64  // failed rows per group
-template <int DMAX>
-__global__ __launch_bounds__(256) void knn_fx_scan_kernel(const double* __restrict__ rows, int n, int d,
-                                                          const int* __restrict__ fail_list,
-                                                          const int* __restrict__ fail_count,
-                                                          const double* __restrict__ fail_tau, int* __restrict__ cnt,
-                                                          int* __restrict__ bi, int* __restrict__ ovf_count) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    __shared__ __attribute__((aligned(16))) float sx[KNN_FX_QG][DMAX];
-    __shared__ float sA[KNN_FX_QG];
-    __shared__ int sq[KNN_FX_QG];
+// The scan on the fp16 matrix core (round 5).  Every row is scaled by its
+// own power of two 2^e (max_k |x_k| 2^e < 2^12) and split into fp16 hi + lo
+// (knn_split16); x'.y' ~ hi.hi + hi.lo + lo.hi on v_mfma_f32_32x32x16_f16
+// with A = 32 failed rows (LDS) and B = 32 references (registers), so lane
+// (h, j) gets 16 failed rows against reference j, and x.y = x'.y' 2^-(ex+ey)
+// (a product of powers of two: one fp32 multiply, exact).  The error of the
+// product is below 2^-17.2 |x||y| (split residuals 2^-22 relative per
+// factor, fp32 accumulation of 48 KSTEPS exact products) plus the parts
+// flushed below 2^-14 of each scaled row (< 2^-25 max|x| per component),
+// inside the margin the test takes: a pair within the radius,
+// nx + ny - 2 x.y <= tau, passes
+//   2 x.y (fp32, from the matrix core) >= A_x + B_y,
+//   A_x = (1 - 2^-14) nx - tau - 2^-60 - 2^-21 (nx + tau),
+//   B_y = (1 - 2^-14 - 2^-21) ny
+// (both rounded down to fp32: 2^-14 (nx + ny) covers the product's error
+// and the fp32 sums), so the candidates are a superset of the pairs within
+// the radius, and knn_fx_select_kernel keeps exactly those whose fp64 d2
+// is.  Per pair 3 MACs of 16 KSTEPS dims on the matrix core and ~4 VALU,
+// against the round-4 scan's 16 KSTEPS packed fp32 FMAs and 8 LDS reads.
+// (A first matrix-core version, round 5, scaled by the rows' global max|x|:
+// its same-address atomicMax in the distinct-row gather cost 80 us per
+// bootstrap; per-row scales need no reduction.)
+// Failed rows: KNN_FXQ per staged group; prep writes each row's image
+// (chunks (s, hi/lo, h) of 8 fp16, chunk q of row c at q ^ (c & (NCH - 1))),
+// A_x, its scale 2^-e and its id.
+#define KNN_FXQ 128
+
+__device__ __forceinline__ int knn_row_exp(double mx) {
+    return mx > 0.0 ? 11 - ilogb(mx) : 0;  // mx 2^e < 2^12
+}
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __restrict__ rows, int d,
+                                                            const int* __restrict__ fail_list,
+                                                            const int* __restrict__ fail_count,
+                                                            const double* __restrict__ fail_tau,
+                                                            uint4* __restrict__ qimg, float* __restrict__ qa,
+                                                            float* __restrict__ qs, int* __restrict__ qid,
+                                                            int* __restrict__ ovf_count) {
+    constexpr int NCH = 4 * KSTEPS;
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
     const int nf = min(*fail_count, KNN_FX_ROWS);
-    const int ng = (nf + KNN_FX_QG - 1) / KNN_FX_QG;
-    const int nrb = (n + 255) / 256;
-    for (int64_t u = blockIdx.x; u < (int64_t)ng * nrb; u += gridDim.x) {
-        const int g = (int)(u / nrb), r = (int)(u - (int64_t)g * nrb);
-        const int f0 = g * KNN_FX_QG, nq = min(KNN_FX_QG, nf - f0);
-        __syncthreads();  // the previous unit's reads of the stage are done
-        for (int e = threadIdx.x; e < KNN_FX_QG * DMAX; e += 256) {
-            const int i = e / DMAX, k = e - i * DMAX;
-            float v = 0.f;
-            if (i < nq && k < d) v = (float)rows[(int64_t)fail_list[f0 + i] * d + k];
-            sx[i][k] = v;
+    const int nfp = (nf + KNN_FXQ - 1) / KNN_FXQ * KNN_FXQ;
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfp; f += gridDim.x * blockDim.x) {
+        const bool valid = f < nf;
+        const int q = valid ? fail_list[f] : -1;
+        double t = valid ? fail_tau[f] : -1.0;
+        if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
+        double x[KSTEPS * 16];
+        double mx = 0.0, nx = 0.0;
+#pragma unroll
+        for (int k = 0; k < KSTEPS * 16; ++k) {
+            x[k] = (valid && k < d) ? rows[(int64_t)q * d + k] : 0.0;
+            mx = fmax(mx, fabs(x[k]));
+            nx = fma(x[k], x[k], nx);
         }
-        if (threadIdx.x < KNN_FX_QG) {
-            const int i = threadIdx.x;
-            double nx = 0.0, t = -1.0;
-            int q = -1;
-            if (i < nq) {
-                q = fail_list[f0 + i];
-                t = fail_tau[f0 + i];
-                if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
-                for (int k = 0; k < DMAX; ++k) {
-                    const double y = k < d ? rows[(int64_t)q * d + k] : 0.0;
-                    nx = fma(y, y, nx);
-                }
-            }
-            // the row's part of the fp32 test below, rounded down
-            sA[i] = t < 0.0 ? INFINITY
-                            : __double2float_rd((1.0 - 0x1p-14) * nx - t - 0x1p-60 - 0x1p-21 * (nx + t));
-            sq[i] = q;
+        const int e = knn_row_exp(mx);
+        _Float16 hv[NCH * 8];
+#pragma unroll
+        for (int k = 0; k < KSTEPS * 16; ++k) {
+            _Float16 hi, lo;
+            knn_split16(ldexp(x[k], e), hi, lo);
+            const int s = k >> 4, h = (k >> 3) & 1, i = k & 7;
+            hv[(s * 4 + h) * 8 + i] = hi;
+            hv[(s * 4 + 2 + h) * 8 + i] = lo;
+        }
+        const int c = f % KNN_FXQ;  // the row's place in its staged group (the swizzle's row)
+        uint4* out = qimg + (int64_t)f * NCH;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) out[ch ^ (c & (NCH - 1))] = *reinterpret_cast<const uint4*>(&hv[ch * 8]);
+        qa[f] = t < 0.0 ? INFINITY : __double2float_rd((1.0 - 0x1p-14) * nx - t - 0x1p-60 - 0x1p-21 * (nx + t));
+        qs[f] = ldexpf(1.0f, -e);
+        qid[f] = q;
+    }
+}
+
+// Grid: 128 references per block (4 waves x 32); every block walks the
+// failed rows in staged groups of KNN_FXQ.  An empty failed list exits at
+// once.
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __restrict__ rows, int n, int d,
+                                                            const int* __restrict__ fail_count,
+                                                            const uint4* __restrict__ qimg,
+                                                            const float* __restrict__ qa,
+                                                            const float* __restrict__ qs,
+                                                            const int* __restrict__ qid, int* __restrict__ cnt,
+                                                            int* __restrict__ bi) {
+    constexpr int NCH = 4 * KSTEPS;
+    __shared__ uint4 sq[KNN_FXQ * NCH];
+    __shared__ __attribute__((aligned(16))) float sa[KNN_FXQ];
+    __shared__ __attribute__((aligned(16))) float ss[KNN_FXQ];
+    __shared__ int sid[KNN_FXQ];
+    const int nf = min(*fail_count, KNN_FX_ROWS);
+    if (nf == 0) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, j = lane & 31;
+    // the wave's 32 references: B fragments (dims 16 s + 8 h ..), the
+    // reference's scale and its part of the test
+    const int jr = blockIdx.x * 128 + wave * 32 + j;
+    const bool inr = jr < n;
+    double y[KSTEPS * 8];
+    double my = 0.0, ny = 0.0;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = 16 * s + 8 * h + i;
+            y[8 * s + i] = (inr && k < d) ? rows[(int64_t)jr * d + k] : 0.0;
+            my = fmax(my, fabs(y[8 * s + i]));
+            ny = fma(y[8 * s + i], y[8 * s + i], ny);
+        }
+    my = fmax(my, __shfl_xor(my, 32, 64));
+    ny += __shfl_xor(ny, 32, 64);
+    const int ey = knn_row_exp(my);
+    h8 bh[KSTEPS], bl[KSTEPS];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            _Float16 hi, lo;
+            knn_split16(ldexp(y[8 * s + i], ey), hi, lo);
+            bh[s][i] = hi;
+            bl[s][i] = lo;
+        }
+    const float sy = 2.0f * ldexpf(1.0f, -ey);  // (the test's factor 2 folded in)
+    const float bj = inr ? __double2float_rd((1.0 - 0x1p-14 - 0x1p-21) * ny) : INFINITY;
+    for (int g0 = 0; g0 < nf; g0 += KNN_FXQ) {
+        const int nq = min(KNN_FXQ, nf - g0);
+        __syncthreads();  // the previous group's reads of the stage are done
+        for (int t = threadIdx.x; t < KNN_FXQ * NCH; t += 256) sq[t] = qimg[(int64_t)g0 * NCH + t];
+        if (threadIdx.x < KNN_FXQ) {
+            sa[threadIdx.x] = qa[g0 + threadIdx.x];  // (the prep writes whole groups: INFINITY past nf)
+            ss[threadIdx.x] = qs[g0 + threadIdx.x];
+            sid[threadIdx.x] = qid[g0 + threadIdx.x];
         }
         __syncthreads();
-        const int j = r * 256 + threadIdx.x;
-        const int jc = j < n ? j : n - 1;
-        f2 yf[DMAX / 2];
-        double ny = 0.0;
+        for (int t = 0; t < (nq + 31) >> 5; ++t) {  // block-uniform
+            f32x16 acc;
 #pragma unroll
-        for (int k2 = 0; k2 < DMAX / 2; ++k2) {
-            const double y0 = 2 * k2 < d ? rows[(int64_t)jc * d + 2 * k2] : 0.0;
-            const double y1 = 2 * k2 + 1 < d ? rows[(int64_t)jc * d + 2 * k2 + 1] : 0.0;
-            ny = fma(y0, y0, ny);
-            ny = fma(y1, y1, ny);
-            yf[k2] = f2{(float)y0, (float)y1};
-        }
-        // the reference's part, rounded down
-        const float bj = __double2float_rd((1.0 - 0x1p-14 - 0x1p-21) * ny);
-        for (int i = 0; i < nq; ++i) {  // block-uniform
-            const float4* xp = reinterpret_cast<const float4*>(&sx[i][0]);
-            f2 acc = {0.f, 0.f};
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            const int c = t * 32 + j;
+            const uint4* ar = sq + c * NCH;
 #pragma unroll
-            for (int k4 = 0; k4 < DMAX / 4; ++k4) {
-                const float4 x = xp[k4];
-                acc = __builtin_elementwise_fma(f2{x.x, x.y}, yf[2 * k4], acc);
-                acc = __builtin_elementwise_fma(f2{x.z, x.w}, yf[2 * k4 + 1], acc);
+            for (int s = 0; s < KSTEPS; ++s) {
+                const uint4 ahv = ar[(s * 4 + h) ^ (c & (NCH - 1))];
+                const uint4 alv = ar[(s * 4 + 2 + h) ^ (c & (NCH - 1))];
+                const h8 ah = *reinterpret_cast<const h8*>(&ahv);
+                const h8 al = *reinterpret_cast<const h8*>(&alv);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
             }
-            // nx + ny - 2 x.y <= tau + 2^-14 (nx + ny) + 2^-60, with the fp32
-            // dot product (error <= 2^-17 (nx + ny)), rearranged as
-            // 2 x.y >= A_i + B_j in fp32 (A_i, B_j rounded down): the fp32
-            // sums here err by <= 2^-23 (nx + ny + tau), inside the 2^-21
-            // slack taken out of A_i and B_j, so the candidates stay a
-            // superset of the pairs within the radius.  An fp64 test here
-            // cost ~7 fp64 operations per pair.
-            const float lhs = 2.0f * (acc.x + acc.y);
-            // a pair within radius + margin joins the row's candidates; its
-            // exact distance is taken in knn_fx_select_kernel (no fp64 row
-            // loads inside this loop: they stall the whole wave for one lane)
-            if (j < n && j != sq[i] && lhs >= sA[i] + bj) {
-                const int slot = atomicAdd(&cnt[f0 + i], 1);
-                if (slot < KNN_FX_CAP) bi[(int64_t)(f0 + i) * KNN_FX_CAP + slot] = j;
+            // register r holds failed row t*32 + (r & 3) + 8 (r >> 2) + 4h against reference jr
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 a4 = *reinterpret_cast<const float4*>(&sa[t * 32 + 8 * g + 4 * h]);
+                const float4 s4 = *reinterpret_cast<const float4*>(&ss[t * 32 + 8 * g + 4 * h]);
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+                const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (acc[4 * g + q] * (sv[q] * sy) >= av[q] + bj) {  // rare: the candidates
+                        const int i = t * 32 + 8 * g + 4 * h + q;
+                        if (jr != sid[i]) {
+                            const int slot = atomicAdd(&cnt[g0 + i], 1);
+                            if (slot < KNN_FX_CAP) bi[(int64_t)(g0 + i) * KNN_FX_CAP + slot] = jr;
+                        }
+                    }
+                }
             }
         }
     }
@@ -1391,25 +1465,36 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
                                int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr) {
     if (!seg_off && fail_tau) {
         // the radius search; its leftovers (overflow) continue below
-        int* cnt = (int*)ccg_ws(ctx, WS_FX_A, sizeof(int) * (KNN_FX_ROWS + 64 + n));
+        // WS_FX_A: counters [KNN_FX_ROWS], overflow count + list [64 + n], the
+        // failed rows' A_x, scales, ids [3 x KNN_FX_ROWS] and images
+        const int nch = d <= 16 ? 4 : (d <= 32 ? 8 : 16);
+        const size_t fx_ints = (size_t)KNN_FX_ROWS + 64 + (size_t)n + 3 * (size_t)KNN_FX_ROWS + 4;
+        char* fxa = (char*)ccg_ws(ctx, WS_FX_A, sizeof(int) * fx_ints + 16 + sizeof(uint4) * (size_t)KNN_FX_ROWS * nch);
+        int* cnt = (int*)fxa;
         int* bi = (int*)ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
-        if (!cnt || !bi) return CCG_ENOMEM;
+        if (!fxa || !bi) return CCG_ENOMEM;
         if (ctx->fx_zeroed != (void*)cnt) {  // fresh buffer: the select kernel keeps the counters zero afterwards
             CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * KNN_FX_ROWS, st));
             ctx->fx_zeroed = (void*)cnt;
         }
         int* ovf_count = cnt + KNN_FX_ROWS;
         int* ovf_list = ovf_count + 64;
-#define CCG_FX(DM_)                                                                                              \
+        float* qa = (float*)(ovf_list + n);
+        float* qs = qa + KNN_FX_ROWS;
+        int* qid = (int*)(qs + KNN_FX_ROWS);
+        uint4* qimg = (uint4*)(fxa + ccg_cdiv(sizeof(int) * fx_ints, 16) * 16);
+        const unsigned gs = (unsigned)ccg_cdiv(n, 128);
+#define CCG_FX(DM_, KS_)                                                                                          \
     do {                                                                                                         \
-        knn_fx_scan_kernel<DM_><<<KNN_FX_GRID, 256, 0, st>>>(rows, (int)n, d, fail_list, fail_count, fail_tau, cnt, \
-                                                             bi, ovf_count);                                      \
+        knn_fx_prep16_kernel<KS_><<<KNN_FX_PREP_GRID, 256, 0, st>>>(rows, d, fail_list, fail_count, fail_tau, qimg, \
+                                                                    qa, qs, qid, ovf_count);                     \
+        knn_fx_scan16_kernel<KS_><<<gs, 256, 0, st>>>(rows, (int)n, d, fail_count, qimg, qa, qs, qid, cnt, bi);      \
         knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, fail_list, fail_count, fail_tau, cnt, bi,     \
                                                        out_idx, out_dist, dist_sq, ovf_list, ovf_count);          \
     } while (0)
-        if (d <= 16) CCG_FX(16);
-        else if (d <= 32) CCG_FX(32);
-        else CCG_FX(64);
+        if (d <= 16) CCG_FX(16, 1);
+        else if (d <= 32) CCG_FX(32, 2);
+        else CCG_FX(64, 4);
 #undef CCG_FX
         fail_list = ovf_list;
         fail_count = ovf_count;
