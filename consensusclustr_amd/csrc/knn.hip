@@ -2164,7 +2164,6 @@ __global__ void kt_transpose_kernel(const double* __restrict__ pcs, int64_t N, i
 #define KT_TB 8  // table entries tested per round in kt_tau_wave
 struct KtTauLds {
     int hset[128];  // the cell's own table row as an open-addressing set (K <= 48 of 128 slots)
-    int pick[64];
     double val[128];
 };
 __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int K, int d, int uid, int64_t c, int v,
@@ -2208,10 +2207,11 @@ __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int
             }
         }
     }
-    S.pick[lane] = w;
-    KT_SYNC();
+    // a pick already made by a lower lane is a duplicate (the lanes' picks by
+    // v_readlane: no LDS round trips)
     bool dup = false;
-    for (int t = 0; t < lane; ++t) dup |= w >= 0 && S.pick[t] == w;
+#pragma unroll 16
+    for (int t = 0; t < 64; ++t) dup |= t < lane && w >= 0 && __builtin_amdgcn_readlane(w, t) == w;
     double val2 = INFINITY;
     if (w >= 0 && !dup) {
         const double* xr = urows + (int64_t)uid * d;
