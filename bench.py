@@ -654,8 +654,13 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
                                 [means[c][j] for c, j in segs], [nclust[c][j] for c, j in segs],
                                 [minsize[c][j] for c, j in segs])
 
-    def step():
+    def step(evs=None):
+        def mark(name):
+            if evs is not None:
+                evs[name] = torch.cuda.Event(enable_timing=True)
+                evs[name].record()
         cur = torch.cuda.current_stream()
+        mark("start")
         for st_ in streams:
             st_.wait_stream(cur)
         for t in range(len(batches)):
@@ -664,10 +669,15 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
                 run_batch(t, si)
         for st_ in streams:
             cur.wait_stream(st_)
+        mark("boots_done")
         for c in range(nsub):
             eng.select_mapback_t("robust", labels[c], boots_t[c], sizes[c], A[c], 0, means=means[c],
                                  nclust=nclust[c], minsize=minsize[c])
+        mark("selected")
+        mark("gathered")  # (one GPU per level: no all-gather)
+        for c in range(nsub):
             eng.cocluster_t(A[c], 0, sizes[c], co=co[c], both=both[c])
+        mark("slab_done")
 
     def barrier():
         if G > 1:

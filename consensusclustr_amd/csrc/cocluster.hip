@@ -187,12 +187,16 @@ __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ 
 
 // Consensus-kNN candidate lists (COF_CAND): pair (i, j) of the triangle is
 // offered to row i if sim_ij >= tau_i and to row j if sim_ij >= tau_j, where
-// tau is a lower bound of each row's k-th largest similarity.  The test is
-// exact in fp64: (double)co >= tstar * (double)both with tstar = tau - ulp/2
-// (a superset of fp32 sim >= tau; 25 x 16 bits multiply exactly).  A row's
-// entries go to cand[row * cap + slot] as (original column id, co | both << 16).
+// tau is a lower bound of each row's k-th largest similarity.  Round 5: the
+// bound is a multiple of 1 / CKC_NBK, tnum / CKC_NBK (ckc_tau_kernel), so
+// the test is exact in int32: co CKC_NBK >= tnum both (< 2^26 on both sides;
+// tnum = -1: every pair with both > 0) -- three VALU where round 4's fp64
+// test against tau - ulp/2 took two conversions, a multiply and a compare.
+// A row's entries go to cand[row * cap + slot] as (original column id,
+// co | both << 16).
+#define CKC_NBK 4096
 struct CofCand {
-    const double* tstar;
+    const int* tnum;
     int* cnt;
     uint2* cand;
     int cap;
@@ -235,11 +239,11 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
     // the lane's 4 columns' thresholds once (not per row); an interior
     // quarter (every column above every row, inside N and the slab) needs no
     // per-element masks
-    double tj[4];
+    int tj[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
         const int64_t gj = jb0 + 32 * ni + col;
-        tj[ni] = gj < N ? cc.tstar[gj] : INFINITY;
+        tj[ni] = gj < N ? cc.tnum[gj] : 0;  // (columns past N never pass: ok is false)
     }
     const bool interior = jb0 > ia0 + 63 && jb0 + 128 <= N && ia0 + 64 <= r1;
     bool nan = false;
@@ -249,7 +253,7 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
         for (int r = 0; r < 16; ++r) {
             const int64_t gi = ia0 + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h;
             const bool row_ok = gi < r1;
-            const double ti = row_ok ? cc.tstar[gi] : INFINITY;
+            const int ti = row_ok ? cc.tnum[gi] : 0;  // (rows past the slab never pass: ok is false)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int64_t gj = jb0 + 32 * ni + col;
@@ -257,11 +261,11 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
                 const int cv = a & 16383, bv = a >> 14;
                 const bool ok = interior || (row_ok && gj < N && gj > gi);
                 nan |= ok && bv == 0;
-                const double dc = (double)cv, db = (double)bv;
+                const int dc = cv * CKC_NBK;
                 const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
                 // row gi is shared by the 32 lanes of this half: one counter
                 // add per half for all its passing pairs (lane order)
-                const bool pi = ok && bv > 0 && dc >= ti * db;
+                const bool pi = ok && bv > 0 && dc >= ti * bv;
                 const unsigned long long m = __ballot(pi);
                 if (m) {
                     const unsigned long long hm = h ? (m & 0xFFFFFFFF00000000ull) : (m & 0xFFFFFFFFull);
@@ -275,7 +279,7 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
                         else cc.flags[1] = 1;
                     }
                 }
-                if (ok && bv > 0 && dc >= tj[ni] * db) cof_cand_push(cc, gj, gi, N, val);
+                if (ok && bv > 0 && dc >= tj[ni] * bv) cof_cand_push(cc, gj, gi, N, val);
             }
         }
     if (__any(nan) && lane == 0) cc.flags[0] = 1;
@@ -860,9 +864,10 @@ __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B
     }
 }
 
-// tstar[row] for rows [a, b): a lower bound of the k-th largest fp32
-// similarity over the sampled columns q != row with both > 0 (-inf when fewer
-// than k are usable).  One wave per row counts its sampled similarities into
+// tnum[row] for rows [a, b): tnum / CKC_NBK is a lower bound of the k-th
+// largest fp32 similarity over the sampled columns q != row with both > 0
+// (-1, every pair, when fewer than k are usable).  One wave per row counts
+// its sampled similarities into
 // CKC_NBK buckets of width 1 / CKC_NBK in LDS (bucket of the approximate
 // quotient c * rcp(u), within one bucket of the exact one), finds the bucket
 // bk holding the k-th largest by a suffix count, and takes (bk - 1) /
@@ -870,9 +875,8 @@ __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B
 // a sorted 32-entry register list per lane (a 32-step insertion chain per
 // value: 5.5 ms per call at N = 100k); the bound is now looser by at most
 // 2 / CKC_NBK, a few more candidates per row.
-#define CKC_NBK 4096
 __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict__ cb, int64_t a, int64_t b,
-                                                      int64_t NS, int k, double* __restrict__ tstar) {
+                                                      int64_t NS, int k, int* __restrict__ tnum) {
     __shared__ unsigned hist[4][CKC_NBK];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = a + (int64_t)blockIdx.x * 4 + wv;
@@ -909,7 +913,7 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
     }
     // the highest lane whose suffix reaches k (suffix sums fall with the lane)
     const unsigned long long reach = __ballot(suf >= k);
-    double t = -INFINITY;
+    int t = -1;  // (fewer than k usable: every pair with both > 0 qualifies)
     if (usable >= k && reach) {
         const int L = 63 - __clzll(reach);
         int bk = 0;
@@ -924,9 +928,9 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
             }
         }
         bk = __shfl(bk, L, 64);
-        t = bk >= 2 ? (double)(bk - 1) / (double)CKC_NBK : -1.0;  // (<= 0: every co-sampled pair qualifies)
+        t = bk >= 2 ? bk - 1 : -1;  // (<= 0: every co-sampled pair qualifies)
     }
-    if (lane == 0) tstar[row] = t;
+    if (lane == 0) tnum[row] = t;
 }
 
 // Per permuted row (one wave): the row's candidates, exact fp32 similarity,
@@ -984,8 +988,8 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     uint2* cand = (uint2*)ccg_ws(ctx, WS_COC_E, sizeof(uint2) * (size_t)N * CKC_CAP);
     char* small = (char*)ccg_ws(ctx, WS_COC_F, sizeof(double) * N + sizeof(int) * (N + 64));
     if (!Ap || !cand || !small) return CCG_ENOMEM;
-    double* tstar = (double*)small;
-    int* cnt = (int*)(tstar + N);
+    int* tnum = (int*)small;
+    int* cnt = tnum + N;
     int* flags = cnt + N;  // [0] both == 0 somewhere, [1] overflow
     const unsigned pg = (unsigned)std::min<int64_t>(ccg_cdiv(B * N, 256), 65536);
     if (label_bits == 8) ckc_permute_kernel<uint8_t><<<pg, 256, 0, st>>>((const uint8_t*)A, N, B, pmul, padd, (uint8_t*)Ap);
@@ -999,7 +1003,7 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
         const int64_t b = std::min(N, a + R);
         int rc = ccg_cocluster_rows_packed(ctx, Ap, label_bits, N, B, a, b, cb, st, NS);
         if (rc) return rc;
-        ckc_tau_kernel<<<(unsigned)ccg_cdiv(b - a, 4), 256, 0, st>>>(cb, a, b, NS, k, tstar);
+        ckc_tau_kernel<<<(unsigned)ccg_cdiv(b - a, 4), 256, 0, st>>>(cb, a, b, NS, k, tnum);
     }
     // 2. the triangle with the candidate epilogue
     CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (N + 64), st));
@@ -1011,7 +1015,7 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - fl(TR);
     CCG_REQUIRE(cof_tile_blocks(TR, TC, 0, true) < (1LL << 31), "consensus kNN: too many tiles");
-    CofCand cc{tstar, cnt, cand, CKC_CAP, pmul, padd, ~0ull / (uint64_t)N, flags};
+    CofCand cc{tnum, cnt, cand, CKC_CAP, pmul, padd, ~0ull / (uint64_t)N, flags};
     cof_launch<COF_CAND>(label_bits, Ap, 0, B, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
                          nullptr, nullptr, st, N, cc);
     CCG_HIP(hipGetLastError());
