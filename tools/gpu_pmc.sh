@@ -1,11 +1,13 @@
 #!/bin/bash
 # rocprofv3 --pmc passes of "python3 $PMC_CMD", one counter group per run
 # (groups separated by ';'), into gpurun_out/pmc/pass_<i>; each pass under its
-# own kill timeout; stops at the first failure.  Summarise with
-# tools/pmc_summary.py gpurun_out/pmc.
-mkdir -p gpurun_out/pmc
+# own kill timeout; stops at the first failure.  Output directory
+# gpurun_out/$PMC_OUT (default pmc).  Summarise with
+# tools/pmc_summary.py gpurun_out/$PMC_OUT.
+PO=${PMC_OUT:-pmc}
+mkdir -p gpurun_out/$PO
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT/gpurun_out/pmc
+R=$GRAFT_REPO_ROOT/gpurun_out/$PO
 IFS=';' read -ra GRP <<< "${PMC_GROUPS:?}"
 i=0
 cd /tmp
