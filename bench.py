@@ -81,8 +81,10 @@ def parse():
     ap.add_argument("--boot-size", type=float, default=0.9)
     ap.add_argument("--cpu-sample-rows", type=int, default=6000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="bootstraps in flight per GPU (one engine context + HIP stream each)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="bootstraps in flight per GPU (one engine context + HIP stream each; 4 = one per "
+                         "hardware queue, GPU_MAX_HW_QUEUES=4: measured 2/3/4/5/6/8 -> 987/1156/1200/1085/1142/"
+                         "1210 bootstraps/s at cfg3, round 5)")
     ap.add_argument("--seg-batch", type=int, default=16,
                     help="cfg5: bootstraps of every subcluster per segmented launch set")
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
