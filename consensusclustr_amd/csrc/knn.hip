@@ -63,14 +63,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_F16_FLOOR 0x1p-14
 
 // --------------------------------------------------------------- gather --
-__global__ void gather_rows_kernel(const double* __restrict__ pcs, int64_t N, int d,
-                                   const int32_t* __restrict__ idx, int64_t n,
-                                   double* __restrict__ rows) {
-    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * d) return;
-    int64_t i = t / d;
-    int k = (int)(t - i * d);
-    rows[t] = pcs[(int64_t)k * N + idx[i]];
+// (column-major source: LPR lanes per output row, a lane per dimension --
+// coalesced row writes, no per-element 64-bit division)
+template <int LPR>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const double* __restrict__ pcs, int64_t N, int d,
+                                                          const int32_t* __restrict__ idx, int64_t n,
+                                                          double* __restrict__ rows) {
+    const int64_t i = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    if (i >= n) return;
+    const int c = idx[i];
+    for (int k = threadIdx.x & (LPR - 1); k < d; k += LPR) rows[i * d + k] = pcs[(int64_t)k * N + c];
 }
 
 // --------------------------------------------------------------- screen --
@@ -976,31 +978,44 @@ extern "C" int ccg_gather_rows_dev(ccg_ctx* ctx, const double* pcs, int64_t N, i
     CCG_REQUIRE(ctx && pcs && idx && rows, "ccg_gather_rows_dev: NULL argument");
     CCG_REQUIRE(N > 0 && n > 0 && d > 0, "ccg_gather_rows_dev: bad sizes");
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    int64_t tot = n * d;
-    gather_rows_kernel<<<(unsigned)ccg_cdiv(tot, 256), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    if (d <= 16) gather_rows_kernel<16><<<(unsigned)ccg_cdiv(n, 16), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    else if (d <= 32) gather_rows_kernel<32><<<(unsigned)ccg_cdiv(n, 8), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    else gather_rows_kernel<64><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(pcs, N, d, idx, n, rows);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
 
-// row-major source: one thread per 16-byte piece of an output row (d even) or per value
-__global__ void gather_rows_rm_kernel(const double* __restrict__ pcs, int64_t N, int d,
-                                      const int32_t* __restrict__ idx, int64_t n, double* __restrict__ rows) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// row-major source: GR_LPR lanes per output row (a power of two >= the
+// row's 16-byte pieces, d <= 2 GR_LPR), 256 / GR_LPR rows per block: no
+// per-element division (round 4 divided a 64-bit thread index by d / 2:
+// ~19 us per 90k-row bootstrap at d = 30).  Odd d: one value per lane.
+template <int LPR>
+__global__ __launch_bounds__(256) void gather_rows_rm_kernel(const double* __restrict__ pcs, int64_t N, int d,
+                                                             const int32_t* __restrict__ idx, int64_t n,
+                                                             double* __restrict__ rows) {
+    const int64_t i = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const int k = threadIdx.x & (LPR - 1);
+    if (i >= n) return;
+    const int c = idx[i];
+    const bool ok = c >= 0 && c < N;
     if ((d & 1) == 0) {
         const int h = d >> 1;
-        if (t >= n * h) return;
-        const int64_t i = t / h;
-        const int k = (int)(t - i * h);
-        const int c = idx[i];
-        reinterpret_cast<double2*>(rows)[t] =
-            (c >= 0 && c < N) ? reinterpret_cast<const double2*>(pcs)[(int64_t)c * h + k] : make_double2(0.0, 0.0);
+        if (k < h)
+            reinterpret_cast<double2*>(rows)[i * h + k] =
+                ok ? reinterpret_cast<const double2*>(pcs)[(int64_t)c * h + k] : make_double2(0.0, 0.0);
     } else {
-        if (t >= n * d) return;
-        const int64_t i = t / d;
-        const int k = (int)(t - i * d);
-        const int c = idx[i];
-        rows[t] = (c >= 0 && c < N) ? pcs[(int64_t)c * d + k] : 0.0;
+        for (int kk = k; kk < d; kk += LPR) rows[i * d + kk] = ok ? pcs[(int64_t)c * d + kk] : 0.0;
     }
+}
+
+// lanes per row: the row's 16-byte pieces (or values, odd d) rounded up to a power of two, <= 64
+static void knn_gather_rm(const double* pcs, int64_t N, int d, const int32_t* idx, int64_t n, double* rows,
+                          hipStream_t st) {
+    const int pieces = (d & 1) == 0 ? d / 2 : d;
+    if (pieces <= 8) gather_rows_rm_kernel<8><<<(unsigned)ccg_cdiv(n, 32), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    else if (pieces <= 16) gather_rows_rm_kernel<16><<<(unsigned)ccg_cdiv(n, 16), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    else if (pieces <= 32) gather_rows_rm_kernel<32><<<(unsigned)ccg_cdiv(n, 8), 256, 0, st>>>(pcs, N, d, idx, n, rows);
+    else gather_rows_rm_kernel<64><<<(unsigned)ccg_cdiv(n, 4), 256, 0, st>>>(pcs, N, d, idx, n, rows);
 }
 
 extern "C" int ccg_gather_rows_rm_dev(ccg_ctx* ctx, const double* pcs_rm, int64_t N, int d, const int32_t* idx,
@@ -1008,8 +1023,7 @@ extern "C" int ccg_gather_rows_rm_dev(ccg_ctx* ctx, const double* pcs_rm, int64_
     CCG_REQUIRE(ctx && pcs_rm && idx && rows, "ccg_gather_rows_rm_dev: NULL argument");
     CCG_REQUIRE(N > 0 && n > 0 && d > 0, "ccg_gather_rows_rm_dev: bad sizes");
     hipStream_t st = ccg_pick_stream(ctx, stream);
-    const int64_t tot = (d & 1) == 0 ? n * (d / 2) : n * d;
-    gather_rows_rm_kernel<<<(unsigned)ccg_cdiv(tot, 256), 256, 0, st>>>(pcs_rm, N, d, idx, n, rows);
+    knn_gather_rm(pcs_rm, N, d, idx, n, rows, st);
     CCG_HIP(hipGetLastError());
     return CCG_OK;
 }
@@ -1881,16 +1895,19 @@ __global__ void kb_tables_kernel(const int32_t* __restrict__ scell, const int32_
 // the distinct cells' rows, copied from the gathered (row-major) bootstrap
 // rows of each cell's first copy: coalesced, unlike a gather from the
 // column-major PCs
-__global__ void kb_urows_kernel(const double* __restrict__ rows, int d, int u, const int* __restrict__ ustart,
-                                const int* __restrict__ srow, double* __restrict__ urows,
-                                const int32_t* __restrict__ idx, const float* __restrict__ cell_hint,
-                                float* __restrict__ urow_hint) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)u * d) return;
-    const int64_t uid = t / d;
-    const int k = (int)(t - uid * d);
+// (LPR lanes per distinct cell, a lane per dimension: no per-element 64-bit
+// division)
+template <int LPR>
+__global__ __launch_bounds__(256) void kb_urows_kernel(const double* __restrict__ rows, int d, int u,
+                                                       const int* __restrict__ ustart, const int* __restrict__ srow,
+                                                       double* __restrict__ urows, const int32_t* __restrict__ idx,
+                                                       const float* __restrict__ cell_hint,
+                                                       float* __restrict__ urow_hint) {
+    const int64_t uid = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+    const int k = threadIdx.x & (LPR - 1);
+    if (uid >= u) return;
     const int r0 = srow[ustart[uid]];
-    urows[t] = rows[(int64_t)r0 * d + k];
+    if (k < d) urows[uid * d + k] = rows[(int64_t)r0 * d + k];
     if (k == 0 && urow_hint) urow_hint[uid] = cell_hint[idx[r0]];
 }
 
@@ -2421,8 +2438,12 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
     // the table path: fail counts and the expansion tie count (misc[4..6]) zeroed first
     if (kq >= 1 && tab_idx) CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));
-    kb_urows_kernel<<<(unsigned)ccg_cdiv((int64_t)u * d, 256), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx,
-                                                                            cell_hint, urow_hint);
+    if (d <= 32)
+        kb_urows_kernel<32><<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, cell_hint,
+                                                                      urow_hint);
+    else
+        kb_urows_kernel<64><<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, cell_hint,
+                                                                      urow_hint);
     ccg_knn_stats us = {0, 0};
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
@@ -2569,8 +2590,7 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
     const unsigned ng = (unsigned)ccg_cdiv(n, 256);
     // 1. the rows, and (segment, cell) keys sorted stably: each segment's cells, each cell's rows ascending
-    gather_rows_rm_kernel<<<(unsigned)ccg_cdiv((d & 1) == 0 ? n * (d / 2) : n * d, 256), 256, 0, st>>>(
-        cells, Ntot, d, idx, n, rows);
+    knn_gather_rm(cells, Ntot, d, idx, n, rows, st);
     kbs_keys_kernel<<<ng, 256, 0, st>>>(idx, n, Ntot, dso, nseg, keys, rid, ctx->d_err);
     int bits = 1;
     while (bits < 31 && (1LL << bits) < (int64_t)nseg * Ntot) ++bits;
@@ -2581,7 +2601,11 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     rc = ccg_scan_i64(ctx, head, head, n, st);
     if (rc) return rc;
     kb_tables_kernel<<<ng, 256, 0, st>>>(skeys, srow, n, head, (int)u, ustart, row2u, ctx->d_err);
-    kb_urows_kernel<<<(unsigned)ccg_cdiv(u * d, 256), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
+    if (d <= 32)
+        kb_urows_kernel<32><<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
+                                                                      nullptr);
+    else
+        kb_urows_kernel<64><<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(rows, d, (int)u, ustart, srow, urows, idx, nullptr,
                                                                       nullptr);
     // 3. every segment's distinct cells among themselves (kq = kmax: each has >= kmax + 1)
     std::vector<int64_t> po;
