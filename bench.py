@@ -92,10 +92,13 @@ def parse():
                          "screen: a screen per bootstrap (warm-started)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues for this process (0: the runtime's default)")
-    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
+    ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="graph: the step's bootstrap phase (table, every bootstrap's gather, kNN, SNN, silhouette "
                          "on the S streams) is captured once after the warmup as one HIP graph and replayed per step; "
-                         "eager: launched from the host every step")
+                         "eager: launched from the host every step; auto: graph when a bootstrap has >= 50k rows "
+                         "(round 5, 4 streams: cfg3 graph 1187 / eager 1041 bootstraps/s; cfg2, 18k-row "
+                         "bootstraps x 500 per step, graph 2799 / eager 3658 -- the replay of ~20k graph nodes "
+                         "costs more host time than launching them)")
     ap.add_argument("--table-k", type=int, default=48,
                     help="cell-table length K (<= 48): cells with fewer than 20 of their K nearest cells in a "
                          "bootstrap take the exact search")
@@ -1058,7 +1061,8 @@ def main():
     # the graph's baked pointers stay valid); the replay is checked against an
     # eager step's outputs before timing
     launch_note = "eager"
-    if args.launch == "graph" and not W.get("no_graph"):
+    use_graph = args.launch == "graph" or (args.launch == "auto" and n >= 50000)
+    if use_graph and not W.get("no_graph"):
         try:
             torch.cuda.synchronize()
             ref_means = means.clone()
