@@ -81,10 +81,11 @@ def parse():
     ap.add_argument("--boot-size", type=float, default=0.9)
     ap.add_argument("--cpu-sample-rows", type=int, default=6000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=4,
-                    help="bootstraps in flight per GPU (one engine context + HIP stream each; 4 = one per "
-                         "hardware queue, GPU_MAX_HW_QUEUES=4: measured 2/3/4/5/6/8 -> 987/1156/1200/1085/1142/"
-                         "1210 bootstraps/s at cfg3, round 5)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="bootstraps in flight per GPU (one engine context + HIP stream each); 0 = auto: 4 (one per "
+                         "hardware queue, GPU_MAX_HW_QUEUES=4) for bootstraps of >= 50k rows, 3 below, 2 for cfg5. "
+                         "Round 5: cfg3 2/3/4/5/6/8 -> 987/1156/1200/1085/1142/1210 bootstraps/s; cfg2 (18k-row "
+                         "bootstraps, host-bound) 2/3/4 -> 3828/4385/3774; cfg5 2/3/4 -> 1062/1025/967")
     ap.add_argument("--seg-batch", type=int, default=16,
                     help="cfg5: bootstraps of every subcluster per segmented launch set")
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
@@ -890,8 +891,13 @@ def main():
     # what libccg's own communicator saw (ccg_group_info), per rank:
     # [torch rank, device, the group's nranks, the group's first rank]
     ranks_seen = group_ranks_seen(torch, dist, world, rank, local, grp, dev)
-    S = max(1, args.streams)
     W = WORKLOADS[args.workload]
+    if args.streams > 0:
+        S = args.streams
+    elif args.workload == "cfg5":
+        S = 2
+    else:
+        S = 4 if int(args.boot_size * (args.cells or W["cells"])) >= 50000 else 3
     if args.workload == "cfg5":
         return run_cfg5(args, torch, dist, grp, [grp.engines[0]] + [Engine(local) for _ in range(S - 1)], dev, world,
                         rank, json_fd, ranks_seen)
