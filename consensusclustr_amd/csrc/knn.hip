@@ -1742,11 +1742,14 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
 // exactly the stable sort's.
 // (also zeroes the ucap + 1 words of ustart, so a wrong caller u leaves no
 // garbage offsets behind)
+// (zc: three counters zeroed by the first threads -- the table path's fail
+// counts -- in place of a memset launch; may be NULL)
 __global__ void kb_count_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N,
                                 unsigned long long* __restrict__ pk, int* __restrict__ err,
-                                int32_t* __restrict__ ztab, int64_t nz) {
+                                int32_t* __restrict__ ztab, int64_t nz, unsigned* __restrict__ zc) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = t; i < nz; i += (int64_t)gridDim.x * blockDim.x) ztab[i] = 0;
+    if (zc && t < 3) zc[t] = 0u;
     if (t >= n) return;
     int c = idx[t];
     if (c < 0 || c >= N) {
@@ -2412,7 +2415,9 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         ctx->kb_zeroed = (void*)tc;
         ctx->kb_zero_n = N;
     }
-    kb_count_kernel<<<ng, 256, 0, st>>>(idx, n, N, pk, ctx->d_err, srow + n, (int64_t)ucap + 1);
+    // (the table path: its fail counts and the expansion tie count, misc[4..6], zeroed here)
+    kb_count_kernel<<<ng, 256, 0, st>>>(idx, n, N, pk, ctx->d_err, srow + n, (int64_t)ucap + 1,
+                                        tab_idx ? misc + 4 : nullptr);
     int rc = ccg_scan_i64(ctx, (const int64_t*)pk, pko, N, st);
     if (rc) {
         ctx->kb_zeroed = nullptr;  // the counts were not cleared: the next call zeroes them
@@ -2436,8 +2441,7 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     kb_fixup_big_kernel<<<16, 256, 0, st>>>(n, ustart, srow, row2u, big, nbig, rid);
     // 3. the distinct cells' rows and their kq nearest distinct cells
     float* urow_hint = cell_hint ? (float*)(uidx + (size_t)u * kq) : nullptr;
-    // the table path: fail counts and the expansion tie count (misc[4..6]) zeroed first
-    if (kq >= 1 && tab_idx) CCG_HIP(hipMemsetAsync(misc + 4, 0, 3 * sizeof(unsigned), st));
+    // (the table path's fail counts and tie count, misc[4..6]: zeroed by kb_count_kernel)
     if (d <= 32)
         kb_urows_kernel<32><<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, cell_hint,
                                                                       urow_hint);

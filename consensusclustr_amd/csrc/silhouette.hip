@@ -1342,11 +1342,15 @@ __global__ void sil_first_kernel(const int32_t* __restrict__ cell, int64_t m, in
     if (r < m) atomicMin(&first[cell[r]], (int)r);
 }
 
-__global__ void sil_init_kernel(int* __restrict__ first, int64_t ncell, int* __restrict__ zero, int64_t nzero) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ncell || t < nzero;
+// (also zeroes the call's sums and width partials, zw words: one launch
+// instead of a memset and this kernel)
+__global__ void sil_init_kernel(int* __restrict__ first, int64_t ncell, int* __restrict__ zero, int64_t nzero,
+                                unsigned long long* __restrict__ zw, int64_t nzw) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ncell || t < nzero || t < nzw;
          t += (int64_t)gridDim.x * blockDim.x) {
         if (t < ncell) first[t] = 0x7fffffff;
         if (t < nzero) zero[t] = 0;
+        if (t < nzw) zw[t] = 0ull;
     }
 }
 
@@ -1659,10 +1663,10 @@ static int sil_cells_run(ccg_ctx* ctx, const double* x, int64_t m, int d, const 
     unsigned long long* exc =
         (unsigned long long*)(tb + ccg_cdiv((int64_t)((char*)(mult + (int64_t)L * m) - tb), 16) * 16);
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
-    CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
     const unsigned gm = (unsigned)ccg_cdiv(m, 256);
-    sil_init_kernel<<<(unsigned)std::min<int64_t>(ccg_cdiv(std::max(ncell, (int64_t)(L + 1) * m + 4), 256), 4096), 256,
-                      0, st>>>(first, ncell, nexc, (int64_t)(L + 1) * m + 4);
+    sil_init_kernel<<<(unsigned)std::min<int64_t>(
+                          ccg_cdiv(std::max(std::max(ncell, (int64_t)(L + 1) * m + 4), words), 256), 4096),
+                      256, 0, st>>>(first, ncell, nexc, (int64_t)(L + 1) * m + 4, buf, words);
     sil_first_kernel<<<gm, 256, 0, st>>>(cell, m, first);
     sil_isrep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan);
     int rc = ccg_scan_i64(ctx, scan, scan, m, st);
