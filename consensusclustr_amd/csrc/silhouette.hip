@@ -95,11 +95,13 @@ __device__ __forceinline__ int sil_label(const int32_t* __restrict__ labels, int
 }
 
 // one atomic per block on one word: a small grid (a 1024-block grid spent
-// ~10 us serialising its atomics at the L2)
+// ~10 us serialising its atomics at the L2) of 1024-thread blocks (16 waves
+// per CU in flight: 256-thread blocks read at ~2.3 TB/s)
 #define SIL_MAXABS_GRID 256
-__global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, int64_t tot,
-                                                  unsigned* __restrict__ bits) {
-    __shared__ unsigned red[4];
+#define SIL_MAXABS_T 1024
+__global__ __launch_bounds__(SIL_MAXABS_T) void sil_maxabs(const double* __restrict__ x, int64_t tot,
+                                                           unsigned* __restrict__ bits) {
+    __shared__ unsigned red[SIL_MAXABS_T / 64];
     double mx = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;  // four loads in flight per step
     const int64_t stp = (int64_t)gridDim.x * blockDim.x;
     int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -116,7 +118,12 @@ __global__ __launch_bounds__(256) void sil_maxabs(const double* __restrict__ x, 
     for (int o = 32; o > 0; o >>= 1) local = max(local, (unsigned)__shfl_xor((int)local, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(bits, max(max(red[0], red[1]), max(red[2], red[3])));  // one atomic per block
+    if (threadIdx.x == 0) {
+        unsigned b = red[0];
+#pragma unroll
+        for (int w = 1; w < SIL_MAXABS_T / 64; ++w) b = max(b, red[w]);
+        atomicMax(bits, b);  // one atomic per block
+    }
 }
 
 template <int DMAX>
@@ -1377,24 +1384,41 @@ __global__ void sil_rep_kernel(const int32_t* __restrict__ cell, int64_t m, cons
     else nonrep[r - scan[r]] = make_int3((int)r, rp, pp);
 }
 
-// Per labeling (blockIdx.y strides), every non-representative row whose
-// label differs from its representative's: dis[l][pos] += 1 (the weight is
-// cnt - dis) and the row joins the exception list (l << 32 | row).
-__global__ void sil_mult_kernel(int64_t m, int L, const int32_t* __restrict__ labels,
-                                const int64_t* __restrict__ scan, const int3* __restrict__ nonrep, int64_t mw,
-                                int* __restrict__ dis, unsigned long long* __restrict__ exc, int* __restrict__ nexc,
-                                SilSegs sgs) {
+// Every non-representative row whose label differs from its
+// representative's: dis[l][pos] += 1 (the weight is cnt - dis) and the row
+// joins the exception list (l << 32 | row).  A thread takes one row and
+// SIL_MULT_LG labelings (blockIdx.y: the group): one (row, representative)
+// load and the group's label pairs in flight together (one labeling per
+// thread and a grid-stride row loop chained two dependent loads per row).
+#define SIL_MULT_LG 8
+__global__ __launch_bounds__(256) void sil_mult_kernel(int64_t m, int L, const int32_t* __restrict__ labels,
+                                                       const int64_t* __restrict__ scan,
+                                                       const int3* __restrict__ nonrep, int64_t mw,
+                                                       int* __restrict__ dis, unsigned long long* __restrict__ exc,
+                                                       int* __restrict__ nexc, SilSegs sgs) {
     const int64_t nn = m - scan[m];
-    for (int l = blockIdx.y; l < L; l += gridDim.y) {
-        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nn; j += (int64_t)gridDim.x * blockDim.x) {
-            const int3 e = nonrep[j];
-            const int r = e.x, rp = e.y;
-            // (a row and its representative are in one segment: the cell ids are per segment)
-            const int q = sgs.nseg ? sil_seg_row(sgs.off, sgs.nseg, r) : 0;
-            if (sil_label(labels, m, sgs, q, l, r) != sil_label(labels, m, sgs, q, l, rp)) {
+    for (int l0 = blockIdx.y * SIL_MULT_LG; l0 < L; l0 += gridDim.y * SIL_MULT_LG)
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nn; j += (int64_t)gridDim.x * blockDim.x) {
+        const int3 e = nonrep[j];
+        const int r = e.x, rp = e.y;
+        // (a row and its representative are in one segment: the cell ids are per segment)
+        const int q = sgs.nseg ? sil_seg_row(sgs.off, sgs.nseg, r) : 0;
+        int a[SIL_MULT_LG], b[SIL_MULT_LG];
+#pragma unroll
+        for (int t = 0; t < SIL_MULT_LG; ++t) {
+            a[t] = b[t] = 0;
+            if (l0 + t < L) {
+                a[t] = sil_label(labels, m, sgs, q, l0 + t, r);
+                b[t] = sil_label(labels, m, sgs, q, l0 + t, rp);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < SIL_MULT_LG; ++t) {
+            if (a[t] != b[t]) {
+                const int l = l0 + t;
                 atomicAdd(&dis[(int64_t)l * mw + e.z], 1);
-                const int e = atomicAdd(nexc, 1);
-                exc[e] = ((unsigned long long)l << 32) | (unsigned long long)r;
+                const int x = atomicAdd(nexc, 1);
+                exc[x] = ((unsigned long long)l << 32) | (unsigned long long)r;
             }
         }
     }
@@ -1592,7 +1616,8 @@ extern "C" int ccg_silhouette_dev(ccg_ctx* ctx, const double* x, int64_t m, int 
     }
     const int t_all = ccg_timer_start(ctx, CCG_KT_SILHOUETTE, st);
     CCG_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned long long) * words, st));
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4 * SIL_MAXABS_T), SIL_MAXABS_GRID), SIL_MAXABS_T, 0,
+                 st>>>(x, m * d, maxabs);
     if (d <= 16)
         sil_launch<16>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, auxc, q,
                         img, out_width, nbw, st);
@@ -1674,9 +1699,11 @@ static int sil_cells_run(ccg_ctx* ctx, const double* x, int64_t m, int d, const 
     sil_rep_kernel<<<gm, 256, 0, st>>>(cell, m, first, scan, rep, cnt, nonrep);
     // mw = the number of representatives (the distinct cells): device-side
     // only, so the width grid covers m positions and the weights' stride is m
-    dim3 gx((unsigned)std::min<int64_t>(ccg_cdiv(m, 256), 32), (unsigned)std::min(L, 65535));
+    // rows: the non-representatives are typically about a third of m (grid-stride past half)
+    dim3 gx((unsigned)ccg_cdiv(m, 512), (unsigned)std::min<int64_t>(ccg_cdiv(L, SIL_MULT_LG), 65535));
     sil_mult_kernel<<<gx, 256, 0, st>>>(m, L, labels, scan, nonrep, m, mult, exc, nexc, sgs);
-    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4096), SIL_MAXABS_GRID), 256, 0, st>>>(x, m * d, maxabs);
+    sil_maxabs<<<(unsigned)std::min<int64_t>(ccg_cdiv(m * d, 4 * SIL_MAXABS_T), SIL_MAXABS_GRID), SIL_MAXABS_T, 0,
+                 st>>>(x, m * d, maxabs);
 #define SIL_CELLS(DM_)                                                                                              \
     sil_launch<DM_>(x, m, d, labels, L, cmax, maxabs, gsum, gsum2, gcnt, gvar, wsum, wcnt, npres, codes, pos, mu, muc, \
                     auxc, q, img, nullptr, nbw, st, rep, mult, cnt, m, exc, nexc, scan + m, scan, sgs, ts_tiles,     \
