@@ -34,6 +34,14 @@
 #define RS_ADAPT 1  // tools only: 0 = tiles of 4096 pairs always (A/B)
 #endif
 
+// Block b runs on XCD b mod 8; each XCD takes a contiguous range of tiles so
+// neighbouring tiles' histogram columns and output runs (adjacent in the
+// digit-major order) are written through one L2 instead of eight.
+__device__ __forceinline__ int rs_tile(int b, int ntiles) {
+    const int full = ntiles >> 3, rem = ntiles & 7, x = b & 7;
+    return x * full + min(x, rem) + (b >> 3);
+}
+
 template <int RS_IPT>
 __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift,
                                                       int bits, int ntiles, int64_t* __restrict__ cnt) {
@@ -41,14 +49,15 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist(const int32_t* __restrict_
     const int nb = 1 << bits;
     for (int t = threadIdx.x; t < nb; t += RS_THREADS) h[t] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT);
+    const int tile = rs_tile(blockIdx.x, ntiles);
+    const int64_t base = (int64_t)tile * (RS_THREADS * RS_IPT);
 #pragma unroll 4
     for (int i = 0; i < RS_IPT; ++i) {
         const int64_t e = base + (int64_t)i * RS_THREADS + threadIdx.x;
         if (e < n) atomicAdd(&h[((unsigned)keys[e] >> shift) & (nb - 1)], 1);
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < nb; t += RS_THREADS) cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) cnt[(int64_t)t * ntiles + tile] = h[t];
 }
 
 __device__ __forceinline__ unsigned long long rs_lanemask_lt() {
@@ -68,11 +77,12 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
     __shared__ int2 stage[RS_THREADS * RS_IPT];
     const int nb = 1 << bits;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tile = rs_tile(blockIdx.x, ntiles);
     for (int t = threadIdx.x; t < RS_WAVES * nb; t += RS_THREADS) wcnt[t / nb][t % nb] = 0;
-    for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = (int)off[(int64_t)t * ntiles + blockIdx.x];
+    for (int t = threadIdx.x; t < nb; t += RS_THREADS) goff[t] = (int)off[(int64_t)t * ntiles + tile];
     __syncthreads();
     // wave w's run: pairs [base, base + 64 * RS_IPT), item i at base + 64 i + lane
-    const int64_t base = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT) + (int64_t)w * 64 * RS_IPT;
+    const int64_t base = (int64_t)tile * (RS_THREADS * RS_IPT) + (int64_t)w * 64 * RS_IPT;
     int kk[RS_IPT], vv[RS_IPT], rk[RS_IPT];
     const unsigned long long lt = rs_lanemask_lt();
 #pragma unroll
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter(const int32_t* __restri
         stage[dstart[dg] + wcnt[w][dg] + rk[i]] = make_int2(kk[i], vv[i]);
     }
     __syncthreads();
-    const int64_t tbase = (int64_t)blockIdx.x * (RS_THREADS * RS_IPT);
+    const int64_t tbase = (int64_t)tile * (RS_THREADS * RS_IPT);
     const int tn = (int)min((int64_t)(RS_THREADS * RS_IPT), n - tbase);
     for (int j = threadIdx.x; j < tn; j += RS_THREADS) {
         const int2 kv = stage[j];
