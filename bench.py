@@ -88,6 +88,10 @@ def parse():
                          "bootstraps, host-bound) 2/3/4 -> 3828/4385/3774; cfg5 2/3/4 -> 1062/1025/967")
     ap.add_argument("--seg-batch", type=int, default=16,
                     help="cfg5: bootstraps of every subcluster per segmented launch set")
+    ap.add_argument("--boot-batch", type=int, default=0,
+                    help="table path: bootstraps per launch set (ccg_knn_boots_table_dev, one SNN class pass over "
+                         "the batch's disjoint union, one ccg_silhouette_segments_dev); 1 = one bootstrap per launch "
+                         "set (the round-5 step); 0 = auto")
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
                     help="table: one cell table per step (ccg_knn_table_dev) filtered per bootstrap; "
                          "screen: a screen per bootstrap (warm-started)")
@@ -282,42 +286,75 @@ def cpu_baseline(pcs_np, B, n, N, d, sample_rows, seed=0, robust=True, coc_cols=
 
 
 def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, robust, A_full=None, co=None,
-                       both=None, r0=0, r1=0, sample=256):
+                       both=None, r0=0, r1=0, sample=256, batch=None):
     """Part of the cpu_baseline leg: the oracle as the CHECKER of one timed
     bootstrap.  Bootstrap 0 runs again through the step's calls (gather, kNN
     from the cell table, SNN rows, silhouette) into fresh buffers; sampled kNN
     rows (plus every row the fast paths sent to the exact search) must be
     bit-exact, all three SNN graphs must equal the oracle's edge lists, the
     60 silhouette means must agree within 1e-5, and sampled rows of the
-    step's co/both slab must equal orc_cocluster_rows."""
+    step's co/both slab must equal orc_cocluster_rows.  batch (the batched
+    step): the step's first launch set runs again -- ccg_knn_boots_table_dev,
+    one class-level SNN pass over the batch, one ccg_silhouette_segments_dev
+    -- and its first bootstrap is checked as above, plus sampled kNN rows of
+    its last bootstrap."""
     import concurrent.futures as cf
     import oracle as O
     N, d = pcs.shape
     n = boot.numel()
     dev = pcs.device
-    rows = torch.empty((n, d), dtype=torch.float64, device=dev)
-    knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
-    eng.gather_rows_rm_t(pcs, N, d, boot, rows)
-    if tab is not None:
-        eng.knn_boot_table_t(pcs_cm, N, d, boot, u, rows, 20, tab[0], tab[1], knn)
-    else:
-        eng.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, knn)
-    cut = eng.knn_last_fallback()
-    sb = SnnBufs(torch, n, 400 * n, dev)
-    info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
-    sb.run(eng, knn, boot, info)
-    L = labels0.shape[0]
-    mean = torch.empty(L, dtype=torch.float64, device=dev)
-    ncl = torch.empty(L, dtype=torch.int32, device=dev)
-    mns = torch.empty(L, dtype=torch.int32, device=dev)
-    if robust:
-        eng.silhouette_cells_t(rows, labels0, cmax, boot, N, mean, ncl, mns)
-    torch.cuda.synchronize()
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     out = {}
+    L = labels0.shape[0]
+    rng = np.random.default_rng(5)
+    if batch is not None:
+        nbb = batch["idx"].shape[0]
+        m = nbb * n
+        rows = torch.empty((m, d), dtype=torch.float64, device=dev)
+        knn = torch.empty((m, 20), dtype=torch.int32, device=dev)
+        eng.gather_rows_rm_t(pcs, N, d, batch["idx"].reshape(-1), rows)
+        eng.knn_boots_table_t(N, d, batch["idx"], batch["uniq"], rows, 20, tab[0], tab[1], knn)
+        cut_all = eng.knn_last_fallback()
+        sb = SnnBufs(torch, m, 400 * m, dev)
+        info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
+        sb.run(eng, knn, batch["keys"], info, n=m)
+        ms = [torch.empty(L, dtype=torch.float64, device=dev) for _ in range(nbb)]
+        if robust:
+            eng.silhouette_segments_t(rows, np.arange(nbb + 1, dtype=np.int64) * n, batch["labels"], cmax,
+                                      batch["keys"], nbb * N, ms)
+        torch.cuda.synchronize()
+        mean = ms[0]
+        # the batch's last bootstrap: sampled kNN rows and its cut-tie rows (ids of the concatenation)
+        a = (nbb - 1) * n
+        XL = rows[a:].cpu().numpy()
+        cl = cut_all[cut_all >= a] - a
+        ql = np.unique(np.concatenate([cl[:2048], rng.choice(n, min(sample, n), replace=False)])).astype(np.int32)
+        oi, _ = O.knn_queries(XL, 20, ql, nthreads=threads)
+        out["batch_bootstraps"] = int(nbb)
+        out["knn_last_boot_rows_checked"] = int(ql.size)
+        out["knn_last_boot_exact"] = bool(np.array_equal(knn[a:].cpu().numpy()[ql] - a, oi))
+        cut = cut_all[cut_all < n]
+        rows, knn = rows[:n], knn[:n]
+    else:
+        rows = torch.empty((n, d), dtype=torch.float64, device=dev)
+        knn = torch.empty((n, 20), dtype=torch.int32, device=dev)
+        eng.gather_rows_rm_t(pcs, N, d, boot, rows)
+        if tab is not None:
+            eng.knn_boot_table_t(pcs_cm, N, d, boot, u, rows, 20, tab[0], tab[1], knn)
+        else:
+            eng.knn_boot_t(pcs_cm, N, d, boot, u, rows, 20, knn)
+        cut = eng.knn_last_fallback()
+        sb = SnnBufs(torch, n, 400 * n, dev)
+        info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
+        sb.run(eng, knn, boot, info)
+        mean = torch.empty(L, dtype=torch.float64, device=dev)
+        ncl = torch.empty(L, dtype=torch.int32, device=dev)
+        mns = torch.empty(L, dtype=torch.int32, device=dev)
+        if robust:
+            eng.silhouette_cells_t(rows, labels0, cmax, boot, N, mean, ncl, mns)
+        torch.cuda.synchronize()
     X = rows.cpu().numpy()
     kn = knn.cpu().numpy()
-    rng = np.random.default_rng(5)
     q = np.unique(np.concatenate([cut[:4096], rng.choice(n, min(sample, n), replace=False)])).astype(np.int32)
     oi, _ = O.knn_queries(X, 20, q, nthreads=threads)
     out["knn_rows_checked"] = int(q.size)
@@ -326,7 +363,7 @@ def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, rob
     ok = int(inf[1]) == 0 and int(inf[3:].min()) >= 0
     out["snn_classes"] = int(inf[0])
     if ok:
-        got = sb.decode(n, int(inf[0]))
+        got = sb.decode(sb.n if batch is not None else n, int(inf[0]), 0, n)
         for g, k in enumerate(K_NUM):
             ei, ej, ew = O.snn(kn, k, "number")
             ok = ok and np.array_equal(got[g][0], ei) and np.array_equal(got[g][1], ej) and \
@@ -892,10 +929,17 @@ def main():
     # [torch rank, device, the group's nranks, the group's first rank]
     ranks_seen = group_ranks_seen(torch, dist, world, rank, local, grp, dev)
     W = WORKLOADS[args.workload]
+    # bootstraps per launch set (table path): one set of launches for the
+    # batch's kNN, SNN and silhouettes (round 6)
+    NBB = args.boot_batch if args.boot_batch > 0 else W.get("boot_batch", 16)
+    if args.knn_path != "table":
+        NBB = 1
     if args.streams > 0:
         S = args.streams
     elif args.workload == "cfg5":
         S = 2
+    elif NBB > 1:
+        S = W.get("batch_streams", 2)
     else:
         S = 4 if int(args.boot_size * (args.cells or W["cells"])) >= 50000 else 3
     if args.workload == "cfg5":
@@ -943,24 +987,53 @@ def main():
         labels[j] = synth_labels(torch, pop, boots[j], L, dev, 1000 + bids[j], chi=W["cmax"])
     cmax = int(labels.max().item())
 
-    RING = S  # bootstrap buffers (gathered rows, kNN) in flight
-    rows_s = [torch.empty((n, d), dtype=torch.float64, device=dev) for _ in range(RING)]
-    knn_s = [torch.empty((n, 20), dtype=torch.int32, device=dev) for _ in range(RING)]
-    rows, knn = rows_s[0], knn_s[0]
-    rcap = 300 * n  # SNN class-row entries (items per class ~ 190 at cfg3); grown once after the warmup if short
+    NBB = max(1, min(NBB, B))
+    batched = NBB > 1
+    batches = [(b0, min(B, b0 + NBB)) for b0 in range(0, B, NBB)]
+    nrow = NBB * n  # rows of a launch set
+    RING = S  # launch-set buffers (gathered rows, kNN) in flight
+    rows_s = [torch.empty((nrow, d), dtype=torch.float64, device=dev) for _ in range(RING)]
+    knn_s = [torch.empty((nrow, 20), dtype=torch.int32, device=dev) for _ in range(RING)]
+    rows, knn = rows_s[0][:n], knn_s[0][:n]
+    rcap = 300 * nrow  # SNN class-row entries (items per class ~ 190 at cfg3); grown once after the warmup if short
 
     def alloc_snn(rcap):
         # per stream: the class-level rows of ccg_snn_classes_dev
-        return [SnnBufs(torch, n, rcap, dev) for _ in range(S)]
+        return [SnnBufs(torch, nrow, rcap, dev) for _ in range(S)]
     snn_out = alloc_snn(rcap)
     if os.environ.get("CCG_BENCH_TORCH_STREAMS"):
         streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     else:
         streams = [e.torch_stream() for e in engs]  # each context's own non-blocking HIP stream
-    snn_info = torch.zeros((B, 3 + len(K_NUM)), dtype=torch.int64, device=dev)  # [u, status, cap, class edges]
+    # [u, status, cap, class edges] per bootstrap, or per launch set (batched)
+    snn_info = torch.zeros((len(batches) if batched else B, 3 + len(K_NUM)), dtype=torch.int64, device=dev)
     means = torch.empty((B, L), dtype=torch.float64, device=dev)
     nclust = torch.empty((B, L), dtype=torch.int32, device=dev)
     minsize = torch.empty((B, L), dtype=torch.int32, device=dev)
+    # launch sets: bootstrap j's rows are slot (j - b0) of its set; its cells
+    # get the keys slot N + cell (SNN classes and silhouette cells stay apart
+    # between the set's bootstraps); everything a launch needs is built here,
+    # before timing
+    vkeys = boots + (torch.tensor([j - (j // NBB) * NBB for j in range(B)], dtype=torch.int32,
+                                  device=dev) * N)[:, None]
+    sets = [dict(idx=boots[b0:b1], flat=boots[b0:b1].reshape(-1), keys=vkeys[b0:b1].reshape(-1),
+                 uniq=np.array(uniq[b0:b1], np.int32), m=(b1 - b0) * n,
+                 off=np.arange(b1 - b0 + 1, dtype=np.int64) * n, ncell=(b1 - b0) * N,
+                 labels=[labels[j] for j in range(b0, b1)], means=[means[j] for j in range(b0, b1)],
+                 nclust=[nclust[j] for j in range(b0, b1)], minsize=[minsize[j] for j in range(b0, b1)])
+            for b0, b1 in batches]
+
+    def run_set(e, si, t, info=None):
+        # one launch set: gather, kNN from the table, SNN classes, silhouettes of its bootstraps
+        c = sets[t]
+        m = c["m"]
+        r, k = rows_s[si][:m], knn_s[si][:m]
+        e.gather_rows_rm_t(pcs, N, d, c["flat"], r)
+        e.knn_boots_table_t(N, d, c["idx"], c["uniq"], r, 20, tab_idx, tab_d2, k)
+        snn_out[si].run(e, k, c["keys"], snn_info[t] if info is None else info, n=m)
+        if robust:  # granular mode scores no clustering (:688)
+            e.silhouette_segments_t(r, c["off"], c["labels"], cmax, c["keys"], c["ncell"], c["means"], c["nclust"],
+                                    c["minsize"])
     choice = torch.empty(B, dtype=torch.int32, device=dev)
     A_full = torch.zeros((Gc * cpr, N), dtype=torch.uint8, device=dev)  # all ranks' columns
     A_local = A_full[rank * cpr:(rank + 1) * cpr]  # this rank's block, all-gathered in place
@@ -1009,15 +1082,22 @@ def main():
             eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
         for st_ in streams:
             st_.wait_stream(cur)
-        for j in range(B):
-            si = j % S
-            e = engs[si]
-            with torch.cuda.stream(streams[si]):
-                e.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[si])
-                boot_knn(e, j, rows_s[si], knn_s[si])
-                snn_out[si].run(e, knn_s[si], boots[j], snn_info[j])
-                if robust:  # granular mode scores no clustering (:688)
-                    e.silhouette_cells_t(rows_s[si], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+        if batched:
+            for t in range(len(batches)):
+                si = t % S
+                with torch.cuda.stream(streams[si]):
+                    run_set(engs[si], si, t)
+        else:
+            for j in range(B):
+                si = j % S
+                e = engs[si]
+                with torch.cuda.stream(streams[si]):
+                    e.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[si][:n])
+                    boot_knn(e, j, rows_s[si][:n], knn_s[si][:n])
+                    snn_out[si].run(e, knn_s[si][:n], boots[j], snn_info[j], n=n)
+                    if robust:  # granular mode scores no clustering (:688)
+                        e.silhouette_cells_t(rows_s[si][:n], labels[j], cmax, boots[j], N, means[j], nclust[j],
+                                             minsize[j])
         for st_ in streams:
             cur.wait_stream(st_)
 
@@ -1067,7 +1147,9 @@ def main():
     # the graph's baked pointers stay valid); the replay is checked against an
     # eager step's outputs before timing
     launch_note = "eager"
-    use_graph = args.launch == "graph" or (args.launch == "auto" and n >= 50000)
+    # (launch sets upload small host tables -- segment offsets, label and
+    # output pointers -- and issue ~80 launches per set: eager)
+    use_graph = args.launch == "graph" or (args.launch == "auto" and n >= 50000 and not batched)
     if use_graph and not W.get("no_graph"):
         try:
             torch.cuda.synchronize()
@@ -1122,18 +1204,23 @@ def main():
         kt[w] = (sum(x[0] for x in r), sum(x[1] for x in r))
     for e in engs:
         e.timing(False)
-    # host cost of one bootstrap's launches on an idle GPU (no queue back-pressure)
+    # host cost of one bootstrap's launches on an idle GPU (no queue
+    # back-pressure): one launch set divided by its bootstraps when batched
     host_idle = []
-    for j in range(min(B, 6)):
+    iso_info = torch.zeros(3 + len(K_NUM), dtype=torch.int64, device=dev)
+    for j in range(min(len(batches) if batched else B, 6)):
         torch.cuda.synchronize()
         th = time.perf_counter()
         with torch.cuda.stream(streams[0]):
-            eng.gather_rows_rm_t(pcs, N, d, boots[j], rows_s[0])
-            boot_knn(eng, j, rows_s[0], knn_s[0])
-            snn_out[0].run(eng, knn_s[0], boots[j], snn_info[j])
-            if robust:
-                eng.silhouette_cells_t(rows_s[0], labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
-        host_idle.append(time.perf_counter() - th)
+            if batched:
+                run_set(eng, 0, j, iso_info)
+            else:
+                eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
+                boot_knn(eng, j, rows, knn)
+                snn_out[0].run(eng, knn, boots[j], iso_info, n=n)
+                if robust:
+                    eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+        host_idle.append((time.perf_counter() - th) / (sets[j]["m"] // n if batched else 1))
         torch.cuda.synchronize()
     host_idle_ms = 1000 * float(np.median(host_idle))
     # roofline of the kNN screens, measured in isolation (one launch at a
@@ -1152,6 +1239,15 @@ def main():
         eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         eng.knn_boot_table_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, tab_idx, tab_d2, knn)
     iso_boot_table = eng.timing_read("knn_total")
+    iso_set_table = None
+    if batched:  # the launch set's kNN (ccg_knn_boots_table_dev), per bootstrap
+        c0 = sets[0]
+        eng.gather_rows_rm_t(pcs, N, d, c0["flat"], rows_s[0][:c0["m"]])
+        for _ in range(2):
+            eng.knn_boots_table_t(N, d, c0["idx"], c0["uniq"], rows_s[0][:c0["m"]], 20, tab_idx, tab_d2,
+                                  knn_s[0][:c0["m"]])
+        t_, c_ = eng.timing_read("knn_total")
+        iso_set_table = (t_, c_ * (c0["m"] // n))
     for j in range(min(B, 8)):  # as in the screen path: warm-started by earlier bootstraps
         eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
         eng.knn_boot_hint_t(pcs_cm, N, d, boots[j], uniq[j], rows, 20, knn, hint)
@@ -1166,19 +1262,40 @@ def main():
     # on the GPU): the per-bootstrap rooflines below
     eng.timing_read("snn")
     eng.timing_read("silhouette")
-    nis = min(B, 4)
-    for j in range(nis):
-        eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
-        boot_knn(eng, j, rows, knn)
-        snn_out[0].run(eng, knn, boots[j], snn_info[j])
-        if robust:
-            eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
-    iso_snn = eng.timing_read("snn")
-    iso_sil = eng.timing_read("silhouette")
+    if batched:  # one launch set (its SNN pass and its silhouette launch set), per bootstrap
+        nis = sets[0]["m"] // n
+        iso_infos = torch.zeros((1, 3 + len(K_NUM)), dtype=torch.int64, device=dev)
+        run_set(eng, 0, 0, iso_infos[0])
+        iso_snn = eng.timing_read("snn")
+        iso_sil = eng.timing_read("silhouette")
+        iso_snn, iso_sil = (iso_snn[0], iso_snn[1] * nis), (iso_sil[0], iso_sil[1] * nis)
+    else:
+        nis = min(B, 4)
+        iso_infos = torch.zeros((nis, 3 + len(K_NUM)), dtype=torch.int64, device=dev)
+        for j in range(nis):
+            eng.gather_rows_rm_t(pcs, N, d, boots[j], rows)
+            boot_knn(eng, j, rows, knn)
+            snn_out[0].run(eng, knn, boots[j], iso_infos[j], n=n)
+            if robust:
+                eng.silhouette_cells_t(rows, labels[j], cmax, boots[j], N, means[j], nclust[j], minsize[j])
+        iso_snn = eng.timing_read("snn")
+        iso_sil = eng.timing_read("silhouette")
     torch.cuda.synchronize()
-    iso_edges = snn_info[:nis, 3:].sum(0).tolist()  # class edges per graph, over the nis bootstraps
-    iso_classes = float(snn_info[:nis, 0].double().mean().item())
+    iso_edges = iso_infos[:, 3:].sum(0).tolist()  # class edges per graph, over the nis bootstraps
+    iso_classes = float(iso_infos[:, 0].double().sum().item()) / nis
     iso_npres = int(nclust[:nis].sum().item())  # sum over the bootstraps' labelings of present clusters
+    # the drop-in's host side of the SNN (R: igraph::make_graph of each graph,
+    # :656-658): ccg_snn_graphs_cells (device pass + copy to pinned memory)
+    # and the host expansion of the class rows (ccg_snn_graph_fetch), for
+    # bootstrap 0 through Engine.snn_multi; outside value
+    eng.gather_rows_rm_t(pcs, N, d, boots[0], rows)
+    boot_knn(eng, 0, rows, knn)
+    torch.cuda.synchronize()
+    kn0 = knn.cpu().numpy()
+    b0np = boots_np[0]
+    eng.snn_multi(kn0, K_NUM, "number", cell=b0np)  # (warm: pinned staging sized)
+    eng.snn_multi(kn0, K_NUM, "number", cell=b0np)
+    host_snn = eng.last_snn_times
     eng.timing(False)
     if G > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -1240,7 +1357,8 @@ def main():
         "avg_launch_ms": round(ms_table, 4),
         "table_total_ms": round(avg(iso_table_total), 4),
         "table_fallback_cells": int(fb_tab_build[1]),
-        "knn_total_ms_per_boot_from_table": round(avg(iso_boot_table), 4),
+        "knn_total_ms_per_boot_from_table": round(avg(iso_set_table if batched else iso_boot_table), 4),
+        "knn_total_ms_per_boot_from_table_one_boot_per_call": round(avg(iso_boot_table), 4),
         "boot_fallback_last_boot": int(fb_tab[1]),
         "avg_launch_ms_note": f"{iso_table[1]} launches timed in isolation after the timed region; one per step "
                               f"serves the step's {B} bootstraps",
@@ -1371,17 +1489,26 @@ def main():
         "launch": launch_note,
         "host_enqueue_ms_per_step": round(host_ms, 3),
         "host_launch_ms_per_boot_idle_gpu": round(host_idle_ms, 3),
+        "boots_per_launch_set": NBB,
+        "launch_sets_per_step": len(batches) if batched else B,
+        "host_snn_pass_ms_per_boot": round(1e3 * host_snn[0], 2),
+        "host_snn_decode_ms_per_boot": round(1e3 * host_snn[1], 2),
+        "host_snn_note": "the drop-in's host consumer path for one bootstrap (Engine.snn_multi: ccg_snn_graphs_cells "
+                         "= device class pass + copy of the class rows to pinned memory, then ccg_snn_graph_fetch "
+                         "expanding them into the three (i, j, w) edge lists on host threads); outside value",
         "cocluster_avg_ms": round(coc_ms, 3),
         "knn_fallback_rows_last_boot": int(fb[1]),
         "knn_fallback_rows_last_boot_cold": int(fb_cold[1]),
-        "snn_class_edges_max_per_boot": [int(e) for e in need],
+        ("snn_class_edges_max_per_launch_set" if batched else "snn_class_edges_max_per_boot"): [int(e) for e in need],
     }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pcs.cpu().numpy(), B, n, N, d, args.cpu_sample_rows, robust=robust,
                                            coc_cols=Gc * cpr, coc_pairs=P)
         out["cpu_baseline"]["check"] = cpu_baseline_check(
             eng, torch, pcs, pcs_cm, boots[0], uniq[0], labels[0], (tab_idx, tab_d2) if use_table else None, cmax,
-            robust, A_full, co, both, int(r0), int(r1))
+            robust, A_full, co, both, int(r0), int(r1),
+            batch=dict(idx=sets[0]["idx"], uniq=sets[0]["uniq"], keys=sets[0]["keys"], labels=sets[0]["labels"])
+            if batched else None)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

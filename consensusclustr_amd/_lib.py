@@ -74,6 +74,7 @@ SIGNATURES = {
     "ccg_knn_boot_segments_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
     "ccg_knn_boot_segments": (_i, [_p, _p, _i64, _i, _p, _i64, _p, _p, _i, _i, _p, _p, _p]),
     "ccg_knn_boot_table_dev": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _p, _i, _p, _p, _i, _p, _p, _p, _p]),
+    "ccg_knn_boots_table_dev": (_i, [_p, _i64, _i, _p, _i64, _i, _p, _p, _i, _p, _p, _i, _i, _p, _p, _p, _p]),
     "ccg_knn_segments_dev": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p, _p]),
     "ccg_knn_segments": (_i, [_p, _p, _i64, _i, _p, _i, _i, _p, _p, _p]),
     "ccg_snn": (_i, [_p, _p, _i64, _i, _i, _i, _p, _p, _p, _i64, _p]),
@@ -120,6 +121,7 @@ SIGNATURES = {
     "ccg_group_consensus_knn_assign": (_i, [_p, _p, _i, _i64, _i64, _i, _p]),
     "ccg_group_knn_boot": (_i, [_p, _p, _i64, _i, _p, _i64, _i, _i, _p, _p, _p]),
     "ccg_sort_pairs_dev": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p]),
+    "ccg_scan_i64_dev": (_i, [_p, _p, _p, _i64, _p]),
     "ccg_timing_enable": (_i, [_p, _i]),
     "ccg_timing_read": (_i, [_p, _i, _p, _p]),
 }

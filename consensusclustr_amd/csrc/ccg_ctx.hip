@@ -57,8 +57,9 @@ extern "C" int ccg_open(const ccg_config* cfg, ccg_ctx** out) {
     }
     e = hipMalloc(&c->d_err, 64);
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, 64);
-    if (e == hipSuccess) e = hipMalloc(&c->d_scan, SCAN_LB_BYTES);
-    if (e == hipSuccess) e = hipMemset(c->d_scan, 0, SCAN_LB_BYTES);
+    c->scan_nstreams = 0;
+    if (e == hipSuccess) e = hipMalloc(&c->d_scan, (size_t)SCAN_LB_BYTES * CCG_SCAN_SLOTS);
+    if (e == hipSuccess) e = hipMemset(c->d_scan, 0, (size_t)SCAN_LB_BYTES * CCG_SCAN_SLOTS);
     if (e != hipSuccess) {
         if (c->d_err) (void)hipFree(c->d_err);
         if (c->d_scan) (void)hipFree(c->d_scan);
@@ -95,6 +96,15 @@ extern "C" int ccg_close(ccg_ctx* ctx) {
 
 int ccg_h2d_staged(ccg_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t st) {
     if (bytes == 0) return CCG_OK;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    CCG_HIP(hipStreamIsCapturing(st, &cap));
+    if (cap != hipStreamCaptureStatusNone) {
+        // the ring slot's event wait cannot be captured, and a replay would
+        // copy whatever a later call left in the slot
+        ccg_set_error("this entry point uploads a host table (segment offsets / pointer tables) and cannot be "
+                      "captured into a HIP graph; launch it eagerly");
+        return CCG_EINVAL;
+    }
     const int s = ctx->pin_next;
     ctx->pin_next = (s + 1) % CCG_PIN_RING;
     if (!ctx->pin_ev[s]) CCG_HIP(hipEventCreateWithFlags(&ctx->pin_ev[s], hipEventDisableTiming));
@@ -424,8 +434,19 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipSt
         return CCG_OK;
     }
     int64_t nb = ccg_cdiv(n, SCAN_TILE);
-    if (nb <= SCAN_LB_MAX) {
-        unsigned long long* stat = (unsigned long long*)ctx->d_scan;
+    // the stream's own slice of the single-pass state: two streams' scans
+    // never share status words (a shared word could make a tile of one wait
+    // on a word the other's last tile already cleared: a hang); a context
+    // used from more than CCG_SCAN_SLOTS streams takes the two-pass scan
+    int slot = -1;
+    for (int i = 0; i < ctx->scan_nstreams; ++i)
+        if (ctx->scan_stream[i] == st) slot = i;
+    if (slot < 0 && ctx->scan_nstreams < CCG_SCAN_SLOTS) {
+        slot = ctx->scan_nstreams++;
+        ctx->scan_stream[slot] = st;
+    }
+    if (nb <= SCAN_LB_MAX && slot >= 0) {
+        unsigned long long* stat = (unsigned long long*)((char*)ctx->d_scan + (size_t)slot * SCAN_LB_BYTES);
         scan_onepass<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, (int)nb, stat, (unsigned*)(stat + SCAN_LB_MAX));
         CCG_HIP(hipGetLastError());
         return CCG_OK;

@@ -1,6 +1,7 @@
 // Internal declarations of libccg.so (not part of the ABI).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -62,6 +63,8 @@ enum ccg_ws_slot {
     WS_KB_C,         // distinct-cell kNN: per-cell counts / offsets / cursors / cell -> distinct id (counting grouping)
     WS_SIL_IMG,      // silhouette: per-labeling LDS images of the fp16-screen width kernel
     WS_SIL_SEG,      // silhouette segments: offsets, tile starts, label and output pointers
+    WS_FX_C,         // kNN segmented exact search: the compacted failed list, radii, segment offsets
+    WS_KBT,          // kNN bootstrap batches: segment offsets (distinct cells, rows), per-segment fail counts
     WS_NSLOTS
 };
 
@@ -79,6 +82,7 @@ struct ccg_timer_rec {
 #define CCG_DERR_KNN_UNIQUE 8     // ccg_knn_boot_dev: n_unique differs from the distinct cells of idx
 
 #define CCG_PIN_RING 8
+#define CCG_SCAN_SLOTS 8  // streams with their own single-pass scan state per context
 
 struct ccg_ctx {
     int device;
@@ -104,8 +108,11 @@ struct ccg_ctx {
     int pin_next;
     // single-pass scan state (ccg_scan_i64): per-tile status words and the
     // finished-tile count, zero between calls (the kernel's last tile clears
-    // them)
+    // them); one slice per stream the context has scanned on (CCG_SCAN_SLOTS),
+    // so scans enqueued on two streams never share status words
     void* d_scan;
+    hipStream_t scan_stream[CCG_SCAN_SLOTS];
+    int scan_nstreams;
     // kernel timing (ccg_timing_*)
     int timing;
     ccg_timer_rec* timers;   // pool, grows
@@ -152,8 +159,17 @@ int ccg_take_device_error(ccg_ctx* ctx);
 // with the error message set).
 void* ccg_ws(ccg_ctx* ctx, int slot, size_t bytes);
 
+// The stream a _dev entry point enqueues on.  NULL is HIP's legacy default
+// stream (hipStreamLegacy) of the current device, as for any HIP library:
+// ordered after every earlier call on that stream and every blocking stream
+// (torch's default stream is that stream), so an input written just before a
+// call is complete when the library reads it and a temporary freed just
+// after is not reused while it still runs.  (Through round 5 NULL meant the
+// context's own non-blocking stream, unordered with the caller's work.)  The
+// host flavours pass ctx->stream explicitly.
 static inline hipStream_t ccg_pick_stream(ccg_ctx* ctx, void* s) {
-    return s ? (hipStream_t)s : ctx->stream;
+    (void)ctx;
+    return s ? (hipStream_t)s : hipStreamLegacy;
 }
 
 // Exclusive scan of int64 values on device: out[i] = sum_{t<i} in[i]; the
@@ -161,7 +177,7 @@ static inline hipStream_t ccg_pick_stream(ccg_ctx* ctx, void* s) {
 // ccg_scan_i64's single pass: up to SCAN_LB_MAX tiles; its state (status
 // words, finished count) in ctx->d_scan
 #define SCAN_LB_MAX 1024
-#define SCAN_LB_BYTES (SCAN_LB_MAX * 8 + 64)
+#define SCAN_LB_BYTES (SCAN_LB_MAX * 8 + 64)  // one stream's slice of ctx->d_scan
 int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n,
                  hipStream_t st);
 

@@ -314,7 +314,7 @@ extern "C" int ccg_cocluster_sharded_dev(ccg_group* g, const void* const* A, int
     return for_each_local(g, [&](int l) {
         const int r = g->rank0 + l;
         return ccg_cocluster_dev(g->ctx[l], A[l], label_bits, N, B, cut[r], cut[r + 1], co ? co[l] : nullptr,
-                                 both ? both[l] : nullptr, dist ? dist[l] : nullptr, nullptr);
+                                 both ? both[l] : nullptr, dist ? dist[l] : nullptr, g->ctx[l]->stream);
     });
 }
 
@@ -328,7 +328,7 @@ extern "C" int ccg_consensus_knn_sharded_dev(ccg_group* g, const void* const* A,
     rc = for_each_local(g, [&](int l) {
         const int r = g->rank0 + l;
         return ccg_consensus_knn_assign_dev(g->ctx[l], A[l], label_bits, N, B, k, cut[r], cut[r + 1], out_idx[l],
-                                            d_nan_flag[l], nullptr);
+                                            d_nan_flag[l], g->ctx[l]->stream);
     });
     if (rc) return rc;
     // every device gets the whole N x k matrix (in place: each rank's rows are
@@ -399,7 +399,7 @@ extern "C" int ccg_group_cocluster(ccg_group* g, const void* A, int label_bits, 
         uint16_t* dboth = both ? (uint16_t*)ccg_ws(c, WS_HOST_C, sizeof(uint16_t) * P) : nullptr;
         double* ddist = dist ? (double*)ccg_ws(c, WS_HOST_D, sizeof(double) * P) : nullptr;
         if ((co && !dco) || (both && !dboth) || (dist && !ddist)) return (int)CCG_ENOMEM;
-        int rc2 = ccg_cocluster_dev(c, dA[l], label_bits, N, B, r0, r1, dco, dboth, ddist, nullptr);
+        int rc2 = ccg_cocluster_dev(c, dA[l], label_bits, N, B, r0, r1, dco, dboth, ddist, c->stream);
         if (rc2) return rc2;
         if (co) CCG_HIP(hipMemcpyAsync(co + o, dco, sizeof(uint16_t) * P, hipMemcpyDeviceToHost, c->stream));
         if (both) CCG_HIP(hipMemcpyAsync(both + o, dboth, sizeof(uint16_t) * P, hipMemcpyDeviceToHost, c->stream));

@@ -806,6 +806,7 @@ __global__ __launch_bounds__(256) void knn_fallback_kernel(
     const double* __restrict__ rows, int n, int d, int kmax,
     const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
     double* __restrict__ lst_d, int* __restrict__ lst_i, const int64_t* __restrict__ seg_off, int nseg) {
+    // (with seg_off: each row searches only its own segment's references)
     __shared__ double sd[4][KNN_FB_K];
     __shared__ int si[4][KNN_FB_K];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -935,13 +936,13 @@ __global__ __launch_bounds__(64) void knn_fallback_merge_kernel(
     int kmax, const int* __restrict__ fail_list, const int* __restrict__ fail_count, int slots,
     const double* __restrict__ lst_d, const int* __restrict__ lst_i,
     int32_t* __restrict__ out_idx, double* __restrict__ out_dist, const int64_t* __restrict__ seg_off, int nseg,
-    bool dist_sq) {
+    bool dist_sq, bool seg_local = true) {
     const int lane = threadIdx.x;
     const int nfail = *fail_count;
     const int S = knn_fb_splits(nfail, slots);
     for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
         const int q = fail_list[f];
-        const int base = seg_off ? (int)seg_off[knn_seg_of(seg_off, nseg, q)] : 0;
+        const int base = (seg_off && seg_local) ? (int)seg_off[knn_seg_of(seg_off, nseg, q)] : 0;
         const double* ld = lst_d + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
         const int* li = lst_i + (int64_t)f * S * KNN_FB_K + (int64_t)lane * KNN_FB_K;
         int pos = 0;
@@ -1191,26 +1192,92 @@ __device__ void knn_lds_bitonic(double* kd, int* ki, int m) {
 // A_x, its scale 2^-e and its id.
 #define KNN_FXQ 128
 
+// Segmented exact search (a batch of bootstraps, ccg_knn_boots_table_dev):
+// the references of segment s are [soff[s], soff[s+1]) and its failed
+// entries sit at list[soff[s] .. soff[s] + fcnt[s]) (each segment appends to
+// its own region).  The prep compacts them, segment by segment, into
+// cf_list / cf_tau (cf_count entries; segment s from cf_off[s]) and writes
+// each compact entry's segment (qsg); the scan walks, per block of
+// references, only the failed rows of the segments its references belong to
+// (a pair of different segments never becomes a candidate); the select runs
+// on the compact list.  nseg <= KNN_SEG_MAX.
+#define KNN_SEG_MAX 64
+struct FxSeg {
+    const int* fcnt;
+    const int64_t* soff;
+    int nseg;
+    int* cf_list;
+    double* cf_tau;
+    int* cf_count;
+    int* cf_off;
+    int* qsg;
+};
+
 __device__ __forceinline__ int knn_row_exp(double mx) {
     return mx > 0.0 ? 11 - ilogb(mx) : 0;  // mx 2^e < 2^12
 }
 
-template <int KSTEPS>
+template <int KSTEPS, bool SEG>
 __global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __restrict__ rows, int d,
                                                             const int* __restrict__ fail_list,
                                                             const int* __restrict__ fail_count,
                                                             const double* __restrict__ fail_tau,
                                                             uint4* __restrict__ qimg, float* __restrict__ qa,
                                                             float* __restrict__ qs, int* __restrict__ qid,
-                                                            int* __restrict__ ovf_count) {
+                                                            int* __restrict__ ovf_count, FxSeg sg) {
     constexpr int NCH = 4 * KSTEPS;
+    __shared__ int sfo[KNN_SEG_MAX + 1];  // (SEG) compact offsets of the segments' failed entries
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = 0;
-    const int nf = min(*fail_count, KNN_FX_ROWS);
+    int F;
+    if (SEG) {
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            int incl = lane < sg.nseg ? sg.fcnt[lane] : 0;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            sfo[lane + 1] = incl;
+            if (lane == 0) sfo[0] = 0;
+        }
+        __syncthreads();
+        F = sfo[sg.nseg];
+        if (blockIdx.x == 0) {
+            for (int t = threadIdx.x; t <= sg.nseg; t += blockDim.x) sg.cf_off[t] = sfo[t];
+            if (threadIdx.x == 0) *sg.cf_count = F;
+        }
+    } else {
+        F = *fail_count;
+    }
+    const int nf = min(F, KNN_FX_ROWS);
     const int nfp = (nf + KNN_FXQ - 1) / KNN_FXQ * KNN_FXQ;
-    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nfp; f += gridDim.x * blockDim.x) {
+    const int fend = SEG ? max(nfp, F) : nfp;  // (SEG: entries past KNN_FX_ROWS are compacted too)
+    for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < fend; f += gridDim.x * blockDim.x) {
         const bool valid = f < nf;
-        const int q = valid ? fail_list[f] : -1;
-        double t = valid ? fail_tau[f] : -1.0;
+        int q;
+        double t;
+        if (SEG) {
+            q = -1;
+            t = -1.0;
+            if (f < F) {
+                int lo = 0, hi = sg.nseg;  // the segment: the last s with sfo[s] <= f
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sfo[mid] <= f) lo = mid; else hi = mid;
+                }
+                const int64_t p = sg.soff[lo] + (f - sfo[lo]);
+                q = fail_list[p];
+                t = fail_tau[p];
+                sg.cf_list[f] = q;
+                sg.cf_tau[f] = t;
+                if (valid) sg.qsg[f] = lo;
+            }
+            if (f >= nfp) continue;
+            if (!valid) t = -1.0;
+        } else {
+            q = valid ? fail_list[f] : -1;
+            t = valid ? fail_tau[f] : -1.0;
+        }
         if (!(t < INFINITY)) t = -1.0;  // no radius: the per-thread-list kernels
         double x[KSTEPS * 16];
         double mx = 0.0, nx = 0.0;
@@ -1230,10 +1297,10 @@ __global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __rest
             hv[(s * 4 + h) * 8 + i] = hi;
             hv[(s * 4 + 2 + h) * 8 + i] = lo;
         }
-        const int c = f % KNN_FXQ;  // the row's place in its staged group (the swizzle's row)
+        const int c = f & (NCH - 1);  // the swizzle key (the scan stages rows g0 .. g0 + KNN_FXQ, any g0)
         uint4* out = qimg + (int64_t)f * NCH;
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) out[ch ^ (c & (NCH - 1))] = *reinterpret_cast<const uint4*>(&hv[ch * 8]);
+        for (int ch = 0; ch < NCH; ++ch) out[ch ^ c] = *reinterpret_cast<const uint4*>(&hv[ch * 8]);
         qa[f] = t < 0.0 ? INFINITY : __double2float_rd((1.0 - 0x1p-14) * nx - t - 0x1p-60 - 0x1p-21 * (nx + t));
         qs[f] = ldexpf(1.0f, -e);
         qid[f] = q;
@@ -1243,19 +1310,20 @@ __global__ __launch_bounds__(256) void knn_fx_prep16_kernel(const double* __rest
 // Grid: 128 references per block (4 waves x 32); every block walks the
 // failed rows in staged groups of KNN_FXQ.  An empty failed list exits at
 // once.
-template <int KSTEPS>
+template <int KSTEPS, bool SEG>
 __global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __restrict__ rows, int n, int d,
                                                             const int* __restrict__ fail_count,
                                                             const uint4* __restrict__ qimg,
                                                             const float* __restrict__ qa,
                                                             const float* __restrict__ qs,
                                                             const int* __restrict__ qid, int* __restrict__ cnt,
-                                                            int* __restrict__ bi) {
+                                                            int* __restrict__ bi, FxSeg sg) {
     constexpr int NCH = 4 * KSTEPS;
     __shared__ uint4 sq[KNN_FXQ * NCH];
     __shared__ __attribute__((aligned(16))) float sa[KNN_FXQ];
     __shared__ __attribute__((aligned(16))) float ss[KNN_FXQ];
     __shared__ int sid[KNN_FXQ];
+    __shared__ int ssg[SEG ? KNN_FXQ : 1];
     const int nf = min(*fail_count, KNN_FX_ROWS);
     if (nf == 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1264,6 +1332,15 @@ __global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __rest
     // reference's scale and its part of the test
     const int jr = blockIdx.x * 128 + wave * 32 + j;
     const bool inr = jr < n;
+    int gb = 0, ge = nf, sj = 0;
+    if (SEG) {  // the failed rows of the segments of the block's references (block-uniform range)
+        const int sa0 = knn_seg_of(sg.soff, sg.nseg, (int64_t)blockIdx.x * 128);
+        const int sb0 = knn_seg_of(sg.soff, sg.nseg, min((int64_t)blockIdx.x * 128 + 127, (int64_t)n - 1));
+        gb = sg.cf_off[sa0];
+        ge = min(sg.cf_off[sb0 + 1], nf);
+        if (gb >= ge) return;
+        sj = inr ? knn_seg_of(sg.soff, sg.nseg, jr) : -1;
+    }
     double y[KSTEPS * 8];
     double my = 0.0, ny = 0.0;
 #pragma unroll
@@ -1290,14 +1367,17 @@ __global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __rest
         }
     const float sy = 2.0f * ldexpf(1.0f, -ey);  // (the test's factor 2 folded in)
     const float bj = inr ? __double2float_rd((1.0 - 0x1p-14 - 0x1p-21) * ny) : INFINITY;
-    for (int g0 = 0; g0 < nf; g0 += KNN_FXQ) {
-        const int nq = min(KNN_FXQ, nf - g0);
+    for (int g0 = gb; g0 < ge; g0 += KNN_FXQ) {
+        const int nq = min(KNN_FXQ, ge - g0);
         __syncthreads();  // the previous group's reads of the stage are done
+        // (SEG: g0 need not be a multiple of KNN_FXQ; the buffers hold
+        // KNN_FX_ROWS + KNN_FXQ rows, and rows past nq are masked below)
         for (int t = threadIdx.x; t < KNN_FXQ * NCH; t += 256) sq[t] = qimg[(int64_t)g0 * NCH + t];
         if (threadIdx.x < KNN_FXQ) {
             sa[threadIdx.x] = qa[g0 + threadIdx.x];  // (the prep writes whole groups: INFINITY past nf)
             ss[threadIdx.x] = qs[g0 + threadIdx.x];
             sid[threadIdx.x] = qid[g0 + threadIdx.x];
+            if (SEG) ssg[threadIdx.x] = sg.qsg[g0 + threadIdx.x];
         }
         __syncthreads();
         for (int t = 0; t < (nq + 31) >> 5; ++t) {  // block-uniform
@@ -1306,10 +1386,11 @@ __global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __rest
             for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
             const int c = t * 32 + j;
             const uint4* ar = sq + c * NCH;
+            const int cx = (g0 + c) & (NCH - 1);  // the prep's swizzle key of failed row g0 + c
 #pragma unroll
             for (int s = 0; s < KSTEPS; ++s) {
-                const uint4 ahv = ar[(s * 4 + h) ^ (c & (NCH - 1))];
-                const uint4 alv = ar[(s * 4 + 2 + h) ^ (c & (NCH - 1))];
+                const uint4 ahv = ar[(s * 4 + h) ^ cx];
+                const uint4 alv = ar[(s * 4 + 2 + h) ^ cx];
                 const h8 ah = *reinterpret_cast<const h8*>(&ahv);
                 const h8 al = *reinterpret_cast<const h8*>(&alv);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
@@ -1327,7 +1408,7 @@ __global__ __launch_bounds__(256) void knn_fx_scan16_kernel(const double* __rest
                 for (int q = 0; q < 4; ++q) {
                     if (acc[4 * g + q] * (sv[q] * sy) >= av[q] + bj) {  // rare: the candidates
                         const int i = t * 32 + 8 * g + 4 * h + q;
-                        if (jr != sid[i]) {
+                        if (i < nq && jr != sid[i] && (!SEG || ssg[i] == sj)) {
                             const int slot = atomicAdd(&cnt[g0 + i], 1);
                             if (slot < KNN_FX_CAP) bi[(int64_t)(g0 + i) * KNN_FX_CAP + slot] = jr;
                         }
@@ -1473,17 +1554,48 @@ static int* knn_fail_ws(ccg_ctx* ctx, int64_t n, double** tau) {
     return p;
 }
 
+// Workspace bytes of the exact search of n rows (knn_fallback_launch): the
+// radius search's WS_FX_A / WS_FX_C, the per-thread-list search's WS_FB_D /
+// WS_FB_I.  knn_fx_reserve sizes them up front (a batch runs the search on
+// its distinct cells, then on its rows: no growth -- a device
+// synchronisation -- between the two, nor inside a graph capture).
+static size_t knn_fx_ints(int64_t n) { return (size_t)KNN_FX_ROWS + 64 + (size_t)n + 4 * ((size_t)KNN_FX_ROWS + KNN_FXQ) + 4; }
+static size_t knn_fxa_bytes(int64_t n, int d) {
+    const int nch = d <= 16 ? 4 : (d <= 32 ? 8 : 16);
+    return sizeof(int) * knn_fx_ints(n) + 16 + sizeof(uint4) * ((size_t)KNN_FX_ROWS + KNN_FXQ) * nch;
+}
+static size_t knn_fxc_bytes(int64_t n) { return (sizeof(double) + sizeof(int)) * (size_t)n + sizeof(int) * (KNN_SEG_MAX + 8); }
+static int knn_fb_slots(int64_t n) { return (int)std::max<int64_t>(n, KNN_FB_SLOTS); }
+static int knn_fx_reserve(ccg_ctx* ctx, int64_t n, int d) {
+    const size_t fb = (size_t)knn_fb_slots(n) * KNN_FB_K;
+    if (!ccg_ws(ctx, WS_FX_A, knn_fxa_bytes(n, d)) || !ccg_ws(ctx, WS_FX_C, knn_fxc_bytes(n)) ||
+        !ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP) ||
+        !ccg_ws(ctx, WS_FB_D, sizeof(double) * fb) || !ccg_ws(ctx, WS_FB_I, sizeof(int) * fb))
+        return CCG_ENOMEM;
+    return CCG_OK;
+}
+
 // Exact fp64 search (fallback + merge kernels) for the rows in fail_list.
+// seg_fcnt (segmented batch, ccg_knn_boots_table_dev): segment s's failed
+// rows are fail_list[seg_off[s] .. + seg_fcnt[s]) with radii in fail_tau,
+// its references [seg_off[s], seg_off[s+1]); outputs are ids of the
+// concatenation (not segment-local).
 static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int d, int kmax, const int* fail_list,
                                const int* fail_count, int32_t* out_idx, double* out_dist, const int64_t* seg_off,
-                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr) {
-    if (!seg_off && fail_tau) {
+                               int nseg, hipStream_t st, bool dist_sq = false, const double* fail_tau = nullptr,
+                               const int* seg_fcnt = nullptr, const int** cf_out = nullptr,
+                               const int** cf_count_out = nullptr) {
+    bool seg_local = true;
+    if (fail_tau && (!seg_off || seg_fcnt)) {
         // the radius search; its leftovers (overflow) continue below
         // WS_FX_A: counters [KNN_FX_ROWS], overflow count + list [64 + n], the
-        // failed rows' A_x, scales, ids [3 x KNN_FX_ROWS] and images
-        const int nch = d <= 16 ? 4 : (d <= 32 ? 8 : 16);
-        const size_t fx_ints = (size_t)KNN_FX_ROWS + 64 + (size_t)n + 3 * (size_t)KNN_FX_ROWS + 4;
-        char* fxa = (char*)ccg_ws(ctx, WS_FX_A, sizeof(int) * fx_ints + 16 + sizeof(uint4) * (size_t)KNN_FX_ROWS * nch);
+        // failed rows' A_x, scales, ids, segments [4 x (KNN_FX_ROWS + KNN_FXQ)]
+        // and images [KNN_FX_ROWS + KNN_FXQ] (the segmented scan stages
+        // groups from any row); WS_FX_C (segmented): the compact list and
+        // radii [n], its count and segment offsets
+        const size_t fxr = (size_t)KNN_FX_ROWS + KNN_FXQ;
+        const size_t fx_ints = knn_fx_ints(n);
+        char* fxa = (char*)ccg_ws(ctx, WS_FX_A, knn_fxa_bytes(n, d));
         int* cnt = (int*)fxa;
         int* bi = (int*)ccg_ws(ctx, WS_FX_B, sizeof(int) * (size_t)KNN_FX_ROWS * KNN_FX_CAP);
         if (!fxa || !bi) return CCG_ENOMEM;
@@ -1494,26 +1606,53 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
         int* ovf_count = cnt + KNN_FX_ROWS;
         int* ovf_list = ovf_count + 64;
         float* qa = (float*)(ovf_list + n);
-        float* qs = qa + KNN_FX_ROWS;
-        int* qid = (int*)(qs + KNN_FX_ROWS);
+        float* qs = qa + fxr;
+        int* qid = (int*)(qs + fxr);
+        int* qsg = qid + fxr;
         uint4* qimg = (uint4*)(fxa + ccg_cdiv(sizeof(int) * fx_ints, 16) * 16);
         const unsigned gs = (unsigned)ccg_cdiv(n, 128);
-#define CCG_FX(DM_, KS_)                                                                                          \
+        FxSeg sg = {seg_fcnt, seg_off, nseg, nullptr, nullptr, nullptr, nullptr, qsg};
+        const int* sl_list = fail_list;  // what the select walks
+        const int* sl_count = fail_count;
+        const double* sl_tau = fail_tau;
+        if (seg_fcnt) {
+            CCG_REQUIRE(nseg <= KNN_SEG_MAX, "knn: %d segments (max %d)", nseg, KNN_SEG_MAX);
+            double* fxc = (double*)ccg_ws(ctx, WS_FX_C, knn_fxc_bytes(n));
+            if (!fxc) return CCG_ENOMEM;
+            sg.cf_tau = fxc;
+            sg.cf_list = (int*)(fxc + n);
+            sg.cf_count = sg.cf_list + n;
+            sg.cf_off = sg.cf_count + 4;
+            sl_list = sg.cf_list;
+            sl_count = sg.cf_count;
+            sl_tau = sg.cf_tau;
+            if (cf_out) *cf_out = sg.cf_list;  // the compacted list (ccg_knn_last_fallback)
+            if (cf_count_out) *cf_count_out = sg.cf_count;
+        }
+#define CCG_FX(DM_, KS_, SEG_)                                                                                    \
     do {                                                                                                         \
-        knn_fx_prep16_kernel<KS_><<<KNN_FX_PREP_GRID, 256, 0, st>>>(rows, d, fail_list, fail_count, fail_tau, qimg, \
-                                                                    qa, qs, qid, ovf_count);                     \
-        knn_fx_scan16_kernel<KS_><<<gs, 256, 0, st>>>(rows, (int)n, d, fail_count, qimg, qa, qs, qid, cnt, bi);      \
-        knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, fail_list, fail_count, fail_tau, cnt, bi,     \
+        knn_fx_prep16_kernel<KS_, SEG_><<<KNN_FX_PREP_GRID, 256, 0, st>>>(rows, d, fail_list, fail_count, fail_tau, \
+                                                                          qimg, qa, qs, qid, ovf_count, sg);     \
+        knn_fx_scan16_kernel<KS_, SEG_><<<gs, 256, 0, st>>>(rows, (int)n, d, sl_count, qimg, qa, qs, qid, cnt, bi, \
+                                                            sg);                                                 \
+        knn_fx_select_kernel<DM_><<<256, 256, 0, st>>>(rows, d, kmax, sl_list, sl_count, sl_tau, cnt, bi,         \
                                                        out_idx, out_dist, dist_sq, ovf_list, ovf_count);          \
     } while (0)
-        if (d <= 16) CCG_FX(16, 1);
-        else if (d <= 32) CCG_FX(32, 2);
-        else CCG_FX(64, 4);
+        if (seg_fcnt) {
+            if (d <= 16) CCG_FX(16, 1, true);
+            else if (d <= 32) CCG_FX(32, 2, true);
+            else CCG_FX(64, 4, true);
+        } else {
+            if (d <= 16) CCG_FX(16, 1, false);
+            else if (d <= 32) CCG_FX(32, 2, false);
+            else CCG_FX(64, 4, false);
+        }
 #undef CCG_FX
         fail_list = ovf_list;
         fail_count = ovf_count;
+        seg_local = !seg_fcnt;
     }
-    const int fb_slots = (int)std::max<int64_t>(n, KNN_FB_SLOTS);
+    const int fb_slots = knn_fb_slots(n);
     double* fb_d = (double*)ccg_ws(ctx, WS_FB_D, sizeof(double) * (size_t)fb_slots * KNN_FB_K);
     int* fb_i = (int*)ccg_ws(ctx, WS_FB_I, sizeof(int) * (size_t)fb_slots * KNN_FB_K);
     if (!fb_d || !fb_i) return CCG_ENOMEM;
@@ -1536,7 +1675,7 @@ static int knn_fallback_launch(ccg_ctx* ctx, const double* rows, int64_t n, int 
     }
 #undef CCG_FALLBACK
     knn_fallback_merge_kernel<<<KNN_FB_GRID, 64, 0, st>>>(kmax, fail_list, fail_count, fb_slots, fb_d, fb_i, out_idx,
-                                                   out_dist, seg_off, nseg, dist_sq);
+                                                   out_dist, seg_off, nseg, dist_sq, seg_local);
     return CCG_OK;
 }
 
@@ -1744,30 +1883,40 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
 // garbage offsets behind)
 // (zc: three counters zeroed by the first threads -- the table path's fail
 // counts -- in place of a memset launch; may be NULL)
+// (segn > 0: a batch of bootstraps of segn rows each -- row t belongs to
+// bootstrap t / segn, whose cell c is the virtual cell (t / segn) N + c, so
+// the bootstraps' distinct cells get disjoint, bootstrap-major ids)
 __global__ void kb_count_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N,
                                 unsigned long long* __restrict__ pk, int* __restrict__ err,
-                                int32_t* __restrict__ ztab, int64_t nz, unsigned* __restrict__ zc) {
+                                int32_t* __restrict__ ztab, int64_t nz, unsigned* __restrict__ zc, int nzc = 3,
+                                int64_t segn = 0) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = t; i < nz; i += (int64_t)gridDim.x * blockDim.x) ztab[i] = 0;
-    if (zc && t < 3) zc[t] = 0u;
+    if (zc && t < nzc) zc[t] = 0u;
     if (t >= n) return;
     int c = idx[t];
     if (c < 0 || c >= N) {
         atomicOr(err, CCG_DERR_KNN_UNIQUE);
         c = 0;
     }
-    const unsigned long long old = atomicAdd(&pk[c], 1ull);
-    if ((old & 0xffffffffull) == 0ull) atomicAdd(&pk[c], 1ull << 32);  // the first row: the presence bit
+    const int64_t vc = segn ? (t / segn) * N + c : c;
+    const unsigned long long old = atomicAdd(&pk[vc], 1ull);
+    if ((old & 0xffffffffull) == 0ull) atomicAdd(&pk[vc], 1ull << 32);  // the first row: the presence bit
 }
 
 // Per cell c (and c = N): cell2u[c] (-1: absent), ustart[uid]; pk[c] back to
 // 0 and the scatter cursor zeroed (for every cell, whatever the caller's u).
 // A caller's u that differs from the count sets the sticky error; ids are
 // clamped into [0, ucap) so every later access stays in bounds.
+// (a batch, nseg > 0: N = nseg Nc virtual cells; the bootstraps' first
+// distinct ids go to useg, their first rows to dso, and a bootstrap with
+// fewer than kmin distinct cells sets the sticky error)
 __global__ void kb_cells_kernel(unsigned long long* __restrict__ pk, const int64_t* __restrict__ pko, int64_t N,
                                 int64_t n, int ucap, int u_given, int* __restrict__ cell2u,
                                 int* __restrict__ ustart, int* __restrict__ cursor, int* __restrict__ nbig,
-                                int* __restrict__ err) {
+                                int* __restrict__ err, int nseg = 0, int64_t Nc = 0, int kmin = 0,
+                                int64_t* __restrict__ useg = nullptr, int64_t* __restrict__ dso = nullptr,
+                                int64_t segn = 0) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c < N) {
         const unsigned long long a = (unsigned long long)pko[c], b = (unsigned long long)pko[c + 1];
@@ -1777,21 +1926,34 @@ __global__ void kb_cells_kernel(unsigned long long* __restrict__ pk, const int64
         if (present) ustart[uid] = (int)(a & 0xffffffffull);
         pk[c] = 0ull;
         cursor[c] = 0;
+        if (nseg > 0 && c % Nc == 0) {
+            const int sg = (int)(c / Nc);
+            const int64_t us = (int64_t)((unsigned long long)pko[c + Nc] >> 32) - (int64_t)(a >> 32);
+            if (us < kmin) atomicOr(err, CCG_DERR_KNN_UNIQUE);
+            useg[sg] = (int64_t)(a >> 32);
+            dso[sg] = sg * segn;
+        }
     } else if (c == N) {
         const int u = (int)((unsigned long long)pko[N] >> 32);
         if (u_given >= 0 && u != u_given) atomicOr(err, CCG_DERR_KNN_UNIQUE);
         ustart[min(u, ucap)] = (int)n;
         *nbig = 0;
+        if (nseg > 0) {
+            useg[nseg] = min(u, ucap);
+            dso[nseg] = nseg * segn;
+        }
     }
 }
 
 __global__ void kb_scatter_kernel(const int32_t* __restrict__ idx, int64_t n, int64_t N,
                                   const int* __restrict__ cell2u, const int* __restrict__ ustart,
-                                  int* __restrict__ cursor, int32_t* __restrict__ srow, int32_t* __restrict__ scell) {
+                                  int* __restrict__ cursor, int32_t* __restrict__ srow, int32_t* __restrict__ scell,
+                                  int64_t segn = 0) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     int c = idx[t];
     if (c < 0 || c >= N) c = 0;  // (flagged by the count kernel)
+    if (segn) c = (int)((t / segn) * N + c);  // the virtual cell (a batch)
     const int64_t pos = min((int64_t)ustart[max(cell2u[c], 0)] + atomicAdd(&cursor[c], 1), n - 1);
     srow[pos] = (int32_t)t;
     scell[pos] = c;
@@ -1932,10 +2094,12 @@ __device__ void kb_expand_row(int64_t i, int u, int kq, const int* __restrict__ 
                               const int* __restrict__ row2u, int kmax, int32_t* __restrict__ out_idx,
                               double* __restrict__ out_dist, int* __restrict__ fail_list, int* __restrict__ fail_count,
                               double* __restrict__ fail_tau, const int64_t* __restrict__ useg = nullptr,
-                              int nseg = 1) {
+                              int nseg = 1, const int64_t* __restrict__ fbase = nullptr,
+                              int* __restrict__ fcnt = nullptr) {
     const int uc = row2u[i];
+    int sg = 0;
     if (useg) {  // segmented run: the distinct cells of the row's own segment
-        const int sg = knn_seg_of(useg, nseg, uc);
+        sg = knn_seg_of(useg, nseg, uc);
         u = (int)(useg[sg + 1] - useg[sg]);
     }
     // the distinct cell's kq nearest distinct cells with their certified d2
@@ -2019,7 +2183,8 @@ __device__ void kb_expand_row(int64_t i, int u, int kq, const int* __restrict__ 
         first = false;
     }
     if (fail) {
-        const int p = atomicAdd(fail_count, 1);
+        // (fbase: a batch -- each segment appends to its own region)
+        const int64_t p = fbase ? fbase[sg] + atomicAdd(&fcnt[sg], 1) : atomicAdd(fail_count, 1);
         fail_list[p] = (int)i;
         if (fail_tau) fail_tau[p] = ftau;
     }
@@ -2050,13 +2215,14 @@ __global__ __launch_bounds__(256) void kb_expand_ties_kernel(int u, int kq, cons
                                                              const int* __restrict__ tie_list,
                                                              const int* __restrict__ tie_count,
                                                              const int64_t* __restrict__ useg = nullptr,
-                                                             int nseg = 1) {
+                                                             int nseg = 1, const int64_t* __restrict__ fbase = nullptr,
+                                                             int* __restrict__ fcnt = nullptr) {
     const int nt = *tie_count;
     for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < nt; f += gridDim.x * blockDim.x) {
         const int uc = tie_list[f];
         for (int z = ustart[uc]; z < ustart[uc + 1]; ++z)
             kb_expand_row(srow[z], u, kq, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist, fail_list,
-                          fail_count, fail_tau, useg, nseg);
+                          fail_count, fail_tau, useg, nseg, fbase, fcnt);
     }
 }
 
@@ -2077,7 +2243,8 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
                                                               double* __restrict__ fail_tau,
                                                               int* __restrict__ tie_list, int* __restrict__ tie_count,
                                                               const int64_t* __restrict__ useg = nullptr,
-                                                              int nseg = 1) {
+                                                              int nseg = 1, const int64_t* __restrict__ fbase = nullptr,
+                                                              int* __restrict__ fcnt = nullptr) {
     // two distinct cells per wave, one per 32-lane half (kq <= kmax <= 32):
     // a cell's list takes at most 32 lanes
     const int lane = threadIdx.x & 31;
@@ -2085,9 +2252,9 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
     const int uc = blockIdx.x * 8 + (threadIdx.x >> 5);
     const bool live = uc < u;
     if (__ballot(live) == 0ull) return;
-    int uu = u;
+    int uu = u, sg = 0;
     if (useg && live) {  // segmented run: the cut test counts the distinct cells of the cell's own segment
-        const int sg = knn_seg_of(useg, nseg, uc);
+        sg = knn_seg_of(useg, nseg, uc);
         uu = (int)(useg[sg + 1] - useg[sg]);
     }
     const int oa = live ? ustart[uc] : 0, ob = live ? ustart[uc + 1] : 0, oc = ob - oa;  // the own cell's rows
@@ -2119,7 +2286,7 @@ __global__ __launch_bounds__(256) void kb_expand_cells_kernel(int64_t n, int u, 
         const int i = srow[z];  // a copy (uniform in the half)
         if (cut || shortl) {
             if (lane == 0) {
-                const int p = atomicAdd(fail_count, 1);
+                const int64_t p = fbase ? fbase[sg] + atomicAdd(&fcnt[sg], 1) : atomicAdd(fail_count, 1);
                 fail_list[p] = i;
                 if (fail_tau) fail_tau[p] = cut ? glast : INFINITY;
             }
@@ -2280,7 +2447,11 @@ __device__ __forceinline__ double kt_tau_wave(KtTauLds& S, int lane, int kq, int
 // kt_tau pass over the failed list).  The kernel is a chain of dependent
 // gathers (distinct id -> cell -> table row -> presence); the cells of a wave
 // issue each level's loads together.
+// SEG (a batch, ccg_knn_boots_table_dev): scell holds virtual cells
+// s Nc + c; bootstrap s's presence map is cell2u + s Nc, and a short cell
+// appends to its bootstrap's region of the failed list (useg[s] + fcnt[s]).
 #define KT_CPW 2
+template <bool SEG>
 __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, int d, const int* __restrict__ ustart,
                                                         const int32_t* __restrict__ scell,
                                                         const int* __restrict__ cell2u,
@@ -2288,18 +2459,30 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, in
                                                         const double* __restrict__ tab_d2,
                                                         const double* __restrict__ urows, int32_t* __restrict__ uidx,
                                                         double* __restrict__ ud2, int* __restrict__ fail_list,
-                                                        int* __restrict__ fail_count, double* __restrict__ tau) {
+                                                        int* __restrict__ fail_count, double* __restrict__ tau,
+                                                        int64_t Nc = 0, const int64_t* __restrict__ useg = nullptr,
+                                                        int* __restrict__ fcnt = nullptr) {
     __shared__ KtTauLds tl[4];
     const int u0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * KT_CPW;
     if (u0 >= u) return;
     const int lane = threadIdx.x & 63;
     int64_t c[KT_CPW];
-    int v[KT_CPW], w[KT_CPW];
+    int v[KT_CPW], w[KT_CPW], sg[KT_CPW];
+    const int* c2u[KT_CPW];
     double dv[KT_CPW];
 #pragma unroll
     for (int i = 0; i < KT_CPW; ++i) c[i] = u0 + i < u ? ustart[u0 + i] : -1;
 #pragma unroll
-    for (int i = 0; i < KT_CPW; ++i) c[i] = c[i] >= 0 ? scell[c[i]] : -1;
+    for (int i = 0; i < KT_CPW; ++i) {
+        c[i] = c[i] >= 0 ? scell[c[i]] : -1;
+        sg[i] = 0;
+        c2u[i] = cell2u;
+        if (SEG && c[i] >= 0) {  // virtual cell -> (bootstrap, cell)
+            sg[i] = (int)(c[i] / Nc);
+            c[i] -= (int64_t)sg[i] * Nc;
+            c2u[i] = cell2u + (int64_t)sg[i] * Nc;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < KT_CPW; ++i) {
         const bool e = c[i] >= 0 && lane < K;
@@ -2307,7 +2490,7 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, in
         dv[i] = e ? tab_d2[c[i] * K + lane] : INFINITY;
     }
 #pragma unroll
-    for (int i = 0; i < KT_CPW; ++i) w[i] = v[i] >= 0 ? cell2u[v[i]] : -1;
+    for (int i = 0; i < KT_CPW; ++i) w[i] = v[i] >= 0 ? c2u[i][v[i]] : -1;
     for (int i = 0; i < KT_CPW; ++i) {
         const int uid = u0 + i;
         if (uid >= u) break;  // (wave-uniform)
@@ -2319,10 +2502,10 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, in
             ud2[(int64_t)uid * kq + rank] = di;
         }
         if (__popcll(m) < kq) {  // (wave-uniform)
-            const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c[i], v[i], w[i], di, cell2u,
+            const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c[i], v[i], w[i], di, c2u[i],
                                             tab_idx, urows);
             if (lane == 0) {
-                const int f = atomicAdd(fail_count, 1);
+                const int64_t f = SEG ? useg[sg[i]] + atomicAdd(&fcnt[sg[i]], 1) : atomicAdd(fail_count, 1);
                 fail_list[f] = uid;
                 tau[f] = best;
             }
@@ -2452,8 +2635,8 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
     if (kq >= 1 && tab_idx) {
         // the table's present entries; cells short of kq of them: exact search among the distinct cells
         int* ufail = (int*)(misc + 5);
-        kt_filter_kernel<<<(unsigned)ccg_cdiv(u, 4 * KT_CPW), 256, 0, st>>>(u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2,
-                                                                   urows, uidx, ud2, fail_list, ufail, ftau);
+        kt_filter_kernel<false><<<(unsigned)ccg_cdiv(u, 4 * KT_CPW), 256, 0, st>>>(
+            u, kq, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, uidx, ud2, fail_list, ufail, ftau);
         rc = knn_fallback_launch(ctx, urows, u, d, kq, fail_list, ufail, uidx, ud2, nullptr, 1, st, true, ftau);
         if (rc) return rc;
         if (stats) {
@@ -2499,6 +2682,148 @@ static int knn_boot_impl(ccg_ctx* ctx, const double* pcs, int64_t N, int d, cons
         CCG_HIP(hipStreamSynchronize(st));
         stats->queries = n;
         stats->fallback = us.fallback + nf;
+        ctx->last_stats = *stats;
+    }
+    return CCG_OK;
+}
+
+// ------------------------------------------------- bootstrap batches --
+// ccg_knn_boots_table_dev: nb bootstraps of the same PCs (n rows each, the
+// rows of bootstrap s at s n .. (s + 1) n) through ONE set of launches of the
+// table path above.  Bootstrap s's cell c is the virtual cell s N + c, so one
+// counting sort over nb N virtual cells groups every bootstrap's rows by
+// cell and numbers the distinct cells bootstrap by bootstrap (useg: the first
+// distinct id of each bootstrap); the filter reads the cell's table row
+// against its own bootstrap's presence map (cell2u + s N); cells short of kq
+// present entries and rows with a cut tie go to the segmented radius search
+// (each bootstrap's failed entries in their own region of the list, each
+// searched among its own bootstrap's distinct cells or rows).  The result is
+// every bootstrap's ccg_knn_boot_table_dev result, bit for bit, with row ids
+// of the concatenation (local_ids = 0: the disjoint union of the nb graphs,
+// ready for one SNN pass) or of the bootstrap (local_ids = 1).  Per batch the
+// launches are those of one bootstrap (about 20), so a step of 125
+// bootstraps in batches of 16 issues ~170 kNN launches instead of ~2000.
+__global__ void kbs_rebase_kernel(int64_t n, int kmax, const int64_t* __restrict__ seg_off, int nseg, int sign,
+                                  int32_t* __restrict__ out_idx);
+
+extern "C" int ccg_knn_boots_table_dev(ccg_ctx* ctx, int64_t N, int d, const int32_t* idx, int64_t n, int nb,
+                                       const int* n_unique, const double* rows, int kmax, const int32_t* tab_idx,
+                                       const double* tab_d2, int K, int local_ids, int32_t* out_idx,
+                                       double* out_dist, ccg_knn_stats* stats, void* stream) {
+    CCG_REQUIRE(ctx && idx && n_unique && rows && tab_idx && tab_d2 && out_idx,
+                "ccg_knn_boots_table_dev: NULL argument");
+    CCG_REQUIRE(d >= 1 && d <= 63, "ccg_knn_boots_table_dev: d=%d must be in [1, 63]", d);
+    CCG_REQUIRE(nb >= 1 && nb <= KNN_SEG_MAX, "ccg_knn_boots_table_dev: nb=%d must be in [1, %d]", nb, KNN_SEG_MAX);
+    CCG_REQUIRE(N >= 2 && n >= 2 && (int64_t)nb * n < (1LL << 30) && (int64_t)nb * N < (1LL << 31) - 1,
+                "ccg_knn_boots_table_dev: bad sizes (N=%lld, n=%lld, nb=%d: nb n < 2^30, nb N < 2^31 - 1)",
+                (long long)N, (long long)n, nb);
+    CCG_REQUIRE(K >= 1 && K <= KNN_TAB_K && K <= N - 1,
+                "ccg_knn_boots_table_dev: K=%d must be in [1, min(%d, N-1)]", K, KNN_TAB_K);
+    CCG_REQUIRE(kmax >= 1 && kmax <= KNN_KP_BIG && kmax <= n - 1,
+                "ccg_knn_boots_table_dev: kmax=%d must be in [1, min(%d, n-1)]", kmax, KNN_KP_BIG);
+    int64_t ut = 0;
+    for (int s = 0; s < nb; ++s) {
+        CCG_REQUIRE(n_unique[s] >= kmax + 1 && n_unique[s] <= n && n_unique[s] <= N,
+                    "ccg_knn_boots_table_dev: bootstrap %d has n_unique=%d (needs kmax + 1 = %d .. min(n, N))", s,
+                    n_unique[s], kmax + 1);
+        ut += n_unique[s];
+    }
+    const int u = (int)ut;
+    const int64_t nt = (int64_t)nb * n, V = (int64_t)nb * N;
+    hipStream_t st = ccg_pick_stream(ctx, stream);
+    // workspaces (the exact search's for the larger of its two runs first)
+    double* ftau = nullptr;
+    int* fail_list = knn_fail_ws(ctx, nt, &ftau);  // per-bootstrap regions: distinct cells, then rows
+    if (knn_fx_reserve(ctx, nt, d)) return CCG_ENOMEM;
+    char* ta = (char*)ccg_ws(ctx, WS_KB_A, sizeof(int64_t) * (nt + 1) + sizeof(int32_t) * (4 * nt + (size_t)u + 1));
+    double* urows = (double*)ccg_ws(ctx, WS_KB_B, sizeof(double) * (size_t)u * (d + kmax) +
+                                                      sizeof(int32_t) * (size_t)u * kmax + 64);
+    char* tc = (char*)ccg_ws(ctx, WS_KB_C, 2 * sizeof(int64_t) * (size_t)(V + 1) +
+                                               sizeof(int) * (2 * (size_t)V + (size_t)u + 8));
+    int64_t* useg = (int64_t*)ccg_ws(ctx, WS_KBT, sizeof(int64_t) * 2 * (KNN_SEG_MAX + 1) +
+                                                      sizeof(int) * (2 * KNN_SEG_MAX + 8));
+    if (!fail_list || !ta || !urows || !tc || !useg) return CCG_ENOMEM;
+    int64_t* dso = useg + KNN_SEG_MAX + 1;              // [nb + 1] first row of every bootstrap
+    int* fcnt_u = (int*)(dso + KNN_SEG_MAX + 1);        // [nb] failed distinct cells per bootstrap
+    int* fcnt_r = fcnt_u + nb;                          // [nb] failed rows per bootstrap
+    int* tie_count = fcnt_r + nb;                       // [1]
+    int64_t* head = (int64_t*)ta;
+    int32_t* cells = (int32_t*)(head + nt + 1);
+    int32_t* scell = cells + nt;
+    int32_t* rid = scell + nt;
+    int32_t* srow = rid + nt;
+    int32_t* ustart = srow + nt;                        // [u + 1]
+    int32_t* row2u = cells;
+    int32_t* tie_list = (int32_t*)head;
+    unsigned long long* pk = (unsigned long long*)tc;   // [V + 1] counts | presence (zero between calls)
+    int64_t* pko = (int64_t*)(pk + V + 1);
+    int* cursor = (int*)(pko + V + 1);
+    int* cell2u = cursor + V;
+    int* nbig = cell2u + V;
+    int* big = nbig + 4;
+    double* ud2 = urows + (size_t)u * d;
+    int32_t* uidx = (int32_t*)(ud2 + (size_t)u * kmax);
+    const int t_all = ccg_timer_start(ctx, CCG_KT_KNN_TOTAL, st);
+    if (ctx->kb_zeroed != (void*)tc || ctx->kb_zero_n != V) {
+        CCG_HIP(hipMemsetAsync(pk, 0, sizeof(int64_t) * (size_t)(V + 1), st));
+        ctx->kb_zeroed = (void*)tc;
+        ctx->kb_zero_n = V;
+    }
+    // 1. every bootstrap's rows grouped by cell (one counting sort over the
+    // virtual cells); the per-bootstrap fail counts and the tie count zeroed
+    const unsigned ng = (unsigned)ccg_cdiv(nt, 256);
+    kb_count_kernel<<<ng, 256, 0, st>>>(idx, nt, N, pk, ctx->d_err, ustart, (int64_t)u + 1, (unsigned*)fcnt_u,
+                                        2 * nb + 1, n);
+    int rc = ccg_scan_i64(ctx, (const int64_t*)pk, pko, V, st);
+    if (rc) {
+        ctx->kb_zeroed = nullptr;
+        return rc;
+    }
+    kb_cells_kernel<<<(unsigned)ccg_cdiv(V + 1, 256), 256, 0, st>>>(pk, pko, V, nt, u, u, cell2u, ustart, cursor,
+                                                                    nbig, ctx->d_err, nb, N, kmax + 1, useg, dso, n);
+    kb_scatter_kernel<<<ng, 256, 0, st>>>(idx, nt, N, cell2u, ustart, cursor, srow, scell, n);
+    kb_fixup_kernel<<<(unsigned)ccg_cdiv(u, 256), 256, 0, st>>>(u, nt, ustart, srow, row2u, big, nbig);
+    kb_fixup_big_kernel<<<16, 256, 0, st>>>(nt, ustart, srow, row2u, big, nbig, rid);
+    // 2. the distinct cells' rows; their kmax nearest distinct cells of the
+    // same bootstrap from the table; short cells: the radius search among
+    // their bootstrap's distinct cells
+    if (d <= 32)
+        kb_urows_kernel<32><<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, nullptr,
+                                                                      nullptr);
+    else
+        kb_urows_kernel<64><<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, nullptr,
+                                                                      nullptr);
+    kt_filter_kernel<true><<<(unsigned)ccg_cdiv(u, 4 * KT_CPW), 256, 0, st>>>(
+        u, kmax, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, uidx, ud2, fail_list, nullptr, ftau, N, useg,
+        fcnt_u);
+    rc = knn_fallback_launch(ctx, urows, u, d, kmax, fail_list, fcnt_u, uidx, ud2, useg, nb, st, true, ftau, fcnt_u);
+    if (rc) return rc;
+    // 3. expansion to rows (ids of the concatenation); cut ties: the radius
+    // search among the bootstrap's rows
+    kb_expand_cells_kernel<<<(unsigned)ccg_cdiv(u, 8), 256, 0, st>>>(nt, u, kmax, uidx, ud2, ustart, srow, row2u,
+                                                                     kmax, out_idx, out_dist, fail_list, nullptr, ftau,
+                                                                     tie_list, tie_count, useg, nb, dso, fcnt_r);
+    kb_expand_ties_kernel<<<64, 256, 0, st>>>(u, kmax, uidx, ud2, ustart, srow, row2u, kmax, out_idx, out_dist,
+                                              fail_list, nullptr, ftau, tie_list, tie_count, useg, nb, dso, fcnt_r);
+    const int* cf = nullptr;
+    const int* cfc = nullptr;
+    rc = knn_fallback_launch(ctx, rows, nt, d, kmax, fail_list, fcnt_r, out_idx, out_dist, dso, nb, st, false, ftau,
+                             fcnt_r, &cf, &cfc);
+    if (rc) return rc;
+    if (local_ids)
+        kbs_rebase_kernel<<<(unsigned)ccg_cdiv(nt * kmax, 256), 256, 0, st>>>(nt, kmax, dso, nb, -1, out_idx);
+    ctx->last_fail_list = cf;
+    ctx->last_fail_count = cfc;
+    ccg_timer_stop(ctx, t_all, st);
+    CCG_HIP(hipGetLastError());
+    if (stats) {
+        int h[2 * KNN_SEG_MAX];
+        CCG_HIP(hipMemcpyAsync(h, fcnt_u, sizeof(int) * 2 * nb, hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
+        int64_t f = 0;
+        for (int s = 0; s < 2 * nb; ++s) f += h[s];
+        stats->queries = nt;
+        stats->fallback = f;
         ctx->last_stats = *stats;
     }
     return CCG_OK;

@@ -213,3 +213,9 @@ extern "C" int ccg_sort_pairs_dev(ccg_ctx* ctx, const int32_t* keys_in, int32_t*
     CCG_REQUIRE(keys_in != keys_out && vals_in != vals_out, "ccg_sort_pairs_dev: in-place sorting is not supported");
     return ccg_sort_pairs_i32(ctx, keys_in, keys_out, vals_in, vals_out, n, key_bits, ccg_pick_stream(ctx, stream));
 }
+
+extern "C" int ccg_scan_i64_dev(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, void* stream) {
+    CCG_REQUIRE(ctx && (n <= 0 || in) && out, "ccg_scan_i64_dev: NULL argument");
+    CCG_REQUIRE(n >= 0, "ccg_scan_i64_dev: n=%lld", (long long)n);
+    return ccg_scan_i64(ctx, in, out, n, ccg_pick_stream(ctx, stream));
+}

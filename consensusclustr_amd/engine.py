@@ -7,6 +7,7 @@ stream (torch is plumbing for device memory and streams only; all compute
 runs in libccg.so).
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -20,8 +21,12 @@ def _ptr(a):
     if a is None:
         return None
     if isinstance(a, np.ndarray):
+        if not a.flags.c_contiguous:  # the C ABI reads dense row-major memory
+            raise ValueError(f"array of shape {a.shape} is not C-contiguous")
         return a.ctypes.data_as(_vp)
-    return _vp(a.data_ptr())  # torch tensor
+    if not a.is_contiguous():  # torch tensor: a strided view would be read in the wrong order
+        raise ValueError(f"tensor of shape {tuple(a.shape)} and strides {a.stride()} is not contiguous")
+    return _vp(a.data_ptr())
 
 
 _HIP_STREAM_LEGACY = 1  # hipStreamLegacy
@@ -29,9 +34,10 @@ _HIP_STREAM_LEGACY = 1  # hipStreamLegacy
 
 def _stream():
     """torch's current stream for the library's launches.  torch's default
-    stream is HIP's legacy null stream (handle 0), which the C API reads as
-    "the context's own stream" (a non-blocking stream, unordered with
-    torch's work); hipStreamLegacy is passed instead, so a tensor torch
+    stream is HIP's legacy null stream (handle 0); hipStreamLegacy is passed
+    for it (the C API reads NULL the same way since ABI 7; through ABI 6 NULL
+    meant the context's own non-blocking stream, unordered with torch's work
+    -- the cause of round 5's illegal-address fault), so a tensor torch
     computed just before a call is complete when the library reads it, and a
     temporary freed just after a call is not reused while the library still
     reads it."""
@@ -224,18 +230,32 @@ class Engine:
         knn_idx = np.ascontiguousarray(knn_idx, dtype=np.int32)
         n, kst = knn_idx.shape
         t = {"number": _lib.CCG_SNN_NUMBER, "rank": _lib.CCG_SNN_RANK}[type]
-        cl = None if cell is None else np.ascontiguousarray(cell, dtype=np.int32)
+        cl = None if cell is None else np.ascontiguousarray(cell, dtype=np.int32).ravel()
+        if cl is not None and cl.size != n:  # the library reads n entries
+            raise ValueError(f"snn_multi: cell has {cl.size} entries, knn_idx has {n} rows")
         uk = sorted({int(k) for k in ks})
         got = {}
+        t_pass = t_fetch = 0.0
         for c0 in range(0, len(uk), 4):  # the library builds at most 4 graphs per pass
             chunk = uk[c0:c0 + 4]
             nk = len(chunk)
             ne = (ctypes.c_int64 * nk)()
+            t0 = time.perf_counter()
             check(self.lib.ccg_snn_graphs_cells(self.ctx, _ptr(knn_idx), n, kst, _ptr(cl),
                                                 (ctypes.c_int * nk)(*chunk), nk, t, ne))
+            t1 = time.perf_counter()
             for g, k in enumerate(chunk):
                 got[k] = self._snn_fetch(g, ne[g])
+            t_pass += t1 - t0
+            t_fetch += time.perf_counter() - t1
+        # host seconds: the device pass with its copies to pinned memory, then
+        # the host expansion of the class rows into the per-graph edge lists
+        self.last_snn_times = (t_pass, t_fetch)
         return [got[int(k)] for k in ks]
+
+    def scan_i64_t(self, x, out):
+        """Exclusive scan (ccg_scan_i64_dev): out[:n] prefix sums of x, out[n] the total."""
+        check(self.lib.ccg_scan_i64_dev(self.ctx, _ptr(x), _ptr(out), x.numel(), _stream()))
 
     def silhouette_cells(self, x, labels, cell, ncell, cmax=None):
         """ccg_silhouette_cells: means over bootstrap rows x whose cells are
@@ -466,6 +486,29 @@ class Engine:
             return self.last_knn_stats
         return None
 
+    def knn_boots_table_t(self, N, d, idx, n_unique, rows, kmax, tab_idx, tab_d2, out_idx, out_dist=None,
+                          local_ids=False, stats=False):
+        """A batch of bootstraps through one set of launches
+        (ccg_knn_boots_table_dev): idx (nb, n) int32 cell indices, n_unique
+        nb host ints, rows (nb n, d) the gathered rows of every bootstrap,
+        out_idx (nb n, kmax) -- ids of the concatenation unless local_ids."""
+        nb, n = idx.shape
+        nu = np.ascontiguousarray(n_unique, dtype=np.int32)
+        if nu.size != nb:
+            raise ValueError(f"knn_boots_table_t: {nu.size} n_unique values for {nb} bootstraps")
+        if rows.shape[0] != nb * n or out_idx.shape[0] != nb * n:
+            raise ValueError("knn_boots_table_t: rows / out_idx must have nb * n rows")
+        K = tab_idx.shape[1]
+        st = _lib.ccg_knn_stats() if stats else None
+        check(self.lib.ccg_knn_boots_table_dev(self.ctx, N, d, _ptr(idx), n, nb, _ptr(nu), _ptr(rows), kmax,
+                                               _ptr(tab_idx), _ptr(tab_d2), K, 1 if local_ids else 0,
+                                               _ptr(out_idx), _ptr(out_dist), ctypes.byref(st) if stats else None,
+                                               _stream()))
+        if stats:
+            self.last_knn_stats = (st.queries, st.fallback)
+            return self.last_knn_stats
+        return None
+
     def knn_segments_t(self, rows, seg_off, kmax, out_idx, out_dist=None, stats=False):
         """Device flavour: rows (n, d) tensor of concatenated segments, seg_off a
         host int64 array of nseg+1 offsets; out_idx (n, kmax) segment-local."""
@@ -558,7 +601,7 @@ class Engine:
         def arr(ts):
             if ts is None:
                 return None
-            a = (ctypes.c_void_p * nseg)(*[t.data_ptr() if t is not None else None for t in ts])
+            a = (ctypes.c_void_p * nseg)(*[_ptr(t).value if t is not None else None for t in ts])
             return a
         lab = arr(labels)
         om, onc, oms = arr(means), arr(nclust), arr(minsize)

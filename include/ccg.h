@@ -12,10 +12,20 @@
  *     glue binds.  They copy in, run, copy out and
  *     synchronise.
  *   - device-pointer functions (*_dev): inputs/outputs already in HBM,
- *     enqueued on `stream` (a hipStream_t; NULL = the context's stream, a
- *     non-blocking stream: a caller whose inputs come from the legacy null
- *     stream -- torch's default stream -- passes hipStreamLegacy, or orders
- *     the streams itself).  No host synchronisation unless stated.
+ *     enqueued on `stream` (a hipStream_t).  NULL is HIP's legacy default
+ *     stream of the current device (hipStreamLegacy; torch's default stream),
+ *     as for any HIP library: the call is ordered after the caller's earlier
+ *     work on that stream and on every blocking stream, so an input written
+ *     just before the call is complete when the library reads it.  (Through
+ *     ABI 6, NULL meant the context's own non-blocking stream.)  The
+ *     context's device must be current.  No host synchronisation unless
+ *     stated.
+ *   - one stream at a time per context: a context's workspaces are shared
+ *     by its calls, so calls on one context must not run concurrently on
+ *     different streams (order them, or open one context per stream -- what
+ *     bench.py does for its bootstraps in flight).  The single-pass scan
+ *     keeps separate state per stream (up to 8), so a violation corrupts
+ *     data but cannot hang the GPU.
  *
  * Reference interfaces replaced (paths relative to the reference repo):
  *   ccg_knn_boot / ccg_knn_rows_dev : BiocNeighbors::findKNN as reached by
@@ -55,7 +65,7 @@
 extern "C" {
 #endif
 
-#define CCG_ABI_VERSION 6
+#define CCG_ABI_VERSION 7
 
 #define CCG_OK 0
 #define CCG_EINVAL (-1)  /* bad argument / shape */
@@ -196,6 +206,30 @@ int ccg_knn_boot_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d,
                            const int32_t* tab_idx, const double* tab_d2, int K,
                            int32_t* out_idx, double* out_dist,
                            ccg_knn_stats* stats, void* stream);
+
+/* A batch of nb bootstraps of the same PCs through ONE set of launches of
+ * ccg_knn_boot_table_dev's path (the bootstrap loop of R/consensusClust.R:
+ * 391-400 with :656-658's findKNN on each pca[sample(...), ]): every
+ * bootstrap gets ccg_knn_boot_table_dev's result, bit for bit.
+ *   idx      : device, nb x n int32 cell indices (bootstrap s = idx[s n ..
+ *              (s+1) n), R's sample() - 1)
+ *   n_unique : HOST, nb values: each bootstrap's length(unique(idx_s)), each
+ *              >= kmax + 1 (a wrong value sets the sticky device error)
+ *   rows     : device, (nb n) x d row-major: the gathered rows of every
+ *              bootstrap (ccg_gather_rows_rm_dev on the whole idx)
+ *   tab_idx / tab_d2 / K : the cell table of the same pcs (ccg_knn_table_dev)
+ *   local_ids: 1 = out_idx holds each bootstrap's own row indices (0 .. n-1),
+ *              0 = rows of the concatenation (s n + i: the disjoint union of
+ *              the nb graphs, ready for one ccg_snn_classes_dev pass)
+ *   out_idx  : device, (nb n) x kmax; out_dist optional (nb n) x kmax
+ * Requires 1 <= nb <= 64, nb n < 2^30, nb N < 2^31 - 1, kmax <= 32.  No host
+ * synchronisation (unless stats).  ccg_knn_last_fallback then returns the
+ * rows of cut ties (ids of the concatenation). */
+int ccg_knn_boots_table_dev(ccg_ctx* ctx, int64_t N, int d, const int32_t* idx, int64_t n, int nb,
+                            const int* n_unique, const double* rows, int kmax,
+                            const int32_t* tab_idx, const double* tab_d2, int K, int local_ids,
+                            int32_t* out_idx, double* out_dist, ccg_knn_stats* stats,
+                            void* stream);
 
 /* The bootstrap kNN of many small PC matrices in one set of launches:
  * iterate=TRUE (R/consensusClust.R:541-567, BASELINE config 5) re-runs the
@@ -650,6 +684,13 @@ int ccg_group_knn_boot(ccg_group* g, const double* pcs, int64_t N, int d, const 
  * Requires 0 <= key_bits <= 31, n < 2^31. */
 int ccg_sort_pairs_dev(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
                        int32_t* vals_out, int64_t n, int key_bits, void* stream);
+
+/* Exclusive scan of n int64 values (device pointers; out has n + 1 entries,
+ * out[n] = the total; out may alias in): the single-pass look-back scan the
+ * library's counting sorts and SNN offsets use (up to 2^21 values in one
+ * launch, the two-pass scan beyond), exported for testing.  Values and their
+ * partial sums must lie in [0, 2^62). */
+int ccg_scan_i64_dev(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, void* stream);
 
 /* ------------------------------------------------------ kernel timing -- */
 /* Device time of selected kernels, measured with hipEvents recorded on the

@@ -35,7 +35,7 @@ def test_nm_exports_are_extern_c():
 
 def test_abi_version_and_error_path():
     lib = _lib.load()
-    assert lib.ccg_abi_version() == 6
+    assert lib.ccg_abi_version() == 7
     # NULL out-pointer: rejected before any device work, message set
     assert lib.ccg_open(None, None) == _lib.CCG_EINVAL
     assert b"NULL" in lib.ccg_last_error()
