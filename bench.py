@@ -57,10 +57,14 @@ K_NUM = (10, 15, 20)
 N_RES = 20
 # BASELINE.json configs: shapes per workload (weak scaling: bootstraps per GPU)
 WORKLOADS = {
-    "cfg3": dict(cells=100000, pcs=30, boots_per_gpu=125, mode="robust", emul_ranks=0, cmax=40),
-    "cfg3job": dict(cells=100000, pcs=30, boots_per_gpu=1000, mode="robust", emul_ranks=0, cmax=40),
-    "cfg2": dict(cells=20000, pcs=20, boots_per_gpu=500, mode="robust", emul_ranks=0, cmax=40),
-    "cfg4": dict(cells=250000, pcs=30, boots_per_gpu=125, mode="granular", emul_ranks=8, cmax=60),
+    "cfg3": dict(cells=100000, pcs=30, boots_per_gpu=125, mode="robust", emul_ranks=0, cmax=40, boot_batch=8,
+                 batch_streams=3),
+    "cfg3job": dict(cells=100000, pcs=30, boots_per_gpu=1000, mode="robust", emul_ranks=0, cmax=40, boot_batch=8,
+                    batch_streams=3),
+    "cfg2": dict(cells=20000, pcs=20, boots_per_gpu=500, mode="robust", emul_ranks=0, cmax=40, boot_batch=32,
+                 batch_streams=3),
+    "cfg4": dict(cells=250000, pcs=30, boots_per_gpu=125, mode="granular", emul_ranks=8, cmax=60, boot_batch=8,
+                 batch_streams=3),
     "cfg5": dict(cells=100000, pcs=30, boots_per_gpu=125, mode="robust", emul_ranks=0, cmax=40),
 }
 

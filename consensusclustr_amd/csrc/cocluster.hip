@@ -17,15 +17,13 @@
 // Outputs: the packed upper triangle by rows (== R's "dist" order) for a row
 // slab [r0, r1), or (consensus kNN) full rows [r0, r1) x [0, N) packed as
 // co | both << 16.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <vector>
 
-#include "ccg_internal.h"
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
+#include "cocluster_common.h"
 
 template <typename T>
 __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __restrict__ colC) {
@@ -63,9 +61,6 @@ __global__ void coc_colmax_kernel(const T* __restrict__ A, int64_t N, int* __res
 // fragment.  Columns with no label (never sampled) own no half.
 #define COF_BM 128          // output rows per block (2 waves x 64)
 #define COF_BN 256          // output cols per block (2 waves x 128)
-#ifndef COF_SLOTS
-#define COF_SLOTS 32        // slots per stage (16 K-steps of v_mfma_i32_32x32x32_i8)
-#endif
 #define COF_ROWS (COF_BM + COF_BN)
 #define COF_CHUNK 16383     // columns per accumulation chunk
 #define COF_SB 14           // desc = column << COF_SB | half-in-column (half < 8193)
@@ -139,7 +134,6 @@ __global__ __launch_bounds__(1024) void cof_slots_kernel(const int* __restrict__
 // only (label >= 8), 1 + x = flag + one-hot byte x (label x = 1..7).  The flag
 // is int8 -128 in byte 0.  The zero entries of the four types sit in distinct
 // 16-byte bank groups.
-#define COF_TAB (4 * 81)
 
 __device__ __forceinline__ int cof_sigma(int d, int lab) {
     if (d < 0 || lab == 0) return 0;
@@ -181,9 +175,6 @@ __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ 
 
 // Output modes: packed upper triangle of rows [r0, r1) (R "dist" order), or
 // full rows [r0, r1) x [0, N) as one uint32 co | both << 16 per pair.
-#define COF_TRI 0
-#define COF_RECT 1
-#define COF_CAND 2  // packed-triangle tiles whose epilogue appends consensus-kNN candidates
 
 // Consensus-kNN candidate lists (COF_CAND): pair (i, j) of the triangle is
 // offered to row i if sim_ij >= tau_i and to row j if sim_ij >= tau_j, where
@@ -374,19 +365,7 @@ __global__ __launch_bounds__(256, 2) void cof_tile_kernel(
 #pragma unroll
         for (int i = 0; i < LOADS; ++i) reinterpret_cast<unsigned*>(&panel[bb][0][0])[i * 256 + tid] = pf[i];
     };
-    for (int x = tid; x < COF_TAB; x += 256) {
-        const int ty = x / 81, en = x - ty * 81;
-        int w[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {  // half hf: dwords 2 hf, 2 hf + 1
-            const int sg = hf ? en / 9 : en % 9;
-            const bool first = (ty >> hf) & 1;
-            if (sg >= 1 && first) w[2 * hf] |= 0x80;  // the flag
-            const int ob = first ? (sg >= 2 ? sg - 1 : -1) : sg - 1;  // one-hot byte
-            if (ob >= 0) w[2 * hf + (ob >> 2)] |= 1 << (8 * (ob & 3));
-        }
-        ftab[x] = (v4i){w[0], w[1], w[2], w[3]};
-    }
+    for (int x = tid; x < COF_TAB; x += 256) ftab[x] = cof_ftab_entry(x);
     if (nstage > 0) {
         issue(0);
         commit(0);
@@ -607,6 +586,17 @@ static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int6
     return CCG_OK;
 }
 
+// The triangle and full-row GEMMs take the wide-tile kernel (coc_wide.hip);
+// CCG_COF_WIDE=0 restores the 128 x 256 tile kernel (A/B).  The consensus
+// kNN's candidate epilogue stays on the 128 x 256 tiles.
+static bool cof_wide_on() {
+    static const int on = [] {
+        const char* e = getenv("CCG_COF_WIDE");
+        return e ? atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
 // One column chunk [cb0, cb0 + Bc): slot tables, entry matrix, GEMM tiles.
 template <int MODE>
 static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, int64_t N, int64_t r0, int64_t r1,
@@ -622,6 +612,11 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
     else
         cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                          pl.nslot, pl.E);
+    if (MODE != COF_CAND && cof_wide_on()) {  // 128 x 128 wave tiles (coc_wide.hip)
+        cof_wide_launch(MODE, pl.E, pl.Npad, N, r0, r1, NB ? NB : N, pl.nslot, pl.tmask, co_prev, both_prev, co, both,
+                        dist, cb_prev, cb, st);
+        return;
+    }
     cof_tile_kernel<MODE><<<(unsigned)cof_tile_blocks(ccg_cdiv(r1 - r0, COF_BM), TC, I0, MODE != COF_RECT), 256, 0,
                             st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
                                                             both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
@@ -647,7 +642,8 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
-    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, true) < (1LL << 31), "ccg_cocluster_dev: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, true) < (1LL << 31) && cof_wide_blocks(N, r0, r1, N, true) < (1LL << 31),
+                "ccg_cocluster_dev: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     uint16_t *pco = co, *pboth = both;  // partial counts between chunks
     if (nch > 1 && (!co || !both)) {
@@ -683,7 +679,8 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
     const int64_t I0 = r0 / COF_BM;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     const int64_t ntiles = TR * TC;
-    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, false) < (1LL << 31), "ccg_cocluster_rows: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, false) < (1LL << 31) && cof_wide_blocks(N, r0, r1, NB, false) < (1LL << 31),
+                "ccg_cocluster_rows: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t cb0 = pl.cuts[c], Bc = pl.cuts[c + 1] - cb0;
