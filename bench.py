@@ -99,6 +99,11 @@ def parse():
     ap.add_argument("--knn-path", choices=["table", "screen"], default="table",
                     help="table: one cell table per step (ccg_knn_table_dev) filtered per bootstrap; "
                          "screen: a screen per bootstrap (warm-started)")
+    ap.add_argument("--split-sil", type=int, default=0,
+                    help="launch sets: the silhouettes of set t on a stream (and context) of their own, after the "
+                         "set's gather and beside its kNN + SNN (they depend on the rows only), so the MFMA/VALU-bound "
+                         "widths overlap the latency-bound SNN (round 6, cfg3: boot phase 87.4 ms against 87.8 -- the GPU "
+                         "is already full); 0 = one stream per set (default)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues for this process (0: the runtime's default)")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
@@ -842,7 +847,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         out["cpu_baseline"] = None
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    for e in engs[1:]:
+    for e in engs[1:] + engs_sil:
         e.close()
     grp.close()
     if G > 1:
@@ -1027,6 +1032,32 @@ def main():
                  nclust=[nclust[j] for j in range(b0, b1)], minsize=[minsize[j] for j in range(b0, b1)])
             for b0, b1 in batches]
 
+    # --split-sil: the silhouettes of a set on their own stream and context
+    # (a context's workspaces serve one stream at a time), ordered after the
+    # set's gather; the next set on the same buffers waits for them
+    split = batched and robust and args.split_sil > 0
+    engs_sil = [Engine(local) for _ in range(S)] if split else []
+    streams_sil = [e.torch_stream() for e in engs_sil]
+    ev_g = [torch.cuda.Event() for _ in range(S)]
+    ev_s = [torch.cuda.Event() for _ in range(S)]
+
+    def run_set_split(si, t):
+        c = sets[t]
+        m = c["m"]
+        r, k = rows_s[si][:m], knn_s[si][:m]
+        e, es = engs[si], engs_sil[si]
+        with torch.cuda.stream(streams[si]):
+            streams[si].wait_event(ev_s[si])  # set t - S's silhouettes have read the rows
+            e.gather_rows_rm_t(pcs, N, d, c["flat"], r)
+            ev_g[si].record(streams[si])
+            e.knn_boots_table_t(N, d, c["idx"], c["uniq"], r, 20, tab_idx, tab_d2, k)
+            snn_out[si].run(e, k, c["keys"], snn_info[t], n=m)
+        with torch.cuda.stream(streams_sil[si]):
+            streams_sil[si].wait_event(ev_g[si])
+            es.silhouette_segments_t(r, c["off"], c["labels"], cmax, c["keys"], c["ncell"], c["means"],
+                                     c["nclust"], c["minsize"])
+            ev_s[si].record(streams_sil[si])
+
     def run_set(e, si, t, info=None):
         # one launch set: gather, kNN from the table, SNN classes, silhouettes of its bootstraps
         c = sets[t]
@@ -1084,9 +1115,12 @@ def main():
         cur = torch.cuda.current_stream()
         if use_table:  # one table per step: every bootstrap of the step filters it
             eng.knn_table_t(pcs_cm, N, d, KT, tab_idx, tab_d2)
-        for st_ in streams:
+        for st_ in streams + streams_sil:
             st_.wait_stream(cur)
-        if batched:
+        if batched and split:
+            for t in range(len(batches)):
+                run_set_split(t % S, t)
+        elif batched:
             for t in range(len(batches)):
                 si = t % S
                 with torch.cuda.stream(streams[si]):
@@ -1102,7 +1136,7 @@ def main():
                     if robust:  # granular mode scores no clustering (:688)
                         e.silhouette_cells_t(rows_s[si][:n], labels[j], cmax, boots[j], N, means[j], nclust[j],
                                              minsize[j])
-        for st_ in streams:
+        for st_ in streams + streams_sil:
             cur.wait_stream(st_)
 
     graph = [None]  # the captured bootstrap phase (--launch graph)
@@ -1189,7 +1223,7 @@ def main():
     host_ms = host_t[0] / args.steps * 1000
     # kernel-time breakdown: one more (untimed) step with the library's
     # hipEvent timers on
-    for e in engs:
+    for e in engs + engs_sil:
         e.timing(True)
         for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
             e.timing_read(w)
@@ -1204,9 +1238,9 @@ def main():
     per_rank = per_rank_report(torch, dist, G, phase, dev)
     kt = {}
     for w in ("knn_screen", "knn_total", "snn", "silhouette", "cocluster"):
-        r = [e.timing_read(w) for e in engs]
+        r = [e.timing_read(w) for e in engs + engs_sil]
         kt[w] = (sum(x[0] for x in r), sum(x[1] for x in r))
-    for e in engs:
+    for e in engs + engs_sil:
         e.timing(False)
     # host cost of one bootstrap's launches on an idle GPU (no queue
     # back-pressure): one launch set divided by its bootstraps when batched
@@ -1473,7 +1507,7 @@ def main():
             "cells": N, "pcs": d, "bootstrap_rows": n, "distinct_cells_mean": round(float(np.mean(uniq)), 1),
             "boots_per_gpu": B, "clusterings_per_boot": L,
             "parallelism": f"bootstraps x{G}, co-cluster row slabs x{G}", "streams_per_gpu": S,
-            "knn_path": args.knn_path,
+            "knn_path": args.knn_path, "silhouette_streams": len(streams_sil),
         },
         "roofline": roof_coc,
         "roofline_note": "the co-cluster GEMM is the largest single launch of a step; the per-bootstrap "

@@ -586,17 +586,6 @@ static int cof_plan(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int6
     return CCG_OK;
 }
 
-// The triangle and full-row GEMMs take the wide-tile kernel (coc_wide.hip);
-// CCG_COF_WIDE=0 restores the 128 x 256 tile kernel (A/B).  The consensus
-// kNN's candidate epilogue stays on the 128 x 256 tiles.
-static bool cof_wide_on() {
-    static const int on = [] {
-        const char* e = getenv("CCG_COF_WIDE");
-        return e ? atoi(e) : 1;
-    }();
-    return on != 0;
-}
-
 // One column chunk [cb0, cb0 + Bc): slot tables, entry matrix, GEMM tiles.
 template <int MODE>
 static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, int64_t N, int64_t r0, int64_t r1,
@@ -612,11 +601,6 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
     else
         cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                          pl.nslot, pl.E);
-    if (MODE != COF_CAND && cof_wide_on()) {  // 128 x 128 wave tiles (coc_wide.hip)
-        cof_wide_launch(MODE, pl.E, pl.Npad, N, r0, r1, NB ? NB : N, pl.nslot, pl.tmask, co_prev, both_prev, co, both,
-                        dist, cb_prev, cb, st);
-        return;
-    }
     cof_tile_kernel<MODE><<<(unsigned)cof_tile_blocks(ccg_cdiv(r1 - r0, COF_BM), TC, I0, MODE != COF_RECT), 256, 0,
                             st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
                                                             both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
@@ -642,8 +626,7 @@ extern "C" int ccg_cocluster_dev(ccg_ctx* ctx, const void* A, int label_bits, in
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - (fl(I0 + TR) - fl(I0));
-    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, true) < (1LL << 31) && cof_wide_blocks(N, r0, r1, N, true) < (1LL << 31),
-                "ccg_cocluster_dev: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, true) < (1LL << 31), "ccg_cocluster_dev: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     uint16_t *pco = co, *pboth = both;  // partial counts between chunks
     if (nch > 1 && (!co || !both)) {
@@ -679,8 +662,7 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
     const int64_t I0 = r0 / COF_BM;
     const int64_t TR = ccg_cdiv(r1 - r0, COF_BM);
     const int64_t ntiles = TR * TC;
-    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, false) < (1LL << 31) && cof_wide_blocks(N, r0, r1, NB, false) < (1LL << 31),
-                "ccg_cocluster_rows: too many tiles");
+    CCG_REQUIRE(cof_tile_blocks(TR, TC, I0, false) < (1LL << 31), "ccg_cocluster_rows: too many tiles");
     const int64_t nch = (int64_t)pl.cuts.size() - 1;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t cb0 = pl.cuts[c], Bc = pl.cuts[c + 1] - cb0;

@@ -1,6 +1,5 @@
-// Shared between the co-cluster translation units (cocluster.hip: plan,
-// entry matrix, the 128 x 256 tile kernel for candidates; coc_wide.hip: the
-// 256 x 256 wide-tile kernel).  Internal, not part of the ABI.
+// Co-cluster constants and the fragment-table entry (cocluster.hip).
+// Internal, not part of the ABI.
 #pragma once
 #include "ccg_internal.h"
 
@@ -31,12 +30,3 @@ __device__ __forceinline__ v4i cof_ftab_entry(int x) {
     }
     return (v4i){w[0], w[1], w[2], w[3]};
 }
-
-// The wide-tile GEMM (coc_wide.hip) for the packed triangle (COF_TRI) or full
-// rows (COF_RECT) of rows [r0, r1): same entry matrix, slot tables and
-// outputs as cof_tile_kernel.
-void cof_wide_launch(int mode, const uint8_t* E, int64_t Npad, int64_t N, int64_t r0, int64_t r1, int64_t NB,
-                     const int* nslot, const unsigned long long* tmask, const uint16_t* co_prev,
-                     const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
-                     uint32_t* cb, hipStream_t st);
-int64_t cof_wide_blocks(int64_t N, int64_t r0, int64_t r1, int64_t NB, bool tri);

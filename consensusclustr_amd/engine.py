@@ -21,8 +21,8 @@ def _ptr(a):
     if a is None:
         return None
     if isinstance(a, np.ndarray):
-        if not a.flags.c_contiguous:  # the C ABI reads dense row-major memory
-            raise ValueError(f"array of shape {a.shape} is not C-contiguous")
+        if not (a.flags.c_contiguous or a.flags.f_contiguous):  # (the wrappers pick the layout: R's column-major
+            raise ValueError(f"array of shape {a.shape} is not contiguous")  # PCs are asfortranarray)
         return a.ctypes.data_as(_vp)
     if not a.is_contiguous():  # torch tensor: a strided view would be read in the wrong order
         raise ValueError(f"tensor of shape {tuple(a.shape)} and strides {a.stride()} is not contiguous")
