@@ -138,6 +138,10 @@ int ccg_take_device_error(ccg_ctx* ctx) {
         ccg_set_error("cluster position outside [0, K)");
         return CCG_EINVAL;
     }
+    if (bits & CCG_DERR_SCAN_RANGE) {
+        ccg_set_error("scan: a tile sum or prefix outside [0, 2^62)");
+        return CCG_ERANGE;
+    }
     if (bits & CCG_DERR_KNN_UNIQUE) {
         ccg_set_error("ccg_knn_boot_dev: n_unique is not the number of distinct cells in idx");
         return CCG_EINVAL;
@@ -261,7 +265,9 @@ extern "C" int ccg_timing_read(ccg_ctx* ctx, int which, double* total_ms, int64_
 
 // ------------------------------------------------------------------ scan --
 #define SCAN_T 256
+#ifndef SCAN_TILE
 #define SCAN_TILE 2048  // 8 elements per thread
+#endif
 
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* total) {
     const int t = threadIdx.x;
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_tiles(const int64_t* in, int64_t*
 #define SCAN_VAL_MASK ((1ull << 62) - 1)
 __global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_t* out, int64_t n, int nb,
                                                        unsigned long long* __restrict__ stat,
-                                                       unsigned* __restrict__ done) {
+                                                       unsigned* __restrict__ done, int* __restrict__ err) {
     __shared__ int64_t sh[SCAN_T / 64];
     __shared__ int64_t pref;
     constexpr int E = SCAN_TILE / SCAN_T;
@@ -374,6 +380,9 @@ __global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_
     }
     int64_t tot;
     int64_t ex = block_excl_scan(s, sh, &tot);
+    // the status words hold 62-bit values: a negative or too large tile sum
+    // (a caller's contract violation) is reported, not silently wrapped
+    if (threadIdx.x == 0 && (uint64_t)tot >> 62) atomicOr(err, CCG_DERR_SCAN_RANGE);
     if (threadIdx.x < 64) {  // wave 0: the look-back, 64 predecessors per round (one per lane)
         const int lane = threadIdx.x;
         unsigned long long run = 0;
@@ -417,7 +426,10 @@ __global__ __launch_bounds__(SCAN_T) void scan_onepass(const int64_t* in, int64_
         if (base + e < n) out[base + e] = ex;
         ex += v[e];
     }
-    if (b == nb - 1 && threadIdx.x == 0) out[n] = pref + tot;
+    if (b == nb - 1 && threadIdx.x == 0) {
+        out[n] = pref + tot;
+        if ((uint64_t)(pref + tot) >> 62) atomicOr(err, CCG_DERR_SCAN_RANGE);
+    }
     if (threadIdx.x == 0) {
         // every block counted here has finished its look-back
         const unsigned t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -447,7 +459,8 @@ int ccg_scan_i64(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, hipSt
     }
     if (nb <= SCAN_LB_MAX && slot >= 0) {
         unsigned long long* stat = (unsigned long long*)((char*)ctx->d_scan + (size_t)slot * SCAN_LB_BYTES);
-        scan_onepass<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, (int)nb, stat, (unsigned*)(stat + SCAN_LB_MAX));
+        scan_onepass<<<(unsigned)nb, SCAN_T, 0, st>>>(in, out, n, (int)nb, stat, (unsigned*)(stat + SCAN_LB_MAX),
+                                                      ctx->d_err);
         CCG_HIP(hipGetLastError());
         return CCG_OK;
     }

@@ -80,6 +80,7 @@ struct ccg_timer_rec {
 #define CCG_DERR_SNN_INDEX 2    // SNN: neighbour index out of range or self
 #define CCG_DERR_CLUSTER_INDEX 4  // block sums / contingency: cluster position outside [0, K)
 #define CCG_DERR_KNN_UNIQUE 8     // ccg_knn_boot_dev: n_unique differs from the distinct cells of idx
+#define CCG_DERR_SCAN_RANGE 16    // ccg_scan_i64: a tile sum or prefix outside [0, 2^62) (the status-word packing)
 
 #define CCG_PIN_RING 64  // (a launch set uploads its tables here: the host runs this many uploads ahead)
 #define CCG_SCAN_SLOTS 8  // streams with their own single-pass scan state per context

@@ -689,7 +689,9 @@ int ccg_sort_pairs_dev(ccg_ctx* ctx, const int32_t* keys_in, int32_t* keys_out, 
  * out[n] = the total; out may alias in): the single-pass look-back scan the
  * library's counting sorts and SNN offsets use (up to 2^21 values in one
  * launch, the two-pass scan beyond), exported for testing.  Values and their
- * partial sums must lie in [0, 2^62). */
+ * partial sums must lie in [0, 2^62); in the single-pass range a tile sum or
+ * total outside it sets the sticky device error (CCG_ERANGE at the next
+ * ccg_synchronize). */
 int ccg_scan_i64_dev(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, void* stream);
 
 /* ------------------------------------------------------ kernel timing -- */

@@ -124,6 +124,20 @@ def test_scan_tile_counts_in_place_and_repeated(engine, n):
         assert np.array_equal(buf.cpu().numpy(), want), rep
 
 
+def test_scan_reports_values_outside_its_range(engine):
+    """The status words pack 62-bit values: a prefix at or past 2^62 sets the
+    sticky error instead of wrapping silently."""
+    import torch
+    from consensusclustr_amd import CcgError
+    x = torch.zeros(3 * 2048, dtype=torch.int64, device="cuda:0")
+    x[2048] = 1 << 62  # tile 1's sum
+    out = torch.empty(x.numel() + 1, dtype=torch.int64, device="cuda:0")
+    engine.scan_i64_t(x, out)
+    with pytest.raises(CcgError):
+        engine.synchronize()
+    engine.synchronize()  # (the error is taken once)
+
+
 def test_scan_alternating_streams_one_context(engine):
     import torch
     dev = torch.device("cuda", 0)
