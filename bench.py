@@ -116,7 +116,7 @@ def parse():
     ap.add_argument("--table-k", type=int, default=48,
                     help="cell-table length K (<= 48): cells with fewer than 20 of their K nearest cells in a "
                          "bootstrap take the exact search")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks, all-gather their ids over gloo and print them (no GPU)")
     a = ap.parse_args()
@@ -847,7 +847,7 @@ def run_cfg5(args, torch, dist, grp, engs, dev, world, rank, json_fd, ranks_seen
         out["cpu_baseline"] = None
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    for e in engs[1:] + engs_sil:
+    for e in engs[1:]:
         e.close()
     grp.close()
     if G > 1:
@@ -1213,6 +1213,9 @@ def main():
     # cost host time on every launch group)
     barrier()
     torch.cuda.synchronize()
+    ring_engs = list({id(e): e for e in [eng] + engs + engs_sil}.values())
+    for e in ring_engs:
+        e.timing_read("host_ring_wait")  # (reset: host-side accounting, always on)
     t0 = time.perf_counter()
     host_t[0] = 0.0
     for _ in range(args.steps):
@@ -1221,6 +1224,7 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     host_ms = host_t[0] / args.steps * 1000
+    ring_ms = sum(e.timing_read("host_ring_wait")[0] for e in ring_engs) / args.steps
     # kernel-time breakdown: one more (untimed) step with the library's
     # hipEvent timers on
     for e in engs + engs_sil:
@@ -1472,7 +1476,7 @@ def main():
         "achieved": round(sil_flop / (sil_ms * 1e-3) / 1e12, 2) if robust else None,
         "frac": round(sil_flop / (sil_ms * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4) if robust else None,
         "traffic": sil_traffic,
-        "traffic_note": "HBM bytes per bootstrap over the stage's kernels (profiles/traffic_r05.json); the "
+        "traffic_note": "HBM bytes per bootstrap over the stage's kernels (profiles/traffic_r06.json); the "
                         "stage is bound by VALU issue (the screen's min tracking, the exact fp64 distances) "
                         "and the sums' LDS atomics, not by either peak",
         "algorithmic_per_launch": f"2 d u sum_l C_l = {sil_flop:.3e} flop per bootstrap (x.mu of the u distinct "
@@ -1526,6 +1530,11 @@ def main():
                          "co/both row slab",
         "launch": launch_note,
         "host_enqueue_ms_per_step": round(host_ms, 3),
+        "host_ring_wait_ms_per_step": round(ring_ms, 3),
+        "host_launch_ms_per_step": round(host_ms - ring_ms, 3),
+        "host_enqueue_note": "host time in the step's launch loop; of it, host_ring_wait is time blocked on the "
+                             "pinned upload ring (the host is that many launch sets ahead of the GPU: "
+                             "back-pressure), host_launch the rest (issuing work)",
         "host_launch_ms_per_boot_idle_gpu": round(host_idle_ms, 3),
         "boots_per_launch_set": NBB,
         "launch_sets_per_step": len(batches) if batched else B,

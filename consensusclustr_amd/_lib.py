@@ -123,9 +123,10 @@ SIGNATURES = {
     "ccg_sort_pairs_dev": (_i, [_p, _p, _p, _p, _p, _i64, _i, _p]),
     "ccg_scan_i64_dev": (_i, [_p, _p, _p, _i64, _p]),
     "ccg_timing_enable": (_i, [_p, _i]),
+    "ccg_host_louvain": (_i, [_i64, _i64, _p, _p, _p, ctypes.c_double, ctypes.c_uint64, _p]),
     "ccg_timing_read": (_i, [_p, _i, _p, _p]),
 }
-CCG_KT = {"knn_screen": 0, "knn_total": 1, "snn": 2, "silhouette": 3, "cocluster": 4}
+CCG_KT = {"knn_screen": 0, "knn_total": 1, "snn": 2, "silhouette": 3, "cocluster": 4, "host_ring_wait": 100}
 
 _LIB = None
 

@@ -5,13 +5,36 @@ The reference keeps ``igraph::cluster_leiden`` on the host (R/consensusClust.R
 produces the SNN graph, the host clusters it.  python-igraph / leidenalg are
 not installed in this image, so this module provides a deterministic
 modularity optimiser (Louvain local moving + aggregation, resolution
-parameter as in igraph's modularity objective) as the default stand-in.
-It is NOT bit-compatible with igraph's Leiden (different algorithm and RNG);
-pass ``clusterFun=`` a callable wrapping igraph where it is available.
-A callable has the signature ``f(n, ei, ej, w, resolution, seed) -> labels``
-with labels 1..C.
+parameter as in igraph's modularity objective) as the default stand-in:
+``louvain`` runs libccg's host implementation (``ccg_host_louvain``, C++ on
+the calling thread, GIL released), ``louvain_py`` is the same algorithm in
+Python (readable, seconds per graph at 18k rows; different node order, so
+its labels can differ).  Neither is bit-compatible with igraph's Leiden
+(different algorithm and RNG); pass ``clusterFun=`` a callable wrapping
+igraph where it is available.  A callable has the signature
+``f(n, ei, ej, w, resolution, seed) -> labels`` with labels 1..C.
 """
+import ctypes
+
 import numpy as np
+
+from . import _lib
+
+
+def louvain(n, ei, ej, w, resolution=1.0, seed=0):
+    """Modularity (with resolution) community detection on host threads
+    (ccg_host_louvain); returns int32 labels 1..C in order of first appearance."""
+    ei = np.ascontiguousarray(ei, dtype=np.int32)
+    ej = np.ascontiguousarray(ej, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    if not (ei.size == ej.size == w.size):
+        raise ValueError("louvain: ei, ej and w must have the same length")
+    out = np.empty(int(n), np.int32)
+    vp = ctypes.c_void_p
+    _lib.check(_lib.load().ccg_host_louvain(int(n), ei.size, vp(ei.ctypes.data), vp(ej.ctypes.data),
+                                            vp(w.ctypes.data), float(resolution), int(seed) & (2**64 - 1),
+                                            vp(out.ctypes.data)))
+    return out
 
 
 def _csr(n, ei, ej, w):
@@ -64,8 +87,8 @@ def _one_level(n, indptr, nbr, wts, self_w, gamma, rng):
     return comm, moved_any
 
 
-def louvain(n, ei, ej, w, resolution=1.0, seed=0, max_levels=16):
-    """Modularity (with resolution) community detection; returns labels 1..C."""
+def louvain_py(n, ei, ej, w, resolution=1.0, seed=0, max_levels=16):
+    """Modularity (with resolution) community detection in Python; returns labels 1..C."""
     rng = np.random.default_rng(seed)
     ei = np.asarray(ei, np.int64)
     ej = np.asarray(ej, np.int64)

@@ -8,6 +8,9 @@ small per-bootstrap decision logic.
 
 Indices are 0-based; "NA" cluster assignments are -1 as after :408.
 """
+import os
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 from .cluster_host import louvain
@@ -27,12 +30,33 @@ def default_engine():
     return _DEFAULT_ENGINE
 
 
+def _native_louvain(n, ei, ej, w, res, seed):
+    return louvain(n, ei, ej, w, resolution=res, seed=seed)
+
+
 def _cluster_fn(clusterFun):
     if callable(clusterFun):
         return clusterFun
     if clusterFun in ("leiden", "louvain"):
-        return lambda n, ei, ej, w, res, seed: louvain(n, ei, ej, w, resolution=res, seed=seed)
+        return _native_louvain
     raise ValueError(f"clusterFun must be 'leiden', 'louvain' or a callable, got {clusterFun!r}")
+
+
+_POOL = None
+
+
+def _cluster_all(fn, jobs):
+    """fn(*job) for every job, in order.  The built-in clusterer
+    (ccg_host_louvain: no shared state, the GIL released) runs the jobs on
+    host threads -- the reference runs one bootstrap per BiocParallel worker
+    (:391-400); here the clusterings of one bootstrap share the workers.  A
+    caller's callable runs serially (its thread safety is unknown)."""
+    global _POOL
+    if fn is not _native_louvain or len(jobs) < 2:
+        return [fn(*j) for j in jobs]
+    if _POOL is None:
+        _POOL = ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1)))
+    return list(_POOL.map(lambda j: fn(*j), jobs))
 
 
 # ------------------------------------------------------------ decisions --
@@ -123,14 +147,10 @@ def getClustAssignments(pca, boot_idx=None, clusterFun="leiden", resRange=RES_RA
     elif knn.shape != (n, kmax):
         raise ValueError(f"knn must be {n} x {kmax}, got {knn.shape}")
     fn = _cluster_fn(clusterFun)
-    labels = []
     # every k in one pass (:656-658); copies of a cell share a row class
     graphs = eng.snn_multi(knn, [int(k) for k in kNum], "number", cell=boot_idx)
-    for g, k in enumerate(kNum):  # :653-654, k outer, resolution inner
-        ei, ej, w = graphs[g]
-        for res in resRange:
-            labels.append(np.asarray(fn(n, ei, ej, w, float(res), seed), np.int32))
-    lab = np.stack(labels)
+    jobs = [(n, *graphs[g], float(res), seed) for g in range(len(kNum)) for res in resRange]  # :653-654, k outer
+    lab = np.stack([np.asarray(x, np.int32) for x in _cluster_all(fn, jobs)])
     if mode == "robust":
         X = pca[boot_idx]
         # :664 on the bootstrap rows: widths once per (cell, label), copies weighted
@@ -247,11 +267,11 @@ def consensus_cluster(pca, nboots=100, bootSize=0.9, clusterFun="leiden", resRan
         out.update(jaccardDist=cc["dist"], co=cc["co"], both=cc["both"])
     kmax = max(kNum)
     cknn = eng.consensus_knn_assign(A, kmax)  # dbscan::kNN(jaccardDist, k), :425 (k < kmax: prefixes)
-    finals = []
+    jobs = []
     for k in kNum:  # :423-441
         ei, ej, w = eng.snn(np.ascontiguousarray(cknn[:, :k]), k, "rank")  # neighborsToSNNGraph(knn, "rank"), :426
-        for res in resRange:
-            finals.append(np.asarray(fn(N, ei, ej, w, float(res), seed), np.int32))
+        jobs += [(N, ei, ej, w, float(res), seed) for res in resRange]
+    finals = [np.asarray(x, np.int32) for x in _cluster_all(fn, jobs)]
     lab = np.stack(finals)
     nuniq = np.array([np.unique(l_).size for l_ in finals])
     # approxSilhouette on the full pca only where it is used, 1 < C < N/10 (:446-452)

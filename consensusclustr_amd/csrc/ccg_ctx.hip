@@ -4,6 +4,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+
 #include "ccg_internal.h"
 
 static thread_local char g_err[1024] = "";
@@ -108,7 +110,13 @@ int ccg_h2d_staged(ccg_ctx* ctx, void* dst, const void* src, size_t bytes, hipSt
     const int s = ctx->pin_next;
     ctx->pin_next = (s + 1) % CCG_PIN_RING;
     if (!ctx->pin_ev[s]) CCG_HIP(hipEventCreateWithFlags(&ctx->pin_ev[s], hipEventDisableTiming));
-    else CCG_HIP(hipEventSynchronize(ctx->pin_ev[s]));  // the slot's previous copy has run
+    else if (hipEventQuery(ctx->pin_ev[s]) == hipErrorNotReady) {  // the slot's previous copy has not run
+        (void)hipGetLastError();  // (not-ready is a status, not an error: keep it out of the next launch check)
+        const auto t0 = std::chrono::steady_clock::now();
+        CCG_HIP(hipEventSynchronize(ctx->pin_ev[s]));
+        ctx->pin_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        ctx->pin_waits++;
+    }
     if (ctx->pin_bytes[s] < bytes) {
         if (ctx->pin_buf[s]) CCG_HIP(hipHostFree(ctx->pin_buf[s]));
         ctx->pin_buf[s] = nullptr;
@@ -239,6 +247,13 @@ extern "C" int ccg_timing_enable(ccg_ctx* ctx, int enable) {
 
 extern "C" int ccg_timing_read(ccg_ctx* ctx, int which, double* total_ms, int64_t* launches) {
     CCG_REQUIRE(ctx && total_ms && launches, "ccg_timing_read: NULL argument");
+    if (which == CCG_KT_HOST_RING_WAIT) {  // host-side accounting, read and reset
+        *total_ms = ctx->pin_wait_ms;
+        *launches = ctx->pin_waits;
+        ctx->pin_wait_ms = 0.0;
+        ctx->pin_waits = 0;
+        return CCG_OK;
+    }
     CCG_REQUIRE(which >= 0 && which < CCG_KT_COUNT, "ccg_timing_read: bad kernel id");
     double tot = 0.0;
     int64_t n = 0;

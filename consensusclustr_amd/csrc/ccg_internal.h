@@ -107,6 +107,8 @@ struct ccg_ctx {
     size_t pin_bytes[CCG_PIN_RING];
     hipEvent_t pin_ev[CCG_PIN_RING];
     int pin_next;
+    double pin_wait_ms;    // host time blocked on ring slots (ccg_timing_read CCG_KT_HOST_RING_WAIT)
+    int64_t pin_waits;
     // single-pass scan state (ccg_scan_i64): per-tile status words and the
     // finished-tile count, zero between calls (the kernel's last tile clears
     // them); one slice per stream the context has scanned on (CCG_SCAN_SLOTS),

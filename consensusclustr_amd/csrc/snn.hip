@@ -29,6 +29,9 @@
 //   4. per-graph edge lists (i < j sorted by (i, j)) are streamed from the
 //      rows when the caller wants them (ccg_snn_multi_dev).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -1856,9 +1859,14 @@ struct SnnStage {
     int32_t* rcls = nullptr;   // n: class ordinal of every row (classes)
     size_t cap_n = 0, cap_l = 0, cap_e = 0, cap_w = 0, cap_c = 0, cap_r = 0;
     int64_t ne[SNN_MAXK] = {0, 0, 0, 0};  // row-level edges per graph
-    // classes: the rows of every class (ascending), built on the first fetch
+    // classes: the rows of every class (ascending) and the symmetric class
+    // adjacency over the entries present in any graph (partner, packed
+    // values), built once per pass for every graph's fetch
     std::vector<int64_t> mstart;
     std::vector<int32_t> mrows;
+    std::vector<int64_t> aoff;
+    std::vector<int32_t> adj;
+    std::vector<uint32_t> av;
     bool valid = false;
 };
 
@@ -1921,6 +1929,112 @@ static void snn_host_parallel(int64_t n, unsigned nt, F&& f) {
     std::vector<std::thread> th;
     for (unsigned q = 0; q < nt; ++q) th.emplace_back(f, n * q / nt, n * (q + 1) / nt);
     for (auto& x : th) x.join();
+}
+
+// The same with the thread's index: f(q, lo, hi) for q < nt.
+template <typename F>
+static void snn_host_parallel_q(int64_t n, unsigned nt, F&& f) {
+    if (nt <= 1) {
+        f(0u, (int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned q = 0; q < nt; ++q) th.emplace_back(f, q, n * q / nt, n * (q + 1) / nt);
+    for (auto& x : th) x.join();
+}
+
+// Phase times of the host decode on stderr when CCG_SNN_HOST_PROFILE is set
+// (tools and tuning only).
+struct SnnHostClock {
+    bool on = std::getenv("CCG_SNN_HOST_PROFILE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ccg snn host] %-28s %8.2f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
+// Class-level staging (NUMBER graphs): the rows of every class, the
+// symmetric class adjacency over the entries present in any graph, and the
+// row-level edge count of every graph, on host threads.  The adjacency's
+// order within a class depends on the thread schedule; the fetch sorts each
+// output row, so the edge lists do not.
+static void snn_stage_classes(SnnStage* S, unsigned nt) {
+    const int64_t n = S->n, u = S->u;
+    const SnnSpec& sp = S->sp;
+    const int nk = sp.nk;
+    S->mstart.assign(u + 1, 0);
+    for (int64_t x = 0; x < n; ++x) S->mstart[S->rcls[x] + 1]++;
+    for (int64_t c = 0; c < u; ++c) S->mstart[c + 1] += S->mstart[c];
+    S->mrows.resize(n);
+    {
+        std::vector<int64_t> cur(S->mstart.begin(), S->mstart.end() - 1);
+        for (int64_t x = 0; x < n; ++x) S->mrows[cur[S->rcls[x]]++] = (int32_t)x;  // ascending within a class
+    }
+    const int64_t* ms = S->mstart.data();
+    // A counting sort by class without atomics: thread q owns classes
+    // [u q / nt, u (q + 1) / nt) and counts the entries naming each class in
+    // its own histogram; a class's adjacency is its own present entries, then
+    // the entries naming it in thread order (deterministic).
+    std::vector<int64_t> own(u, 0);
+    std::vector<int64_t> hist((size_t)nt * u, 0);
+    snn_host_parallel_q(u, nt, [&](unsigned q, int64_t c0, int64_t c1) {
+        int64_t* hq = hist.data() + (size_t)q * u;
+        for (int64_t c = c0; c < c1; ++c) {
+            int64_t k = 0;
+            for (int r = 0; r < S->rlen[c]; ++r) {
+                const int64_t e = S->roff[c] + r;
+                if (S->wpk[e] == 0u) continue;  // (NUMBER: no graph has this pair)
+                ++k;
+                hq[S->nbr[e]]++;
+            }
+            own[c] = k;
+        }
+    });
+    S->aoff.assign(u + 1, 0);
+    for (int64_t c = 0; c < u; ++c) {  // offsets; the histograms become each thread's fill cursors
+        int64_t base = S->aoff[c] + own[c];
+        for (unsigned q = 0; q < nt; ++q) {
+            const int64_t h = hist[(size_t)q * u + c];
+            hist[(size_t)q * u + c] = base;
+            base += h;
+        }
+        S->aoff[c + 1] = base;
+    }
+    S->adj.resize(S->aoff[u]);
+    S->av.resize(S->aoff[u]);
+    std::atomic<int64_t> netot[SNN_MAXK];
+    for (auto& z : netot) z.store(0, std::memory_order_relaxed);
+    snn_host_parallel_q(u, nt, [&](unsigned q, int64_t c0, int64_t c1) {
+        int64_t* hq = hist.data() + (size_t)q * u;
+        int64_t tot[SNN_MAXK] = {0, 0, 0, 0};
+        for (int64_t c = c0; c < c1; ++c) {
+            const int64_t mc = ms[c + 1] - ms[c];
+            int64_t sm[SNN_MAXK] = {0, 0, 0, 0};
+            int64_t a = S->aoff[c];
+            for (int r = 0; r < S->rlen[c]; ++r) {
+                const int64_t e = S->roff[c] + r;
+                const unsigned v = S->wpk[e];
+                if (v == 0u) continue;
+                const int32_t h = S->nbr[e];
+                S->adj[a] = h;
+                S->av[a++] = v;
+                const int64_t b = hq[h]++;
+                S->adj[b] = (int32_t)c;
+                S->av[b] = v;
+                const int64_t mh = ms[h + 1] - ms[h];
+                for (int t = 0; t < nk; ++t)
+                    if (snn_host_has(sp, v, t)) sm[t] += mh;
+            }
+            // row-level edges: m_C m_H per class edge, m_C (m_C - 1) / 2 inside a class
+            for (int t = 0; t < nk; ++t) tot[t] += mc * (mc - 1) / 2 + mc * sm[t];
+        }
+        for (int t = 0; t < nk; ++t) netot[t].fetch_add(tot[t], std::memory_order_relaxed);
+    });
+    for (int t = 0; t < nk; ++t) S->ne[t] = netot[t].load();
 }
 
 // One device pass + the copy to the host staging (rows or classes).
@@ -1998,31 +2112,15 @@ static int snn_graphs_stage(ccg_ctx* ctx, const int32_t* knn, int64_t n, int kst
         S->u = classes ? info[0] : n;
         S->mstart.clear();
         S->mrows.clear();
+        S->aoff.clear();
+        S->adj.clear();
+        S->av.clear();
         if (!classes) {
             for (int t = 0; t < nk; ++t) S->ne[t] = S->cnt[(int64_t)t * (n + 1) + n] - S->cnt[(int64_t)t * (n + 1)];
         } else {
-            // row-level counts: m_C m_H per class edge of graph t, m_C (m_C - 1) / 2 inside a class
-            const int64_t u = S->u;
-            S->mstart.assign(u + 1, 0);
-            for (int64_t x = 0; x < n; ++x) S->mstart[S->rcls[x] + 1]++;
-            for (int64_t c = 0; c < u; ++c) S->mstart[c + 1] += S->mstart[c];
-            S->mrows.resize(n);
-            std::vector<int64_t> cur(S->mstart.begin(), S->mstart.end() - 1);
-            for (int64_t x = 0; x < n; ++x) S->mrows[cur[S->rcls[x]]++] = (int32_t)x;  // ascending within a class
-            for (int t = 0; t < nk; ++t) {
-                int64_t tot = 0;
-                for (int64_t c = 0; c < u; ++c) {
-                    const int64_t mc = S->mstart[c + 1] - S->mstart[c];
-                    tot += mc * (mc - 1) / 2;
-                    int64_t sm = 0;
-                    for (int q = 0; q < S->rlen[c]; ++q) {
-                        const int64_t e = S->roff[c] + q;
-                        if (snn_host_has(sp, S->wpk[e], t)) sm += S->mstart[S->nbr[e] + 1] - S->mstart[S->nbr[e]];
-                    }
-                    tot += mc * sm;
-                }
-                S->ne[t] = tot;
-            }
+            SnnHostClock clk;
+            snn_stage_classes(S, snn_host_threads(need * nk));
+            clk.lap("stage: classes + adjacency");
         }
         S->valid = true;
         return CCG_OK;
@@ -2092,45 +2190,23 @@ extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t*
         snn_host_parallel(n, nt, work);
         return CCG_OK;
     }
-    // classes: the symmetric class adjacency of graph t, then per row x of
-    // class C every row y > x of C (weight k + 1: one common set) and of each
-    // neighbouring class, sorted by y
-    const int64_t u = S->u;
+    // classes: per row x of class C every row y > x of C (weight k + 1: one
+    // common set) and of each class adjacent to C in graph t (the staged
+    // adjacency's entries present in t), sorted by y
+    SnnHostClock clk;
     const int64_t* ms = S->mstart.data();
     const int32_t* mr = S->mrows.data();
-    std::vector<int64_t> aoff(u + 1, 0);
-    for (int64_t c = 0; c < u; ++c)
-        for (int q = 0; q < S->rlen[c]; ++q) {
-            const int64_t e = S->roff[c] + q;
-            if (snn_host_has(sp, S->wpk[e], t)) {
-                aoff[c + 1]++;
-                aoff[S->nbr[e] + 1]++;
-            }
-        }
-    for (int64_t c = 0; c < u; ++c) aoff[c + 1] += aoff[c];
-    std::vector<int32_t> adj(aoff[u]);
-    std::vector<uint8_t> aw(aoff[u]);
-    {
-        std::vector<int64_t> cur(aoff.begin(), aoff.end() - 1);
-        for (int64_t c = 0; c < u; ++c)
-            for (int q = 0; q < S->rlen[c]; ++q) {
-                const int64_t e = S->roff[c] + q;
-                const unsigned v = S->wpk[e];
-                if (!snn_host_has(sp, v, t)) continue;
-                const int h = S->nbr[e];
-                const uint8_t w = (uint8_t)((v >> (8 * t)) & 0xFFu);
-                adj[cur[c]] = h;
-                aw[cur[c]++] = w;
-                adj[cur[h]] = (int32_t)c;
-                aw[cur[h]++] = w;
-            }
-    }
-    const uint8_t wself = (uint8_t)(sp.kk[t] + 1);
+    const int64_t* aoff = S->aoff.data();
+    const int32_t* adj = S->adj.data();
+    const uint32_t* av = S->av.data();
+    const unsigned wself = (unsigned)(sp.kk[t] + 1);
     // rows of class h above x: [first, end) of its ascending member list
     auto above = [&](int64_t h, int32_t x) {
         const int32_t* b = mr + ms[h];
         const int32_t* e = mr + ms[h + 1];
-        return std::make_pair(std::upper_bound(b, e, x), e);
+        if (e - b > 16) return std::make_pair(std::upper_bound(b, e, x), e);
+        while (b < e && *b <= x) ++b;  // (a class is mostly a handful of rows: a linear scan)
+        return std::make_pair(b, e);
     };
     std::vector<int64_t> roff(n + 1, 0);
     snn_host_parallel(n, nt, [&](int64_t x0, int64_t x1) {
@@ -2139,6 +2215,7 @@ extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t*
             auto r = above(c, (int32_t)x);
             int64_t k = r.second - r.first;
             for (int64_t a = aoff[c]; a < aoff[c + 1]; ++a) {
+                if (!snn_host_has(sp, av[a], t)) continue;
                 auto q = above(adj[a], (int32_t)x);
                 k += q.second - q.first;
             }
@@ -2146,31 +2223,36 @@ extern "C" int ccg_snn_graph_fetch(ccg_ctx* ctx, int t, int32_t* out_i, int32_t*
         }
     });
     for (int64_t x = 0; x < n; ++x) roff[x + 1] += roff[x];
+    clk.lap("fetch: row counts");
     if (roff[n] != ne) {
         ccg_set_error("ccg_snn_graph_fetch: internal count mismatch (%lld vs %lld)", (long long)roff[n], (long long)ne);
         return CCG_EINVAL;
     }
     snn_host_parallel(n, nt, [&](int64_t x0, int64_t x1) {
-        std::vector<std::pair<int32_t, uint8_t>> buf;
+        std::vector<uint64_t> buf;  // y << 8 | weight: one 64-bit sort key per edge
         for (int64_t x = x0; x < x1; ++x) {
             buf.clear();
             const int64_t c = S->rcls[x];
             auto r = above(c, (int32_t)x);
-            for (auto p = r.first; p < r.second; ++p) buf.emplace_back(*p, wself);
+            for (auto p = r.first; p < r.second; ++p) buf.push_back((uint64_t)*p << 8 | wself);
             for (int64_t a = aoff[c]; a < aoff[c + 1]; ++a) {
+                const unsigned v = av[a];
+                if (!snn_host_has(sp, v, t)) continue;
+                const uint64_t w = (v >> (8 * t)) & 0xFFu;
                 auto q = above(adj[a], (int32_t)x);
-                for (auto p = q.first; p < q.second; ++p) buf.emplace_back(*p, aw[a]);
+                for (auto p = q.first; p < q.second; ++p) buf.push_back((uint64_t)*p << 8 | w);
             }
             std::sort(buf.begin(), buf.end());
-            int64_t e = roff[x];
-            for (const auto& pw : buf) {
-                if (out_i) out_i[e] = (int32_t)x;
-                if (out_j) out_j[e] = pw.first;
-                if (out_w) out_w[e] = (double)pw.second;
-                ++e;
-            }
+            const int64_t e = roff[x];
+            const int64_t m = (int64_t)buf.size();
+            if (out_i) std::fill(out_i + e, out_i + e + m, (int32_t)x);
+            if (out_j)
+                for (int64_t z = 0; z < m; ++z) out_j[e + z] = (int32_t)(buf[z] >> 8);
+            if (out_w)
+                for (int64_t z = 0; z < m; ++z) out_w[e + z] = (double)(buf[z] & 0xFFu);
         }
     });
+    clk.lap("fetch: rows");
     return CCG_OK;
 }
 

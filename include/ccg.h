@@ -704,10 +704,26 @@ int ccg_scan_i64_dev(ccg_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, v
 #define CCG_KT_SILHOUETTE 3   /* whole ccg_silhouette_dev call */
 #define CCG_KT_COCLUSTER 4    /* the co-cluster tile kernel */
 #define CCG_KT_COUNT 5
+/* Not a kernel: host milliseconds spent blocked on the pinned upload ring
+ * (a full ring means the host is CCG_PIN_RING uploads ahead of the GPU:
+ * back-pressure, not launch cost) and the number of such waits since the
+ * last read.  Always accounted (no ccg_timing_enable needed). */
+#define CCG_KT_HOST_RING_WAIT 100
 int ccg_timing_enable(ccg_ctx* ctx, int enable);
 /* Synchronises, returns the summed milliseconds and launch count of kernel
  * `which` since the last read, and resets that counter. */
 int ccg_timing_read(ccg_ctx* ctx, int which, double* total_ms, int64_t* launches);
+
+/* ------------------------------------------ host clustering stand-in -- */
+/* Louvain community detection (modularity with igraph's resolution-scaled
+ * gain, local moving + aggregation) of an undirected weighted edge list, on
+ * the calling host thread; no device, no context.  The Python drop-in's
+ * stand-in for igraph::cluster_leiden (R/consensusClust.R:656-658 via
+ * bluster, :430-433), which R keeps.  Not igraph's algorithm: labels differ
+ * from igraph's.  Edges (ei[e], ej[e]) with ei != ej in [0, n), weights >= 0;
+ * labels[n] receives 1..C in order of first appearance.  Thread-safe. */
+int ccg_host_louvain(int64_t n, int64_t ne, const int32_t* ei, const int32_t* ej, const double* w,
+                     double resolution, uint64_t seed, int32_t* labels);
 
 #ifdef __cplusplus
 }

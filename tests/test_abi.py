@@ -2,6 +2,7 @@
 (no compute: this runs without a GPU)."""
 import ctypes
 import os
+import shutil
 import subprocess
 
 import pytest
@@ -41,9 +42,12 @@ def test_abi_version_and_error_path():
     assert b"NULL" in lib.ccg_last_error()
 
 
-def test_library_is_gfx950_code_object():
-    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
-                                  stderr=subprocess.STDOUT).decode(errors="replace")
+def test_library_is_gfx950_code_object(tmp_path):
+    # (--offloading extracts the bundled code objects next to its input: run it on a copy)
+    lib = tmp_path / "libccg.so"
+    shutil.copyfile(_lib.LIB_PATH, lib)
+    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                                  stderr=subprocess.STDOUT, cwd=tmp_path).decode(errors="replace")
     assert "gfx950" in out
 
 

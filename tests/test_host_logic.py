@@ -5,7 +5,8 @@ import pytest
 
 import oracle as O
 from consensusclustr_amd import consensus as C
-from consensusclustr_amd.cluster_host import louvain
+from consensusclustr_amd import _lib
+from consensusclustr_amd.cluster_host import louvain, louvain_py
 from consensusclustr_amd.sharding import boot_shard, row_slabs, slab_offset, slab_pairs
 
 
@@ -87,9 +88,58 @@ def test_louvain_recovers_two_cliques():
                 ej.append(base + b)
     ei.append(0)
     ej.append(10)
-    lab = louvain(20, np.array(ei), np.array(ej), np.ones(len(ei)), resolution=1.0, seed=0)
-    assert len(set(lab[:10])) == 1 and len(set(lab[10:])) == 1 and lab[0] != lab[10]
-    assert lab.min() == 1
+    for f in (louvain, louvain_py):
+        lab = f(20, np.array(ei), np.array(ej), np.ones(len(ei)), resolution=1.0, seed=0)
+        assert len(set(lab[:10])) == 1 and len(set(lab[10:])) == 1 and lab[0] != lab[10]
+        assert lab.min() == 1 and lab[0] == 1
+
+
+def _planted(n, blocks, m, p_out, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, n, m)
+    size = n // blocks
+    b = np.where(rng.random(m) < p_out, rng.integers(0, n, m), (a // size) * size + rng.integers(0, size, m))
+    keep = a != b
+    a, b = a[keep], b[keep]
+    key = np.unique(np.minimum(a, b) * n + np.maximum(a, b))
+    return key // n, key % n, rng.random(key.size) + 0.5
+
+
+def test_native_louvain_recovers_planted_blocks_like_the_python_restatement():
+    """ccg_host_louvain (the drop-in's default clusterer) and louvain_py (the
+    same algorithm in Python) both recover a planted 4-block partition."""
+    n = 2000
+    ei, ej, w = _planted(n, 4, 40000, 0.1, 3)
+    truth = np.arange(n) // 500
+    for f in (louvain, louvain_py):
+        lab = f(n, ei, ej, w, resolution=1.0, seed=7)
+        assert lab.dtype == np.int32 and lab.min() == 1
+        # same partition as the truth (labels in order of first appearance)
+        assert np.array_equal(lab, np.unique(truth, return_inverse=True)[1] + 1)
+
+
+def test_native_louvain_is_deterministic_and_thread_safe():
+    from concurrent.futures import ThreadPoolExecutor
+    n = 3000
+    ei, ej, w = _planted(n, 12, 30000, 0.4, 5)
+    jobs = [(float(r), s) for r in (0.3, 0.8, 1.5) for s in (1, 2)]
+    serial = [louvain(n, ei, ej, w, resolution=r, seed=s) for r, s in jobs]
+    with ThreadPoolExecutor(6) as ex:
+        par = list(ex.map(lambda j: louvain(n, ei, ej, w, resolution=j[0], seed=j[1]), jobs * 3))
+    for t, lab in enumerate(par):
+        assert np.array_equal(lab, serial[t % len(jobs)])
+    # more resolution, more clusters
+    assert np.unique(serial[0]).size <= np.unique(serial[4]).size
+
+
+def test_native_louvain_rejects_bad_edges():
+    with pytest.raises(_lib.CcgError):
+        louvain(4, np.array([0, 1]), np.array([1, 1]), np.ones(2))  # self loop
+    with pytest.raises(_lib.CcgError):
+        louvain(4, np.array([0]), np.array([4]), np.ones(1))  # out of range
+    with pytest.raises(_lib.CcgError):
+        louvain(4, np.array([0]), np.array([1]), -np.ones(1))  # negative weight
+    assert np.array_equal(louvain(3, np.array([], np.int32), np.array([], np.int32), np.array([])), [1, 2, 3])
 
 
 @pytest.mark.parametrize("N,G", [(300, 8), (1000, 3), (129, 2), (257, 4)])
