@@ -405,7 +405,9 @@ def cpu_baseline_check(eng, torch, pcs, pcs_cm, boot, u, labels0, tab, cmax, rob
 def workload_text(name, N, d, B, G, emul):
     if name == "cfg3":
         return ("BASELINE cfg3 shapes: 100k cells x 30 PCs, robust mode, kNum 10/15/20 x 20 resolutions; "
-                f"{B} bootstraps per GPU per step ({G * B} total) + co-cluster row slab over all columns")
+                f"{B} bootstraps per GPU per step ({G * B} total) + co-cluster row slab over all columns "
+                "(at 1 GPU: one rank's share of the 8-GPU job; the whole 1000-bootstrap job on one GPU is "
+                "--workload cfg3job)")
     if name == "cfg3job":
         return (f"BASELINE cfg3 as one whole job: {N} cells x {d} PCs, robust, {B * G} bootstraps per step, "
                 "one co-cluster over all their columns")

@@ -261,9 +261,13 @@ __global__ void sil_quant(const double* __restrict__ x, int64_t m, int d, const 
 // int64.
 #define SIL_SB 1024   // threads of the sums kernel
 #define SIL_SP 1024   // positions per sums block
+#ifndef SIL_SGMAX
 #define SIL_SGMAX 4   // labelings per sums block
+#endif
 #define SIL_LDS_CU 163840
+#ifndef SIL_LDS_SUMS
 #define SIL_LDS_SUMS 81920  // two blocks per CU
+#endif
 __host__ __device__ inline size_t sil_tile_lds(int d, int cmax, int G) {
     return (size_t)SIL_SP * 4 + (size_t)G * SIL_SP * 8 + (size_t)G * (cmax + 1) * (d + 2) * 8;
 }

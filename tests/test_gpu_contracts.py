@@ -103,6 +103,34 @@ def test_silhouette_segments_input_written_on_default_stream(engine):
         engine.silhouette_segments_t(x, off, [a.t().contiguous().t() for a in src], C, cell, 4000 * len(segs), means)
 
 
+def test_pinned_ring_wait_is_accounted_and_reset(engine):
+    """CCG_KT_HOST_RING_WAIT: more staged uploads than the ring has slots,
+    queued behind a busy GPU, block the host on the oldest slot; the wait is
+    reported once and then reset (bench.py's host_ring_wait_ms_per_step)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(9)
+    segs = [300, 200]
+    off = np.concatenate([[0], np.cumsum(segs)]).astype(np.int64)
+    x = torch.from_numpy(rng.normal(size=(sum(segs), 4))).to(dev)
+    cell = torch.arange(sum(segs), dtype=torch.int32, device=dev)
+    labs = [torch.from_numpy(rng.integers(1, 4, (2, m)).astype(np.int32)).to(dev) for m in segs]
+    means = [torch.empty(2, dtype=torch.float64, device=dev) for _ in segs]
+    engine.silhouette_segments_t(x, off, labs, 3, cell, sum(segs), means)
+    torch.cuda.synchronize()
+    ref = [m.clone() for m in means]
+    engine.timing_read("host_ring_wait")  # (reset)
+    torch.cuda._sleep(300_000_000)
+    for _ in range(80):  # > CCG_PIN_RING (64) uploads on the legacy stream behind the sleep
+        engine.silhouette_segments_t(x, off, labs, 3, cell, sum(segs), means)
+    torch.cuda.synchronize()
+    ms, waits = engine.timing_read("host_ring_wait")
+    assert waits >= 1 and ms > 0.0
+    assert engine.timing_read("host_ring_wait") == (0.0, 0)
+    for a, b in zip(means, ref):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n", [1, 2048, 64 * 2048 + 1, 1024 * 2048, 1024 * 2048 + 1])
 def test_scan_tile_counts_in_place_and_repeated(engine, n):
     import torch
