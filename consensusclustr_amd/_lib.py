@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libccg.so")
+# CCG_LIB_PATH: another build of the library (variant timing); the default is the in-tree build
+LIB_PATH = os.environ.get("CCG_LIB_PATH") or os.path.join(_HERE, "libccg.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ccg.h")
 
 # error codes (include/ccg.h)

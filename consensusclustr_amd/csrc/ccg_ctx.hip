@@ -121,7 +121,11 @@ int ccg_h2d_staged(ccg_ctx* ctx, void* dst, const void* src, size_t bytes, hipSt
         if (ctx->pin_buf[s]) CCG_HIP(hipHostFree(ctx->pin_buf[s]));
         ctx->pin_buf[s] = nullptr;
         ctx->pin_bytes[s] = 0;
-        const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        // at least 64 KB, powers of two: a slot almost never grows after its
+        // first use (hipHostFree synchronises the device: a regrowth inside a
+        // launch loop leaves the GPU idle while the host waits)
+        size_t want = 65536;
+        while (want < bytes) want *= 2;
         CCG_HIP(hipHostMalloc(&ctx->pin_buf[s], want, hipHostMallocDefault));
         ctx->pin_bytes[s] = want;
     }

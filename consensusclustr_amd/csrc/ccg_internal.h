@@ -82,7 +82,14 @@ struct ccg_timer_rec {
 #define CCG_DERR_KNN_UNIQUE 8     // ccg_knn_boot_dev: n_unique differs from the distinct cells of idx
 #define CCG_DERR_SCAN_RANGE 16    // ccg_scan_i64: a tile sum or prefix outside [0, 2^62) (the status-word packing)
 
-#define CCG_PIN_RING 64  // (a launch set uploads its tables here: the host runs this many uploads ahead)
+#ifndef CCG_PIN_RING
+// a launch set uploads its tables here: the host runs at most this many
+// uploads ahead of the GPU.  Measured (round 6): 8 against 16 / 32 / 64
+// slots -- cfg3 and cfg2 within noise, cfg5 1056-1088 against 990-1046
+// bootstraps/s (a host far ahead fills one stream's queue and blocks there
+// while the other stream runs dry).
+#define CCG_PIN_RING 8
+#endif
 #define CCG_SCAN_SLOTS 8  // streams with their own single-pass scan state per context
 
 struct ccg_ctx {

@@ -1852,9 +1852,9 @@ extern "C" int ccg_knn_segments_dev(ccg_ctx* ctx, const double* rows, int64_t n,
     KnnSegs sg;
     int rc0 = knn_seg_plan(ctx, seg_off, nseg, d, kmax, st, po, hperm, hblk, &sg);
     if (rc0) return rc0;
-    const int rc = knn_run(ctx, rows, n, d, kmax, out_idx, out_dist, stats, st, &sg);
-    CCG_HIP(hipStreamSynchronize(st));  // the host plan buffers must outlive the uploads
-    return rc;
+    // (the plan's tables went through the pinned ring, ccg_h2d_staged: the
+    // host vectors may go now, and the call stays asynchronous)
+    return knn_run(ctx, rows, n, d, kmax, out_idx, out_dist, stats, st, &sg);
 }
 
 // ---------------------------------------------------- distinct cells --
@@ -2966,10 +2966,13 @@ extern "C" int ccg_knn_boot_segments_dev(ccg_ctx* ctx, const double* cells, int6
     ctx->last_fail_count = fail_count;
     ccg_timer_stop(ctx, t_all, st);
     CCG_HIP(hipGetLastError());
-    int nf = 0;
-    if (stats) CCG_HIP(hipMemcpyAsync(&nf, fail_count, sizeof(int), hipMemcpyDeviceToHost, st));
-    CCG_HIP(hipStreamSynchronize(st));  // the host plan vectors must outlive their uploads
+    // (the plan's tables went through the pinned ring: no synchronisation
+    // unless statistics are asked for -- round 5 synchronised every call,
+    // which left the GPU idle between the launch sets of cfg5)
     if (stats) {
+        int nf = 0;
+        CCG_HIP(hipMemcpyAsync(&nf, fail_count, sizeof(int), hipMemcpyDeviceToHost, st));
+        CCG_HIP(hipStreamSynchronize(st));
         stats->queries = n;
         stats->fallback = us.fallback + nf;
         ctx->last_stats = *stats;

@@ -121,7 +121,7 @@ def test_pinned_ring_wait_is_accounted_and_reset(engine):
     ref = [m.clone() for m in means]
     engine.timing_read("host_ring_wait")  # (reset)
     torch.cuda._sleep(300_000_000)
-    for _ in range(80):  # > CCG_PIN_RING (64) uploads on the legacy stream behind the sleep
+    for _ in range(80):  # > CCG_PIN_RING (8) uploads on the legacy stream behind the sleep
         engine.silhouette_segments_t(x, off, labs, 3, cell, sum(segs), means)
     torch.cuda.synchronize()
     ms, waits = engine.timing_read("host_ring_wait")
