@@ -38,5 +38,9 @@ if [ -z "$NO_MICRO" ]; then
   echo "$(date +%T) cknn" >> $R/progress.log
   timeout -k 10 300 python tools/cknn_micro.py > $R/cknn_micro.json 2> $R/cknn_micro.err || exit $?
 fi
+if [ -z "$NO_E2E" ]; then
+  echo "$(date +%T) e2e" >> $R/progress.log
+  timeout -k 10 400 python tools/e2e_cfg2.py > $R/e2e_cfg2.json 2> $R/e2e_cfg2.err || exit $?
+fi
 echo "$(date +%T) done" >> $R/progress.log
 exit 0
