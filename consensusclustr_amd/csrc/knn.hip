@@ -2513,6 +2513,85 @@ __global__ __launch_bounds__(256) void kt_filter_kernel(int u, int kq, int K, in
     }
 }
 
+// Cell-major form of kt_filter_kernel<true> for a batch (round 6): one wave
+// per CELL c of the N, over the nb bootstraps: c's table row is read once and
+// filtered against each bootstrap's presence map in turn, instead of once per
+// (bootstrap, distinct cell) -- the same cell's row was read by ~0.6 nb waves
+// scattered over the grid and the XCDs (2.7x10^8 B of table rows per launch
+// set of 8 at cfg3).  Outputs per distinct cell exactly as kt_filter_kernel.
+__global__ __launch_bounds__(256) void kt_filter_cells_kernel(int nb, int64_t Nc, int kq, int K, int d,
+                                                              const int* __restrict__ cell2u,
+                                                              const int32_t* __restrict__ tab_idx,
+                                                              const double* __restrict__ tab_d2,
+                                                              const double* __restrict__ urows,
+                                                              int32_t* __restrict__ uidx, double* __restrict__ ud2,
+                                                              int* __restrict__ fail_list, double* __restrict__ tau,
+                                                              const int64_t* __restrict__ useg,
+                                                              int* __restrict__ fcnt, int u) {
+    __shared__ KtTauLds tl[4];
+    const int64_t cb = ccg_cdiv(Nc, 4);  // blocks of cells; the rest fill phantom ids
+    if ((int64_t)blockIdx.x >= cb) {
+        // a caller's u above the distinct count (the sticky error is set):
+        // ids [count, u) belong to no cell; give them in-bounds lists (the
+        // outputs are undefined then, as in kt_filter_kernel)
+        const int64_t p0 = useg[nb];
+        for (int64_t t = (int64_t)(blockIdx.x - cb) * blockDim.x + threadIdx.x; t < ((int64_t)u - p0) * kq;
+             t += (int64_t)(gridDim.x - cb) * blockDim.x) {
+            uidx[p0 * kq + t] = 0;
+            ud2[p0 * kq + t] = INFINITY;
+        }
+        return;
+    }
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= Nc) return;
+    const int lane = threadIdx.x & 63;
+    // the bootstraps holding c (lane s < nb <= 64: one ballot)
+    const int us = lane < nb ? cell2u[(int64_t)lane * Nc + c] : -1;
+    unsigned long long pres = __ballot(us >= 0);
+    if (!pres) return;
+    const bool e = lane < K;
+    const int v = e ? tab_idx[c * K + lane] : -1;
+    const double dv = e ? tab_d2[c * K + lane] : INFINITY;
+    // KT_BR bootstraps per round: their presence lookups issued together (one
+    // round at nb <= 8: the lookups are the kernel's dependent-load chain)
+    constexpr int KT_BR = 8;
+    while (pres) {
+        int sb[KT_BR], wb[KT_BR];
+#pragma unroll
+        for (int r = 0; r < KT_BR; ++r) {
+            sb[r] = -1;
+            if (pres) {
+                sb[r] = __ffsll((long long)pres) - 1;
+                pres &= pres - 1;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < KT_BR; ++r) wb[r] = (sb[r] >= 0 && v >= 0) ? cell2u[(int64_t)sb[r] * Nc + v] : -1;
+#pragma unroll
+        for (int r = 0; r < KT_BR; ++r) {
+            if (sb[r] < 0) break;  // (wave-uniform)
+            const int uid = __shfl(us, sb[r], 64), w = wb[r];
+            const double di = w >= 0 ? dv : INFINITY;
+            const unsigned long long m = __ballot(w >= 0);
+            const int rank = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+            if (w >= 0 && rank < kq) {
+                uidx[(int64_t)uid * kq + rank] = w;
+                ud2[(int64_t)uid * kq + rank] = di;
+            }
+            if (__popcll(m) < kq) {  // (wave-uniform)
+                const int* c2u = cell2u + (int64_t)sb[r] * Nc;
+                const double best = kt_tau_wave(tl[threadIdx.x >> 6], lane, kq, K, d, uid, c, v, w, di, c2u, tab_idx,
+                                                urows);
+                if (lane == 0) {
+                    const int64_t f = useg[sb[r]] + atomicAdd(&fcnt[sb[r]], 1);
+                    fail_list[f] = uid;
+                    tau[f] = best;
+                }
+            }
+        }
+    }
+}
+
 extern "C" int ccg_knn_table_dev(ccg_ctx* ctx, const double* pcs, int64_t N, int d, int K, int32_t* tab_idx,
                                  double* tab_d2, ccg_knn_stats* stats, void* stream) {
     CCG_REQUIRE(ctx && pcs && tab_idx && tab_d2, "ccg_knn_table_dev: NULL argument");
@@ -2793,9 +2872,14 @@ extern "C" int ccg_knn_boots_table_dev(ccg_ctx* ctx, int64_t N, int d, const int
     else
         kb_urows_kernel<64><<<(unsigned)ccg_cdiv(u, 4), 256, 0, st>>>(rows, d, u, ustart, srow, urows, idx, nullptr,
                                                                       nullptr);
+#ifdef CCG_KT_UID_MAJOR
     kt_filter_kernel<true><<<(unsigned)ccg_cdiv(u, 4 * KT_CPW), 256, 0, st>>>(
         u, kmax, K, d, ustart, scell, cell2u, tab_idx, tab_d2, urows, uidx, ud2, fail_list, nullptr, ftau, N, useg,
         fcnt_u);
+#else
+    kt_filter_cells_kernel<<<(unsigned)(ccg_cdiv(N, 4) + 16), 256, 0, st>>>(
+        nb, N, kmax, K, d, cell2u, tab_idx, tab_d2, urows, uidx, ud2, fail_list, ftau, useg, fcnt_u, u);
+#endif
     rc = knn_fallback_launch(ctx, urows, u, d, kmax, fail_list, fcnt_u, uidx, ud2, useg, nb, st, true, ftau, fcnt_u);
     if (rc) return rc;
     // 3. expansion to rows (ids of the concatenation); cut ties: the radius
