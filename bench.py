@@ -1080,8 +1080,6 @@ def main():
     co = torch.empty(P, dtype=torch.int16, device=dev)      # uint16 counts (viewed as int16)
     both = torch.empty(P, dtype=torch.int16, device=dev)
 
-    ev_k = [torch.cuda.Event() for _ in range(B)]
-    ev_s = [torch.cuda.Event() for _ in range(B)]
 
     def mark(evs, k):
         # phase events on torch's current stream (the tail's calls order their
