@@ -827,7 +827,9 @@ extern "C" int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co, const uin
 //      desc, original column asc) -- dbscan's stable order() -- top k.
 // A row with more than CKC_CAP candidates sends the call back to the
 // sub-slab path (full rows; bounded workspace).
+#ifndef CKC_SAMPLE
 #define CKC_SAMPLE 4096
+#endif
 #define CKC_CAP 2048
 #define CKC_MIN_N 32768
 
