@@ -213,20 +213,127 @@ __device__ __forceinline__ int64_t cof_orig(int64_t p, int64_t N, const CofCand&
 
 // COF_CAND epilogue of one wave's 64 x 128 quarter (rows ia0.., columns
 // jb0..): lane (h, col) holds rows ia0 + 32 mi + (r & 3) + 8 (r >> 2) + 4 h
-// against column jb0 + 32 ni + col.  Passing pairs are rare (a row keeps a
-// few hundred of N columns): each costs one counter add on its row and one
-// 8-byte store; the common element two fp64 compares.  Kept register-light
-// (the 128 accumulators are live throughout): no wave-level aggregation.
-__device__ __forceinline__ void cof_cand_push(const CofCand& cc, int64_t row, int64_t other, int64_t N,
-                                              unsigned val) {
-    const int slot = atomicAdd(&cc.cnt[row], 1);
-    if (slot < cc.cap) cc.cand[row * cc.cap + slot] = make_uint2((unsigned)cof_orig(other, N, cc), val);
-    else cc.flags[1] = 1;
+// against column jb0 + 32 ni + col.  A passing pair (a row keeps a few
+// hundred of N columns) costs one counter add and one 8-byte store per side
+// it enters; the common element two integer tests.
+// Round 6: the epilogue walks groups of 4 rows x 4 column blocks; within a
+// group it first issues every counter add (one per half-row per group on the
+// row side, one per passing element on the column side), then the stores
+// that use the returned slots -- one wait on the adds per group.  The
+// round-5 form waited on each add before the next element (a push is an
+// atomic whose return value addresses the store), which serialised the
+// adds' latency: the candidate tile took 46.5 ms against the plain
+// triangle's 40.1 at N = 100k, B = 1000.
+#ifndef COF_CAND_RG
+#define COF_CAND_RG 1  // rows per group (measured: 1 fastest; 4 spilled with the 128 accumulators)
+#endif
+template <bool INTERIOR>
+__device__ __forceinline__ void cof_cand_rows(const v16i (&acc)[2][4], int64_t ia0, int64_t jb0, int64_t N,
+                                              int64_t r1, const CofCand& cc, const int (&tj)[4], bool& nan) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const unsigned long long below = (1ull << lane) - 1;
+    const unsigned long long half = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+    constexpr int RG = COF_CAND_RG;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int rg = 0; rg < 16 / RG; ++rg) {
+            bool pr[RG][4], pc[RG][4];
+            unsigned val[RG][4];
+            int64_t gi[RG];
+            int ti[RG];
+#pragma unroll
+            for (int q = 0; q < RG; ++q) {
+                const int r = RG * rg + q;
+                gi[q] = ia0 + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h;
+                ti[q] = (INTERIOR || gi[q] < r1) ? cc.tnum[gi[q]] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < RG; ++q)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const int a = acc[mi][ni][RG * rg + q];
+                    const int cv = a & 16383, bv = a >> 14;
+                    bool ok = true;
+                    if (!INTERIOR) {
+                        const int64_t gj = jb0 + 32 * ni + col;
+                        ok = gi[q] < r1 && gj < N && gj > gi[q];
+                    }
+                    nan |= ok && bv == 0;
+                    const int dc = cv * CKC_NBK;
+                    val[q][ni] = (unsigned)cv | ((unsigned)bv << 16);
+                    // (24-bit multiplies: tnum in [-1, CKC_NBK], both < 2^17 -- a
+                    // full-rate v_mul_i32_i24 instead of the quarter-rate
+                    // 32-bit multiply, twice per element)
+                    pr[q][ni] = ok && bv > 0 && dc >= __mul24(ti[q], bv);
+                    pc[q][ni] = ok && bv > 0 && dc >= __mul24(tj[ni], bv);
+                }
+            // row side: per row q, the half's passing elements over the 4
+            // column blocks take consecutive slots (lane order within a block)
+            unsigned long long hm[RG][4];
+            int rbase[RG], rlead[RG];
+            bool rany = false;
+#pragma unroll
+            for (int q = 0; q < RG; ++q) {
+                int tot = 0;
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    hm[q][ni] = __ballot(pr[q][ni]);
+                    tot += __popcll(hm[q][ni] & half);
+                }
+                // the half's first lane issues the add (lanes 0 and 32 lead)
+                rlead[q] = tot;
+                rbase[q] = 0;
+                rany |= tot > 0;
+            }
+            if (__any(rany)) {  // (most groups have a passing pair somewhere)
+#pragma unroll
+                for (int q = 0; q < RG; ++q)
+                    if (col == 0 && rlead[q] > 0) rbase[q] = atomicAdd(&cc.cnt[gi[q]], rlead[q]);
+            }
+            int cslot[RG][4];
+#pragma unroll
+            for (int q = 0; q < RG; ++q)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    cslot[q][ni] = 0;
+                    if (pc[q][ni]) cslot[q][ni] = atomicAdd(&cc.cnt[jb0 + 32 * ni + col], 1);
+                }
+            // the stores (the first use of the returned slots)
+#pragma unroll
+            for (int q = 0; q < RG; ++q) {
+                const int b0 = __builtin_amdgcn_readlane(rbase[q], 0), b1 = __builtin_amdgcn_readlane(rbase[q], 32);
+                int off = h ? b1 : b0;
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const unsigned long long m = hm[q][ni] & half;
+                    if (pr[q][ni]) {
+                        const int slot = off + __popcll(m & below);
+                        const int64_t gj = jb0 + 32 * ni + col;
+                        if (slot < cc.cap)
+                            cc.cand[gi[q] * cc.cap + slot] = make_uint2((unsigned)cof_orig(gj, N, cc), val[q][ni]);
+                        else
+                            cc.flags[1] = 1;
+                    }
+                    off += __popcll(m);
+                }
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    if (pc[q][ni]) {
+                        const int64_t gj = jb0 + 32 * ni + col;
+                        if (cslot[q][ni] < cc.cap)
+                            cc.cand[gj * cc.cap + cslot[q][ni]] =
+                                make_uint2((unsigned)cof_orig(gi[q], N, cc), val[q][ni]);
+                        else
+                            cc.flags[1] = 1;
+                    }
+            }
+        }
 }
 
 __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64_t ia0, int64_t jb0, int64_t N,
                                                   int64_t r1, const CofCand& cc) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const int lane = threadIdx.x & 63, col = lane & 31;
     // the lane's 4 columns' thresholds once (not per row); an interior
     // quarter (every column above every row, inside N and the slab) needs no
     // per-element masks
@@ -238,41 +345,8 @@ __device__ __forceinline__ void cof_cand_epilogue(const v16i (&acc)[2][4], int64
     }
     const bool interior = jb0 > ia0 + 63 && jb0 + 128 <= N && ia0 + 64 <= r1;
     bool nan = false;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t gi = ia0 + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const bool row_ok = gi < r1;
-            const int ti = row_ok ? cc.tnum[gi] : 0;  // (rows past the slab never pass: ok is false)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int64_t gj = jb0 + 32 * ni + col;
-                const int a = acc[mi][ni][r];
-                const int cv = a & 16383, bv = a >> 14;
-                const bool ok = interior || (row_ok && gj < N && gj > gi);
-                nan |= ok && bv == 0;
-                const int dc = cv * CKC_NBK;
-                const unsigned val = (unsigned)cv | ((unsigned)bv << 16);
-                // row gi is shared by the 32 lanes of this half: one counter
-                // add per half for all its passing pairs (lane order)
-                const bool pi = ok && bv > 0 && dc >= ti * bv;
-                const unsigned long long m = __ballot(pi);
-                if (m) {
-                    const unsigned long long hm = h ? (m & 0xFFFFFFFF00000000ull) : (m & 0xFFFFFFFFull);
-                    const int leader = hm ? __ffsll((long long)hm) - 1 : lane;
-                    int base = 0;
-                    if (lane == leader && hm) base = atomicAdd(&cc.cnt[gi], __popcll(hm));
-                    base = __shfl(base, leader, 64);
-                    if (pi) {
-                        const int slot = base + __popcll(hm & ((1ull << lane) - 1));
-                        if (slot < cc.cap) cc.cand[gi * cc.cap + slot] = make_uint2((unsigned)cof_orig(gj, N, cc), val);
-                        else cc.flags[1] = 1;
-                    }
-                }
-                if (ok && bv > 0 && dc >= tj[ni] * bv) cof_cand_push(cc, gj, gi, N, val);
-            }
-        }
+    if (interior) cof_cand_rows<true>(acc, ia0, jb0, N, r1, cc, tj, nan);
+    else cof_cand_rows<false>(acc, ia0, jb0, N, r1, cc, tj, nan);
     if (__any(nan) && lane == 0) cc.flags[0] = 1;
 }
 
