@@ -665,7 +665,9 @@ template <int MODE>
 static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, int64_t N, int64_t r0, int64_t r1,
                        int64_t TC, int64_t I0, int64_t ntiles, const CofPlan& pl, const uint16_t* co_prev,
                        const uint16_t* both_prev, uint16_t* co, uint16_t* both, double* dist, const uint32_t* cb_prev,
-                       uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{}) {
+                       uint32_t* cb, hipStream_t st, int64_t NB = 0, const CofCand& cc = CofCand{},
+                       bool prepared = false) {
+    if (!prepared) {  // (prepared: the chunk's slot tables and entry matrix are in pl from an earlier launch)
     cof_slots_kernel<<<1, 1024, 0, st>>>(pl.colC + cb0, Bc, pl.ccol, pl.nslot, pl.desc, pl.tmask);
     const dim3 eg((unsigned)std::min<int64_t>(ccg_cdiv(pl.Npad / 4, 256), 128),
                   (unsigned)std::min<int64_t>(pl.maxslots, COF_ENT_GRID));
@@ -675,6 +677,7 @@ static void cof_launch(int label_bits, const void* A, int64_t cb0, int64_t Bc, i
     else
         cof_entries_kernel<uint16_t><<<eg, 256, 0, st>>>((const uint16_t*)A + cb0 * N, N, pl.Npad, pl.desc, pl.ccol,
                                                          pl.nslot, pl.E);
+    }
     cof_tile_kernel<MODE><<<(unsigned)cof_tile_blocks(ccg_cdiv(r1 - r0, COF_BM), TC, I0, MODE != COF_RECT), 256, 0,
                             st>>>(pl.E, pl.Npad, N, r0, r1, TC, I0, pl.nslot, pl.tmask, co_prev,
                                                             both_prev, co, both, dist, cb_prev, cb, NB ? NB : N, cc);
@@ -1049,6 +1052,12 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     const unsigned pg = (unsigned)std::min<int64_t>(ccg_cdiv(B * N, 256), 65536);
     if (label_bits == 8) ckc_permute_kernel<uint8_t><<<pg, 256, 0, st>>>((const uint8_t*)A, N, B, pmul, padd, (uint8_t*)Ap);
     else ckc_permute_kernel<uint16_t><<<pg, 256, 0, st>>>((const uint16_t*)A, N, B, pmul, padd, (uint16_t*)Ap);
+    // one column plan and entry matrix for both GEMMs (the permuted columns,
+    // one chunk; round 5 built them twice, 0.7 ms per call at N = 100k)
+    CofPlan pl;
+    int rc = cof_plan(ctx, Ap, label_bits, N, B, st, &pl);
+    if (rc) return rc;
+    if (pl.cuts.size() != 2) return CCG_OK;  // more than one column chunk: not done (the sub-slab path)
     // 1. thresholds, in row chunks of <= 2 GB of sampled similarities
     int64_t R = ((2LL << 30) / (4 * NS)) / COF_BM * COF_BM;
     R = std::max<int64_t>(R, COF_BM);
@@ -1056,23 +1065,21 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     if (!cb) return CCG_ENOMEM;
     for (int64_t a = 0; a < N; a += R) {
         const int64_t b = std::min(N, a + R);
-        int rc = ccg_cocluster_rows_packed(ctx, Ap, label_bits, N, B, a, b, cb, st, NS);
-        if (rc) return rc;
+        const int64_t TCs = ccg_cdiv(NS, COF_BN), I0s = a / COF_BM, TRs = ccg_cdiv(b - a, COF_BM);
+        CCG_REQUIRE(cof_tile_blocks(TRs, TCs, I0s, false) < (1LL << 31), "consensus kNN: too many tiles");
+        cof_launch<COF_RECT>(label_bits, Ap, 0, B, N, a, b, TCs, I0s, TRs * TCs, pl, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, cb, st, NS, CofCand{}, a > 0);
         ckc_tau_kernel<<<(unsigned)ccg_cdiv(b - a, 4), 256, 0, st>>>(cb, a, b, NS, k, tnum);
     }
     // 2. the triangle with the candidate epilogue
     CCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (N + 64), st));
-    CofPlan pl;
-    int rc = cof_plan(ctx, Ap, label_bits, N, B, st, &pl);
-    if (rc) return rc;
-    if (pl.cuts.size() != 2) return CCG_OK;  // more than one column chunk: not done (the sub-slab path)
     const int64_t TC = ccg_cdiv(N, COF_BN), TR = ccg_cdiv(N, COF_BM);
     auto fl = [](int64_t x) { return (x / 2) * (x / 2 - 1) + ((x & 1) ? x / 2 : 0); };
     const int64_t ntiles = TR * TC - fl(TR);
     CCG_REQUIRE(cof_tile_blocks(TR, TC, 0, true) < (1LL << 31), "consensus kNN: too many tiles");
     CofCand cc{tnum, cnt, cand, CKC_CAP, pmul, padd, ~0ull / (uint64_t)N, flags};
     cof_launch<COF_CAND>(label_bits, Ap, 0, B, N, 0, N, TC, 0, ntiles, pl, nullptr, nullptr, nullptr, nullptr, nullptr,
-                         nullptr, nullptr, st, N, cc);
+                         nullptr, nullptr, st, N, cc, true);
     CCG_HIP(hipGetLastError());
     int hf[2] = {0, 0};
     CCG_HIP(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, st));
