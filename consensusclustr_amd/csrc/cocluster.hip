@@ -759,11 +759,14 @@ static int ccg_cocluster_rows_packed(ccg_ctx* ctx, const void* A, int label_bits
 // an equal value never displaces an earlier j) into a sorted register list;
 // the 64 lists are merged by k rounds of wave arg-max.
 #define CKNN_K 32
-__device__ __forceinline__ void cknn_insert(float (&lv)[CKNN_K], int (&li)[CKNN_K], float s, int j) {
+// (KL: the per-lane list length; any KL >= k gives the same top k -- no
+// lane holds more than k of them)
+template <int KL = CKNN_K>
+__device__ __forceinline__ void cknn_insert(float (&lv)[KL], int (&li)[KL], float s, int j) {
     float cv = s;
     int ci = j;
 #pragma unroll
-    for (int t = 0; t < CKNN_K; ++t) {
+    for (int t = 0; t < KL; ++t) {
         const bool sw = (cv > lv[t]) || (cv == lv[t] && ci < li[t]);
         const float tv = lv[t];
         const int ti = li[t];
@@ -774,8 +777,8 @@ __device__ __forceinline__ void cknn_insert(float (&lv)[CKNN_K], int (&li)[CKNN_
     }
 }
 
-__device__ __forceinline__ void cknn_merge_out(float (&lv)[CKNN_K], int (&li)[CKNN_K], int k,
-                                               int32_t* __restrict__ out) {
+template <int KL = CKNN_K>
+__device__ __forceinline__ void cknn_merge_out(float (&lv)[KL], int (&li)[KL], int k, int32_t* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     for (int r = 0; r < k; ++r) {
         float bk = lv[0];
@@ -792,12 +795,12 @@ __device__ __forceinline__ void cknn_merge_out(float (&lv)[CKNN_K], int (&li)[CK
         if (lane == 0) out[r] = bi;
         if (li[0] == bi) {
 #pragma unroll
-            for (int t = 0; t < CKNN_K - 1; ++t) {
+            for (int t = 0; t < KL - 1; ++t) {
                 lv[t] = lv[t + 1];
                 li[t] = li[t + 1];
             }
-            lv[CKNN_K - 1] = -INFINITY;
-            li[CKNN_K - 1] = 0x7fffffff;
+            lv[KL - 1] = -INFINITY;
+            li[KL - 1] = 0x7fffffff;
         }
     }
 }
@@ -935,7 +938,7 @@ __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B
 // 2 / CKC_NBK, a few more candidates per row.
 __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict__ cb, int64_t a, int64_t b,
                                                       int64_t NS, int k, int* __restrict__ tnum) {
-    __shared__ unsigned hist[4][CKC_NBK];
+    __shared__ __attribute__((aligned(16))) unsigned hist[4][CKC_NBK];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = a + (int64_t)blockIdx.x * 4 + wv;
     if (row >= b) return;  // (whole waves: the wave's LDS slice is its own)
@@ -947,14 +950,26 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
     asm volatile("" ::: "memory");
     const uint32_t* r = cb + (row - a) * NS;
     int usable = 0;
-    for (int64_t q = lane; q < NS; q += 64) {
-        const uint32_t v = r[q];
-        const unsigned c = v & 0xFFFFu, u = v >> 16;
-        if (q == row || u == 0) continue;
-        ++usable;
-        const float s = (float)c * __builtin_amdgcn_rcpf((float)u);
-        const int bk = min(CKC_NBK - 1, max(0, (int)(s * (float)CKC_NBK)));
-        atomicAdd(&h[bk], 1u);
+    // (loads 8 at a time ahead of their LDS adds: one load per iteration was a
+    // latency chain at 8 waves per CU)
+    constexpr int TU = 8;
+    for (int64_t q0 = 0; q0 < NS; q0 += 64 * TU) {
+        uint32_t v[TU];
+#pragma unroll
+        for (int t = 0; t < TU; ++t) {
+            const int64_t q = q0 + 64 * t + lane;
+            v[t] = q < NS ? r[q] : 0u;
+        }
+#pragma unroll
+        for (int t = 0; t < TU; ++t) {
+            const int64_t q = q0 + 64 * t + lane;
+            const unsigned c = v[t] & 0xFFFFu, u = v[t] >> 16;
+            if (q == row || u == 0) continue;  // (u == 0 also past NS)
+            ++usable;
+            const float s = (float)c * __builtin_amdgcn_rcpf((float)u);
+            const int bk = min(CKC_NBK - 1, max(0, (int)(s * (float)CKC_NBK)));
+            atomicAdd(&h[bk], 1u);
+        }
     }
     for (int o = 32; o > 0; o >>= 1) usable += __shfl_xor(usable, o, 64);
     __builtin_amdgcn_wave_barrier();
@@ -962,7 +977,10 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
     // the lane holding the k-th largest: suffix sums of the lanes' bucket counts
     int mine = 0;
 #pragma unroll
-    for (int i = 0; i < PB; ++i) mine += (int)h[lane * PB + i];
+    for (int i = 0; i < PB; i += 4) {
+        const uint4 hv = *reinterpret_cast<const uint4*>(&h[lane * PB + i]);
+        mine += (int)(hv.x + hv.y + hv.z + hv.w);
+    }
     int suf = mine;  // inclusive suffix sum over lanes >= lane
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -994,6 +1012,7 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
 // Per permuted row (one wave): the row's candidates, exact fp32 similarity,
 // top k by (sim desc, original column asc), written to the row's original
 // position.
+template <int KL>
 __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict__ cand, const int* __restrict__ cnt,
                                                          int cap, int64_t N, int64_t pmul, int64_t padd, int k,
                                                          int32_t* __restrict__ out) {
@@ -1002,10 +1021,10 @@ __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict
     if (p >= N) return;
     const int n = min(cnt[p], cap);
     const uint2* c = cand + p * cap;
-    float lv[CKNN_K];
-    int li[CKNN_K];
+    float lv[KL];
+    int li[KL];
 #pragma unroll
-    for (int t = 0; t < CKNN_K; ++t) {
+    for (int t = 0; t < KL; ++t) {
         lv[t] = -INFINITY;
         li[t] = 0x7fffffff;
     }
@@ -1014,12 +1033,12 @@ __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict
         const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
         const float s = (float)((double)co / (double)u);
         const int j = (int)v.x;
-        if (s < lv[CKNN_K - 1] || (s == lv[CKNN_K - 1] && j > li[CKNN_K - 1])) continue;
-        cknn_insert(lv, li, s, j);
+        if (s < lv[KL - 1] || (s == lv[KL - 1] && j > li[KL - 1])) continue;
+        cknn_insert<KL>(lv, li, s, j);
     }
     const int64_t o = (int64_t)(((unsigned __int128)p * (unsigned __int128)pmul + (unsigned __int128)padd) %
                                 (unsigned __int128)N);
-    cknn_merge_out(lv, li, k, out + o * k);
+    cknn_merge_out<KL>(lv, li, k, out + o * k);
 }
 
 static int64_t ckc_gcd(int64_t a, int64_t b) {
@@ -1086,7 +1105,9 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     CCG_HIP(hipStreamSynchronize(st));
     if (hf[1]) return CCG_OK;  // overflow: not done
     // 3. per-row selection
-    ckc_select_kernel<<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
+    // (per-lane lists of 20 for k <= 20 -- kNum's usual maximum -- instead of 32: a shorter insertion chain)
+    if (k <= 20) ckc_select_kernel<20><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
+    else ckc_select_kernel<CKNN_K><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
     CCG_HIP(hipMemcpyAsync(d_nan_flag, flags, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     CCG_HIP(hipGetLastError());
     *done = true;
