@@ -183,8 +183,9 @@ __global__ __launch_bounds__(256) void cof_entries_kernel(const T* __restrict__ 
 // the test is exact in int32: co CKC_NBK >= tnum both (< 2^26 on both sides;
 // tnum = -1: every pair with both > 0) -- three VALU where round 4's fp64
 // test against tau - ulp/2 took two conversions, a multiply and a compare.
-// A row's entries go to cand[row * cap + slot] as (original column id,
-// co | both << 16).
+// A row's entries go to cand[row * cap + slot] as (the other position,
+// co | both << 16); the selection maps positions to original ids (round 6:
+// the epilogue no longer runs the modular reduction per push).
 #define CKC_NBK 4096
 struct CofCand {
     const int* tnum;
@@ -206,10 +207,6 @@ __device__ __forceinline__ int64_t ckc_mod(uint64_t x, int64_t N, uint64_t pinv)
     return (int64_t)r;
 }
 
-// p * pmul + padd < N^2 + N < 2^63 for N < 2^31.
-__device__ __forceinline__ int64_t cof_orig(int64_t p, int64_t N, const CofCand& cc) {
-    return ckc_mod((uint64_t)p * (uint64_t)cc.pmul + (uint64_t)cc.padd, N, cc.pinv);
-}
 
 // COF_CAND epilogue of one wave's 64 x 128 quarter (rows ia0.., columns
 // jb0..): lane (h, col) holds rows ia0 + 32 mi + (r & 3) + 8 (r >> 2) + 4 h
@@ -311,7 +308,7 @@ __device__ __forceinline__ void cof_cand_rows(const v16i (&acc)[2][4], int64_t i
                         const int slot = off + __popcll(m & below);
                         const int64_t gj = jb0 + 32 * ni + col;
                         if (slot < cc.cap)
-                            cc.cand[gi[q] * cc.cap + slot] = make_uint2((unsigned)cof_orig(gj, N, cc), val[q][ni]);
+                            cc.cand[gi[q] * cc.cap + slot] = make_uint2((unsigned)gj, val[q][ni]);
                         else
                             cc.flags[1] = 1;
                     }
@@ -323,7 +320,7 @@ __device__ __forceinline__ void cof_cand_rows(const v16i (&acc)[2][4], int64_t i
                         const int64_t gj = jb0 + 32 * ni + col;
                         if (cslot[q][ni] < cc.cap)
                             cc.cand[gj * cc.cap + cslot[q][ni]] =
-                                make_uint2((unsigned)cof_orig(gi[q], N, cc), val[q][ni]);
+                                make_uint2((unsigned)gi[q], val[q][ni]);
                         else
                             cc.flags[1] = 1;
                     }
@@ -1014,8 +1011,8 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
 // position.
 template <int KL>
 __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict__ cand, const int* __restrict__ cnt,
-                                                         int cap, int64_t N, int64_t pmul, int64_t padd, int k,
-                                                         int32_t* __restrict__ out) {
+                                                         int cap, int64_t N, int64_t pmul, int64_t padd, uint64_t pinv,
+                                                         int k, int32_t* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (p >= N) return;
@@ -1032,12 +1029,13 @@ __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict
         const uint2 v = c[e];
         const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
         const float s = (float)((double)co / (double)u);
-        const int j = (int)v.x;
-        if (s < lv[KL - 1] || (s == lv[KL - 1] && j > li[KL - 1])) continue;
+        if (s < lv[KL - 1]) continue;  // (a tie with the list's last needs the original id)
+        // the candidate's original column (the epilogue stores permuted positions)
+        const int j = (int)ckc_mod((uint64_t)v.x * (uint64_t)pmul + (uint64_t)padd, N, pinv);
+        if (s == lv[KL - 1] && j > li[KL - 1]) continue;
         cknn_insert<KL>(lv, li, s, j);
     }
-    const int64_t o = (int64_t)(((unsigned __int128)p * (unsigned __int128)pmul + (unsigned __int128)padd) %
-                                (unsigned __int128)N);
+    const int64_t o = ckc_mod((uint64_t)p * (uint64_t)pmul + (uint64_t)padd, N, pinv);
     cknn_merge_out<KL>(lv, li, k, out + o * k);
 }
 
@@ -1106,8 +1104,13 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     if (hf[1]) return CCG_OK;  // overflow: not done
     // 3. per-row selection
     // (per-lane lists of 20 for k <= 20 -- kNum's usual maximum -- instead of 32: a shorter insertion chain)
-    if (k <= 20) ckc_select_kernel<20><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
-    else ckc_select_kernel<CKNN_K><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, k, out_idx);
+    const uint64_t pinv = ~0ull / (uint64_t)N;
+    if (k <= 20)
+        ckc_select_kernel<20><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, pinv, k,
+                                                                        out_idx);
+    else
+        ckc_select_kernel<CKNN_K><<<(unsigned)ccg_cdiv(N, 4), 256, 0, st>>>(cand, cnt, CKC_CAP, N, pmul, padd, pinv, k,
+                                                                            out_idx);
     CCG_HIP(hipMemcpyAsync(d_nan_flag, flags, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     CCG_HIP(hipGetLastError());
     *done = true;
