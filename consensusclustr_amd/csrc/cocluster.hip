@@ -913,12 +913,13 @@ extern "C" int ccg_consensus_knn_dev(ccg_ctx* ctx, const uint16_t* co, const uin
 template <typename T>
 __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B, int64_t pmul, int64_t padd,
                                    T* __restrict__ Ap) {
-    const int64_t tot = B * N;
+    // a thread per position p: its source cell once, then every column b
+    // (round 5 divided a flat index by N per element: a 64-bit software
+    // division per byte)
     const uint64_t pinv = ~0ull / (uint64_t)N;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t b = t / N, p = t - b * N;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
         const int64_t o = ckc_mod((uint64_t)p * (uint64_t)pmul + (uint64_t)padd, N, pinv);
-        Ap[t] = A[b * N + o];
+        for (int64_t b = blockIdx.y; b < B; b += gridDim.y) Ap[b * N + p] = A[b * N + o];
     }
 }
 
@@ -1066,7 +1067,7 @@ static int ckc_run(ccg_ctx* ctx, const void* A, int label_bits, int64_t N, int64
     int* tnum = (int*)small;
     int* cnt = tnum + N;
     int* flags = cnt + N;  // [0] both == 0 somewhere, [1] overflow
-    const unsigned pg = (unsigned)std::min<int64_t>(ccg_cdiv(B * N, 256), 65536);
+    const dim3 pg((unsigned)std::min<int64_t>(ccg_cdiv(N, 256), 1024), (unsigned)std::min<int64_t>(B, 64));
     if (label_bits == 8) ckc_permute_kernel<uint8_t><<<pg, 256, 0, st>>>((const uint8_t*)A, N, B, pmul, padd, (uint8_t*)Ap);
     else ckc_permute_kernel<uint16_t><<<pg, 256, 0, st>>>((const uint16_t*)A, N, B, pmul, padd, (uint16_t*)Ap);
     // one column plan and entry matrix for both GEMMs (the permuted columns,
