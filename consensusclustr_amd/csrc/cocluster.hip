@@ -936,20 +936,23 @@ __global__ void ckc_permute_kernel(const T* __restrict__ A, int64_t N, int64_t B
 // 2 / CKC_NBK, a few more candidates per row.
 __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict__ cb, int64_t a, int64_t b,
                                                       int64_t NS, int k, int* __restrict__ tnum) {
-    __shared__ __attribute__((aligned(16))) unsigned hist[4][CKC_NBK];
+    // two 16-bit bucket counts per LDS word (a row counts at most NS <= 2^16
+    // values): 8 KB per wave instead of 16, so 5 blocks per CU instead of 2
+    __shared__ __attribute__((aligned(16))) unsigned hist[4][CKC_NBK / 2];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = a + (int64_t)blockIdx.x * 4 + wv;
     if (row >= b) return;  // (whole waves: the wave's LDS slice is its own)
     unsigned* h = hist[wv];
     constexpr int PB = CKC_NBK / 64;  // buckets per lane, lane l owning [l PB, (l + 1) PB)
+    constexpr int PW = PB / 2;        // their words
 #pragma unroll
-    for (int i = 0; i < PB; i += 4) *reinterpret_cast<uint4*>(&h[lane * PB + i]) = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = 0; i < PW; i += 4) *reinterpret_cast<uint4*>(&h[lane * PW + i]) = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     const uint32_t* r = cb + (row - a) * NS;
     int usable = 0;
     // (loads 8 at a time ahead of their LDS adds: one load per iteration was a
-    // latency chain at 8 waves per CU)
+    // latency chain)
     constexpr int TU = 8;
     for (int64_t q0 = 0; q0 < NS; q0 += 64 * TU) {
         uint32_t v[TU];
@@ -966,7 +969,7 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
             ++usable;
             const float s = (float)c * __builtin_amdgcn_rcpf((float)u);
             const int bk = min(CKC_NBK - 1, max(0, (int)(s * (float)CKC_NBK)));
-            atomicAdd(&h[bk], 1u);
+            atomicAdd(&h[bk >> 1], (bk & 1) ? 0x10000u : 1u);
         }
     }
     for (int o = 32; o > 0; o >>= 1) usable += __shfl_xor(usable, o, 64);
@@ -975,9 +978,10 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
     // the lane holding the k-th largest: suffix sums of the lanes' bucket counts
     int mine = 0;
 #pragma unroll
-    for (int i = 0; i < PB; i += 4) {
-        const uint4 hv = *reinterpret_cast<const uint4*>(&h[lane * PB + i]);
-        mine += (int)(hv.x + hv.y + hv.z + hv.w);
+    for (int i = 0; i < PW; i += 4) {
+        const uint4 hv = *reinterpret_cast<const uint4*>(&h[lane * PW + i]);
+        const unsigned lo = (hv.x & 0xFFFFu) + (hv.y & 0xFFFFu) + (hv.z & 0xFFFFu) + (hv.w & 0xFFFFu);
+        mine += (int)(lo + (hv.x >> 16) + (hv.y >> 16) + (hv.z >> 16) + (hv.w >> 16));
     }
     int suf = mine;  // inclusive suffix sum over lanes >= lane
 #pragma unroll
@@ -994,7 +998,8 @@ __global__ __launch_bounds__(256) void ckc_tau_kernel(const uint32_t* __restrict
         if (lane == L) {
             int acc = suf - mine;  // values above this lane's buckets
             for (int i = PB - 1; i >= 0; --i) {
-                acc += (int)h[lane * PB + i];
+                const unsigned w = h[(lane * PB + i) >> 1];
+                acc += (int)((i & 1) ? (w >> 16) : (w & 0xFFFFu));
                 if (acc >= k) {
                     bk = lane * PB + i;
                     break;
@@ -1029,7 +1034,9 @@ __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict
     for (int e = lane; e < n; e += 64) {
         const uint2 v = c[e];
         const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
-        const float s = (float)((double)co / (double)u);
+        // (the correctly rounded fp32 quotient: equal to (float)((double)co / u)
+        // for operands below 2^24 -- double rounding is innocuous there)
+        const float s = __fdiv_rn((float)co, (float)u);
         if (s < lv[KL - 1]) continue;  // (a tie with the list's last needs the original id)
         // the candidate's original column (the epilogue stores permuted positions)
         const int j = (int)ckc_mod((uint64_t)v.x * (uint64_t)pmul + (uint64_t)padd, N, pinv);
