@@ -1031,17 +1031,29 @@ __global__ __launch_bounds__(256) void ckc_select_kernel(const uint2* __restrict
         lv[t] = -INFINITY;
         li[t] = 0x7fffffff;
     }
-    for (int e = lane; e < n; e += 64) {
-        const uint2 v = c[e];
-        const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
-        // (the correctly rounded fp32 quotient: equal to (float)((double)co / u)
-        // for operands below 2^24 -- double rounding is innocuous there)
-        const float s = __fdiv_rn((float)co, (float)u);
-        if (s < lv[KL - 1]) continue;  // (a tie with the list's last needs the original id)
-        // the candidate's original column (the epilogue stores permuted positions)
-        const int j = (int)ckc_mod((uint64_t)v.x * (uint64_t)pmul + (uint64_t)padd, N, pinv);
-        if (s == lv[KL - 1] && j > li[KL - 1]) continue;
-        cknn_insert<KL>(lv, li, s, j);
+    // (4 candidates' loads per lane issued together: one load per iteration
+    // was a latency chain)
+    for (int e0 = 0; e0 < n; e0 += 256) {
+        uint2 vv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int e = e0 + 64 * t + lane;
+            vv[t] = e < n ? c[e] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint2 v = vv[t];
+            const unsigned co = v.y & 0xFFFFu, u = v.y >> 16;
+            if (u == 0) continue;  // (past n: a candidate always has both > 0)
+            // (the correctly rounded fp32 quotient: equal to (float)((double)co / u)
+            // for operands below 2^24 -- double rounding is innocuous there)
+            const float s = __fdiv_rn((float)co, (float)u);
+            if (s < lv[KL - 1]) continue;  // (a tie with the list's last needs the original id)
+            // the candidate's original column (the epilogue stores permuted positions)
+            const int j = (int)ckc_mod((uint64_t)v.x * (uint64_t)pmul + (uint64_t)padd, N, pinv);
+            if (s == lv[KL - 1] && j > li[KL - 1]) continue;
+            cknn_insert<KL>(lv, li, s, j);
+        }
     }
     const int64_t o = ckc_mod((uint64_t)p * (uint64_t)pmul + (uint64_t)padd, N, pinv);
     cknn_merge_out<KL>(lv, li, k, out + o * k);
